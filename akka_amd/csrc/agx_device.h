@@ -1,0 +1,178 @@
+// agx_device.h — device-side building blocks for the gfx950 dispatch engine:
+// wave64 / block scans, the behaviour table (typed Behaviors.receive subset)
+// and the counter RNG.  Integer only; no MFMA (the path is HBM/scatter-bound).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/akka_gpu.h"
+
+namespace agx {
+
+constexpr int kWave = 64;               // CDNA wavefront
+constexpr uint32_t kLocalMask = 0x0FFFFFFFu;  // key = (owner << 28) | local
+constexpr int kOwnerShift = 28;
+
+// ------------------------------------------------------------------ params
+struct DevParams {
+  uint32_t n_global, n_local, W, T, C, R, rank, kmax;
+  uint32_t ring_stride, fan_k;
+  uint64_t fan_seed, zipf_n;
+  const uint32_t* zipf_cdf;
+  const uint32_t* zipf_perm;
+  const uint64_t* row_ptr;  // local rows
+  const uint32_t* col;      // global dst ids
+  const uint32_t* route;    // global id -> (owner<<28)|local   (R > 1 only)
+  const uint32_t* gid;      // local -> global id              (R > 1 only)
+  uint8_t* kind;
+  uint8_t* alive;           // read-only inside k_apply; stops are committed after it
+  uint32_t* stopq;          // actors that returned Behaviors.stopped this step
+  uint32_t* nstop;
+  uint64_t* state;          // word-major SoA: state[w * n_local + l]
+};
+
+// ------------------------------------------------------------------ RNG
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t fanout_rand(uint64_t seed, uint32_t self, uint32_t h, uint32_t j) {
+  return splitmix64(seed ^ splitmix64(((uint64_t)self << 32) ^ ((uint64_t)h << 4) ^ (uint64_t)j));
+}
+__device__ __forceinline__ uint32_t zipf_index(const uint32_t* cdf, uint64_t n, uint64_t r) {
+  uint32_t u = (uint32_t)(r >> 32);
+  uint64_t lo = 0, hi = n - 1;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (cdf[mid] >= u) hi = mid; else lo = mid + 1;
+  }
+  return (uint32_t)lo;
+}
+
+// ------------------------------------------------------------------ scans
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// inclusive wave64 sum scan
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    uint32_t t = __shfl_up(v, d, kWave);
+    if (lane >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_incl_max(int v) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    int t = __shfl_up(v, d, kWave);
+    if (lane >= (uint32_t)d) v = max(v, t);
+  }
+  return v;
+}
+
+// Block exclusive sum over NT threads (NT multiple of 64, <= 1024).
+// `scratch` needs NT/64 + 1 u32.  Returns exclusive prefix; *total = block sum.
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* scratch, uint32_t* total) {
+  constexpr int NW = NT / kWave;
+  const int tid = threadIdx.x, w = tid / kWave, lane = tid % kWave;
+  uint32_t inc = wave_incl_sum(v);
+  if (lane == kWave - 1) scratch[w] = inc;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t run = 0;
+    for (int i = 0; i < NW; ++i) { uint32_t t = scratch[i]; scratch[i] = run; run += t; }
+    scratch[NW] = run;
+  }
+  __syncthreads();
+  uint32_t r = scratch[w] + inc - v;
+  *total = scratch[NW];
+  __syncthreads();
+  return r;
+}
+
+// Block exclusive max over NT threads; identity -1.
+template <int NT>
+__device__ __forceinline__ int block_excl_max(int v, int* scratch) {
+  constexpr int NW = NT / kWave;
+  const int tid = threadIdx.x, w = tid / kWave, lane = tid % kWave;
+  int inc = wave_incl_max(v);
+  int exc = __shfl_up(inc, 1, kWave);
+  if (lane == 0) exc = -1;
+  if (lane == kWave - 1) scratch[w] = inc;
+  __syncthreads();
+  if (tid == 0) {
+    int run = -1;
+    for (int i = 0; i < NW; ++i) { int t = scratch[i]; scratch[i] = run; run = max(run, t); }
+  }
+  __syncthreads();
+  int r = max(scratch[w], exc);
+  __syncthreads();
+  return r;
+}
+
+// ------------------------------------------------------------------ behaviours
+// One ActorCell.invoke of one message (akka-actor/.../ActorCell.scala:539-555)
+// through the typed ActorAdapter (TY/internal/adapter/ActorAdapter.scala:77-168).
+// `Emit` is called for each tell: emit(dst_global, payload).
+template <typename Emit>
+__device__ __forceinline__ uint32_t apply_msg(const DevParams& P, uint32_t kind, uint32_t self, uint32_t local,
+                                              uint64_t* w, uint32_t src, uint32_t pay, Emit&& emit) {
+  switch (kind) {
+    case AGX_KIND_COUNTER:
+      w[0] += 1;
+      w[1] += pay;  // w[1] exists (array of AGX_MAX_WORDS); only stored back if W > 1
+      return AGX_RES_SAME;
+    case AGX_KIND_RING:
+      w[0] += 1;
+      if (pay > 0) emit((uint32_t)(((uint64_t)self + P.ring_stride) % P.n_global), pay - 1);
+      return AGX_RES_SAME;
+    case AGX_KIND_FANOUT: {
+      w[0] += 1;
+      w[1] += pay;
+      const uint32_t ttl = pay >> 28, h = pay & 0x0FFFFFFFu;
+      if (ttl > 0)
+        for (uint32_t j = 0; j < P.fan_k; ++j) {
+          uint64_t r = fanout_rand(P.fan_seed, self, h, j);
+          uint32_t d = P.zipf_perm[zipf_index(P.zipf_cdf, P.zipf_n, r)];
+          emit(d, ((ttl - 1) << 28) | ((uint32_t)r & 0x0FFFFFFFu));
+        }
+      return AGX_RES_SAME;
+    }
+    case AGX_KIND_FORWARD_RR: {
+      w[0] += 1;
+      if (pay > 0) {
+        uint64_t b = P.row_ptr[local], deg = P.row_ptr[local + 1] - b;
+        if (deg) {
+          uint64_t e = b + (w[1] % deg);
+          w[1] += 1;
+          emit(P.col[e], pay - 1);
+        }
+      }
+      return AGX_RES_SAME;
+    }
+    case AGX_KIND_STOP_AFTER:
+      w[0] += 1;
+      return (w[0] >= w[1]) ? AGX_RES_STOPPED : AGX_RES_SAME;
+    case AGX_KIND_PINGPONG: {
+      // BenchmarkActors.PingPong (akka-bench-jmh/.../actor/BenchmarkActors.scala:20-32)
+      uint32_t res = (w[0] == 0) ? AGX_RES_STOPPED : AGX_RES_SAME;
+      w[1] += 1;
+      emit(src, pay);
+      w[0] -= 1;
+      return res;
+    }
+    case AGX_KIND_EVEN:
+      if (pay & 1u) return AGX_RES_UNHANDLED;
+      w[0] += 1;
+      return AGX_RES_SAME;
+    default:
+      return AGX_RES_SAME;
+  }
+}
+
+}  // namespace agx

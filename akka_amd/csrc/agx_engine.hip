@@ -1,0 +1,989 @@
+// agx_engine.hip — host runtime of the MI355X batched actor-dispatch engine
+// and the C ABI declared in include/akka_gpu.h.
+//
+// One engine = one rank = one GPU (or one virtual rank of a loopback group).
+// Actor state and envelopes live structure-of-arrays in HBM; a superstep is
+//   [exchange (R > 1)] -> compaction -> stable radix sort by destination ->
+//   segmented drain + behaviour-apply (emits the next step's tells).
+// No host round trip per superstep on one GPU; with R > 1 the host reads the
+// per-peer counts once per superstep to size the RCCL send/recv group.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "agx_kernels.h"
+
+using namespace agx;
+
+namespace {
+
+thread_local std::string g_err;
+
+agx_status set_err(agx_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return st;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return set_err(AGX_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                     __LINE__);                                                                \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                            \
+  do {                                                                                            \
+    ncclResult_t _r = (expr);                                                                     \
+    if (_r != ncclSuccess)                                                                        \
+      return set_err(AGX_ECOMM, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(_r), __FILE__, \
+                     __LINE__);                                                                   \
+  } while (0)
+
+#define AGX_TRY(expr)              \
+  do {                             \
+    agx_status _s = (expr);        \
+    if (_s != AGX_OK) return _s;   \
+  } while (0)
+
+uint32_t ceil_log2(uint64_t x) {
+  uint32_t b = 0;
+  while ((1ull << b) < x) ++b;
+  return b;
+}
+
+int32_t java_hash_decimal(uint32_t id) {
+  char buf[16];
+  int n = 0;
+  do {
+    buf[n++] = (char)('0' + id % 10u);
+    id /= 10u;
+  } while (id);
+  uint32_t h = 0;
+  for (int i = n - 1; i >= 0; --i) h = h * 31u + (uint32_t)buf[i];
+  return (int32_t)h;
+}
+
+struct DevMsgs {
+  uint32_t* key = nullptr;
+  uint32_t* src = nullptr;
+  uint32_t* pay = nullptr;
+  Msgs m() const { return {key, src, pay}; }
+  CMsgs c() const { return {key, src, pay}; }
+};
+
+enum KClass { K_COMPACT_SCAN, K_COMPACT_COPY, K_UPSWEEP, K_ROWSCAN, K_DOWNSWEEP, K_APPLY, K_EXCHANGE, K_NCLASS };
+const char* kClassNames[K_NCLASS] = {"compact_scan", "compact_copy", "sort_upsweep", "sort_rowscan",
+                                     "sort_downsweep", "apply", "exchange"};
+
+}  // namespace
+
+struct agx_engine {
+  agx_cfg cfg{};
+  hipStream_t stream = nullptr;
+  uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0, max_tiles_a = 0, max_tiles_s = 0;
+  uint32_t T = 1, C = 0, W = 1, kmax = 1, R = 1, rank = 0, num_shards = 1000, key_bits = 1;
+
+  // sharding tables (R > 1)
+  std::vector<uint32_t> h_gid, h_route;
+  // host mirrors of the actor SoA (uploaded before the first run after a change)
+  std::vector<uint8_t> h_kind, h_alive;
+  std::vector<uint64_t> h_state;  // word-major
+  bool actors_dirty = true;
+  std::vector<uint64_t> h_row;  // local CSR rows (graph)
+  std::vector<uint32_t> h_col;
+  bool graph_set = false;
+
+  uint8_t *d_kind = nullptr, *d_alive = nullptr;
+  uint32_t *d_stopq = nullptr, *d_nstop = nullptr;
+  uint64_t* d_state = nullptr;
+  uint32_t *d_gid = nullptr, *d_route = nullptr;
+  uint32_t ring_stride = 1, fan_k = 0;
+  uint64_t fan_seed = 0, zipf_n = 0;
+  uint32_t *d_zcdf = nullptr, *d_zperm = nullptr;
+  uint64_t* d_row = nullptr;
+  uint32_t* d_col = nullptr;
+
+  DevMsgs A, B, bl, em, stg, s1, s2;
+  uint64_t stg_cap = 0;
+  uint32_t *d_cnt_bl = nullptr, *d_cnt_em = nullptr, *d_base_em = nullptr, *d_off_bl = nullptr,
+           *d_off_em = nullptr, *d_n = nullptr, *d_total = nullptr, *d_bump = nullptr, *d_hist = nullptr,
+           *d_tot = nullptr;
+  uint64_t *d_stats = nullptr, *d_cvec = nullptr, *d_cmat = nullptr, *d_inflight = nullptr;
+  uint32_t* h_pin = nullptr;     // pinned ring of per-step totals
+  uint64_t* h_pin64 = nullptr;   // pinned scratch (count matrix, stats)
+
+  // host-staged tells (consumed by the next superstep)
+  std::vector<uint32_t> hs_key, hs_src, hs_pay;
+  uint32_t n_staged_dev = 0;  // staged tells uploaded for the next step
+  uint64_t staged_total = 0, staged_dead = 0;
+
+  ncclComm_t comm = nullptr;
+  bool started = false;
+
+  // profiling
+  bool prof = false;
+  struct Rec { int cls; hipEvent_t a, b; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  double prof_ms[K_NCLASS] = {0};
+  uint64_t prof_n[K_NCLASS] = {0};
+};
+
+namespace {
+
+agx_status ensure_dev(agx_engine* e) {
+  HIP_TRY(hipSetDevice((int)e->cfg.device));
+  return AGX_OK;
+}
+
+template <typename T>
+agx_status dalloc(T** p, uint64_t n) {
+  if (n == 0) n = 1;
+  HIP_TRY(hipMalloc((void**)p, n * sizeof(T)));
+  return AGX_OK;
+}
+
+agx_status alloc_msgs(DevMsgs& m, uint64_t n) {
+  AGX_TRY(dalloc(&m.key, n));
+  AGX_TRY(dalloc(&m.src, n));
+  AGX_TRY(dalloc(&m.pay, n));
+  return AGX_OK;
+}
+
+void free_msgs(DevMsgs& m) {
+  hipFree(m.key);
+  hipFree(m.src);
+  hipFree(m.pay);
+  m = DevMsgs{};
+}
+
+// --------------------------------------------------------------- profiling
+void prof_begin(agx_engine* e, int cls, hipEvent_t* out_b) {
+  *out_b = nullptr;
+  if (!e->prof) return;
+  if (e->ev_used + 2 > e->ev_pool.size()) {
+    if (e->ev_pool.size() >= 200000) return;
+    for (int i = 0; i < 1024; ++i) {
+      hipEvent_t ev;
+      if (hipEventCreate(&ev) != hipSuccess) return;
+      e->ev_pool.push_back(ev);
+    }
+  }
+  hipEvent_t a = e->ev_pool[e->ev_used++], b = e->ev_pool[e->ev_used++];
+  hipEventRecord(a, e->stream);
+  e->recs.push_back({cls, a, b});
+  *out_b = b;
+}
+void prof_end(agx_engine* e, hipEvent_t b) {
+  if (b) hipEventRecord(b, e->stream);
+}
+void prof_collect(agx_engine* e) {
+  if (e->recs.empty()) return;
+  hipStreamSynchronize(e->stream);
+  for (auto& r : e->recs) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+      e->prof_ms[r.cls] += ms;
+      e->prof_n[r.cls] += 1;
+    }
+  }
+  e->recs.clear();
+  e->ev_used = 0;
+}
+
+struct Scope {
+  agx_engine* e;
+  hipEvent_t b;
+  Scope(agx_engine* e_, int cls) : e(e_) { prof_begin(e, cls, &b); }
+  ~Scope() { prof_end(e, b); }
+};
+
+DevParams make_params(agx_engine* e) {
+  DevParams P{};
+  P.n_global = (uint32_t)e->n_global;
+  P.n_local = (uint32_t)e->n_local;
+  P.W = e->W;
+  P.T = e->T;
+  P.C = e->C;
+  P.R = e->R;
+  P.rank = e->rank;
+  P.kmax = e->kmax;
+  P.ring_stride = e->ring_stride;
+  P.fan_k = e->fan_k;
+  P.fan_seed = e->fan_seed;
+  P.zipf_n = e->zipf_n;
+  P.zipf_cdf = e->d_zcdf;
+  P.zipf_perm = e->d_zperm;
+  P.row_ptr = e->d_row;
+  P.col = e->d_col;
+  P.route = e->d_route;
+  P.gid = e->d_gid;
+  P.kind = e->d_kind;
+  P.alive = e->d_alive;
+  P.state = e->d_state;
+  P.stopq = e->d_stopq;
+  P.nstop = e->d_nstop;
+  return P;
+}
+
+uint32_t grid_for(uint64_t tiles, uint32_t cap) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, cap)); }
+
+// ------------------------------------------------------------ kernel steps
+agx_status launch_compact(agx_engine* e, uint32_t mode) {
+  CompactArgs ca{};
+  ca.alive = e->d_alive;
+  ca.stopq = e->d_stopq;
+  ca.nstop = e->d_nstop;
+  ca.d_bump = e->d_bump;
+  ca.cnt_bl = e->d_cnt_bl;
+  ca.cnt_em = e->d_cnt_em;
+  ca.off_bl = e->d_off_bl;
+  ca.off_em = e->d_off_em;
+  ca.d_n = e->d_n;
+  ca.d_total = e->d_total;
+  ca.stats = e->d_stats;
+  ca.n_staged = mode == 0 ? e->n_staged_dev : 0u;
+  ca.mode = mode;
+  ca.cap0 = e->cap;
+  ca.cap1 = e->cap_emit;
+  {
+    Scope s(e, K_COMPACT_SCAN);
+    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kScanThreads), 0, e->stream, ca);
+  }
+  CopyArgs cp{};
+  cp.bl = e->bl.c();
+  cp.em = e->em.c();
+  cp.st = e->stg.c();
+  cp.out0 = e->A.m();
+  cp.out1 = e->s1.m();
+  cp.cnt_bl = e->d_cnt_bl;
+  cp.cnt_em = e->d_cnt_em;
+  cp.off_bl = e->d_off_bl;
+  cp.off_em = e->d_off_em;
+  cp.base_em = e->d_base_em;
+  cp.d_total = e->d_total;
+  cp.n_staged = ca.n_staged;
+  cp.mode = mode;
+  {
+    Scope s(e, K_COMPACT_COPY);
+    hipLaunchKernelGGL(k_compact_copy, dim3(grid_for(2 * e->max_tiles_a + 1, 4096)), dim3(256), 0, e->stream, cp);
+  }
+  HIP_TRY(hipGetLastError());
+  return AGX_OK;
+}
+
+// Stable LSD radix sort of `in` (n at d_n) over key bits [lo, hi); returns the
+// buffer holding the result (in or tmp).
+agx_status launch_sort(agx_engine* e, DevMsgs& in, DevMsgs& tmp, const uint32_t* d_n, uint32_t lo, uint32_t hi,
+                       DevMsgs** result) {
+  DevMsgs* src = &in;
+  DevMsgs* dst = &tmp;
+  const uint32_t g = grid_for(e->max_tiles_s, 2048);
+  for (uint32_t shift = lo; shift < hi; shift += kRadixBits) {
+    SortArgs sa{};
+    sa.in = src->c();
+    sa.out = dst->m();
+    sa.d_n = d_n;
+    sa.hist = e->d_hist;
+    sa.tot = e->d_tot;
+    sa.stride = (uint32_t)e->max_tiles_s;
+    sa.shift = shift;
+    sa.bits = std::min<uint32_t>(kRadixBits, hi - shift);
+    {
+      Scope s(e, K_UPSWEEP);
+      hipLaunchKernelGGL(k_sort_upsweep, dim3(g), dim3(kSortThreads), 0, e->stream, sa);
+    }
+    {
+      Scope s(e, K_ROWSCAN);
+      hipLaunchKernelGGL(k_sort_rowscan, dim3(1u << sa.bits), dim3(256), 0, e->stream, sa);
+    }
+    {
+      Scope s(e, K_DOWNSWEEP);
+      hipLaunchKernelGGL(k_sort_downsweep, dim3(g), dim3(kSortThreads), 0, e->stream, sa);
+    }
+    std::swap(src, dst);
+  }
+  HIP_TRY(hipGetLastError());
+  *result = src;
+  return AGX_OK;
+}
+
+agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
+  ApplyArgs aa{};
+  aa.P = make_params(e);
+  aa.in = sorted.c();
+  aa.d_n = e->d_n;
+  aa.bl = e->bl.m();
+  aa.em = e->em.m();
+  aa.cnt_bl = e->d_cnt_bl;
+  aa.cnt_em = e->d_cnt_em;
+  aa.base_em = e->d_base_em;
+  aa.d_bump = e->d_bump;
+  aa.cap_em = e->cap_emit;
+  aa.stats = e->d_stats;
+  {
+    Scope s(e, K_APPLY);
+    hipLaunchKernelGGL(k_apply, dim3(grid_for(e->max_tiles_a, 2048)), dim3(kApplyThreads), 0, e->stream, aa);
+  }
+  HIP_TRY(hipGetLastError());
+  return AGX_OK;
+}
+
+// upload host mirrors / staged tells before a run
+agx_status prepare_run(agx_engine* e) {
+  if (e->actors_dirty) {
+    HIP_TRY(hipMemcpyAsync(e->d_kind, e->h_kind.data(), e->n_local, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_alive, e->h_alive.data(), e->n_local, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_state, e->h_state.data(), e->n_local * e->W * 8, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->actors_dirty = false;
+  }
+  if (!e->hs_key.empty()) {
+    uint64_t n = e->hs_key.size();
+    if (n > e->stg_cap) {
+      free_msgs(e->stg);
+      AGX_TRY(alloc_msgs(e->stg, n));
+      e->stg_cap = n;
+    }
+    HIP_TRY(hipMemcpyAsync(e->stg.key, e->hs_key.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->stg.src, e->hs_src.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->stg.pay, e->hs_pay.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->n_staged_dev = (uint32_t)n;
+    e->hs_key.clear();
+    e->hs_src.clear();
+    e->hs_pay.clear();
+  }
+  return AGX_OK;
+}
+
+// ----------------------------------------------------------- multi-rank step
+// phase 1: compaction (backlog -> A front, tells -> s1), partition tells by owner
+// rank (stable), pack [send counts..., n_backlog, n_staged] into d_cvec.
+agx_status phase1(agx_engine* e) {
+  AGX_TRY(launch_compact(e, 1));
+  DevMsgs* part = nullptr;
+  AGX_TRY(launch_sort(e, e->s1, e->s2, e->d_total + 1, kOwnerShift, kOwnerShift + ceil_log2(e->R), &part));
+  if (part != &e->s2) {  // keep the partitioned send buffer in s2
+    std::swap(e->s1, e->s2);
+  }
+  hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(64), 0, e->stream, e->d_tot, e->d_total, e->d_cvec, e->R,
+                     e->n_staged_dev);
+  HIP_TRY(hipGetLastError());
+  return AGX_OK;
+}
+
+// phase 2: place staged tells after the received mail, sort by local key, apply.
+agx_status phase2(agx_engine* e, uint64_t n_sorted, uint64_t staged_at) {
+  if (e->n_staged_dev) {
+    HIP_TRY(hipMemcpyAsync(e->A.key + staged_at, e->stg.key, e->n_staged_dev * 4ull, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->A.src + staged_at, e->stg.src, e->n_staged_dev * 4ull, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->A.pay + staged_at, e->stg.pay, e->n_staged_dev * 4ull, hipMemcpyDeviceToDevice, e->stream));
+    e->n_staged_dev = 0;
+  }
+  e->h_pin[0] = (uint32_t)n_sorted;
+  HIP_TRY(hipMemcpyAsync(e->d_n, e->h_pin, 4, hipMemcpyHostToDevice, e->stream));
+  // the pinned word is reused next step only after the host sync in the exchange
+  DevMsgs* sorted = nullptr;
+  AGX_TRY(launch_sort(e, e->A, e->B, e->d_n, 0, e->key_bits, &sorted));
+  AGX_TRY(launch_apply(e, *sorted));
+  return AGX_OK;
+}
+
+struct Plan {
+  uint64_t total_inflight = 0;
+  uint64_t n_bl = 0, n_recv = 0, n_staged = 0;
+  std::vector<uint64_t> send_cnt, send_off, recv_cnt, recv_off;
+};
+
+void make_plan(agx_engine* e, const uint64_t* mat, Plan& p) {
+  const uint32_t R = e->R, S = R + 2;
+  p.send_cnt.assign(R, 0);
+  p.send_off.assign(R, 0);
+  p.recv_cnt.assign(R, 0);
+  p.recv_off.assign(R, 0);
+  p.total_inflight = 0;
+  for (uint32_t r = 0; r < R; ++r)
+    for (uint32_t c = 0; c < S; ++c) p.total_inflight += mat[r * S + c];
+  p.n_bl = mat[e->rank * S + R];
+  p.n_staged = mat[e->rank * S + R + 1];
+  uint64_t so = 0, ro = p.n_bl;
+  for (uint32_t q = 0; q < R; ++q) {
+    p.send_cnt[q] = mat[e->rank * S + q];
+    p.send_off[q] = so;
+    so += p.send_cnt[q];
+    p.recv_cnt[q] = mat[q * S + e->rank];
+    p.recv_off[q] = ro;
+    ro += p.recv_cnt[q];
+  }
+  p.n_recv = ro - p.n_bl;
+}
+
+// bring the host mirrors up to date with the device (commits pending stops)
+agx_status sync_mirrors(agx_engine* e) {
+  if (e->actors_dirty) return AGX_OK;  // host mirror is newer than the device
+  hipLaunchKernelGGL(k_commit_stops, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_alive, e->d_stopq, e->d_nstop);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(e->h_alive.data(), e->d_alive, e->n_local, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(e->h_state.data(), e->d_state, e->n_local * e->W * 8, hipMemcpyDeviceToHost));
+  return AGX_OK;
+}
+
+agx_status check_error(agx_engine* e) {
+  uint64_t err = 0;
+  HIP_TRY(hipMemcpy(&err, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost));
+  if (err & kErrCapacity)
+    return set_err(AGX_ECAPACITY, "in-flight messages exceeded engine capacity (msg_capacity=%llu)",
+                   (unsigned long long)e->cap);
+  return AGX_OK;
+}
+
+agx_status fill_stats(agx_engine* e, agx_stats* out, uint64_t inflight) {
+  uint64_t s[ST_N];
+  HIP_TRY(hipMemcpy(s, e->d_stats, sizeof s, hipMemcpyDeviceToHost));
+  agx_stats st{};
+  st.delivered = s[ST_DELIVERED];
+  st.dead_letters = s[ST_DEAD] + e->staged_dead;
+  st.unhandled = s[ST_UNHANDLED];
+  st.emitted = s[ST_EMITTED];
+  st.staged = e->staged_total;
+  st.supersteps = s[ST_STEPS];
+  st.in_flight = inflight;
+  // B = E_in + f_out*E_out + 2*S*(A/M); kind+alive bytes read per activation
+  st.bytes_alg = 12ull * st.delivered + 12ull * (st.emitted) + (16ull * e->W + 2ull) * s[ST_ACTIVE];
+  if (out) *out = st;
+  return AGX_OK;
+}
+
+agx_status single_inflight(agx_engine* e, uint64_t* out) {
+  hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_n, e->d_cnt_bl, e->d_cnt_em,
+                     (unsigned long long*)e->d_inflight);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_inflight, 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  *out = e->h_pin64[0] + e->n_staged_dev;
+  return AGX_OK;
+}
+
+agx_status run_single(agx_engine* e, uint32_t max_steps) {
+  constexpr uint32_t kLag = 16;
+  std::vector<hipEvent_t> ev(kLag);
+  for (auto& x : ev) HIP_TRY(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+  agx_status st = AGX_OK;
+  for (uint32_t s = 0; s < max_steps; ++s) {
+    if (s >= kLag) {
+      hipEventSynchronize(ev[s % kLag]);
+      if (e->h_pin[s % kLag] == 0) break;  // step s-kLag had no mail: quiescent
+    }
+    st = launch_compact(e, 0);
+    if (st) break;
+    e->n_staged_dev = 0;
+    DevMsgs* sorted = nullptr;
+    st = launch_sort(e, e->A, e->B, e->d_n, 0, e->key_bits, &sorted);
+    if (st) break;
+    st = launch_apply(e, *sorted);
+    if (st) break;
+    hipMemcpyAsync(&e->h_pin[s % kLag], e->d_total, 4, hipMemcpyDeviceToHost, e->stream);
+    hipEventRecord(ev[s % kLag], e->stream);
+  }
+  hipStreamSynchronize(e->stream);
+  for (auto& x : ev) hipEventDestroy(x);
+  return st;
+}
+
+agx_status exchange_rccl(agx_engine* e, Plan& p) {
+  NCCL_TRY(ncclGroupStart());
+  for (uint32_t q = 0; q < e->R; ++q) {
+    if (p.send_cnt[q]) {
+      const uint64_t o = p.send_off[q], n = p.send_cnt[q];
+      NCCL_TRY(ncclSend(e->s2.key + o, n, ncclUint32, (int)q, e->comm, e->stream));
+      NCCL_TRY(ncclSend(e->s2.src + o, n, ncclUint32, (int)q, e->comm, e->stream));
+      NCCL_TRY(ncclSend(e->s2.pay + o, n, ncclUint32, (int)q, e->comm, e->stream));
+    }
+    if (p.recv_cnt[q]) {
+      const uint64_t o = p.recv_off[q], n = p.recv_cnt[q];
+      NCCL_TRY(ncclRecv(e->A.key + o, n, ncclUint32, (int)q, e->comm, e->stream));
+      NCCL_TRY(ncclRecv(e->A.src + o, n, ncclUint32, (int)q, e->comm, e->stream));
+      NCCL_TRY(ncclRecv(e->A.pay + o, n, ncclUint32, (int)q, e->comm, e->stream));
+    }
+  }
+  NCCL_TRY(ncclGroupEnd());
+  return AGX_OK;
+}
+
+agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
+  const uint32_t S = e->R + 2;
+  Plan p;
+  for (uint32_t s = 0; s < max_steps; ++s) {
+    AGX_TRY(phase1(e));
+    {
+      Scope sc(e, K_EXCHANGE);
+      NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, S, ncclUint64, e->comm, e->stream));
+    }
+    HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_cmat, (size_t)e->R * S * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    make_plan(e, e->h_pin64, p);
+    if (p.total_inflight == 0) break;
+    if (p.n_bl + p.n_recv + p.n_staged > e->cap)
+      return set_err(AGX_ECAPACITY, "rank %u: %llu messages in flight exceed capacity %llu", e->rank,
+                     (unsigned long long)(p.n_bl + p.n_recv + p.n_staged), (unsigned long long)e->cap);
+    {
+      Scope sc(e, K_EXCHANGE);
+      AGX_TRY(exchange_rccl(e, p));
+    }
+    AGX_TRY(phase2(e, p.n_bl + p.n_recv + p.n_staged, p.n_bl + p.n_recv));
+  }
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return AGX_OK;
+}
+
+agx_status validate_cfg(const agx_cfg* c) {
+  if (!c) return set_err(AGX_EINVAL, "null cfg");
+  if (c->abi_version != AGX_ABI_VERSION) return set_err(AGX_EINVAL, "abi_version %u != %u", c->abi_version, AGX_ABI_VERSION);
+  if (c->n_actors == 0 || c->n_actors >= (1ull << 31)) return set_err(AGX_EINVAL, "n_actors out of range");
+  if (c->n_words == 0 || c->n_words > AGX_MAX_WORDS) return set_err(AGX_EINVAL, "n_words must be 1..%u", AGX_MAX_WORDS);
+  uint32_t R = c->n_ranks ? c->n_ranks : 1;
+  if (R > AGX_MAX_RANKS || c->rank >= R) return set_err(AGX_EINVAL, "bad rank %u / n_ranks %u", c->rank, R);
+  return AGX_OK;
+}
+
+}  // namespace
+
+// =========================================================================
+// C ABI
+// =========================================================================
+extern "C" {
+
+const char* agx_last_error(void) { return g_err.c_str(); }
+uint32_t agx_abi_version(void) { return AGX_ABI_VERSION; }
+
+int32_t agx_shard_id(uint32_t id, uint32_t num_shards) {
+  if (num_shards == 0) return 0;
+  int32_t h = java_hash_decimal(id);
+  int32_t a = (h == INT32_MIN) ? INT32_MIN : (h < 0 ? -h : h);  // math.abs(Int.MinValue) stays negative
+  return a % (int32_t)num_shards;
+}
+
+uint32_t agx_owner(uint32_t id, uint32_t num_shards, uint32_t n_ranks) {
+  if (n_ranks <= 1) return 0;
+  int32_t m = agx_shard_id(id, num_shards) % (int32_t)n_ranks;
+  return (uint32_t)(m < 0 ? m + (int32_t)n_ranks : m);
+}
+
+agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
+  AGX_TRY(validate_cfg(cfg));
+  if (!out) return set_err(AGX_EINVAL, "null out");
+  auto* e = new agx_engine();
+  e->cfg = *cfg;
+  e->n_global = cfg->n_actors;
+  e->T = cfg->throughput == 0 || (int32_t)cfg->throughput < 0 ? 1u : cfg->throughput;  // Mailbox.scala:261
+  e->C = cfg->capacity;
+  e->W = cfg->n_words;
+  e->kmax = std::max<uint32_t>(1, cfg->max_emit);
+  e->R = cfg->n_ranks ? cfg->n_ranks : 1;
+  e->rank = cfg->rank;
+  e->num_shards = cfg->num_shards ? cfg->num_shards : 1000;
+  agx_status st = ensure_dev(e);
+  if (st) { delete e; return st; }
+
+  // ShardRegion hash sharding: owner(id) = floor-mod(shardId(id), R); local index = rank among owned ids
+  if (e->R > 1) {
+    e->h_route.resize(e->n_global);
+    uint64_t nl = 0;
+    std::vector<uint32_t> cnt(e->R, 0);
+    for (uint64_t id = 0; id < e->n_global; ++id) {
+      uint32_t o = agx_owner((uint32_t)id, e->num_shards, e->R);
+      e->h_route[id] = (o << kOwnerShift) | cnt[o];
+      if (o == e->rank) e->h_gid.push_back((uint32_t)id);
+      cnt[o]++;
+    }
+    nl = cnt[e->rank];
+    for (uint32_t o = 0; o < e->R; ++o)
+      if (cnt[o] > kLocalMask) { delete e; return set_err(AGX_EINVAL, "too many actors per rank"); }
+    e->n_local = nl;
+  } else {
+    if (e->n_global > kLocalMask) { delete e; return set_err(AGX_EINVAL, "n_actors exceeds 2^28 per rank"); }
+    e->n_local = e->n_global;
+  }
+  const uint64_t nl = std::max<uint64_t>(e->n_local, 1);
+  e->key_bits = std::max<uint32_t>(1, ceil_log2(nl));
+  e->cap = cfg->msg_capacity ? cfg->msg_capacity : std::max<uint64_t>(4 * nl, 1u << 16);
+  if (e->cap >= (1ull << 32) - kSortTile) { delete e; return set_err(AGX_EINVAL, "msg_capacity too large"); }
+  e->cap_emit = std::min<uint64_t>(e->cap * e->kmax, (1ull << 32) - kSortTile - 1);
+  e->max_tiles_a = (e->cap + kApplyTile - 1) / kApplyTile + 1;
+  e->max_tiles_s = (std::max(e->cap, e->cap_emit) + kSortTile - 1) / kSortTile + 1;
+
+  e->h_kind.assign(e->n_local, 0);
+  e->h_alive.assign(e->n_local, 0);
+  e->h_state.assign(e->n_local * e->W, 0);
+
+#define CREATE_TRY(x)            \
+  do {                           \
+    agx_status _s = (x);         \
+    if (_s) { agx_destroy(e); return _s; } \
+  } while (0)
+  CREATE_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess
+                 ? AGX_OK
+                 : set_err(AGX_EDEVICE, "hipStreamCreate failed"));
+  CREATE_TRY(dalloc(&e->d_kind, nl));
+  CREATE_TRY(dalloc(&e->d_alive, nl));
+  CREATE_TRY(dalloc(&e->d_stopq, nl));
+  CREATE_TRY(dalloc(&e->d_nstop, 4));
+  CREATE_TRY(hipMemset(e->d_nstop, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(dalloc(&e->d_state, nl * e->W));
+  if (e->R > 1) {
+    CREATE_TRY(dalloc(&e->d_gid, nl));
+    CREATE_TRY(dalloc(&e->d_route, e->n_global));
+    CREATE_TRY(hipMemcpy(e->d_gid, e->h_gid.data(), e->n_local * 4, hipMemcpyHostToDevice) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "upload gid"));
+    CREATE_TRY(hipMemcpy(e->d_route, e->h_route.data(), e->n_global * 4, hipMemcpyHostToDevice) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "upload route"));
+  }
+  CREATE_TRY(alloc_msgs(e->A, e->cap));
+  CREATE_TRY(alloc_msgs(e->B, e->cap));
+  CREATE_TRY(alloc_msgs(e->bl, e->max_tiles_a * kApplyTile));
+  CREATE_TRY(alloc_msgs(e->em, e->cap_emit));
+  if (e->R > 1) {
+    CREATE_TRY(alloc_msgs(e->s1, e->cap_emit));
+    CREATE_TRY(alloc_msgs(e->s2, e->cap_emit));
+  }
+  CREATE_TRY(dalloc(&e->d_cnt_bl, e->max_tiles_a));
+  CREATE_TRY(dalloc(&e->d_cnt_em, e->max_tiles_a));
+  CREATE_TRY(dalloc(&e->d_base_em, e->max_tiles_a));
+  CREATE_TRY(dalloc(&e->d_off_bl, e->max_tiles_a));
+  CREATE_TRY(dalloc(&e->d_off_em, e->max_tiles_a));
+  CREATE_TRY(dalloc(&e->d_n, 4));
+  CREATE_TRY(dalloc(&e->d_total, 4));
+  CREATE_TRY(dalloc(&e->d_bump, 4));
+  CREATE_TRY(dalloc(&e->d_hist, (uint64_t)kRadix * e->max_tiles_s));
+  CREATE_TRY(dalloc(&e->d_tot, kRadix));
+  CREATE_TRY(dalloc(&e->d_stats, ST_N));
+  CREATE_TRY(dalloc(&e->d_inflight, 1));
+  CREATE_TRY(dalloc(&e->d_cvec, AGX_MAX_RANKS + 2));
+  CREATE_TRY(dalloc(&e->d_cmat, (uint64_t)AGX_MAX_RANKS * (AGX_MAX_RANKS + 2)));
+  CREATE_TRY(hipMemset(e->d_n, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipMemset(e->d_total, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipMemset(e->d_bump, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipMemset(e->d_stats, 0, ST_N * 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipMemset(e->d_cnt_bl, 0, e->max_tiles_a * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipMemset(e->d_cnt_em, 0, e->max_tiles_a * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipHostMalloc((void**)&e->h_pin, 64 * 4, hipHostMallocDefault) == hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
+  CREATE_TRY(hipHostMalloc((void**)&e->h_pin64, (AGX_MAX_RANKS * (AGX_MAX_RANKS + 2) + 8) * 8, hipHostMallocDefault) == hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
+  // empty graph rows so FORWARD_RR on an engine without a graph is well defined
+  e->h_row.assign(e->n_local + 1, 0);
+  CREATE_TRY(dalloc(&e->d_row, e->n_local + 1));
+  CREATE_TRY(hipMemset(e->d_row, 0, (e->n_local + 1) * 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+#undef CREATE_TRY
+  *out = e;
+  return AGX_OK;
+}
+
+agx_status agx_destroy(agx_engine* e) {
+  if (!e) return AGX_OK;
+  hipSetDevice((int)e->cfg.device);
+  if (e->stream) hipStreamSynchronize(e->stream);
+  if (e->comm) ncclCommDestroy(e->comm);
+  hipFree(e->d_kind); hipFree(e->d_alive); hipFree(e->d_stopq); hipFree(e->d_nstop); hipFree(e->d_state); hipFree(e->d_gid); hipFree(e->d_route);
+  hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_row); hipFree(e->d_col);
+  free_msgs(e->A); free_msgs(e->B); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
+  free_msgs(e->s1); free_msgs(e->s2);
+  hipFree(e->d_cnt_bl); hipFree(e->d_cnt_em); hipFree(e->d_base_em); hipFree(e->d_off_bl); hipFree(e->d_off_em);
+  hipFree(e->d_n); hipFree(e->d_total); hipFree(e->d_bump); hipFree(e->d_hist); hipFree(e->d_tot);
+  hipFree(e->d_stats); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);
+  if (e->h_pin) hipHostFree(e->h_pin);
+  if (e->h_pin64) hipHostFree(e->h_pin64);
+  for (auto ev : e->ev_pool) hipEventDestroy(ev);
+  if (e->stream) hipStreamDestroy(e->stream);
+  delete e;
+  return AGX_OK;
+}
+
+agx_status agx_register_range(agx_engine* e, uint64_t first_id, uint64_t count, uint32_t kind, const void* init,
+                              size_t stride) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  AGX_TRY(ensure_dev(e));
+  AGX_TRY(sync_mirrors(e));  // device state is authoritative after a run
+  if (first_id + count > e->n_global || kind >= AGX_KIND_MAX) return set_err(AGX_EINVAL, "bad range or kind");
+  if ((kind == AGX_KIND_FORWARD_RR || kind == AGX_KIND_STOP_AFTER) && e->W < 2)
+    return set_err(AGX_EINVAL, "behaviour kind %u needs n_words >= 2", kind);
+  if (init && stride < e->W * 8ull) return set_err(AGX_EINVAL, "state_stride smaller than n_words*8");
+  const uint8_t* ib = (const uint8_t*)init;
+  for (uint64_t i = 0; i < count; ++i) {
+    uint64_t id = first_id + i, l;
+    if (e->R > 1) {
+      uint32_t r = e->h_route[id];
+      if ((r >> kOwnerShift) != e->rank) continue;
+      l = r & kLocalMask;
+    } else {
+      l = id;
+    }
+    e->h_kind[l] = (uint8_t)kind;
+    e->h_alive[l] = kind != AGX_KIND_NONE;
+    for (uint32_t w = 0; w < e->W; ++w) {
+      uint64_t v = 0;
+      if (ib) memcpy(&v, ib + i * stride + w * 8, 8);
+      e->h_state[(uint64_t)w * e->n_local + l] = v;
+    }
+  }
+  e->actors_dirty = true;
+  return AGX_OK;
+}
+
+agx_status agx_set_ring(agx_engine* e, uint32_t stride) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  e->ring_stride = stride;
+  return AGX_OK;
+}
+
+agx_status agx_set_fanout(agx_engine* e, uint32_t k, uint64_t seed, const uint32_t* cdf, const uint32_t* perm,
+                          uint64_t n) {
+  if (!e || !cdf || !perm || n == 0) return set_err(AGX_EINVAL, "bad fanout args");
+  if (k > e->kmax) return set_err(AGX_EINVAL, "fanout k=%u exceeds max_emit=%u", k, e->kmax);
+  for (uint64_t i = 0; i < n; ++i)
+    if (perm[i] >= e->n_global) return set_err(AGX_EINVAL, "perm entry out of range");
+  AGX_TRY(ensure_dev(e));
+  hipFree(e->d_zcdf);
+  hipFree(e->d_zperm);
+  e->d_zcdf = e->d_zperm = nullptr;
+  AGX_TRY(dalloc(&e->d_zcdf, n));
+  AGX_TRY(dalloc(&e->d_zperm, n));
+  HIP_TRY(hipMemcpy(e->d_zcdf, cdf, n * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_zperm, perm, n * 4, hipMemcpyHostToDevice));
+  e->fan_k = k;
+  e->fan_seed = seed;
+  e->zipf_n = n;
+  return AGX_OK;
+}
+
+agx_status agx_set_graph(agx_engine* e, const uint64_t* row_ptr, const uint32_t* col) {
+  if (!e || !row_ptr) return set_err(AGX_EINVAL, "bad graph args");
+  AGX_TRY(ensure_dev(e));
+  // keep only the rows of local actors (rows indexed by local id)
+  std::vector<uint64_t> row(e->n_local + 1, 0);
+  std::vector<uint32_t> c;
+  for (uint64_t l = 0; l < e->n_local; ++l) {
+    uint64_t id = e->R > 1 ? e->h_gid[l] : l;
+    uint64_t b = row_ptr[id], en = row_ptr[id + 1];
+    if (en < b) return set_err(AGX_EINVAL, "row_ptr not monotone at %llu", (unsigned long long)id);
+    for (uint64_t j = b; j < en; ++j) c.push_back(col[j]);
+    row[l + 1] = c.size();
+  }
+  hipFree(e->d_row);
+  hipFree(e->d_col);
+  e->d_row = nullptr;
+  e->d_col = nullptr;
+  AGX_TRY(dalloc(&e->d_row, row.size()));
+  AGX_TRY(dalloc(&e->d_col, c.size()));
+  HIP_TRY(hipMemcpy(e->d_row, row.data(), row.size() * 8, hipMemcpyHostToDevice));
+  if (!c.empty()) HIP_TRY(hipMemcpy(e->d_col, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+  e->graph_set = true;
+  return AGX_OK;
+}
+
+agx_status agx_stage_tells(agx_engine* e, const uint32_t* dst, const uint32_t* src, const uint32_t* payload, size_t n) {
+  if (!e || (n && (!dst || !payload))) return set_err(AGX_EINVAL, "bad tells");
+  for (size_t i = 0; i < n; ++i) {
+    uint32_t d = dst[i];
+    if (d >= e->n_global) {  // unknown ref -> deadLetters (counted once, on rank 0)
+      if (e->rank == 0) { e->staged_total++; e->staged_dead++; }
+      continue;
+    }
+    uint32_t key = d;
+    if (e->R > 1) {
+      uint32_t r = e->h_route[d];
+      if ((r >> kOwnerShift) != e->rank) continue;
+      key = r;
+    }
+    e->staged_total++;
+    e->hs_key.push_back(key);
+    e->hs_src.push_back(src ? src[i] : AGX_NO_SENDER);
+    e->hs_pay.push_back(payload[i]);
+  }
+  if (e->hs_key.size() + e->n_staged_dev > e->cap) return set_err(AGX_ECAPACITY, "too many staged tells");
+  return AGX_OK;
+}
+
+agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  AGX_TRY(ensure_dev(e));
+  if (e->R > 1 && !e->comm) return set_err(AGX_ESTATE, "n_ranks > 1 needs agx_comm_init (or agx_group_run)");
+  AGX_TRY(prepare_run(e));
+  if (e->R > 1) {
+    AGX_TRY(run_multi_rccl(e, max_supersteps));
+  } else {
+    AGX_TRY(run_single(e, max_supersteps));
+  }
+  prof_collect(e);
+  AGX_TRY(check_error(e));
+  return agx_get_stats(e, out);
+}
+
+agx_status agx_get_stats(agx_engine* e, agx_stats* out) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  AGX_TRY(ensure_dev(e));
+  uint64_t infl = 0;
+  if (e->R > 1) {
+    // backlog + tells produced by the last apply, not yet exchanged
+    hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_n, e->d_cnt_bl, e->d_cnt_em,
+                       (unsigned long long*)e->d_inflight);
+    HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_inflight, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    infl = e->h_pin64[0] + e->n_staged_dev + e->hs_key.size();
+  } else {
+    AGX_TRY(single_inflight(e, &infl));
+    infl += e->hs_key.size();
+  }
+  return fill_stats(e, out, infl);
+}
+
+agx_status agx_read_state(agx_engine* e, uint64_t first_id, uint64_t count, uint64_t* words, uint8_t* alive) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  if (first_id + count > e->n_global) return set_err(AGX_EINVAL, "range out of bounds");
+  AGX_TRY(ensure_dev(e));
+  AGX_TRY(sync_mirrors(e));
+  for (uint64_t i = 0; i < count; ++i) {
+    uint64_t id = first_id + i, l;
+    if (e->R > 1) {
+      uint32_t r = e->h_route[id];
+      if ((r >> kOwnerShift) != e->rank) continue;
+      l = r & kLocalMask;
+    } else {
+      l = id;
+    }
+    if (words)
+      for (uint32_t w = 0; w < e->W; ++w) words[i * e->W + w] = e->h_state[(uint64_t)w * e->n_local + l];
+    if (alive) alive[i] = e->h_alive[l];
+  }
+  return AGX_OK;
+}
+
+agx_status agx_comm_unique_id(uint8_t out[128]) {
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  memcpy(out, &id, 128);
+  return AGX_OK;
+}
+
+agx_status agx_comm_init(agx_engine* e, const uint8_t id[128]) {
+  if (!e || !id) return set_err(AGX_EINVAL, "bad comm args");
+  AGX_TRY(ensure_dev(e));
+  ncclUniqueId uid;
+  memcpy(&uid, id, 128);
+  NCCL_TRY(ncclCommInitRank(&e->comm, (int)e->R, uid, (int)e->rank));
+  return AGX_OK;
+}
+
+agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_steps, agx_stats* out) {
+  if (!engs || n == 0) return set_err(AGX_EINVAL, "bad group");
+  if (n == 1) return agx_run(engs[0], max_steps, out);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!engs[i] || engs[i]->R != n || engs[i]->rank != i || engs[i]->n_global != engs[0]->n_global)
+      return set_err(AGX_EINVAL, "group engines must be ranks 0..n-1 of one population");
+    AGX_TRY(ensure_dev(engs[i]));
+    AGX_TRY(prepare_run(engs[i]));
+  }
+  const uint32_t S = n + 2;
+  std::vector<uint64_t> mat((size_t)n * S);
+  std::vector<Plan> plans(n);
+  for (uint32_t s = 0; s < max_steps; ++s) {
+    for (uint32_t i = 0; i < n; ++i) AGX_TRY(phase1(engs[i]));
+    for (uint32_t i = 0; i < n; ++i) {
+      agx_engine* e = engs[i];
+      HIP_TRY(hipMemcpyAsync(&mat[(size_t)i * S], e->d_cvec, S * 8, hipMemcpyDeviceToHost, e->stream));
+      HIP_TRY(hipStreamSynchronize(e->stream));
+    }
+    uint64_t total = 0;
+    for (auto v : mat) total += v;
+    if (total == 0) break;
+    for (uint32_t i = 0; i < n; ++i) {
+      make_plan(engs[i], mat.data(), plans[i]);
+      if (plans[i].n_bl + plans[i].n_recv + plans[i].n_staged > engs[i]->cap)
+        return set_err(AGX_ECAPACITY, "rank %u over capacity", i);
+    }
+    // loopback exchange: receiver i pulls its slice of every sender's partitioned buffer
+    for (uint32_t i = 0; i < n; ++i) {
+      agx_engine* r = engs[i];
+      for (uint32_t q = 0; q < n; ++q) {
+        uint64_t cnt = plans[i].recv_cnt[q];
+        if (!cnt) continue;
+        agx_engine* snd = engs[q];
+        uint64_t so = plans[q].send_off[i], ro = plans[i].recv_off[q];
+        HIP_TRY(hipMemcpyAsync(r->A.key + ro, snd->s2.key + so, cnt * 4, hipMemcpyDeviceToDevice, r->stream));
+        HIP_TRY(hipMemcpyAsync(r->A.src + ro, snd->s2.src + so, cnt * 4, hipMemcpyDeviceToDevice, r->stream));
+        HIP_TRY(hipMemcpyAsync(r->A.pay + ro, snd->s2.pay + so, cnt * 4, hipMemcpyDeviceToDevice, r->stream));
+      }
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+      Plan& p = plans[i];
+      AGX_TRY(phase2(engs[i], p.n_bl + p.n_recv + p.n_staged, p.n_bl + p.n_recv));
+    }
+    for (uint32_t i = 0; i < n; ++i) HIP_TRY(hipStreamSynchronize(engs[i]->stream));
+  }
+  agx_stats tot{};
+  for (uint32_t i = 0; i < n; ++i) {
+    prof_collect(engs[i]);
+    AGX_TRY(check_error(engs[i]));
+    agx_stats st{};
+    AGX_TRY(agx_get_stats(engs[i], &st));
+    tot.delivered += st.delivered;
+    tot.dead_letters += st.dead_letters;
+    tot.unhandled += st.unhandled;
+    tot.emitted += st.emitted;
+    tot.staged += st.staged;
+    tot.supersteps = std::max(tot.supersteps, st.supersteps);
+    tot.in_flight += st.in_flight;
+    tot.bytes_alg += st.bytes_alg;
+  }
+  if (out) *out = tot;
+  return AGX_OK;
+}
+
+agx_status agx_profile_enable(agx_engine* e, int on) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  e->prof = on != 0;
+  return AGX_OK;
+}
+
+agx_status agx_profile_reset(agx_engine* e) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  prof_collect(e);
+  for (int i = 0; i < K_NCLASS; ++i) {
+    e->prof_ms[i] = 0;
+    e->prof_n[i] = 0;
+  }
+  return AGX_OK;
+}
+
+agx_status agx_profile_read(agx_engine* e, char (*names)[32], double* total_ms, uint64_t* launches, uint64_t* items,
+                            uint32_t cap, uint32_t* n) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  prof_collect(e);
+  uint32_t k = 0;
+  for (int i = 0; i < K_NCLASS && k < cap; ++i, ++k) {
+    if (names) {
+      strncpy(names[k], kClassNames[i], 31);
+      names[k][31] = 0;
+    }
+    if (total_ms) total_ms[k] = e->prof_ms[i];
+    if (launches) launches[k] = e->prof_n[i];
+    if (items) items[k] = 0;
+  }
+  if (n) *n = K_NCLASS;
+  return AGX_OK;
+}
+
+}  // extern "C"

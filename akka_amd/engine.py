@@ -1,0 +1,222 @@
+"""GpuEngine: the Python host over the C ABI (include/akka_gpu.h).
+
+One GpuEngine = one rank of the actor population on one GPU.  All arrays that
+cross the boundary are plain numpy buffers (u32 ids/payloads, u64 state words).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import AgxCfg, AgxStats, check
+
+NO_SENDER = 0xFFFFFFFF
+
+
+class Kind:
+    """Behaviour kinds (enum agx_behavior_kind)."""
+    NONE = 0
+    COUNTER = 1
+    RING = 2
+    FANOUT = 3
+    FORWARD_RR = 4
+    STOP_AFTER = 5
+    PINGPONG = 6
+    EVEN = 7
+
+
+@dataclass
+class EngineConfig:
+    n_actors: int
+    throughput: int = 5          # akka.actor.default-dispatcher.throughput (reference.conf:541)
+    capacity: int = 0            # bounded mailbox capacity, 0 = unbounded
+    n_words: int = 2
+    max_emit: int = 1
+    n_ranks: int = 1
+    rank: int = 0
+    num_shards: int = 1000
+    device: int = 0
+    msg_capacity: int = 0
+
+    def to_c(self) -> AgxCfg:
+        c = AgxCfg()
+        c.abi_version = _lib.ABI_VERSION
+        c.device = self.device
+        c.n_actors = self.n_actors
+        # throughput <= 0 behaves as 1 (Mailbox.scala:261); keep the value, the engine clamps
+        c.throughput = max(int(self.throughput), 0) & 0xFFFFFFFF
+        c.capacity = int(self.capacity)
+        c.n_words = int(self.n_words)
+        c.max_emit = int(self.max_emit)
+        c.n_ranks = int(self.n_ranks)
+        c.rank = int(self.rank)
+        c.num_shards = int(self.num_shards)
+        c.msg_capacity = int(self.msg_capacity)
+        return c
+
+
+@dataclass
+class Stats:
+    delivered: int = 0
+    dead_letters: int = 0
+    unhandled: int = 0
+    emitted: int = 0
+    staged: int = 0
+    supersteps: int = 0
+    in_flight: int = 0
+    bytes_alg: int = 0
+
+    @classmethod
+    def from_c(cls, s: AgxStats) -> "Stats":
+        return cls(**s.as_dict())
+
+
+def _u32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32))
+
+
+def _ptr(a: np.ndarray, ty):
+    return a.ctypes.data_as(ctypes.POINTER(ty))
+
+
+class GpuEngine:
+    """One rank of the batched dispatcher.  Mirrors agx_* one to one."""
+
+    def __init__(self, cfg: EngineConfig):
+        self.lib = _lib.load()
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        c = cfg.to_c()
+        check(self.lib.agx_create(ctypes.byref(c), ctypes.byref(h)))
+        self._h = h
+
+    # -- lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            check(self.lib.agx_destroy(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    # -- registration
+    def register_range(self, first: int, count: int, kind: int, init_state=None) -> None:
+        W = self.cfg.n_words
+        if init_state is None:
+            check(self.lib.agx_register_range(self._h, first, count, kind, None, 0))
+            return
+        st = np.ascontiguousarray(np.asarray(init_state, dtype=np.uint64).reshape(count, -1))
+        if st.shape[1] < W:
+            st = np.concatenate([st, np.zeros((count, W - st.shape[1]), np.uint64)], axis=1)
+        st = np.ascontiguousarray(st[:, :W])
+        check(self.lib.agx_register_range(self._h, first, count, kind, st.ctypes.data_as(ctypes.c_void_p), W * 8))
+
+    def set_ring(self, stride: int = 1) -> None:
+        check(self.lib.agx_set_ring(self._h, stride))
+
+    def set_fanout(self, k: int, seed: int, cdf, perm) -> None:
+        cdf = _u32(cdf)
+        perm = _u32(perm)
+        check(self.lib.agx_set_fanout(self._h, k, seed, _ptr(cdf, ctypes.c_uint32), _ptr(perm, ctypes.c_uint32),
+                                      cdf.size))
+
+    def set_graph(self, row_ptr, col) -> None:
+        rp = np.ascontiguousarray(np.asarray(row_ptr, dtype=np.uint64))
+        cl = _u32(col) if len(col) else np.zeros(1, np.uint32)
+        check(self.lib.agx_set_graph(self._h, _ptr(rp, ctypes.c_uint64), _ptr(cl, ctypes.c_uint32)))
+
+    # -- tell / run
+    def tell(self, dst, payload, src=None) -> None:
+        dst = _u32(dst)
+        pay = _u32(payload)
+        srcp = None
+        if src is not None:
+            s = _u32(np.broadcast_to(np.asarray(src, dtype=np.uint32), dst.shape))
+            srcp = _ptr(s, ctypes.c_uint32)
+        check(self.lib.agx_stage_tells(self._h, _ptr(dst, ctypes.c_uint32), srcp, _ptr(pay, ctypes.c_uint32),
+                                       dst.size))
+
+    def run(self, max_supersteps: int = 1 << 30) -> Stats:
+        st = AgxStats()
+        check(self.lib.agx_run(self._h, min(int(max_supersteps), 0xFFFFFFFF), ctypes.byref(st)))
+        return Stats.from_c(st)
+
+    def stats(self) -> Stats:
+        st = AgxStats()
+        check(self.lib.agx_get_stats(self._h, ctypes.byref(st)))
+        return Stats.from_c(st)
+
+    def read_state(self, first: int = 0, count: int | None = None):
+        if count is None:
+            count = self.cfg.n_actors - first
+        W = self.cfg.n_words
+        words = np.zeros((count, W), np.uint64)
+        alive = np.zeros(count, np.uint8)
+        check(self.lib.agx_read_state(self._h, first, count, _ptr(words, ctypes.c_uint64),
+                                      _ptr(alive, ctypes.c_uint8)))
+        return words, alive
+
+    # -- multi-GPU
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        lib = _lib.load()
+        buf = (ctypes.c_uint8 * 128)()
+        check(lib.agx_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes) -> None:
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(self.lib.agx_comm_init(self._h, buf))
+
+    @staticmethod
+    def group_run(engines: list["GpuEngine"], max_supersteps: int = 1 << 30) -> Stats:
+        lib = _lib.load()
+        arr = (ctypes.c_void_p * len(engines))(*[e._h.value for e in engines])
+        st = AgxStats()
+        check(lib.agx_group_run(arr, len(engines), min(int(max_supersteps), 0xFFFFFFFF), ctypes.byref(st)))
+        return Stats.from_c(st)
+
+    # -- measurement
+    def profile(self, on: bool = True) -> None:
+        check(self.lib.agx_profile_enable(self._h, 1 if on else 0))
+
+    def profile_reset(self) -> None:
+        check(self.lib.agx_profile_reset(self._h))
+
+    def profile_read(self) -> dict:
+        cap = 16
+        names = (ctypes.c_char * 32 * cap)()
+        ms = (ctypes.c_double * cap)()
+        launches = (ctypes.c_uint64 * cap)()
+        items = (ctypes.c_uint64 * cap)()
+        n = ctypes.c_uint32()
+        check(self.lib.agx_profile_read(self._h, names, ms, launches, items, cap, ctypes.byref(n)))
+        out = {}
+        for i in range(min(n.value, cap)):
+            out[bytes(names[i]).split(b"\0")[0].decode()] = {"total_ms": ms[i], "launches": int(launches[i])}
+        return out
+
+
+def shard_id(entity_id: int, num_shards: int = 1000) -> int:
+    """HashCodeMessageExtractor.shardId for a numeric entity id (native helper)."""
+    return int(_lib.load().agx_shard_id(entity_id, num_shards))
+
+
+def owner(entity_id: int, num_shards: int, n_ranks: int) -> int:
+    return int(_lib.load().agx_owner(entity_id, num_shards, n_ranks))

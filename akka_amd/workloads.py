@@ -1,0 +1,199 @@
+"""Deterministic synthetic workloads (BASELINE.json configs C1..C5).
+
+Everything is integer and seeded (SplitMix64 counter RNG),
+so the same inputs feed the GPU engine, the CPU oracles and the benchmark.
+A workload is a plain description: actor ranges + behaviour params + initial
+tells; `apply_to(target)` installs it into anything with the engine's
+register_range / set_* / tell interface.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .engine import Kind, NO_SENDER
+
+SEED = 0x5EED
+M64 = (1 << 64) - 1
+
+
+def splitmix64_np(x: np.ndarray) -> np.ndarray:
+    """Vectorised SplitMix64 finaliser (uint64 wrapping arithmetic)."""
+    z = (np.asarray(x, dtype=np.uint64) + np.uint64(0x9E3779B97F4A7C15))
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+@dataclass
+class Workload:
+    name: str
+    n_actors: int
+    n_words: int
+    max_emit: int
+    throughput: int
+    capacity: int
+    ranges: list = field(default_factory=list)  # (first, count, kind, init_state or None)
+    ring_stride: int | None = None
+    fanout: tuple | None = None  # (k, seed, cdf, perm)
+    graph: tuple | None = None   # (row_ptr, col)
+    tells: tuple | None = None   # (dst, src, payload)
+
+    def engine_kwargs(self) -> dict:
+        return dict(n_actors=self.n_actors, throughput=self.throughput, capacity=self.capacity,
+                    n_words=self.n_words, max_emit=self.max_emit)
+
+    def apply_to(self, target, stage_tells: bool = True) -> None:
+        for first, count, kind, init in self.ranges:
+            target.register_range(first, count, kind, init)
+        if self.ring_stride is not None:
+            target.set_ring(self.ring_stride)
+        if self.fanout is not None:
+            target.set_fanout(*self.fanout)
+        if self.graph is not None:
+            target.set_graph(*self.graph)
+        if stage_tells and self.tells is not None:
+            dst, src, pay = self.tells
+            target.tell(dst, pay, src)
+
+    @property
+    def n_tells(self) -> int:
+        return 0 if self.tells is None else int(len(self.tells[0]))
+
+
+# ------------------------------------------------------------------ C2
+def token_ring(n: int = 1_000_000, hops: int = 256, throughput: int = 5, tokens_per_actor: int = 1) -> Workload:
+    """C2: every actor starts with `tokens_per_actor` tokens with hop budget H;
+    RING behaviour: count++, forward payload-1 to (self+1) mod N while > 0.
+    Delivered = tokens * N * (H + 1)."""
+    dst = np.tile(np.arange(n, dtype=np.uint32), tokens_per_actor)
+    pay = np.full(dst.size, hops, np.uint32)
+    src = np.full(dst.size, NO_SENDER, np.uint32)
+    return Workload("token_ring", n, 1, 1, throughput, 0, [(0, n, Kind.RING, None)], ring_stride=1,
+                    tells=(dst, src, pay))
+
+
+# ------------------------------------------------------------------ C3
+def zipf_tables(n: int, s: float = 1.1, seed: int = SEED):
+    """Zipf(s) over a seeded permutation of the actors, as u32 CDF thresholds:
+    sample i = smallest i with u32(r >> 32) <= cdf[i]; actor = perm[i]."""
+    ranks = np.arange(1, n + 1, dtype=np.float64)
+    w = ranks ** (-s)
+    cum = np.cumsum(w)
+    cum /= cum[-1]
+    cdf = np.floor(cum * 4294967296.0) - 1.0
+    cdf = np.clip(cdf, 0, 4294967295.0).astype(np.uint64)
+    cdf = np.maximum.accumulate(cdf)
+    cdf[-1] = 0xFFFFFFFF
+    key = splitmix64_np(np.arange(n, dtype=np.uint64) ^ np.uint64(seed))
+    perm = np.argsort(key, kind="stable").astype(np.uint32)
+    return cdf.astype(np.uint32), perm
+
+
+def zipf_fanout(n: int = 10_000_000, k: int = 4, ttl: int = 3, root_every: int = 64, s: float = 1.1,
+                throughput: int = 5, seed: int = SEED, capacity: int = 0) -> Workload:
+    """C3: 1/root_every actors are roots holding one message with ttl; FANOUT
+    behaviour: count++, sum += payload, if ttl > 0 emit k tells to Zipf targets."""
+    cdf, perm = zipf_tables(n, s, seed)
+    roots = np.arange(0, n, root_every, dtype=np.uint32)
+    h = (splitmix64_np(roots.astype(np.uint64) ^ np.uint64(seed * 3)) & np.uint64(0x0FFFFFFF)).astype(np.uint32)
+    pay = (np.uint32(ttl) << np.uint32(28)) | h
+    src = np.full(roots.size, NO_SENDER, np.uint32)
+    return Workload("zipf_fanout", n, 2, k, throughput, capacity, [(0, n, Kind.FANOUT, None)],
+                    fanout=(k, seed, cdf, perm), tells=(roots, src, pay.astype(np.uint32)))
+
+
+# ------------------------------------------------------------------ C5
+def power_law_graph(n: int, alpha: float = 2.1, dmax: int = 1024, a: float = 0.57, b: float = 0.19,
+                    c: float = 0.19, seed: int = SEED):
+    """Out-degrees ~ d^-alpha on [1, dmax]; endpoints by R-MAT bit sampling.
+    Integer RNG throughout (float only to build the host-side degree table)."""
+    d = np.arange(1, dmax + 1, dtype=np.float64)
+    p = d ** (-alpha)
+    cdf = np.cumsum(p) / p.sum()
+    thr = np.floor(cdf * 4294967296.0).astype(np.uint64)
+    thr[-1] = 1 << 32
+    r = splitmix64_np(np.arange(n, dtype=np.uint64) ^ np.uint64(seed * 7)) >> np.uint64(32)
+    deg = (np.searchsorted(thr, r, side="right") + 1).astype(np.uint64)
+    deg = np.minimum(deg, dmax)
+    row = np.zeros(n + 1, np.uint64)
+    np.cumsum(deg, out=row[1:])
+    m = int(row[-1])
+    bits = max(1, int(np.ceil(np.log2(max(n, 2)))))
+    ta = np.uint64(int(a * 65536))
+    tb = np.uint64(int((a + b) * 65536))
+    tc = np.uint64(int((a + b + c) * 65536))
+    col = np.zeros(m, np.uint64)
+    eid = np.arange(m, dtype=np.uint64)
+    for bit in range(bits):
+        rr = splitmix64_np(eid * np.uint64(64) + np.uint64(bit) + np.uint64(seed)) & np.uint64(0xFFFF)
+        # quadrant: a -> (0,0)  b -> (0,1)  c -> (1,0)  d -> (1,1); destination bit = column bit
+        dst_bit = ((rr >= ta) & (rr < tb)) | (rr >= tc)
+        col |= dst_bit.astype(np.uint64) << np.uint64(bits - 1 - bit)
+    col %= np.uint64(n)
+    return row, col.astype(np.uint32)
+
+
+def power_law_forward(n: int = 100_000_000, ttl: int = 16, capacity: int = 64, throughput: int = 5,
+                      msgs_per_actor_den: int = 1, seed: int = SEED) -> Workload:
+    """C5: FORWARD_RR over a power-law graph with BoundedMailbox(capacity)."""
+    row, col = power_law_graph(n, seed=seed)
+    dst = np.arange(0, n, msgs_per_actor_den, dtype=np.uint32)
+    pay = np.full(dst.size, ttl, np.uint32)
+    src = np.full(dst.size, NO_SENDER, np.uint32)
+    return Workload("power_law_forward", n, 2, 1, throughput, capacity, [(0, n, Kind.FORWARD_RR, None)],
+                    graph=(row, col), tells=(dst, src, pay))
+
+
+# ------------------------------------------------------------------ C1
+def ping_pong(pairs: int = 1000, messages_per_pair: int = 2_000_000, throughput: int = 50,
+              in_flight: int | None = None) -> Workload:
+    """C1: BenchmarkActors.PingPong pairs (akka-bench-jmh/.../BenchmarkActors.scala:20-32,96-117):
+    left = messagesPerPair/2 per actor, inFlight = 2*throughput initial tells
+    `ping.tell(Message, pong)` per pair."""
+    if in_flight is None:
+        in_flight = 2 * throughput
+    n = 2 * pairs
+    init = np.zeros((n, 2), np.uint64)
+    init[:, 0] = messages_per_pair // 2
+    ping = np.arange(0, n, 2, dtype=np.uint32)
+    dst = np.repeat(ping, in_flight)
+    src = dst + np.uint32(1)
+    pay = np.zeros(dst.size, np.uint32)
+    return Workload("ping_pong", n, 2, 1, throughput, 0, [(0, n, Kind.PINGPONG, init)], tells=(dst, src, pay))
+
+
+# ------------------------------------------------------------------ small mixed workload for parity tests
+def mixed(n: int = 4096, seed: int = 1, throughput: int = 3, capacity: int = 0, tells_per_actor: int = 3) -> Workload:
+    """Every behaviour kind side by side (ranges), random tells between them."""
+    rng = np.random.default_rng(seed)
+    kinds = [Kind.COUNTER, Kind.RING, Kind.FANOUT, Kind.FORWARD_RR, Kind.STOP_AFTER, Kind.PINGPONG, Kind.EVEN,
+             Kind.NONE]
+    per = n // len(kinds)
+    ranges = []
+    for i, kd in enumerate(kinds):
+        first = i * per
+        count = per if i < len(kinds) - 1 else n - first
+        init = None
+        if kd == Kind.STOP_AFTER:
+            init = np.zeros((count, 2), np.uint64)
+            init[:, 1] = rng.integers(1, 6, count)
+        elif kd == Kind.PINGPONG:
+            init = np.zeros((count, 2), np.uint64)
+            init[:, 0] = rng.integers(0, 5, count)
+        ranges.append((first, count, kd, init))
+    cdf, perm = zipf_tables(n, 1.1, seed)
+    row, col = power_law_graph(n, seed=seed)
+    m = n * tells_per_actor
+    dst = rng.integers(0, n + 8, m).astype(np.uint32)  # a few unknown refs -> dead letters
+    src = rng.integers(0, n, m).astype(np.uint32)
+    src[rng.random(m) < 0.1] = NO_SENDER
+    pay = rng.integers(0, 12, m).astype(np.uint32)
+    # fan-out payloads carry ttl in the top 4 bits
+    fan_first, fan_count = ranges[2][0], ranges[2][1]
+    is_fan = (dst >= fan_first) & (dst < fan_first + fan_count)
+    pay[is_fan] = (rng.integers(0, 3, int(is_fan.sum())).astype(np.uint32) << 28) | rng.integers(
+        0, 1 << 28, int(is_fan.sum())).astype(np.uint32)
+    return Workload("mixed", n, 2, 2, throughput, capacity, ranges, ring_stride=7, fanout=(2, seed, cdf, perm),
+                    graph=(row, col), tells=(dst, src, pay))

@@ -1,0 +1,176 @@
+/*
+ * akka_gpu.h — C ABI of the MI355X batched actor-dispatch engine.
+ *
+ * This is the drop-in boundary for Akka's Dispatcher/Mailbox hot loop
+ * (SURVEY.md §8(b)).  A JVM host (JNI or Panama) or the
+ * Python host in akka_amd/ binds exactly these symbols.  Plain C types only:
+ * no torch, no HIP types, no exceptions cross this boundary; every function
+ * returns an agx_status (0 = OK).
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to /root/reference, aliases as in SURVEY.md):
+ *
+ *   agx_create          <- MessageDispatcherConfigurator.dispatcher() +
+ *                          Dispatchers.configuratorFrom
+ *                          (akka-actor/src/main/scala/akka/dispatch/AbstractDispatcher.scala:338-347,
+ *                           akka-actor/src/main/scala/akka/dispatch/Dispatchers.scala:235-262)
+ *                          with MailboxType.create for the bounded/unbounded queue
+ *                          (akka-actor/src/main/scala/akka/dispatch/Mailbox.scala:638-640,
+ *                           akka-actor/src/main/scala/akka/dispatch/Mailboxes.scala:204-260)
+ *   agx_register_range  <- MessageDispatcher.attach / ActorCell.init (Create) for a
+ *                          contiguous range of fixed-layout actors
+ *                          (AbstractDispatcher.scala:145-148, akka-actor/.../actor/dungeon/Dispatch.scala:63-100)
+ *   agx_stage_tells     <- LocalActorRef.! -> ActorCell.sendMessage -> Dispatcher.dispatch
+ *                          (akka-actor/.../actor/ActorRef.scala:412-413, ActorCell.scala:325-326,
+ *                           akka-actor/.../dispatch/Dispatcher.scala:61-65)
+ *   agx_run             <- registerForExecution + Mailbox.run/processMailbox on the
+ *                          ForkJoinPool, as BSP supersteps
+ *                          (Dispatcher.scala:120-143, Mailbox.scala:227-277)
+ *   agx_read_state      <- (no reference counterpart: actor state is private to the
+ *                          JVM object; the GPU engine exposes it for the host/oracle)
+ *   agx_destroy         <- MessageDispatcher.shutdown (AbstractDispatcher.scala:325)
+ *
+ * Threading: an engine handle is driven by one host thread at a time (the
+ * single-writer-per-actor rule at engine granularity, Mailbox.scala:185-203).
+ */
+#ifndef AKKA_GPU_H
+#define AKKA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AGX_ABI_VERSION 1u
+
+typedef int32_t agx_status;
+#define AGX_OK 0
+#define AGX_EINVAL 1    /* bad argument / configuration                     */
+#define AGX_ENOMEM 2    /* device or host allocation failed                 */
+#define AGX_EDEVICE 3   /* HIP runtime error (message via agx_last_error)   */
+#define AGX_ECOMM 4     /* RCCL error                                       */
+#define AGX_ECAPACITY 5 /* in-flight messages exceed the engine's capacity  */
+#define AGX_ESTATE 6    /* call not valid in the engine's current state     */
+
+/* "no sender" (Actor.noSender / deadLetters as sender, AbstractDispatcher.scala:29-37) */
+#define AGX_NO_SENDER 0xFFFFFFFFu
+
+/* Behaviour kinds: the fixed-layout subset of typed Behaviors.receive
+ * (akka-actor-typed/.../scaladsl/Behaviors.scala:101-121).  Each returns
+ * same / stopped / unhandled (TY/Behavior.scala:229-278,
+ * TY/internal/adapter/ActorAdapter.scala:152-168).  State words are u64.   */
+enum agx_behavior_kind {
+  AGX_KIND_NONE = 0,       /* unregistered: every message is a dead letter            */
+  AGX_KIND_COUNTER = 1,    /* w0 += 1; w1 += payload                                  */
+  AGX_KIND_RING = 2,       /* w0 += 1; payload>0 -> tell((self+stride)%N, payload-1)  */
+  AGX_KIND_FANOUT = 3,     /* w0 += 1; w1 += payload; ttl>0 -> k Zipf tells           */
+  AGX_KIND_FORWARD_RR = 4, /* w0 += 1; payload>0 -> tell(next out-edge RR, payload-1) */
+  AGX_KIND_STOP_AFTER = 5, /* w0 += 1; w0 >= w1 -> Behaviors.stopped                  */
+  AGX_KIND_PINGPONG = 6,   /* BenchmarkActors.PingPong: reply to sender, stop at 0    */
+  AGX_KIND_EVEN = 7,       /* odd payload -> Behaviors.unhandled; else w0 += 1         */
+  AGX_KIND_MAX = 8
+};
+
+/* Behaviour results (ActorAdapter.next, TY/internal/adapter/ActorAdapter.scala:152-168) */
+#define AGX_RES_SAME 0u
+#define AGX_RES_STOPPED 1u
+#define AGX_RES_UNHANDLED 2u
+
+#define AGX_MAX_WORDS 8u
+#define AGX_MAX_RANKS 16u
+
+typedef struct agx_cfg {
+  uint32_t abi_version;   /* must be AGX_ABI_VERSION                                   */
+  uint32_t device;        /* HIP device ordinal                                        */
+  uint64_t n_actors;      /* global actor population (ids 0..n_actors-1), < 2^31       */
+  uint32_t throughput;    /* dispatcher `throughput` (RC:541); <=0 behaves as 1 (Mailbox.scala:261) */
+  uint32_t capacity;      /* bounded mailbox capacity C (Mailboxes.scala:212-216); 0 = unbounded */
+  uint32_t n_words;       /* u64 state words per actor, 1..AGX_MAX_WORDS               */
+  uint32_t max_emit;      /* max tells one message may emit (kmax)                     */
+  uint32_t n_ranks;       /* GPUs the population is hash-sharded over (1 = single GPU) */
+  uint32_t rank;          /* this engine's rank                                        */
+  uint32_t num_shards;    /* ShardRegion number-of-shards (1000 in typed sharding)     */
+  uint32_t reserved0;
+  uint64_t msg_capacity;  /* max messages in flight on this rank (0 = 4 x local actors)*/
+} agx_cfg;
+
+typedef struct agx_stats {
+  uint64_t delivered;     /* ActorCell.invoke calls (ActorCell.scala:539)              */
+  uint64_t dead_letters;  /* overflow + to-stopped + to-unknown (Mailbox.scala:337-351,422-428) */
+  uint64_t unhandled;     /* Behaviors.unhandled results (subset of delivered)         */
+  uint64_t emitted;       /* tells emitted by behaviours                               */
+  uint64_t staged;        /* tells staged from the host                                */
+  uint64_t supersteps;    /* supersteps that had messages                              */
+  uint64_t in_flight;     /* backlog + undelivered tells left when agx_run returned    */
+  uint64_t bytes_alg;     /* algorithmic HBM bytes (SURVEY.md §8(d) formula)           */
+} agx_stats;
+
+typedef struct agx_engine agx_engine;
+
+/* --- lifecycle ------------------------------------------------------------ */
+agx_status agx_create(const agx_cfg* cfg, agx_engine** out);
+agx_status agx_destroy(agx_engine* eng);
+const char* agx_last_error(void);
+uint32_t agx_abi_version(void);
+
+/* --- actor registration (actorOf for a contiguous id range) --------------- */
+/* init_state: count x state_stride bytes, actor-major, n_words u64 used per actor
+ * (may be NULL = zero state).  Only ids owned by this rank are kept.         */
+agx_status agx_register_range(agx_engine* eng, uint64_t first_id, uint64_t count,
+                              uint32_t kind, const void* init_state, size_t state_stride);
+
+/* --- behaviour parameters --------------------------------------------------- */
+agx_status agx_set_ring(agx_engine* eng, uint32_t stride);
+/* Zipf targets: cdf[i] = ceil(2^32 * P(rank <= i)) - 1 style u32 thresholds
+ * (non-decreasing, cdf[n-1] = 0xFFFFFFFF); perm maps rank -> actor id.      */
+agx_status agx_set_fanout(agx_engine* eng, uint32_t k, uint64_t seed, const uint32_t* cdf,
+                          const uint32_t* perm, uint64_t n);
+/* Out-edge lists in CSR over GLOBAL ids: row_ptr[n_actors+1], col[row_ptr[n]].  */
+agx_status agx_set_graph(agx_engine* eng, const uint64_t* row_ptr, const uint32_t* col);
+
+/* --- tell / run ------------------------------------------------------------- */
+/* Host tells (caller-owned buffers, copied).  src may be AGX_NO_SENDER.
+ * Tells whose dst is not owned by this rank are ignored on this rank.        */
+agx_status agx_stage_tells(agx_engine* eng, const uint32_t* dst, const uint32_t* src,
+                           const uint32_t* payload, size_t n);
+/* Run up to max_supersteps supersteps or until quiescent; stats are cumulative
+ * over the engine's lifetime.                                                 */
+agx_status agx_run(agx_engine* eng, uint32_t max_supersteps, agx_stats* out);
+agx_status agx_get_stats(agx_engine* eng, agx_stats* out);
+
+/* --- state readback ----------------------------------------------------------- */
+/* words: count x n_words u64 (actor-major); alive: count bytes (may be NULL).
+ * Only ids owned by this rank are written; others are left untouched.       */
+agx_status agx_read_state(agx_engine* eng, uint64_t first_id, uint64_t count, uint64_t* words,
+                          uint8_t* alive);
+
+/* --- multi-GPU (one process per GPU, RCCL over xGMI) ------------------------- */
+/* 128-byte RCCL unique id: rank 0 creates it, the host broadcasts it.        */
+agx_status agx_comm_unique_id(uint8_t out[128]);
+agx_status agx_comm_init(agx_engine* eng, const uint8_t id[128]);
+/* Single-process loopback transport: run `n` engines (ranks 0..n-1 of one
+ * population) that share one device, exchanging mail with device copies.
+ * Same kernels as the RCCL path; used to test sharding on a 1-GPU box.      */
+agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_supersteps, agx_stats* out);
+
+/* --- measurement ----------------------------------------------------------- */
+/* Per-kernel HIP-event timing on the engine's stream (off by default).      */
+agx_status agx_profile_enable(agx_engine* eng, int on);
+/* Fills up to `cap` entries; returns the number of kernel classes in *n.     */
+agx_status agx_profile_read(agx_engine* eng, char (*names)[32], double* total_ms,
+                            uint64_t* launches, uint64_t* items, uint32_t cap, uint32_t* n);
+agx_status agx_profile_reset(agx_engine* eng);
+
+/* --- sharding helpers (ShardRegion.HashCodeMessageExtractor) ---------------- */
+/* (math.abs(entityId.hashCode) % maxNumberOfShards) with entityId = decimal id
+ * (akka-cluster-sharding/.../ShardRegion.scala:154-158).  May be negative.  */
+int32_t agx_shard_id(uint32_t id, uint32_t num_shards);
+/* rank owning `id` = floor-mod(shard_id, n_ranks).                           */
+uint32_t agx_owner(uint32_t id, uint32_t num_shards, uint32_t n_ranks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AKKA_GPU_H */

@@ -1,0 +1,325 @@
+/*
+ * bsp_ref.c — TEST INFRASTRUCTURE ONLY.  CPU oracle for the batched actor
+ * dispatcher.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this; the product path (akka_amd/) never does.
+ *
+ * A single-threaded, deterministic restatement of the reference's
+ * Dispatcher/Mailbox drain loop as bulk-synchronous supersteps
+ * (SURVEY.md §7 "Execution model").  Each step follows these reference
+ * functions (paths relative to /root/reference):
+ *
+ *  - inbox formation: the per-actor FIFO queue, backlog first, new arrivals
+ *    appended in emission order — Mailbox.enqueue / NodeMessageQueue
+ *    (akka-actor/src/main/scala/akka/dispatch/Mailbox.scala:89,392-409;
+ *    akka-actor/src/main/java/akka/dispatch/AbstractNodeQueue.java:79-82).
+ *  - bounded admission: BoundedMailbox with pushTimeOut 0 tail-drops into
+ *    deadLetters (Mailbox.scala:551-565,699-720; AbstractBoundedNodeQueue.java:92-113;
+ *    typed MailboxSelector.bounded -> BoundedMailbox(n, 0) Mailboxes.scala:212-216).
+ *    An arrival of rank r is admitted iff len(backlog) + r < C, i.e. iff its
+ *    position p in the inbox is < C.
+ *  - drain: processMailbox(left = max(throughput, 1)) (Mailbox.scala:260-277):
+ *    the first min(len, max(T,1)) messages are invoked in order, the rest
+ *    stay queued (the backlog for the next step).
+ *  - invoke: ActorCell.invoke -> receiveMessage (akka-actor/.../actor/ActorCell.scala:539-577)
+ *    -> typed Behavior.interpretMessage / ActorAdapter.next
+ *    (akka-actor-typed/.../Behavior.scala:229-278, .../adapter/ActorAdapter.scala:152-168):
+ *    same / stopped / unhandled.
+ *  - stop: context.stop(self) takes effect after the current message
+ *    (Mailbox.scala:273); remaining drained messages and all later arrivals
+ *    are dead letters (AbstractDispatcher.scala:221-227, Mailbox.scala:337-351).
+ *    Messages of a stopping actor that were already queued beyond the
+ *    throughput cap are dead-lettered at the next inbox formation (same
+ *    totals; see DESIGN.md "stop").
+ *  - tell to an unknown ref / noSender -> deadLetters (ActorRef.scala:546,687-695).
+ *  - shard ownership: HashCodeMessageExtractor.shardId
+ *    (akka-cluster-sharding/.../ShardRegion.scala:154-158) with JLS String.hashCode.
+ *
+ * Canonical order (what makes the BSP schedule deterministic): arrivals to an
+ * actor are ordered by (owner rank of sender, sender id, per-sender emission
+ * index), then host-staged tells in staging order.  With n_ranks = 1 this is
+ * (sender id, emission index).  It preserves per-sender FIFO, the only order
+ * Akka guarantees (akka-docs/.../general/message-delivery-reliability.md:110-131).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/akka_gpu.h"
+#include "behaviors_ref.h"
+
+/* ---------------------------------------------------------------- helpers */
+
+/* SplitMix64 finaliser — the counter RNG shared with the device code. */
+uint64_t bsp_splitmix64(uint64_t x) { return ref_splitmix64(x); }
+
+/* JLS String.hashCode of the decimal representation of id (s[0]*31^(n-1)+...). */
+int32_t bsp_java_hash_decimal(uint32_t id) {
+  char buf[16];
+  int n = 0;
+  do {
+    buf[n++] = (char)('0' + id % 10u);
+    id /= 10u;
+  } while (id);
+  uint32_t h = 0;
+  for (int i = n - 1; i >= 0; --i) h = h * 31u + (uint32_t)buf[i];
+  return (int32_t)h;
+}
+
+/* HashCodeMessageExtractor.shardId: (math.abs(id.hashCode) % maxNumberOfShards)
+ * (ShardRegion.scala:154-158).  math.abs(Int.MinValue) == Int.MinValue, so the
+ * result can be negative (e.g. "-648" for hash -2147483648 at 1000 shards).  */
+int32_t bsp_shard_id(uint32_t id, uint32_t num_shards) {
+  int32_t h = bsp_java_hash_decimal(id);
+  int32_t a = (h == INT32_MIN) ? INT32_MIN : (h < 0 ? -h : h);
+  return a % (int32_t)num_shards; /* Java '%' truncates toward zero like C */
+}
+
+uint32_t bsp_owner(uint32_t id, uint32_t num_shards, uint32_t n_ranks) {
+  if (n_ranks <= 1) return 0;
+  int32_t s = bsp_shard_id(id, num_shards);
+  int32_t m = s % (int32_t)n_ranks;
+  if (m < 0) m += (int32_t)n_ranks;
+  return (uint32_t)m;
+}
+
+uint64_t bsp_fanout_rand(uint64_t seed, uint32_t self, uint32_t h, uint32_t j) {
+  return ref_fanout_rand(seed, self, h, j);
+}
+
+/* ---------------------------------------------------------------- sim */
+
+typedef struct {
+  uint32_t dst, src, payload;
+} env_t;
+
+typedef struct {
+  env_t* v;
+  uint64_t n, cap;
+} envvec;
+
+static int ev_push(envvec* e, uint32_t d, uint32_t s, uint32_t p) {
+  if (e->n == e->cap) {
+    uint64_t nc = e->cap ? e->cap * 2 : 1024;
+    env_t* nv = (env_t*)realloc(e->v, nc * sizeof(env_t));
+    if (!nv) return -1;
+    e->v = nv;
+    e->cap = nc;
+  }
+  e->v[e->n].dst = d;
+  e->v[e->n].src = s;
+  e->v[e->n].payload = p;
+  e->n++;
+  return 0;
+}
+
+typedef struct bsp_sim {
+  uint64_t n;
+  uint32_t T, C, W, n_ranks, num_shards;
+  uint8_t* kind;
+  uint8_t* alive;
+  uint64_t* state; /* actor-major: state[a*W + w] */
+  uint32_t* order; /* apply order: by (owner, id) */
+  /* params */
+  ref_params P;
+  uint32_t* zipf_cdf;
+  uint32_t* zipf_perm;
+  uint64_t* row_ptr;
+  uint32_t* col;
+  /* mail */
+  envvec backlog, emitted, staged;
+  agx_stats st;
+} bsp_sim;
+
+bsp_sim* bsp_create(uint64_t n_actors, uint32_t throughput, uint32_t capacity, uint32_t n_words,
+                    uint32_t n_ranks, uint32_t num_shards) {
+  if (n_words == 0 || n_words > AGX_MAX_WORDS || n_actors == 0 || n_actors >= (1ull << 31)) return NULL;
+  bsp_sim* s = (bsp_sim*)calloc(1, sizeof(bsp_sim));
+  if (!s) return NULL;
+  s->n = n_actors;
+  s->T = throughput == 0 ? 1 : throughput; /* max(throughput, 1), Mailbox.scala:261 */
+  if ((int32_t)throughput < 0) s->T = 1;
+  s->C = capacity;
+  s->W = n_words;
+  s->n_ranks = n_ranks ? n_ranks : 1;
+  s->num_shards = num_shards ? num_shards : 1000;
+  s->kind = (uint8_t*)calloc(n_actors, 1);
+  s->alive = (uint8_t*)calloc(n_actors, 1);
+  s->state = (uint64_t*)calloc(n_actors * n_words, 8);
+  s->order = (uint32_t*)malloc(n_actors * 4);
+  s->P.n = n_actors;
+  s->P.W = n_words;
+  s->P.ring_stride = 1;
+  if (!s->kind || !s->alive || !s->state || !s->order) return NULL;
+  if (s->n_ranks == 1) {
+    for (uint64_t a = 0; a < n_actors; ++a) s->order[a] = (uint32_t)a;
+  } else {
+    /* counting sort of ids by owner, stable in id */
+    uint64_t cnt[AGX_MAX_RANKS + 1];
+    memset(cnt, 0, sizeof cnt);
+    uint8_t* own = (uint8_t*)malloc(n_actors);
+    for (uint64_t a = 0; a < n_actors; ++a) {
+      own[a] = (uint8_t)bsp_owner((uint32_t)a, s->num_shards, s->n_ranks);
+      cnt[own[a] + 1]++;
+    }
+    for (uint32_t r = 0; r < s->n_ranks; ++r) cnt[r + 1] += cnt[r];
+    for (uint64_t a = 0; a < n_actors; ++a) s->order[cnt[own[a]]++] = (uint32_t)a;
+    free(own);
+  }
+  return s;
+}
+
+void bsp_destroy(bsp_sim* s) {
+  if (!s) return;
+  free(s->kind); free(s->alive); free(s->state); free(s->order);
+  free(s->zipf_cdf); free(s->zipf_perm); free(s->row_ptr); free(s->col);
+  free(s->backlog.v); free(s->emitted.v); free(s->staged.v);
+  free(s);
+}
+
+int bsp_register_range(bsp_sim* s, uint64_t first, uint64_t count, uint32_t kind, const uint64_t* init,
+                       uint64_t stride_words) {
+  if (first + count > s->n || kind >= AGX_KIND_MAX) return 1;
+  if ((kind == AGX_KIND_FORWARD_RR || kind == AGX_KIND_STOP_AFTER) && s->W < 2) return 1;
+  for (uint64_t i = 0; i < count; ++i) {
+    uint64_t a = first + i;
+    s->kind[a] = (uint8_t)kind;
+    s->alive[a] = kind != AGX_KIND_NONE;
+    for (uint32_t w = 0; w < s->W; ++w) s->state[a * s->W + w] = init ? init[i * stride_words + w] : 0;
+  }
+  return 0;
+}
+
+void bsp_set_ring(bsp_sim* s, uint32_t stride) { s->P.ring_stride = stride; }
+
+int bsp_set_fanout(bsp_sim* s, uint32_t k, uint64_t seed, const uint32_t* cdf, const uint32_t* perm, uint64_t n) {
+  s->P.fan_k = k;
+  s->P.fan_seed = seed;
+  free(s->zipf_cdf); free(s->zipf_perm);
+  s->zipf_cdf = (uint32_t*)malloc(n * 4);
+  s->zipf_perm = (uint32_t*)malloc(n * 4);
+  if (!s->zipf_cdf || !s->zipf_perm) return 2;
+  memcpy(s->zipf_cdf, cdf, n * 4);
+  memcpy(s->zipf_perm, perm, n * 4);
+  s->P.zipf_cdf = s->zipf_cdf;
+  s->P.zipf_perm = s->zipf_perm;
+  s->P.zipf_n = n;
+  return 0;
+}
+
+int bsp_set_graph(bsp_sim* s, const uint64_t* row_ptr, const uint32_t* col) {
+  free(s->row_ptr); free(s->col);
+  s->row_ptr = (uint64_t*)malloc((s->n + 1) * 8);
+  uint64_t e = row_ptr[s->n];
+  s->col = (uint32_t*)malloc((e ? e : 1) * 4);
+  if (!s->row_ptr || !s->col) return 2;
+  memcpy(s->row_ptr, row_ptr, (s->n + 1) * 8);
+  memcpy(s->col, col, e * 4);
+  s->P.row_ptr = s->row_ptr;
+  s->P.col = s->col;
+  return 0;
+}
+
+int bsp_stage(bsp_sim* s, const uint32_t* dst, const uint32_t* src, const uint32_t* payload, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) {
+    s->st.staged++;
+    if (dst[i] >= s->n) { s->st.dead_letters++; continue; }
+    if (ev_push(&s->staged, dst[i], src ? src[i] : AGX_NO_SENDER, payload[i])) return 2;
+  }
+  return 0;
+}
+
+/* emit: tell(dst, payload) from `self`; unknown dst -> deadLetters now. */
+static void emit_cb(void* ctx, uint32_t dst, uint32_t self, uint32_t payload) {
+  bsp_sim* s = (bsp_sim*)ctx;
+  s->st.emitted++;
+  if (dst >= s->n) { s->st.dead_letters++; return; }
+  ev_push(&s->emitted, dst, self, payload);
+}
+
+/* One BSP superstep.  Returns 1 if any message was in flight. */
+static int bsp_step(bsp_sim* s) {
+  uint64_t total = s->backlog.n + s->emitted.n + s->staged.n;
+  if (total == 0) return 0;
+  /* inbox formation: stable counting sort of [backlog ++ emitted ++ staged] by dst */
+  env_t* in = (env_t*)malloc(total * sizeof(env_t));
+  uint64_t* off = (uint64_t*)calloc(s->n + 1, 8);
+  env_t* srcs[3] = {s->backlog.v, s->emitted.v, s->staged.v};
+  uint64_t ns[3] = {s->backlog.n, s->emitted.n, s->staged.n};
+  for (int k = 0; k < 3; ++k)
+    for (uint64_t i = 0; i < ns[k]; ++i) off[srcs[k][i].dst + 1]++;
+  for (uint64_t a = 0; a < s->n; ++a) off[a + 1] += off[a];
+  uint64_t* cur = (uint64_t*)malloc((s->n) * 8);
+  memcpy(cur, off, s->n * 8);
+  for (int k = 0; k < 3; ++k)
+    for (uint64_t i = 0; i < ns[k]; ++i) in[cur[srcs[k][i].dst]++] = srcs[k][i];
+  free(cur);
+  s->backlog.n = 0;
+  s->emitted.n = 0;
+  s->staged.n = 0;
+
+  /* drain + apply, actors in canonical (owner, id) order so that emission
+   * order is (owner(src), src, idx) */
+  for (uint64_t oi = 0; oi < s->n; ++oi) {
+    uint32_t a = s->order[oi];
+    uint64_t b = off[a], L = off[a + 1] - b;
+    if (!L) continue;
+    if (!s->alive[a]) { s->st.dead_letters += L; continue; }
+    uint64_t nd = L < s->T ? L : s->T;
+    for (uint64_t p = 0; p < nd; ++p) {
+      uint32_t r = ref_apply(&s->P, s->kind[a], a, &s->state[(uint64_t)a * s->W], in[b + p].src, in[b + p].payload, emit_cb, s);
+      s->st.delivered++;
+      if (r == AGX_RES_UNHANDLED) s->st.unhandled++;
+      if (r == AGX_RES_STOPPED) {
+        s->alive[a] = 0;
+        s->st.dead_letters += nd - p - 1;
+        break;
+      }
+    }
+    for (uint64_t p = nd; p < L; ++p) {
+      if (s->C == 0 || p < s->C) ev_push(&s->backlog, in[b + p].dst, in[b + p].src, in[b + p].payload);
+      else s->st.dead_letters++;
+    }
+  }
+  free(in);
+  free(off);
+  s->st.supersteps++;
+  return 1;
+}
+
+int bsp_run(bsp_sim* s, uint32_t max_steps, agx_stats* out) {
+  for (uint32_t i = 0; i < max_steps; ++i)
+    if (!bsp_step(s)) break;
+  s->st.in_flight = s->backlog.n + s->emitted.n + s->staged.n;
+  if (out) *out = s->st;
+  return 0;
+}
+
+void bsp_read_state(bsp_sim* s, uint64_t first, uint64_t count, uint64_t* words, uint8_t* alive) {
+  for (uint64_t i = 0; i < count; ++i) {
+    uint64_t a = first + i;
+    if (words) memcpy(&words[i * s->W], &s->state[a * s->W], s->W * 8);
+    if (alive) alive[i] = s->alive[a];
+  }
+}
+
+/* ------------------------------------------------ CRDT restatements (KATs) */
+
+/* GCounter over R node slots (node index 0..R-1 in UniqueAddress order,
+ * akka-cluster/.../Member.scala:303-311).  increment: slot += n
+ * (DD GCounter.scala:97-111); merge: slot-wise max (GCounter.scala:113-125);
+ * value: sum of slots (GCounter.scala:62-64).  BigInt there, u64 here.     */
+void bsp_gcounter_increment(uint64_t* c, uint32_t slot, uint64_t n) { c[slot] += n; }
+void bsp_gcounter_merge(uint64_t* out, const uint64_t* a, const uint64_t* b, uint32_t r) {
+  for (uint32_t i = 0; i < r; ++i) out[i] = a[i] > b[i] ? a[i] : b[i];
+}
+uint64_t bsp_gcounter_value(const uint64_t* c, uint32_t r) {
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < r; ++i) v += c[i];
+  return v;
+}
+/* PNCounter = (increments, decrements) GCounters; merge each (PNCounter.scala:178). */
+void bsp_pncounter_merge(uint64_t* out_p, uint64_t* out_n, const uint64_t* ap, const uint64_t* an,
+                         const uint64_t* bp, const uint64_t* bn, uint32_t r) {
+  bsp_gcounter_merge(out_p, ap, bp, r);
+  bsp_gcounter_merge(out_n, an, bn, r);
+}

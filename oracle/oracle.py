@@ -1,0 +1,260 @@
+"""TEST INFRASTRUCTURE ONLY.  ctypes wrappers of the C/C++ oracles in this
+directory (bsp_ref.c, fjp_ref.cpp).  Never imported by akka_amd/.
+
+The oracles are CPU restatements of the reference's Dispatcher/Mailbox drain
+loop (see the header of bsp_ref.c for the file:line map).  Their interface
+mirrors akka_amd.engine.GpuEngine so tests can drive both with one workload.
+"""
+from __future__ import annotations
+
+import ctypes
+import pathlib
+import subprocess
+import threading
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+BUILD = HERE / "_build"
+_lock = threading.Lock()
+_bsp = None
+_fjp = None
+
+W_MAX = 8
+NO_SENDER = 0xFFFFFFFF
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("delivered", "dead_letters", "unhandled", "emitted", "staged", "supersteps", "in_flight",
+                 "bytes_alg")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+def build(force: bool = False) -> None:
+    """Compile the oracles with the committed Makefile (gcc/g++)."""
+    with _lock:
+        if force or not (BUILD / "libbsp_ref.so").exists() or not (BUILD / "libfjp_ref.so").exists():
+            subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def _u32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32))
+
+
+def _p(a, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def _load_bsp():
+    global _bsp
+    if _bsp is None:
+        build()
+        lib = ctypes.CDLL(str(BUILD / "libbsp_ref.so"))
+        vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        P32, P64, P8 = ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint8)
+        sig = {
+            "bsp_create": (vp, [u64, u32, u32, u32, u32, u32]),
+            "bsp_destroy": (None, [vp]),
+            "bsp_register_range": (ctypes.c_int, [vp, u64, u64, u32, P64, u64]),
+            "bsp_set_ring": (None, [vp, u32]),
+            "bsp_set_fanout": (ctypes.c_int, [vp, u32, u64, P32, P32, u64]),
+            "bsp_set_graph": (ctypes.c_int, [vp, P64, P32]),
+            "bsp_stage": (ctypes.c_int, [vp, P32, P32, P32, u64]),
+            "bsp_run": (ctypes.c_int, [vp, u32, ctypes.POINTER(Stats)]),
+            "bsp_read_state": (None, [vp, u64, u64, P64, P8]),
+            "bsp_java_hash_decimal": (ctypes.c_int32, [u32]),
+            "bsp_shard_id": (ctypes.c_int32, [u32, u32]),
+            "bsp_owner": (u32, [u32, u32, u32]),
+            "bsp_splitmix64": (u64, [u64]),
+            "bsp_gcounter_merge": (None, [P64, P64, P64, u32]),
+            "bsp_gcounter_value": (u64, [P64, u32]),
+            "bsp_gcounter_increment": (None, [P64, u32, u64]),
+        }
+        for k, (r, a) in sig.items():
+            f = getattr(lib, k)
+            f.restype = r
+            f.argtypes = a
+        _bsp = lib
+    return _bsp
+
+
+def _load_fjp():
+    global _fjp
+    if _fjp is None:
+        build()
+        lib = ctypes.CDLL(str(BUILD / "libfjp_ref.so"))
+        vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+        P32, P64, P8 = ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint8)
+        sig = {
+            "fjp_create": (vp, [u64, u32, u32, u32]),
+            "fjp_destroy": (None, [vp]),
+            "fjp_register_range": (ctypes.c_int, [vp, u64, u64, u32, P64, u64]),
+            "fjp_set_ring": (None, [vp, u32]),
+            "fjp_set_fanout": (None, [vp, u32, u64, P32, P32, u64]),
+            "fjp_set_graph": (None, [vp, P64, P32]),
+            "fjp_stage": (None, [vp, P32, P32, P32, u64]),
+            "fjp_run": (ctypes.c_double, [vp, u32, ctypes.POINTER(Stats)]),
+            "fjp_read_state": (None, [vp, u64, u64, P64, P8]),
+        }
+        for k, (r, a) in sig.items():
+            f = getattr(lib, k)
+            f.restype = r
+            f.argtypes = a
+        _fjp = lib
+    return _fjp
+
+
+class _Base:
+    def _init_arr(self, count, init):
+        if init is None:
+            return None, 0
+        st = np.ascontiguousarray(np.asarray(init, dtype=np.uint64).reshape(count, -1))
+        return st, st.shape[1]
+
+
+class BspOracle(_Base):
+    """Deterministic BSP restatement (bsp_ref.c).  n_ranks selects the
+    canonical sharded order (owner rank of the sender first)."""
+
+    def __init__(self, n_actors, throughput=5, capacity=0, n_words=2, max_emit=1, n_ranks=1, num_shards=1000):
+        self.lib = _load_bsp()
+        self.n, self.W = n_actors, n_words
+        self.h = self.lib.bsp_create(n_actors, max(int(throughput), 0), capacity, n_words, n_ranks, num_shards)
+        if not self.h:
+            raise ValueError("bsp_create failed")
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            self.lib.bsp_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def register_range(self, first, count, kind, init=None):
+        st, stride = self._init_arr(count, init)
+        p = _p(st, ctypes.c_uint64) if st is not None else None
+        if self.lib.bsp_register_range(self.h, first, count, kind, p, stride):
+            raise ValueError("bsp_register_range failed")
+
+    def set_ring(self, stride):
+        self.lib.bsp_set_ring(self.h, stride)
+
+    def set_fanout(self, k, seed, cdf, perm):
+        cdf, perm = _u32(cdf), _u32(perm)
+        self.lib.bsp_set_fanout(self.h, k, seed, _p(cdf, ctypes.c_uint32), _p(perm, ctypes.c_uint32), cdf.size)
+
+    def set_graph(self, row_ptr, col):
+        rp = np.ascontiguousarray(np.asarray(row_ptr, dtype=np.uint64))
+        cl = _u32(col) if len(col) else np.zeros(1, np.uint32)
+        self.lib.bsp_set_graph(self.h, _p(rp, ctypes.c_uint64), _p(cl, ctypes.c_uint32))
+
+    def tell(self, dst, payload, src=None):
+        dst, pay = _u32(dst), _u32(payload)
+        s = _u32(np.broadcast_to(np.asarray(NO_SENDER if src is None else src, dtype=np.uint32), dst.shape))
+        self.lib.bsp_stage(self.h, _p(dst, ctypes.c_uint32), _p(s, ctypes.c_uint32), _p(pay, ctypes.c_uint32),
+                           dst.size)
+
+    def run(self, max_supersteps=1 << 30):
+        st = Stats()
+        self.lib.bsp_run(self.h, min(int(max_supersteps), 0xFFFFFFFF), ctypes.byref(st))
+        return st.as_dict()
+
+    def read_state(self, first=0, count=None):
+        count = self.n - first if count is None else count
+        w = np.zeros((count, self.W), np.uint64)
+        a = np.zeros(count, np.uint8)
+        self.lib.bsp_read_state(self.h, first, count, _p(w, ctypes.c_uint64), _p(a, ctypes.c_uint8))
+        return w, a
+
+
+class FjpOracle(_Base):
+    """Multi-threaded Dispatcher/Mailbox/ForkJoinPool restatement (fjp_ref.cpp)."""
+
+    def __init__(self, n_actors, throughput=5, capacity=0, n_words=2, max_emit=1, **_):
+        self.lib = _load_fjp()
+        self.n, self.W = n_actors, n_words
+        self.h = self.lib.fjp_create(n_actors, max(int(throughput), 0), capacity, n_words)
+        if not self.h:
+            raise ValueError("fjp_create failed")
+        self.wall_s = 0.0
+
+    def close(self):
+        if self.h:
+            self.lib.fjp_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def register_range(self, first, count, kind, init=None):
+        st, stride = self._init_arr(count, init)
+        p = _p(st, ctypes.c_uint64) if st is not None else None
+        if self.lib.fjp_register_range(self.h, first, count, kind, p, stride):
+            raise ValueError("fjp_register_range failed")
+
+    def set_ring(self, stride):
+        self.lib.fjp_set_ring(self.h, stride)
+
+    def set_fanout(self, k, seed, cdf, perm):
+        cdf, perm = _u32(cdf), _u32(perm)
+        self.lib.fjp_set_fanout(self.h, k, seed, _p(cdf, ctypes.c_uint32), _p(perm, ctypes.c_uint32), cdf.size)
+
+    def set_graph(self, row_ptr, col):
+        rp = np.ascontiguousarray(np.asarray(row_ptr, dtype=np.uint64))
+        cl = _u32(col) if len(col) else np.zeros(1, np.uint32)
+        self._g = (rp, cl)
+        self.lib.fjp_set_graph(self.h, _p(rp, ctypes.c_uint64), _p(cl, ctypes.c_uint32))
+
+    def tell(self, dst, payload, src=None):
+        dst, pay = _u32(dst), _u32(payload)
+        s = _u32(np.broadcast_to(np.asarray(NO_SENDER if src is None else src, dtype=np.uint32), dst.shape))
+        self.lib.fjp_stage(self.h, _p(dst, ctypes.c_uint32), _p(s, ctypes.c_uint32), _p(pay, ctypes.c_uint32),
+                           dst.size)
+
+    def run(self, threads=1):
+        st = Stats()
+        self.wall_s = self.lib.fjp_run(self.h, threads, ctypes.byref(st))
+        return st.as_dict()
+
+    def read_state(self, first=0, count=None):
+        count = self.n - first if count is None else count
+        w = np.zeros((count, self.W), np.uint64)
+        a = np.zeros(count, np.uint8)
+        self.lib.fjp_read_state(self.h, first, count, _p(w, ctypes.c_uint64), _p(a, ctypes.c_uint8))
+        return w, a
+
+
+# ------------------------------------------------------------------ pure functions
+def java_hash(id_: int) -> int:
+    return int(_load_bsp().bsp_java_hash_decimal(id_))
+
+
+def shard_id(id_: int, num_shards: int = 1000) -> int:
+    return int(_load_bsp().bsp_shard_id(id_, num_shards))
+
+
+class crdt:
+    """GCounter restatement (DD/GCounter.scala:62-64,97-125) over R node slots."""
+
+    @staticmethod
+    def gcounter_merge(a, b):
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+        b = np.ascontiguousarray(np.asarray(b, dtype=np.uint64))
+        out = np.zeros_like(a)
+        _load_bsp().bsp_gcounter_merge(_p(out, ctypes.c_uint64), _p(a, ctypes.c_uint64), _p(b, ctypes.c_uint64),
+                                       a.size)
+        return out
+
+    @staticmethod
+    def gcounter_value(a):
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+        return int(_load_bsp().bsp_gcounter_value(_p(a, ctypes.c_uint64), a.size))
+
+    @staticmethod
+    def gcounter_increment(a, slot, n=1):
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.uint64)).copy()
+        _load_bsp().bsp_gcounter_increment(_p(a, ctypes.c_uint64), slot, n)
+        return a
