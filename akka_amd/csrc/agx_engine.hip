@@ -593,6 +593,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->n_global = cfg->n_actors;
   e->T = cfg->throughput == 0 || (int32_t)cfg->throughput < 0 ? 1u : cfg->throughput;  // Mailbox.scala:261
   e->C = cfg->capacity;
+  if (e->C && e->T > e->C) e->T = e->C;  // a bounded queue never holds more than C: drain <= min(T, C)
   e->W = cfg->n_words;
   e->kmax = std::max<uint32_t>(1, cfg->max_emit);
   e->R = cfg->n_ranks ? cfg->n_ranks : 1;
@@ -949,6 +950,24 @@ agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_steps, agx_
     tot.bytes_alg += st.bytes_alg;
   }
   if (out) *out = tot;
+  return AGX_OK;
+}
+
+agx_status agx_exchange_plan(const uint64_t* mat, uint32_t R, uint32_t rank, uint64_t* send_cnt, uint64_t* send_off,
+                             uint64_t* recv_cnt, uint64_t* recv_off, uint64_t* inflight) {
+  if (!mat || R == 0 || R > AGX_MAX_RANKS || rank >= R) return set_err(AGX_EINVAL, "bad plan args");
+  agx_engine tmp;
+  tmp.R = R;
+  tmp.rank = rank;
+  Plan p;
+  make_plan(&tmp, mat, p);
+  for (uint32_t q = 0; q < R; ++q) {
+    if (send_cnt) send_cnt[q] = p.send_cnt[q];
+    if (send_off) send_off[q] = p.send_off[q];
+    if (recv_cnt) recv_cnt[q] = p.recv_cnt[q];
+    if (recv_off) recv_off[q] = p.recv_off[q];
+  }
+  if (inflight) *inflight = p.total_inflight;
   return AGX_OK;
 }
 

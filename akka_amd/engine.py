@@ -220,3 +220,16 @@ def shard_id(entity_id: int, num_shards: int = 1000) -> int:
 
 def owner(entity_id: int, num_shards: int, n_ranks: int) -> int:
     return int(_lib.load().agx_owner(entity_id, num_shards, n_ranks))
+
+
+def exchange_plan(mat, rank: int) -> dict:
+    """agx_exchange_plan: this rank's send/recv counts and offsets (host only)."""
+    m = np.ascontiguousarray(np.asarray(mat, dtype=np.uint64))
+    R = m.shape[0]
+    out = {k: np.zeros(R, np.uint64) for k in ("send_cnt", "send_off", "recv_cnt", "recv_off")}
+    infl = ctypes.c_uint64()
+    check(_lib.load().agx_exchange_plan(_ptr(m, ctypes.c_uint64), R, rank, *(_ptr(out[k], ctypes.c_uint64) for k in
+                                                                          ("send_cnt", "send_off", "recv_cnt",
+                                                                           "recv_off")), ctypes.byref(infl)))
+    out["inflight"] = int(infl.value)
+    return out

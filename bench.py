@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark: messages delivered/sec of the batched actor dispatcher.
+
+Workload (BASELINE.json configs[1], C2): token ring, 1M actors per GPU, every
+actor holds one token (integer payload = remaining hop budget); RING behaviour
+= count++, forward payload-1 to actor (self+1) mod N.  With N GPUs the ring
+has N x 1M actors hash-sharded by ShardRegion's extractShardId (weak scaling),
+cross-GPU mail is exchanged with RCCL once per superstep.
+
+A "step" is one BSP superstep (one Mailbox.run round over every actor with
+mail) = 1M deliveries per GPU.  Inputs are resident in HBM before timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+N_PER_GPU = 1_000_000
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--actors-per-gpu", type=int, default=N_PER_GPU)
+    ap.add_argument("--hops", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-hops", type=int, default=96, help="hop budget of the bounded CPU sample")
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_r01.json"),
+                    help="PMC traffic summary written by profiles/collect_pmc.py")
+    return ap.parse_args()
+
+
+def kernel_bytes_per_msg(W: int) -> dict:
+    """Algorithmic HBM bytes per message for each kernel class."""
+    return {
+        "apply": 12 + 12 + (16 * W + 2),      # read envelope, write emitted tell, state r/w + kind/alive
+        "sort_downsweep": 24,                # read + write one 12 B envelope (per pass)
+        "sort_upsweep": 4,                   # read key (per pass)
+        "compact_copy": 24,                  # read chunk + write dense
+        "sort_rowscan": 0, "compact_scan": 0, "exchange": 12,
+    }
+
+
+def cpu_baseline(hops: int) -> dict:
+    """fjp_ref (restatement of Dispatcher/Mailbox/ForkJoinPool) on the host cores,
+    bounded sample: the same 1M-actor ring with a smaller hop budget."""
+    from akka_amd import workloads as wl
+    from oracle import BspOracle, FjpOracle
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    w = wl.token_ring(N_PER_GPU, hops, throughput=5)
+    f = FjpOracle(**w.engine_kwargs())
+    w.apply_to(f)
+    st = f.run(cores)
+    fjp_rate = st["delivered"] / f.wall_s
+    f.close()
+    b = BspOracle(**w.engine_kwargs())
+    w.apply_to(b)
+    t0 = time.perf_counter()
+    sb = b.run()
+    bsp_s = time.perf_counter() - t0
+    b.close()
+    return {"value": fjp_rate, "unit": "msg/s", "cores": cores, "kind": "port",
+            "sample": f"fjp_ref ForkJoin-dispatcher restatement, 1M-actor token ring, hops={hops} "
+                      f"({st['delivered']} deliveries, {f.wall_s:.2f} s, throughput=5)",
+            "bsp_ref_1thread_msg_s": sb["delivered"] / bsp_s}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = max(args.gpus, world)
+    if world != args.gpus and world > 1:
+        n_gpus = world
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import __graft_entry__ as g
+    if rank == 0 or world == 1:
+        g.build_native()
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.barrier()
+    torch.cuda.set_device(local)
+
+    from akka_amd import workloads as wl
+    from akka_amd.engine import EngineConfig, GpuEngine
+
+    hops = max(args.hops, args.warmup + args.steps + 1)
+    n_total = args.actors_per_gpu * world
+    w = wl.token_ring(n_total, hops)
+    cfg = EngineConfig(device=local, n_ranks=world, rank=rank, **w.engine_kwargs())
+    cfg.msg_capacity = int(2 * args.actors_per_gpu * 1.25) if world > 1 else 0
+    eng = GpuEngine(cfg)
+    w.apply_to(eng)  # each rank keeps the actors / tells it owns
+    if world > 1:
+        uid = [GpuEngine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0])
+
+    # warmup (includes the upload of actor state and the initial tells)
+    s0 = eng.run(args.warmup)
+    torch.cuda.synchronize()
+    eng.profile(True)
+    eng.profile_reset()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s1 = eng.run(args.steps)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    prof = eng.profile_read()
+    delivered = s1.delivered - s0.delivered
+    steps_done = s1.supersteps - s0.supersteps
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        d = torch.tensor([delivered], dtype=torch.float64)
+        dist.all_reduce(d, op=dist.ReduceOp.SUM)
+        delivered = int(d.item())
+
+    value = delivered / elapsed
+    # roofline of the dominant kernel (largest total time in the timed region)
+    per_msg = kernel_bytes_per_msg(cfg.n_words)
+    local_msgs_per_step = args.actors_per_gpu
+    dom = max((k for k in prof if prof[k]["launches"]), key=lambda k: prof[k]["total_ms"])
+    avg_ms = prof[dom]["total_ms"] / prof[dom]["launches"]
+    alg_bytes = per_msg.get(dom, 0) * local_msgs_per_step
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = pathlib.Path(args.pmc)
+    if pmc_path.exists():
+        try:
+            pmc = json.loads(pmc_path.read_text())
+            traffic = pmc.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    step_time = elapsed / max(args.steps, 1)
+    superstep_bytes = (12 + 12 + 16 * cfg.n_words + 2) * local_msgs_per_step
+    out = {
+        "metric": "messages delivered/sec (whole node) at 1M and 100M actors; % HBM roofline",
+        "value": value,
+        "unit": "msg/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": step_time * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (deterministic SplitMix64-seeded token ring; integer payloads)",
+        "config": {"workload": "C2 token ring, 1M actors/GPU, 1 token/actor, RING behaviour, throughput=5, "
+                               "unbounded mailbox" + (", hash-sharded (ShardRegion extractShardId), RCCL exchange"
+                                                      if world > 1 else ""),
+                   "actors": n_total, "actors_per_gpu": args.actors_per_gpu, "hop_budget": hops,
+                   "supersteps_timed": int(steps_done), "parallelism": f"shard{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                     "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms,
+                     "superstep_frac": superstep_bytes / step_time / 1e9 / PEAK_HBM_GBS * (1 if world == 1 else 1)},
+        "kernel_ms": {k: {"total_ms": round(v["total_ms"], 4), "launches": v["launches"]} for k, v in prof.items()},
+    }
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args.cpu_hops)
+            except Exception as ex:  # the baseline must never hide the GPU number
+                out["cpu_baseline"] = {"error": repr(ex)}
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -155,6 +155,16 @@ agx_status agx_comm_init(agx_engine* eng, const uint8_t id[128]);
  * Same kernels as the RCCL path; used to test sharding on a 1-GPU box.      */
 agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_supersteps, agx_stats* out);
 
+/* Exchange plan of one superstep (pure host function, no GPU).  `mat` is the
+ * gathered R x (R+2) matrix, row r = rank r's [tells to rank 0..R-1,
+ * n_backlog, n_staged].  Outputs (R entries each): this rank's send
+ * counts/offsets into its owner-partitioned tell buffer and receive
+ * counts/offsets into its sort input, where received mail follows the local
+ * backlog in sender-rank order (the sharded canonical order).  *inflight =
+ * global messages in flight (0 = quiescent on every rank).                  */
+agx_status agx_exchange_plan(const uint64_t* mat, uint32_t n_ranks, uint32_t rank, uint64_t* send_cnt,
+                             uint64_t* send_off, uint64_t* recv_cnt, uint64_t* recv_off, uint64_t* inflight);
+
 /* --- measurement ----------------------------------------------------------- */
 /* Per-kernel HIP-event timing on the engine's stream (off by default).      */
 agx_status agx_profile_enable(agx_engine* eng, int on);

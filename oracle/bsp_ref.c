@@ -139,6 +139,8 @@ bsp_sim* bsp_create(uint64_t n_actors, uint32_t throughput, uint32_t capacity, u
   s->T = throughput == 0 ? 1 : throughput; /* max(throughput, 1), Mailbox.scala:261 */
   if ((int32_t)throughput < 0) s->T = 1;
   s->C = capacity;
+  /* a bounded queue never holds more than C messages: drain <= min(T, C) */
+  if (capacity && s->T > capacity) s->T = capacity;
   s->W = n_words;
   s->n_ranks = n_ranks ? n_ranks : 1;
   s->num_shards = num_shards ? num_shards : 1000;

@@ -1,0 +1,148 @@
+"""The CPU oracle (test infrastructure) pinned against the reference's own
+known-answer tests, transcribed into tests/golden/*.json (see make_golden.py)."""
+import json
+import pathlib
+
+import numpy as np
+import pytest
+
+from akka_amd import workloads as wl
+from akka_amd.engine import Kind
+from oracle import BspOracle, FjpOracle, crdt, java_hash, shard_id
+
+GOLD = pathlib.Path(__file__).resolve().parent / "golden"
+
+
+def load(name):
+    return json.loads((GOLD / name).read_text())
+
+
+def test_shard_ids_oracle_and_host_mirror():
+    from akka_amd import sharding
+    for v in load("shard_ids.json")["vectors"]:
+        assert sharding.java_string_hash(v["entity_id"]) == v["hash"]
+        assert int(sharding.shard_id(v["entity_id"], v["num_shards"])) == v["shard"]
+        if v["entity_id"].isdigit() and int(v["entity_id"]) < 2**32:
+            assert java_hash(int(v["entity_id"])) == v["hash"]
+            assert shard_id(int(v["entity_id"]), v["num_shards"]) == v["shard"]
+
+
+def test_vectorised_owner_matches_scalar():
+    from akka_amd import sharding
+    n = 20000
+    own = sharding.owners(n, 1000, 8)
+    ref = np.array([sharding.rank_of_shard(sharding.shard_of_actor(i, 1000), 8) for i in range(n)])
+    assert np.array_equal(own, ref)
+
+
+def _apply_ops(ops, slots):
+    c = np.zeros(slots, np.uint64)
+    for op, slot, n in ops:
+        assert op == "inc"
+        c = crdt.gcounter_increment(c, slot, n)
+    return c
+
+
+def test_gcounter_kats():
+    g = load("gcounter_kat.json")
+    for case in g["cases"]:
+        c = _apply_ops(case["ops"], g["slots"])
+        assert c.tolist() == case["state"], case["name"]
+        if "value" in case:
+            assert crdt.gcounter_value(c) == case["value"]
+    for m in g["merges"]:
+        a = _apply_ops(m["a_ops"], g["slots"])
+        b = _apply_ops(m["b_ops"], g["slots"])
+        assert a.tolist() == m["a_state"] and crdt.gcounter_value(a) == m["a_value"], m["name"]
+        assert b.tolist() == m["b_state"] and crdt.gcounter_value(b) == m["b_value"], m["name"]
+        for x, y in ((a, b), (b, a)):  # merge both ways
+            mg = crdt.gcounter_merge(x, y)
+            assert mg.tolist() == m["merged_state"] and crdt.gcounter_value(mg) == m["merged_value"], m["name"]
+        # join laws: idempotent, commutative
+        assert np.array_equal(crdt.gcounter_merge(a, a), a)
+
+
+@pytest.mark.parametrize("Oracle", [BspOracle, FjpOracle])
+def test_mailbox_kats(Oracle):
+    for case in load("mailbox_kat.json")["cases"]:
+        o = Oracle(1, throughput=case["throughput"], capacity=case["capacity"], n_words=2)
+        o.register_range(0, 1, Kind.COUNTER)
+        o.tell(np.zeros(len(case["payloads"]), np.uint32), case["payloads"])
+        st = o.run() if Oracle is BspOracle else o.run(2)
+        w, _ = o.read_state()
+        assert st["delivered"] == case["delivered"], case["name"]
+        assert st["dead_letters"] == case["dead_letters"], case["name"]
+        assert int(w[0, 1]) == case["sum"], case["name"]
+        if Oracle is BspOracle and "supersteps" in case:
+            assert st["supersteps"] == case["supersteps"], case["name"]
+
+
+@pytest.mark.parametrize("Oracle", [BspOracle, FjpOracle])
+def test_pingpong_kats(Oracle):
+    for c in load("pingpong_kat.json")["cases"]:
+        w = wl.ping_pong(c["pairs"], c["messages_per_pair"], c["throughput"], c["in_flight"])
+        o = Oracle(**w.engine_kwargs())
+        w.apply_to(o)
+        st = o.run() if Oracle is BspOracle else o.run(4)
+        assert st["delivered"] == c["delivered"] and st["dead_letters"] == c["dead_letters"], c
+
+
+def test_ring_kats():
+    for c in load("ring_kat.json")["cases"]:
+        w = wl.token_ring(c["n"], c["hops"])
+        o = BspOracle(**w.engine_kwargs())
+        w.apply_to(o)
+        st = o.run()
+        words, alive = o.read_state()
+        assert st["delivered"] == c["delivered"] and st["supersteps"] == c["supersteps"]
+        assert (words[:, 0] == c["count"]).all() and alive.all()
+
+
+@pytest.mark.parametrize("make", [lambda: wl.token_ring(3000, 17, throughput=2),
+                                  lambda: wl.zipf_fanout(4000, k=3, ttl=3, root_every=8, throughput=7),
+                                  lambda: wl.ping_pong(50, 60, 5)])
+def test_fjp_restatement_agrees_with_bsp_on_confluent_workloads(make):
+    """For confluent workloads the final state is schedule independent: the
+    multi-threaded ForkJoin restatement and the BSP oracle agree bit for bit."""
+    w = make()
+    b = BspOracle(**w.engine_kwargs())
+    w.apply_to(b)
+    sb = b.run()
+    f = FjpOracle(**w.engine_kwargs())
+    w.apply_to(f)
+    sf = f.run(4)
+    for k in ("delivered", "dead_letters", "unhandled", "emitted", "staged"):
+        assert sb[k] == sf[k], k
+    assert np.array_equal(b.read_state()[0], f.read_state()[0])
+
+
+@pytest.mark.parametrize("T,C", [(1, 0), (3, 4), (5, 1), (50, 16)])
+def test_conservation(T, C):
+    """delivered + dead letters + in flight = staged + emitted (MailboxConfigSpec:132-182)."""
+    w = wl.mixed(2000, seed=T + 7 * C, throughput=T, capacity=C)
+    for budget in (1, 4, 1 << 20):
+        o = BspOracle(**w.engine_kwargs())
+        w.apply_to(o)
+        st = o.run(budget)
+        assert st["delivered"] + st["dead_letters"] + st["in_flight"] == st["staged"] + st["emitted"]
+
+
+def test_sharded_order_is_rank_major():
+    """With n_ranks > 1 arrivals are ordered by (owner(src), src): a bounded
+    mailbox then admits a different subset, but totals are conserved."""
+    w = wl.mixed(1500, seed=3, throughput=2, capacity=3)
+    res = []
+    for R in (1, 2, 4):
+        o = BspOracle(n_ranks=R, **w.engine_kwargs())
+        w.apply_to(o)
+        st = o.run()
+        res.append(st)
+        assert st["delivered"] + st["dead_letters"] + st["in_flight"] == st["staged"] + st["emitted"]
+    ring = wl.token_ring(500, 9)
+    outs = []
+    for R in (1, 2, 8):
+        o = BspOracle(n_ranks=R, **ring.engine_kwargs())
+        ring.apply_to(o)
+        o.run()
+        outs.append(o.read_state()[0])
+    assert all(np.array_equal(outs[0], x) for x in outs[1:])  # confluent: same for any R
