@@ -16,7 +16,7 @@ constexpr int kOwnerShift = 28;
 // ------------------------------------------------------------------ params
 struct DevParams {
   uint32_t n_global, n_local, W, T, C, R, rank, kmax;
-  uint32_t ring_stride, fan_k;
+  uint32_t ring_stride, fan_k;  // ring_stride pre-reduced mod n_global
   uint64_t fan_seed, zipf_n;
   const uint32_t* zipf_cdf;
   const uint32_t* zipf_perm;
@@ -129,7 +129,10 @@ __device__ __forceinline__ uint32_t apply_msg(const DevParams& P, uint32_t kind,
       return AGX_RES_SAME;
     case AGX_KIND_RING:
       w[0] += 1;
-      if (pay > 0) emit((uint32_t)(((uint64_t)self + P.ring_stride) % P.n_global), pay - 1);
+      if (pay > 0) {
+        uint32_t d = self + P.ring_stride;  // both < n_global < 2^31: no overflow, one conditional subtract
+        emit(d >= P.n_global ? d - P.n_global : d, pay - 1);
+      }
       return AGX_RES_SAME;
     case AGX_KIND_FANOUT: {
       w[0] += 1;
@@ -148,7 +151,10 @@ __device__ __forceinline__ uint32_t apply_msg(const DevParams& P, uint32_t kind,
       if (pay > 0) {
         uint64_t b = P.row_ptr[local], deg = P.row_ptr[local + 1] - b;
         if (deg) {
-          uint64_t e = b + (w[1] % deg);
+          // cursor mod degree; 32-bit remainder when both fit (the common case)
+          uint64_t r = (w[1] <= 0xFFFFFFFFull && deg <= 0xFFFFFFFFull) ? (uint64_t)((uint32_t)w[1] % (uint32_t)deg)
+                                                                       : w[1] % deg;
+          uint64_t e = b + r;
           w[1] += 1;
           emit(P.col[e], pay - 1);
         }

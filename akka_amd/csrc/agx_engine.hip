@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -84,16 +85,21 @@ struct DevMsgs {
   CMsgs c() const { return {key, src, pay}; }
 };
 
-enum KClass { K_COMPACT_SCAN, K_COMPACT_COPY, K_UPSWEEP, K_ROWSCAN, K_DOWNSWEEP, K_APPLY, K_EXCHANGE, K_NCLASS };
-const char* kClassNames[K_NCLASS] = {"compact_scan", "compact_copy", "sort_upsweep", "sort_rowscan",
-                                     "sort_downsweep", "apply", "exchange"};
+enum KClass { K_CROWSCAN, K_CDOWN, K_UPSWEEP, K_ROWSCAN, K_DOWNSWEEP, K_APPLY, K_EXCHANGE, K_MCOMPACT, K_NCLASS };
+const char* kClassNames[K_NCLASS] = {"chunk_rowscan", "chunk_downsweep", "sort_upsweep", "sort_rowscan",
+                                     "sort_downsweep", "bucket_apply", "exchange", "mcompact"};
+
+struct SortPlan {  // LSD passes over key bits [kBucketBits, key_bits)
+  uint32_t npass = 1;
+  uint32_t shift[4] = {0}, bits[4] = {0};
+};
 
 }  // namespace
 
 struct agx_engine {
   agx_cfg cfg{};
   hipStream_t stream = nullptr;
-  uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0, max_tiles_a = 0, max_tiles_s = 0;
+  uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0, max_tiles = 0;
   uint32_t T = 1, C = 0, W = 1, kmax = 1, R = 1, rank = 0, num_shards = 1000, key_bits = 1;
 
   // sharding tables (R > 1)
@@ -116,11 +122,14 @@ struct agx_engine {
   uint64_t* d_row = nullptr;
   uint32_t* d_col = nullptr;
 
-  DevMsgs A, B, bl, em, stg, s1, s2;
+  DevMsgs A, B, scr, bl, em, stg, s1, s2;
   uint64_t stg_cap = 0;
-  uint32_t *d_cnt_bl = nullptr, *d_cnt_em = nullptr, *d_base_em = nullptr, *d_off_bl = nullptr,
-           *d_off_em = nullptr, *d_n = nullptr, *d_total = nullptr, *d_bump = nullptr, *d_hist = nullptr,
-           *d_tot = nullptr;
+  uint32_t nb = 1, nchunks = 3;                // buckets; chunks = 2 nb + 1
+  SortPlan plan;
+  uint32_t *d_chunk_off = nullptr, *d_chunk_cnt = nullptr;
+  uint32_t* d_hist_c = nullptr;  // [kRadix][nchunks] first-pass chunk histograms, then bump[2]
+  uint32_t* d_hist_d = nullptr;  // [kRadix][max_tiles] dense-pass histograms
+  uint32_t *d_tot = nullptr, *d_bstart = nullptr, *d_n = nullptr, *d_total = nullptr, *d_moff0 = nullptr, *d_moff1 = nullptr;
   uint64_t *d_stats = nullptr, *d_cvec = nullptr, *d_cmat = nullptr, *d_inflight = nullptr;
   uint32_t* h_pin = nullptr;     // pinned ring of per-step totals
   uint64_t* h_pin64 = nullptr;   // pinned scratch (count matrix, stats)
@@ -132,6 +141,10 @@ struct agx_engine {
 
   ncclComm_t comm = nullptr;
   bool started = false;
+  // superstep graphs (single rank)
+  static constexpr uint32_t kGraphSteps = 8;
+  bool graphs_enabled = true;
+  hipGraphExec_t g1 = nullptr, gG = nullptr;
 
   // profiling
   bool prof = false;
@@ -222,7 +235,7 @@ DevParams make_params(agx_engine* e) {
   P.R = e->R;
   P.rank = e->rank;
   P.kmax = e->kmax;
-  P.ring_stride = e->ring_stride;
+  P.ring_stride = (uint32_t)(e->ring_stride % e->n_global);
   P.fan_k = e->fan_k;
   P.fan_seed = e->fan_seed;
   P.zipf_n = e->zipf_n;
@@ -243,103 +256,127 @@ DevParams make_params(agx_engine* e) {
 uint32_t grid_for(uint64_t tiles, uint32_t cap) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, cap)); }
 
 // ------------------------------------------------------------ kernel steps
-agx_status launch_compact(agx_engine* e, uint32_t mode) {
-  CompactArgs ca{};
-  ca.alive = e->d_alive;
-  ca.stopq = e->d_stopq;
-  ca.nstop = e->d_nstop;
-  ca.d_bump = e->d_bump;
-  ca.cnt_bl = e->d_cnt_bl;
-  ca.cnt_em = e->d_cnt_em;
-  ca.off_bl = e->d_off_bl;
-  ca.off_em = e->d_off_em;
-  ca.d_n = e->d_n;
-  ca.d_total = e->d_total;
-  ca.stats = e->d_stats;
-  ca.n_staged = mode == 0 ? e->n_staged_dev : 0u;
-  ca.mode = mode;
-  ca.cap0 = e->cap;
-  ca.cap1 = e->cap_emit;
+Chunks make_chunks(agx_engine* e) {
+  Chunks c{};
+  c.bl = e->bl.c();
+  c.em = e->em.c();
+  c.st = e->stg.c();
+  c.off = e->d_chunk_off;
+  c.cnt = e->d_chunk_cnt;
+  c.nb = e->nb;
+  return c;
+}
+
+// one dense LSD pass (reduce-then-scan) over `bits` bits at `shift`
+agx_status launch_dense_pass(agx_engine* e, const DevMsgs& in, const DevMsgs& out, const uint32_t* d_n, uint32_t shift,
+                             uint32_t bits) {
+  SortArgs sa{};
+  sa.in = in.c();
+  sa.out = out.m();
+  sa.d_n = d_n;
+  sa.hist = e->d_hist_d;
+  sa.tot = e->d_tot;
+  sa.bstart = e->d_bstart;
+  sa.stride = (uint32_t)e->max_tiles;
+  sa.shift = shift;
+  sa.bits = bits;
+  const uint32_t g = grid_for(e->max_tiles, 2048);
   {
-    Scope s(e, K_COMPACT_SCAN);
-    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kScanThreads), 0, e->stream, ca);
+    Scope s(e, K_UPSWEEP);
+    hipLaunchKernelGGL(k_sort_upsweep, dim3(g), dim3(kThreads), 0, e->stream, sa);
   }
-  CopyArgs cp{};
-  cp.bl = e->bl.c();
-  cp.em = e->em.c();
-  cp.st = e->stg.c();
-  cp.out0 = e->A.m();
-  cp.out1 = e->s1.m();
-  cp.cnt_bl = e->d_cnt_bl;
-  cp.cnt_em = e->d_cnt_em;
-  cp.off_bl = e->d_off_bl;
-  cp.off_em = e->d_off_em;
-  cp.base_em = e->d_base_em;
-  cp.d_total = e->d_total;
-  cp.n_staged = ca.n_staged;
-  cp.mode = mode;
   {
-    Scope s(e, K_COMPACT_COPY);
-    hipLaunchKernelGGL(k_compact_copy, dim3(grid_for(2 * e->max_tiles_a + 1, 4096)), dim3(256), 0, e->stream, cp);
+    Scope s(e, K_ROWSCAN);
+    hipLaunchKernelGGL(k_sort_rowscan, dim3(1u << bits), dim3(kThreads), 0, e->stream, sa);
+  }
+  {
+    Scope s(e, K_DOWNSWEEP);
+    hipLaunchKernelGGL(k_sort_downsweep, dim3(g), dim3(kThreads), 0, e->stream, sa);
   }
   HIP_TRY(hipGetLastError());
   return AGX_OK;
 }
 
-// Stable LSD radix sort of `in` (n at d_n) over key bits [lo, hi); returns the
-// buffer holding the result (in or tmp).
-agx_status launch_sort(agx_engine* e, DevMsgs& in, DevMsgs& tmp, const uint32_t* d_n, uint32_t lo, uint32_t hi,
-                       DevMsgs** result) {
-  DevMsgs* src = &in;
-  DevMsgs* dst = &tmp;
-  const uint32_t g = grid_for(e->max_tiles_s, 2048);
-  for (uint32_t shift = lo; shift < hi; shift += kRadixBits) {
-    SortArgs sa{};
-    sa.in = src->c();
-    sa.out = dst->m();
-    sa.d_n = d_n;
-    sa.hist = e->d_hist;
-    sa.tot = e->d_tot;
-    sa.stride = (uint32_t)e->max_tiles_s;
-    sa.shift = shift;
-    sa.bits = std::min<uint32_t>(kRadixBits, hi - shift);
+// Group the mail by bucket.  first_from_chunks: pass 0 reads the chunk list written
+// by the previous k_bucket_apply (single rank); otherwise every pass reads the dense A.
+// Returns the buffer holding the result.
+agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** result) {
+  DevMsgs* src = &e->A;
+  DevMsgs* dst = &e->B;
+  uint32_t p0 = 0;
+  if (first_from_chunks) {
+    ChunkSortArgs ca{};
+    ca.ch = make_chunks(e);
+    ca.out = e->A.m();
+    ca.hist = e->d_hist_c;
+    ca.tot = e->d_tot;
+    ca.d_n = e->d_n;
+    ca.bstart = e->d_bstart;
+    ca.stats = e->d_stats;
+    ca.alive = e->d_alive;
+    ca.stopq = e->d_stopq;
+    ca.nstop = e->d_nstop;
+    ca.cap = e->cap;
+    ca.stride = e->nchunks;
+    ca.nchunks = e->nchunks;
+    ca.shift = e->plan.shift[0];
+    ca.bits = e->plan.bits[0];
     {
-      Scope s(e, K_UPSWEEP);
-      hipLaunchKernelGGL(k_sort_upsweep, dim3(g), dim3(kSortThreads), 0, e->stream, sa);
+      Scope s(e, K_CROWSCAN);
+      hipLaunchKernelGGL(k_chunk_rowscan, dim3(1u << ca.bits), dim3(kThreads), 0, e->stream, ca);
     }
     {
-      Scope s(e, K_ROWSCAN);
-      hipLaunchKernelGGL(k_sort_rowscan, dim3(1u << sa.bits), dim3(256), 0, e->stream, sa);
+      Scope s(e, K_CDOWN);
+      hipLaunchKernelGGL(k_chunk_downsweep, dim3(grid_for(e->nchunks, 4096)), dim3(kThreads), 0, e->stream, ca);
     }
-    {
-      Scope s(e, K_DOWNSWEEP);
-      hipLaunchKernelGGL(k_sort_downsweep, dim3(g), dim3(kSortThreads), 0, e->stream, sa);
-    }
+    HIP_TRY(hipGetLastError());
+    p0 = 1;
+  }
+  for (uint32_t p = p0; p < e->plan.npass; ++p) {
+    AGX_TRY(launch_dense_pass(e, *src, *dst, e->d_n, e->plan.shift[p], e->plan.bits[p]));
     std::swap(src, dst);
   }
-  HIP_TRY(hipGetLastError());
   *result = src;
   return AGX_OK;
 }
 
 agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
-  ApplyArgs aa{};
-  aa.P = make_params(e);
-  aa.in = sorted.c();
-  aa.d_n = e->d_n;
-  aa.bl = e->bl.m();
-  aa.em = e->em.m();
-  aa.cnt_bl = e->d_cnt_bl;
-  aa.cnt_em = e->d_cnt_em;
-  aa.base_em = e->d_base_em;
-  aa.d_bump = e->d_bump;
-  aa.cap_em = e->cap_emit;
-  aa.stats = e->d_stats;
+  // the chunk histograms consumed by this step's first pass are free again
+  HIP_TRY(hipMemsetAsync(e->d_hist_c, 0, (size_t)kRadix * e->nchunks * 4, e->stream));
+  BucketArgs ba{};
+  ba.P = make_params(e);
+  ba.in = sorted.c();
+  ba.d_n = e->d_n;
+  ba.bstart = e->d_bstart;
+  ba.scr = e->scr.m();
+  ba.bl = e->bl.m();
+  ba.em = e->em.m();
+  ba.chunk_off = e->d_chunk_off;
+  ba.chunk_cnt = e->d_chunk_cnt;
+  ba.nhist = e->d_hist_c;
+  ba.nhist_stride = e->nchunks;
+  ba.nx_shift = e->plan.shift[0];
+  ba.nx_bits = e->plan.bits[0];
+  ba.nb = e->nb;
+  ba.single_pass = e->plan.npass == 1;
+  ba.kmax = e->kmax;
+  ba.stats = e->d_stats;
   {
     Scope s(e, K_APPLY);
-    hipLaunchKernelGGL(k_apply, dim3(grid_for(e->max_tiles_a, 2048)), dim3(kApplyThreads), 0, e->stream, aa);
+    hipLaunchKernelGGL(k_bucket_apply, dim3(grid_for(e->nb, 4096)), dim3(kBThreads), 0, e->stream, ba);
   }
   HIP_TRY(hipGetLastError());
+  return AGX_OK;
+}
+
+// host-staged tells enter as chunk 2nb of the next single-rank step
+agx_status launch_staged_chunk(agx_engine* e) {
+  if (!e->n_staged_dev) return AGX_OK;
+  hipLaunchKernelGGL(k_chunk_hist, dim3(kStagedChunks), dim3(kThreads), 0,
+                     e->stream, e->stg.key, e->n_staged_dev, e->d_hist_c, e->nchunks, 2 * e->nb, e->plan.shift[0],
+                     e->plan.bits[0], e->d_chunk_off, e->d_chunk_cnt);
+  HIP_TRY(hipGetLastError());
+  e->n_staged_dev = 0;
   return AGX_OK;
 }
 
@@ -372,22 +409,35 @@ agx_status prepare_run(agx_engine* e) {
 }
 
 // ----------------------------------------------------------- multi-rank step
-// phase 1: compaction (backlog -> A front, tells -> s1), partition tells by owner
-// rank (stable), pack [send counts..., n_backlog, n_staged] into d_cvec.
+// phase 1: chunks -> [backlog at the front of A, tells dense in s1]; stable
+// partition of the tells by owner rank (s1 -> s2); pack [send counts..., n_backlog, n_staged].
 agx_status phase1(agx_engine* e) {
-  AGX_TRY(launch_compact(e, 1));
-  DevMsgs* part = nullptr;
-  AGX_TRY(launch_sort(e, e->s1, e->s2, e->d_total + 1, kOwnerShift, kOwnerShift + ceil_log2(e->R), &part));
-  if (part != &e->s2) {  // keep the partitioned send buffer in s2
-    std::swap(e->s1, e->s2);
+  McompactArgs m{};
+  m.ch = make_chunks(e);
+  m.out0 = e->A.m();
+  m.out1 = e->s1.m();
+  m.off0 = e->d_moff0;
+  m.off1 = e->d_moff1;
+  m.d_total = e->d_total;
+  m.alive = e->d_alive;
+  m.stopq = e->d_stopq;
+  m.nstop = e->d_nstop;
+  m.stats = e->d_stats;
+  m.cap0 = e->cap;
+  m.cap1 = e->cap_emit;
+  {
+    Scope s(e, K_MCOMPACT);
+    hipLaunchKernelGGL(k_mcompact_scan, dim3(1), dim3(kScanThreads), 0, e->stream, m);
+    hipLaunchKernelGGL(k_mcompact_copy, dim3(grid_for(2 * e->nb, 4096)), dim3(kThreads), 0, e->stream, m);
   }
+  AGX_TRY(launch_dense_pass(e, e->s1, e->s2, e->d_total + 1, kOwnerShift, std::max<uint32_t>(1, ceil_log2(e->R))));
   hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(64), 0, e->stream, e->d_tot, e->d_total, e->d_cvec, e->R,
                      e->n_staged_dev);
   HIP_TRY(hipGetLastError());
   return AGX_OK;
 }
 
-// phase 2: place staged tells after the received mail, sort by local key, apply.
+// phase 2: staged tells after the received mail, group by bucket, apply.
 agx_status phase2(agx_engine* e, uint64_t n_sorted, uint64_t staged_at) {
   if (e->n_staged_dev) {
     HIP_TRY(hipMemcpyAsync(e->A.key + staged_at, e->stg.key, e->n_staged_dev * 4ull, hipMemcpyDeviceToDevice, e->stream));
@@ -399,7 +449,7 @@ agx_status phase2(agx_engine* e, uint64_t n_sorted, uint64_t staged_at) {
   HIP_TRY(hipMemcpyAsync(e->d_n, e->h_pin, 4, hipMemcpyHostToDevice, e->stream));
   // the pinned word is reused next step only after the host sync in the exchange
   DevMsgs* sorted = nullptr;
-  AGX_TRY(launch_sort(e, e->A, e->B, e->d_n, 0, e->key_bits, &sorted));
+  AGX_TRY(launch_bucket_sort(e, false, &sorted));
   AGX_TRY(launch_apply(e, *sorted));
   return AGX_OK;
 }
@@ -470,36 +520,78 @@ agx_status fill_stats(agx_engine* e, agx_stats* out, uint64_t inflight) {
   return AGX_OK;
 }
 
-agx_status single_inflight(agx_engine* e, uint64_t* out) {
-  hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_n, e->d_cnt_bl, e->d_cnt_em,
+agx_status chunk_inflight(agx_engine* e, uint64_t* out) {
+  hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_chunk_cnt, e->nchunks,
                      (unsigned long long*)e->d_inflight);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_inflight, 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  *out = e->h_pin64[0] + e->n_staged_dev;
+  *out = e->h_pin64[0];
+  return AGX_OK;
+}
+
+// one superstep on one rank: [chunks] -> group by bucket -> in-bucket sort + drain + apply -> [chunks]
+agx_status launch_step_single(agx_engine* e) {
+  AGX_TRY(launch_staged_chunk(e));
+  DevMsgs* sorted = nullptr;
+  AGX_TRY(launch_bucket_sort(e, true, &sorted));
+  AGX_TRY(launch_apply(e, *sorted));
+  return AGX_OK;
+}
+
+// hipGraph of `steps` supersteps (the launch-bound inner loop): replayed
+// instead of 10+ eager launches per superstep.
+agx_status capture_steps(agx_engine* e, uint32_t steps, hipGraphExec_t* out) {
+  hipGraph_t g = nullptr;
+  HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+  agx_status st = AGX_OK;
+  for (uint32_t i = 0; i < steps && st == AGX_OK; ++i) st = launch_step_single(e);
+  hipError_t ce = hipStreamEndCapture(e->stream, &g);
+  if (st) {
+    if (g) hipGraphDestroy(g);
+    return st;
+  }
+  if (ce != hipSuccess) return set_err(AGX_EDEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ce));
+  hipError_t ie = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (ie != hipSuccess) return set_err(AGX_EDEVICE, "hipGraphInstantiate: %s", hipGetErrorString(ie));
   return AGX_OK;
 }
 
 agx_status run_single(agx_engine* e, uint32_t max_steps) {
-  constexpr uint32_t kLag = 16;
+  constexpr uint32_t kLag = 4;  // replays in flight before the host polls quiescence
   std::vector<hipEvent_t> ev(kLag);
   for (auto& x : ev) HIP_TRY(hipEventCreateWithFlags(&x, hipEventDisableTiming));
   agx_status st = AGX_OK;
-  for (uint32_t s = 0; s < max_steps; ++s) {
-    if (s >= kLag) {
-      hipEventSynchronize(ev[s % kLag]);
-      if (e->h_pin[s % kLag] == 0) break;  // step s-kLag had no mail: quiescent
+  uint32_t left = max_steps;
+  // staged host tells enter through an eager step (the graphs assume none)
+  if (left && e->n_staged_dev) {
+    st = launch_step_single(e);
+    --left;
+  }
+  const bool use_graph = !e->prof && e->graphs_enabled;
+  if (st == AGX_OK && use_graph && !e->g1) {
+    st = capture_steps(e, 1, &e->g1);
+    if (st == AGX_OK) st = capture_steps(e, agx_engine::kGraphSteps, &e->gG);
+  }
+  for (uint32_t it = 0; st == AGX_OK && left > 0; ++it) {
+    const uint32_t slot = it % kLag;
+    if (it >= kLag) {
+      hipEventSynchronize(ev[slot]);
+      if (e->h_pin[slot] == 0) break;  // that replay ended on a superstep with no mail: quiescent
     }
-    st = launch_compact(e, 0);
-    if (st) break;
-    e->n_staged_dev = 0;
-    DevMsgs* sorted = nullptr;
-    st = launch_sort(e, e->A, e->B, e->d_n, 0, e->key_bits, &sorted);
-    if (st) break;
-    st = launch_apply(e, *sorted);
-    if (st) break;
-    hipMemcpyAsync(&e->h_pin[s % kLag], e->d_total, 4, hipMemcpyDeviceToHost, e->stream);
-    hipEventRecord(ev[s % kLag], e->stream);
+    uint32_t cnt;
+    if (use_graph) {
+      cnt = left >= agx_engine::kGraphSteps ? agx_engine::kGraphSteps : 1;
+      hipError_t ge = hipGraphLaunch(cnt == 1 ? e->g1 : e->gG, e->stream);
+      if (ge != hipSuccess) st = set_err(AGX_EDEVICE, "hipGraphLaunch: %s", hipGetErrorString(ge));
+    } else {
+      cnt = 1;
+      st = launch_step_single(e);
+    }
+    left -= cnt;
+    hipMemcpyAsync(&e->h_pin[slot], e->d_n, 4, hipMemcpyDeviceToHost, e->stream);
+    hipEventRecord(ev[slot], e->stream);
   }
   hipStreamSynchronize(e->stream);
   for (auto& x : ev) hipEventDestroy(x);
@@ -599,6 +691,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->R = cfg->n_ranks ? cfg->n_ranks : 1;
   e->rank = cfg->rank;
   e->num_shards = cfg->num_shards ? cfg->num_shards : 1000;
+  e->graphs_enabled = getenv("AGX_NO_GRAPH") == nullptr;
   agx_status st = ensure_dev(e);
   if (st) { delete e; return st; }
 
@@ -624,10 +717,23 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   const uint64_t nl = std::max<uint64_t>(e->n_local, 1);
   e->key_bits = std::max<uint32_t>(1, ceil_log2(nl));
   e->cap = cfg->msg_capacity ? cfg->msg_capacity : std::max<uint64_t>(4 * nl, 1u << 16);
-  if (e->cap >= (1ull << 32) - kSortTile) { delete e; return set_err(AGX_EINVAL, "msg_capacity too large"); }
-  e->cap_emit = std::min<uint64_t>(e->cap * e->kmax, (1ull << 32) - kSortTile - 1);
-  e->max_tiles_a = (e->cap + kApplyTile - 1) / kApplyTile + 1;
-  e->max_tiles_s = (std::max(e->cap, e->cap_emit) + kSortTile - 1) / kSortTile + 1;
+  if (e->cap >= (1ull << 32) - kTile) { delete e; return set_err(AGX_EINVAL, "msg_capacity too large"); }
+  e->cap_emit = e->cap * e->kmax;  // bucket b's tells live at [lo*kmax, (lo+cnt)*kmax)
+  if (e->cap_emit >= (1ull << 32)) { delete e; return set_err(AGX_EINVAL, "msg_capacity * max_emit must be < 2^32"); }
+  e->max_tiles = (std::max(e->cap, e->cap_emit) + kTile - 1) / kTile + 1;
+  // buckets of 2^kBucketBits actors; LSD passes over key bits [kBucketBits, key_bits), <= kRadixBits each
+  e->nb = (uint32_t)((nl + kBucket - 1) / kBucket);
+  e->nchunks = 2 * e->nb + kStagedChunks;
+  {
+    const uint32_t lo = kBucketBits, hi = std::max<uint32_t>(e->key_bits, kBucketBits + 1);
+    e->plan.npass = (hi - lo + kRadixBits - 1) / kRadixBits;
+    for (uint32_t p = 0, sh = lo; p < e->plan.npass; ++p) {
+      const uint32_t b = (hi - sh + (e->plan.npass - p) - 1) / (e->plan.npass - p);  // spread bits evenly
+      e->plan.shift[p] = sh;
+      e->plan.bits[p] = b;
+      sh += b;
+    }
+  }
 
   e->h_kind.assign(e->n_local, 0);
   e->h_alive.assign(e->n_local, 0);
@@ -655,32 +761,33 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   }
   CREATE_TRY(alloc_msgs(e->A, e->cap));
   CREATE_TRY(alloc_msgs(e->B, e->cap));
-  CREATE_TRY(alloc_msgs(e->bl, e->max_tiles_a * kApplyTile));
+  CREATE_TRY(alloc_msgs(e->scr, e->cap));
+  CREATE_TRY(alloc_msgs(e->bl, e->cap));
   CREATE_TRY(alloc_msgs(e->em, e->cap_emit));
   if (e->R > 1) {
     CREATE_TRY(alloc_msgs(e->s1, e->cap_emit));
     CREATE_TRY(alloc_msgs(e->s2, e->cap_emit));
+    CREATE_TRY(dalloc(&e->d_moff0, e->nb));
+    CREATE_TRY(dalloc(&e->d_moff1, e->nb));
   }
-  CREATE_TRY(dalloc(&e->d_cnt_bl, e->max_tiles_a));
-  CREATE_TRY(dalloc(&e->d_cnt_em, e->max_tiles_a));
-  CREATE_TRY(dalloc(&e->d_base_em, e->max_tiles_a));
-  CREATE_TRY(dalloc(&e->d_off_bl, e->max_tiles_a));
-  CREATE_TRY(dalloc(&e->d_off_em, e->max_tiles_a));
+  CREATE_TRY(dalloc(&e->d_chunk_off, e->nchunks));
+  CREATE_TRY(dalloc(&e->d_chunk_cnt, e->nchunks));
+  CREATE_TRY(hipMemset(e->d_chunk_off, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipMemset(e->d_chunk_cnt, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(dalloc(&e->d_hist_c, (uint64_t)kRadix * e->nchunks));
+  CREATE_TRY(hipMemset(e->d_hist_c, 0, (uint64_t)kRadix * e->nchunks * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(dalloc(&e->d_bstart, kRadix + 1));
+  CREATE_TRY(dalloc(&e->d_hist_d, (uint64_t)kRadix * e->max_tiles));
+  CREATE_TRY(dalloc(&e->d_tot, kRadix));
   CREATE_TRY(dalloc(&e->d_n, 4));
   CREATE_TRY(dalloc(&e->d_total, 4));
-  CREATE_TRY(dalloc(&e->d_bump, 4));
-  CREATE_TRY(dalloc(&e->d_hist, (uint64_t)kRadix * e->max_tiles_s));
-  CREATE_TRY(dalloc(&e->d_tot, kRadix));
   CREATE_TRY(dalloc(&e->d_stats, ST_N));
   CREATE_TRY(dalloc(&e->d_inflight, 1));
   CREATE_TRY(dalloc(&e->d_cvec, AGX_MAX_RANKS + 2));
   CREATE_TRY(dalloc(&e->d_cmat, (uint64_t)AGX_MAX_RANKS * (AGX_MAX_RANKS + 2)));
   CREATE_TRY(hipMemset(e->d_n, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(hipMemset(e->d_total, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-  CREATE_TRY(hipMemset(e->d_bump, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(hipMemset(e->d_stats, 0, ST_N * 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-  CREATE_TRY(hipMemset(e->d_cnt_bl, 0, e->max_tiles_a * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-  CREATE_TRY(hipMemset(e->d_cnt_em, 0, e->max_tiles_a * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(hipHostMalloc((void**)&e->h_pin, 64 * 4, hipHostMallocDefault) == hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
   CREATE_TRY(hipHostMalloc((void**)&e->h_pin64, (AGX_MAX_RANKS * (AGX_MAX_RANKS + 2) + 8) * 8, hipHostMallocDefault) == hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
   // empty graph rows so FORWARD_RR on an engine without a graph is well defined
@@ -697,12 +804,14 @@ agx_status agx_destroy(agx_engine* e) {
   hipSetDevice((int)e->cfg.device);
   if (e->stream) hipStreamSynchronize(e->stream);
   if (e->comm) ncclCommDestroy(e->comm);
+  if (e->g1) hipGraphExecDestroy(e->g1);
+  if (e->gG) hipGraphExecDestroy(e->gG);
   hipFree(e->d_kind); hipFree(e->d_alive); hipFree(e->d_stopq); hipFree(e->d_nstop); hipFree(e->d_state); hipFree(e->d_gid); hipFree(e->d_route);
   hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_row); hipFree(e->d_col);
-  free_msgs(e->A); free_msgs(e->B); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
+  free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
   free_msgs(e->s1); free_msgs(e->s2);
-  hipFree(e->d_cnt_bl); hipFree(e->d_cnt_em); hipFree(e->d_base_em); hipFree(e->d_off_bl); hipFree(e->d_off_em);
-  hipFree(e->d_n); hipFree(e->d_total); hipFree(e->d_bump); hipFree(e->d_hist); hipFree(e->d_tot);
+  hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart);
+  hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);
   if (e->h_pin) hipHostFree(e->h_pin);
   if (e->h_pin64) hipHostFree(e->h_pin64);
@@ -836,17 +945,9 @@ agx_status agx_get_stats(agx_engine* e, agx_stats* out) {
   if (!e) return set_err(AGX_EINVAL, "null engine");
   AGX_TRY(ensure_dev(e));
   uint64_t infl = 0;
-  if (e->R > 1) {
-    // backlog + tells produced by the last apply, not yet exchanged
-    hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_n, e->d_cnt_bl, e->d_cnt_em,
-                       (unsigned long long*)e->d_inflight);
-    HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_inflight, 8, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    infl = e->h_pin64[0] + e->n_staged_dev + e->hs_key.size();
-  } else {
-    AGX_TRY(single_inflight(e, &infl));
-    infl += e->hs_key.size();
-  }
+  // backlog + tells produced by the last apply (chunks), plus host tells not yet consumed
+  AGX_TRY(chunk_inflight(e, &infl));
+  infl += e->n_staged_dev + e->hs_key.size();
   return fill_stats(e, out, infl);
 }
 

@@ -1,18 +1,22 @@
-// agx_kernels.h — the superstep kernels (gfx950, wave64, integer only).
+// agx_kernels.h — the superstep kernels (gfx950, wave64, integer only, no MFMA).
 //
-// One BSP superstep replaces one round of Mailbox.run/processMailbox over
-// every scheduled mailbox (akka-actor/src/main/scala/akka/dispatch/Mailbox.scala:227-277):
+// One BSP superstep replaces one round of Mailbox.run/processMailbox over every
+// scheduled mailbox (akka-actor/src/main/scala/akka/dispatch/Mailbox.scala:227-277).
+// Actors are grouped in buckets of 2^kBucketBits consecutive local ids.
 //
-//   k_compact_scan / k_compact_copy   scan-compacted emission: per-tile backlog
-//                                     and emission chunks -> one dense array
-//                                     (backlog first, then tells in sender order)
+//   k_bucket_apply     per bucket: stable in-bucket counting sort of its mail by
+//                      actor (LDS wave multisplit), segmented drain with the
+//                      throughput cap and bounded-mailbox tail-drop, behaviour
+//                      apply (ActorCell.invoke), scan-compacted emission of the
+//                      next step's tells into a per-bucket chunk, and the chunk's
+//                      digit histogram for the next step's first radix pass.
+//   k_chunk_rowscan    per digit: exclusive prefix of the chunk histograms.
+//   k_chunk_downsweep  stable LSD radix pass that reads the chunk list
+//                      [backlog chunks][tell chunks][host-staged tells] directly
+//                      (no separate compaction) and groups mail by bucket.
 //   k_sort_upsweep / k_sort_rowscan / k_sort_downsweep
-//                                     LDS-staged stable LSD radix sort of the
-//                                     envelopes by destination ActorRef
-//                                     (Mailbox.enqueue into per-actor FIFOs)
-//   k_apply                           segmented mailbox drain (throughput cap,
-//                                     bounded tail-drop, dead letters) +
-//                                     behaviour-apply + tell emission
+//                      the same pass over a dense array (later digits, and the
+//                      multi-GPU path after the RCCL exchange).
 //
 // Envelopes are SoA u32 {key, src, payload} = 12 B.
 #pragma once
@@ -21,15 +25,16 @@
 namespace agx {
 
 // ---------------------------------------------------------------- geometry
-constexpr int kApplyThreads = 256;
-constexpr int kApplyIpt = 8;
-constexpr int kApplyTile = kApplyThreads * kApplyIpt;  // 2048 envelopes
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+constexpr int kIpt = 8;
+constexpr int kTile = kThreads * kIpt;  // 2048 envelopes per sort tile
 
-constexpr int kSortThreads = 256;
-constexpr int kSortWaves = kSortThreads / kWave;
-constexpr int kSortIpt = 16;
-constexpr int kSortTile = kSortThreads * kSortIpt;  // 4096 envelopes
-constexpr int kRadixBits = 8;
+constexpr int kBucketBits = 11;
+constexpr int kBucket = 1 << kBucketBits;  // actors per bucket
+constexpr int kActPerThread = kBucket / kThreads;
+
+constexpr int kRadixBits = 9;  // max digit width of one pass
 constexpr int kRadix = 1 << kRadixBits;
 
 constexpr int kScanThreads = 1024;
@@ -51,15 +56,9 @@ struct CMsgs {
 
 __device__ __forceinline__ uint32_t div_up(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
-// =========================================================================
-// Compaction: chunk list = [bl chunk 0..nt) [em chunk 0..nt) [staged]
-//   mode 0 (single rank): all chunks -> stream 0 (sort input), in that order
-//   mode 1 (multi rank):  bl -> stream 0 (sort input), em -> stream 1 (send buffer),
-//                         staged handled by the host after the exchange
-// =========================================================================
 // Commit Behaviors.stopped results of the previous apply: alive[l] = 0.
-// (k_apply never writes `alive`, so every tile classifies against the
-// alive-at-step-start value — deterministic across tile schedules.)
+// (k_bucket_apply never writes `alive`, so every block classifies against the
+// alive-at-step-start value — deterministic across block schedules.)
 __device__ __forceinline__ void commit_stops(uint8_t* alive, const uint32_t* stopq, uint32_t* nstop) {
   const uint32_t ns = *nstop;
   for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) alive[stopq[i]] = 0;
@@ -70,211 +69,323 @@ __global__ void __launch_bounds__(kScanThreads) k_commit_stops(uint8_t* alive, c
   commit_stops(alive, stopq, nstop);
 }
 
-struct CompactArgs {
-  uint8_t* alive;
+// Chunk list written by k_bucket_apply (nb buckets):
+//   chunk b          backlog of bucket b        (in the bl arena)
+//   chunk nb + b     tells emitted by bucket b  (in the em arena)
+//   chunk 2nb        host-staged tells          (staging buffer)
+struct Chunks {
+  CMsgs bl, em, st;
+  const uint32_t* off;
+  const uint32_t* cnt;
+  uint32_t nb;
+  __device__ __forceinline__ const CMsgs& arena(uint32_t c) const { return c < nb ? bl : (c < 2 * nb ? em : st); }
+};
+
+// =========================================================================
+// Wave-level multisplit: rank of this lane's item among the wave's earlier
+// items with the same digit (ballot match over the digit bits); `hist` is the
+// wave's running per-digit count in LDS.
+// =========================================================================
+template <typename HT>
+__device__ __forceinline__ uint32_t wave_rank(bool valid, uint32_t d, uint32_t bits, HT* hist, uint64_t lt_mask) {
+  uint64_t m = __ballot(valid);
+  for (uint32_t b = 0; b < bits; ++b) {
+    const uint32_t bit = (d >> b) & 1u;
+    const uint64_t bal = __ballot(bit);
+    m &= bit ? bal : ~bal;
+  }
+  const uint32_t before = (uint32_t)__popcll(m & lt_mask);
+  const uint32_t c = (uint32_t)__popcll(m);
+  uint32_t old = 0;
+  if (valid) old = hist[d];
+  __builtin_amdgcn_wave_barrier();
+  if (valid && before == 0) hist[d] = (HT)(old + c);
+  __builtin_amdgcn_wave_barrier();
+  return old + before;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const uint32_t lane = lane_id();
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// =========================================================================
+// Chunked first radix pass
+// =========================================================================
+struct ChunkSortArgs {
+  Chunks ch;
+  Msgs out;
+  uint32_t* hist;      // digit-major [nbins][stride]: per-chunk digit counts -> exclusive prefix
+  uint32_t* tot;       // [nbins] digit totals
+  uint32_t* d_n;       // out: total messages
+  uint32_t* bstart;    // out: exclusive scan of digit totals (bucket starts when one pass)
+  uint64_t* stats;
+  uint8_t* alive;      // stop commit
   const uint32_t* stopq;
   uint32_t* nstop;
-  uint32_t* d_bump;    // emission bump allocator, reset here for the next apply
-  const uint32_t* cnt_bl;
-  const uint32_t* cnt_em;
-  uint32_t* off_bl;
-  uint32_t* off_em;
-  uint32_t* d_n;       // in: sorted count of the step that produced the chunks; out: stream-0 total (mode 0)
-  uint32_t* d_total;   // [0] stream-0 total, [1] stream-1 total, [2] nt used
-  uint64_t* stats;
-  uint32_t n_staged;
-  uint32_t mode;
-  uint64_t cap0, cap1;
+  uint64_t cap;
+  uint32_t stride, nchunks, shift, bits;
 };
 
-__global__ void __launch_bounds__(kScanThreads) k_compact_scan(CompactArgs a) {
-  __shared__ uint32_t scratch[kScanThreads / kWave + 1];
-  __shared__ uint32_t s_nt;
-  __shared__ uint64_t s_run0, s_run1;
-  const int tid = threadIdx.x;
-  commit_stops(a.alive, a.stopq, a.nstop);
-  if (tid == 0) {
-    s_nt = div_up(*a.d_n, kApplyTile);
-    s_run0 = 0;
-    s_run1 = 0;
+// one block per digit: exclusive prefix over chunks (in place) + digit total;
+// block 0 also commits the previous step's stops.
+__global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs a) {
+  __shared__ uint32_t scratch[kWaves + 1];
+  __shared__ uint32_t s_run;
+  if (blockIdx.x == 0) commit_stops(a.alive, a.stopq, a.nstop);
+  const uint32_t d = blockIdx.x;
+  if (d >= (1u << a.bits)) return;
+  uint32_t* row = a.hist + (size_t)d * a.stride;
+  if (threadIdx.x == 0) s_run = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < a.nchunks; base += kThreads) {
+    const uint32_t i = base + threadIdx.x;
+    uint32_t v = i < a.nchunks ? row[i] : 0u, t;
+    const uint32_t ex = block_excl_sum<kThreads>(v, scratch, &t);
+    if (i < a.nchunks) row[i] = s_run + ex;
+    __syncthreads();
+    if (threadIdx.x == 0) s_run += t;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.tot[d] = s_run;
+}
+
+__global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
+  __shared__ uint32_t whist[kWaves][kRadix];
+  __shared__ uint32_t s_dbase[kRadix];  // exclusive scan of digit totals
+  __shared__ uint32_t s_run[kRadix];    // items of each digit already placed from this chunk
+  __shared__ uint32_t s_ldig[kRadix];
+  __shared__ uint32_t s_gadj[kRadix];
+  __shared__ uint32_t scratch[kWaves + 1];
+  __shared__ uint32_t s_total;
+  __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
+
+  const int tid = threadIdx.x, w = tid / kWave;
+  const uint32_t lane = lane_id();
+  const uint32_t mask = (1u << a.bits) - 1u, nd = 1u << a.bits;
+  const uint64_t ltm = lanemask_lt();
+  for (uint32_t d = tid; d < kRadix; d += kThreads) {
+    uint32_t v = d < nd ? a.tot[d] : 0u;
+    s_dbase[d] = v;
   }
   __syncthreads();
-  const uint32_t nt = s_nt;
-  // backlog chunks: stream 0
-  for (uint32_t base = 0; base < nt; base += kScanThreads) {
-    uint32_t i = base + tid;
-    uint32_t v = i < nt ? a.cnt_bl[i] : 0u, tot;
-    uint32_t ex = block_excl_sum<kScanThreads>(v, scratch, &tot);
-    if (i < nt) a.off_bl[i] = (uint32_t)(s_run0 + ex);
+  {  // exclusive scan over (up to 512) digit totals: 2 per thread
+    const uint32_t v0 = s_dbase[2 * tid], v1 = s_dbase[2 * tid + 1];
+    uint32_t t;
     __syncthreads();
-    if (tid == 0) s_run0 += tot;
-    __syncthreads();
+    const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, scratch, &t);
+    s_dbase[2 * tid] = ex;
+    s_dbase[2 * tid + 1] = ex + v0;
+    if (tid == 0) s_total = t;
   }
-  // emission chunks: stream 0 (mode 0) or stream 1 (mode 1)
-  for (uint32_t base = 0; base < nt; base += kScanThreads) {
-    uint32_t i = base + tid;
-    uint32_t v = i < nt ? a.cnt_em[i] : 0u, tot;
-    uint32_t ex = block_excl_sum<kScanThreads>(v, scratch, &tot);
-    uint64_t run = a.mode == 0 ? s_run0 : s_run1;
-    if (i < nt) a.off_em[i] = (uint32_t)(run + ex);
-    __syncthreads();
+  __syncthreads();
+  const uint32_t total = s_total;
+  const bool over = total > a.cap;
+  if (blockIdx.x == 0) {
+    for (uint32_t d = tid; d < nd; d += kThreads) a.bstart[d] = s_dbase[d];
     if (tid == 0) {
-      if (a.mode == 0) s_run0 += tot; else s_run1 += tot;
+      a.bstart[nd] = total;
+      *a.d_n = over ? 0u : total;
+      if (over) atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
     }
-    __syncthreads();
   }
-  if (tid == 0) {
-    uint64_t t0 = s_run0, t1 = s_run1;
-    if (a.mode == 0) t0 += a.n_staged;
-    bool over = t0 > a.cap0 || t1 > a.cap1;
-    if (over) atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
-    a.d_total[0] = over ? 0u : (uint32_t)t0;
-    a.d_total[1] = over ? 0u : (uint32_t)t1;
-    a.d_total[2] = nt;
-    if (a.mode == 0) *a.d_n = over ? 0u : (uint32_t)t0;
-    *a.d_bump = 0;
-  }
-}
+  if (over) return;
 
-struct CopyArgs {
-  CMsgs bl, em, st;         // chunk storage (bl: tile * kApplyTile, em: base_em[tile])
-  Msgs out0, out1;          // stream 0 / stream 1
-  const uint32_t* cnt_bl;
-  const uint32_t* cnt_em;
-  const uint32_t* off_bl;
-  const uint32_t* off_em;
-  const uint32_t* base_em;
-  const uint32_t* d_total;  // [0] t0, [1] t1, [2] nt
-  uint32_t n_staged;
-  uint32_t mode;
-};
-
-__device__ __forceinline__ void copy_run(const CMsgs& s, uint64_t s0, const Msgs& d, uint64_t d0, uint32_t n) {
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    d.key[d0 + i] = s.key[s0 + i];
-    d.src[d0 + i] = s.src[s0 + i];
-    d.pay[d0 + i] = s.pay[s0 + i];
-  }
-}
-
-__global__ void __launch_bounds__(256) k_compact_copy(CopyArgs a) {
-  const uint32_t nt = a.d_total[2];
-  if (a.d_total[0] == 0 && a.d_total[1] == 0) return;  // empty or capacity overflow
-  const uint32_t nchunks = 2 * nt + (a.mode == 0 ? 1u : 0u);
-  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    if (c < nt) {
-      copy_run(a.bl, (uint64_t)c * kApplyTile, a.out0, a.off_bl[c], a.cnt_bl[c]);
-    } else if (c < 2 * nt) {
-      uint32_t t = c - nt;
-      copy_run(a.em, a.base_em[t], a.mode == 0 ? a.out0 : a.out1, a.off_em[t], a.cnt_em[t]);
-    } else {
-      copy_run(a.st, 0, a.out0, (uint64_t)a.d_total[0] - a.n_staged, a.n_staged);
+  for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
+    const uint32_t cnt = a.ch.cnt[c];
+    if (cnt == 0) continue;
+    const CMsgs& src = a.ch.arena(c);
+    const uint32_t off = a.ch.off[c];
+    for (uint32_t d = tid; d < nd; d += kThreads) s_run[d] = 0;
+    for (uint32_t sub = 0; sub < cnt; sub += kTile) {
+      for (int i = tid; i < kWaves * kRadix; i += kThreads) (&whist[0][0])[i] = 0;
+      __syncthreads();
+      const uint32_t wbase = sub + w * (kIpt * kWave);
+      uint32_t k[kIpt], sv[kIpt], pv[kIpt], rk[kIpt];
+#pragma unroll
+      for (int r = 0; r < kIpt; ++r) {
+        const uint32_t q = wbase + r * kWave + lane;
+        if (q < cnt) {
+          k[r] = src.key[off + q];
+          sv[r] = src.src[off + q];
+          pv[r] = src.pay[off + q];
+        } else {
+          k[r] = 0xFFFFFFFFu;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kIpt; ++r) {
+        const uint32_t q = wbase + r * kWave + lane;
+        rk[r] = wave_rank(q < cnt, (k[r] >> a.shift) & mask, a.bits, whist[w], ltm);
+      }
+      __syncthreads();
+      uint32_t cd[kRadix / kThreads];
+#pragma unroll
+      for (int j = 0; j < kRadix / kThreads; ++j) {
+        const uint32_t d = tid + j * kThreads;
+        uint32_t run = 0;
+#pragma unroll
+        for (int q = 0; q < kWaves; ++q) {
+          const uint32_t c2 = whist[q][d];
+          whist[q][d] = run;
+          run += c2;
+        }
+        cd[j] = d < nd ? run : 0u;
+      }
+      // tile-local digit bases (scan over 512 digits: 2 per thread, blocked)
+      uint32_t t2;
+      {  // digits tid and tid+256 are in cd[0], cd[1]; exclusive scan over digits, 2 per thread (blocked)
+        const uint32_t e0 = tid * 2, e1 = tid * 2 + 1;
+        s_ldig[tid] = cd[0];
+        s_ldig[tid + kThreads] = cd[1];
+        __syncthreads();
+        const uint32_t v0 = s_ldig[e0], v1 = s_ldig[e1];
+        __syncthreads();
+        const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, scratch, &t2);
+        s_ldig[e0] = ex;
+        s_ldig[e1] = ex + v0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kRadix / kThreads; ++j) {
+        const uint32_t d = tid + j * kThreads;
+        if (d < nd) {
+          s_gadj[d] = s_dbase[d] + a.hist[(size_t)d * a.stride + c] + s_run[d] - s_ldig[d];
+          s_run[d] += cd[j];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kIpt; ++r) {
+        const uint32_t q = wbase + r * kWave + lane;
+        if (q < cnt) {
+          const uint32_t d = (k[r] >> a.shift) & mask;
+          const uint32_t lp = s_ldig[d] + whist[w][d] + rk[r];
+          s_key[lp] = k[r];
+          s_src[lp] = sv[r];
+          s_pay[lp] = pv[r];
+        }
+      }
+      __syncthreads();
+      const uint32_t nsub = min((uint32_t)kTile, cnt - sub);
+      for (uint32_t lp = tid; lp < nsub; lp += kThreads) {
+        const uint32_t kk = s_key[lp];
+        const uint32_t g = s_gadj[(kk >> a.shift) & mask] + lp;
+        a.out.key[g] = kk;
+        a.out.src[g] = s_src[lp];
+        a.out.pay[g] = s_pay[lp];
+      }
+      __syncthreads();
     }
   }
 }
 
 // =========================================================================
-// Stable LSD radix sort pass over `bits` bits at `shift` (bits <= 8).
-//   upsweep:   per-tile digit histogram -> hist[d * stride + t]
-//   rowscan:   per digit, exclusive scan over tiles; tot[d] = digit total
-//   downsweep: wave-level multisplit (ballot match) ranks, LDS staging,
-//              coalesced scatter to the output
+// Dense radix pass (reduce-then-scan): upsweep / rowscan / downsweep
 // =========================================================================
 struct SortArgs {
   CMsgs in;
   Msgs out;
   const uint32_t* d_n;
-  uint32_t* hist;
+  uint32_t* hist;  // digit-major [nbins][stride]
   uint32_t* tot;
-  uint32_t stride;  // >= max tiles
+  uint32_t* bstart;  // out (block 0 of the downsweep): exclusive scan of digit totals
+  uint32_t stride;
   uint32_t shift, bits;
 };
 
-__global__ void __launch_bounds__(kSortThreads) k_sort_upsweep(SortArgs a) {
-  __shared__ uint32_t h[kSortWaves][kRadix];
-  const uint32_t n = *a.d_n, nt = div_up(n, kSortTile);
+__global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
+  __shared__ uint32_t h[kWaves][kRadix];
+  const uint32_t n = *a.d_n, nt = div_up(n, kTile);
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t mask = (1u << a.bits) - 1u, nd = 1u << a.bits;
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    for (int i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&h[0][0])[i] = 0;
+    for (int i = tid; i < kWaves * kRadix; i += kThreads) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t base = t * kSortTile;
-    if (base + kSortTile <= n) {
+    const uint32_t base = t * kTile;
+    if (base + kTile <= n) {
       const uint4* k4 = reinterpret_cast<const uint4*>(a.in.key + base);
 #pragma unroll
-      for (int j = 0; j < kSortIpt / 4; ++j) {
-        uint4 v = k4[j * kSortThreads + tid];
+      for (int j = 0; j < kIpt / 4; ++j) {
+        uint4 v = k4[j * kThreads + tid];
         atomicAdd(&h[w][(v.x >> a.shift) & mask], 1u);
         atomicAdd(&h[w][(v.y >> a.shift) & mask], 1u);
         atomicAdd(&h[w][(v.z >> a.shift) & mask], 1u);
         atomicAdd(&h[w][(v.w >> a.shift) & mask], 1u);
       }
     } else {
-      for (uint32_t i = base + tid; i < n; i += kSortThreads) atomicAdd(&h[w][(a.in.key[i] >> a.shift) & mask], 1u);
+      for (uint32_t i = base + tid; i < n; i += kThreads) atomicAdd(&h[w][(a.in.key[i] >> a.shift) & mask], 1u);
     }
     __syncthreads();
-    for (uint32_t d = tid; d < nd; d += kSortThreads) {
+    for (uint32_t d = tid; d < nd; d += kThreads) {
       uint32_t s = 0;
 #pragma unroll
-      for (int q = 0; q < kSortWaves; ++q) s += h[q][d];
-      a.hist[d * a.stride + t] = s;
+      for (int q = 0; q < kWaves; ++q) s += h[q][d];
+      a.hist[(size_t)d * a.stride + t] = s;
     }
     __syncthreads();
   }
 }
 
-__global__ void __launch_bounds__(256) k_sort_rowscan(SortArgs a) {
-  __shared__ uint32_t scratch[256 / kWave + 1];
+__global__ void __launch_bounds__(kThreads) k_sort_rowscan(SortArgs a) {
+  __shared__ uint32_t scratch[kWaves + 1];
   __shared__ uint32_t s_run;
-  const uint32_t n = *a.d_n, nt = div_up(n, kSortTile);
-  const uint32_t d = blockIdx.x;  // one block per digit
+  const uint32_t n = *a.d_n, nt = div_up(n, kTile);
+  const uint32_t d = blockIdx.x;
   if (d >= (1u << a.bits)) return;
   uint32_t* row = a.hist + (size_t)d * a.stride;
   if (threadIdx.x == 0) s_run = 0;
   __syncthreads();
-  for (uint32_t base = 0; base < nt; base += 256) {
+  for (uint32_t base = 0; base < nt; base += kThreads) {
     uint32_t i = base + threadIdx.x;
-    uint32_t v = i < nt ? row[i] : 0u, tot;
-    uint32_t ex = block_excl_sum<256>(v, scratch, &tot);
+    uint32_t v = i < nt ? row[i] : 0u, t;
+    uint32_t ex = block_excl_sum<kThreads>(v, scratch, &t);
     if (i < nt) row[i] = s_run + ex;
     __syncthreads();
-    if (threadIdx.x == 0) s_run += tot;
+    if (threadIdx.x == 0) s_run += t;
     __syncthreads();
   }
   if (threadIdx.x == 0) a.tot[d] = s_run;
 }
 
-__global__ void __launch_bounds__(kSortThreads) k_sort_downsweep(SortArgs a) {
-  __shared__ uint32_t whist[kSortWaves][kRadix];
-  __shared__ uint32_t s_dbase[kRadix];  // exclusive scan of digit totals
-  __shared__ uint32_t s_ldig[kRadix];   // tile-local digit base
-  __shared__ uint32_t s_gadj[kRadix];   // global pos = s_gadj[d] + local pos
-  __shared__ uint32_t scratch[kSortThreads / kWave + 1];
-  __shared__ uint32_t s_key[kSortTile], s_src[kSortTile], s_pay[kSortTile];
+__global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) {
+  __shared__ uint32_t whist[kWaves][kRadix];
+  __shared__ uint32_t s_dbase[kRadix];
+  __shared__ uint32_t s_ldig[kRadix];
+  __shared__ uint32_t s_gadj[kRadix];
+  __shared__ uint32_t scratch[kWaves + 1];
+  __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
 
-  const uint32_t n = *a.d_n, nt = div_up(n, kSortTile);
+  const uint32_t n = *a.d_n, nt = div_up(n, kTile);
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t lane = lane_id();
   const uint32_t mask = (1u << a.bits) - 1u, nd = 1u << a.bits;
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-
-  if (nt == 0) return;
-  {  // digit bases (same for all tiles)
-    uint32_t v = (uint32_t)tid < nd ? a.tot[tid] : 0u, tot;
-    uint32_t ex = block_excl_sum<kSortThreads>(v, scratch, &tot);
-    if ((uint32_t)tid < nd) s_dbase[tid] = ex;
+  const uint64_t ltm = lanemask_lt();
+  for (uint32_t d = tid; d < kRadix; d += kThreads) s_dbase[d] = d < nd ? a.tot[d] : 0u;
+  __syncthreads();
+  {
+    const uint32_t v0 = s_dbase[2 * tid], v1 = s_dbase[2 * tid + 1];
+    uint32_t t;
+    __syncthreads();
+    const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, scratch, &t);
+    s_dbase[2 * tid] = ex;
+    s_dbase[2 * tid + 1] = ex + v0;
+    if (blockIdx.x == 0 && tid == 0) a.bstart[nd] = t;
   }
   __syncthreads();
+  if (blockIdx.x == 0)
+    for (uint32_t d = tid; d < nd; d += kThreads) a.bstart[d] = s_dbase[d];
+  if (nt == 0) return;  // (bucket starts above are still published for an empty rank)
 
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    for (int i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&whist[0][0])[i] = 0;
+    for (int i = tid; i < kWaves * kRadix; i += kThreads) (&whist[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t base = t * kSortTile;
-    const uint32_t wbase = base + w * (kSortIpt * kWave);
-    uint32_t k[kSortIpt], s[kSortIpt], p[kSortIpt], rk[kSortIpt];
+    const uint32_t base = t * kTile;
+    const uint32_t wbase = base + w * (kIpt * kWave);
+    uint32_t k[kIpt], s[kIpt], p[kIpt], rk[kIpt];
 #pragma unroll
-    for (int r = 0; r < kSortIpt; ++r) {
-      uint32_t i = wbase + r * kWave + lane;
+    for (int r = 0; r < kIpt; ++r) {
+      const uint32_t i = wbase + r * kWave + lane;
       if (i < n) {
         k[r] = a.in.key[i];
         s[r] = a.in.src[i];
@@ -283,63 +394,59 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_downsweep(SortArgs a) {
         k[r] = 0xFFFFFFFFu;
       }
     }
-    // wave-level multisplit: rank of each item among equal digits, in item order
 #pragma unroll
-    for (int r = 0; r < kSortIpt; ++r) {
-      uint32_t i = wbase + r * kWave + lane;
-      bool valid = i < n;
-      uint32_t d = (k[r] >> a.shift) & mask;
-      uint64_t m = __ballot(valid);
-      for (uint32_t b = 0; b < a.bits; ++b) {
-        uint32_t bit = (d >> b) & 1u;
-        uint64_t bal = __ballot(bit);
-        m &= bit ? bal : ~bal;
-      }
-      uint32_t before = (uint32_t)__popcll(m & lt_mask);
-      uint32_t cnt = (uint32_t)__popcll(m);
-      uint32_t old = 0;
-      if (valid) old = whist[w][d];
-      __builtin_amdgcn_wave_barrier();
-      if (valid && before == 0) whist[w][d] = old + cnt;
-      __builtin_amdgcn_wave_barrier();
-      rk[r] = old + before;
+    for (int r = 0; r < kIpt; ++r) {
+      const uint32_t i = wbase + r * kWave + lane;
+      rk[r] = wave_rank(i < n, (k[r] >> a.shift) & mask, a.bits, whist[w], ltm);
     }
     __syncthreads();
-    // per digit: wave prefixes, tile count; tile-local digit base
-    uint32_t cnt_d = 0;
-    if ((uint32_t)tid < nd) {
+    uint32_t cd[kRadix / kThreads];
+#pragma unroll
+    for (int j = 0; j < kRadix / kThreads; ++j) {
+      const uint32_t d = tid + j * kThreads;
       uint32_t run = 0;
 #pragma unroll
-      for (int q = 0; q < kSortWaves; ++q) {
-        uint32_t c = whist[q][tid];
-        whist[q][tid] = run;
-        run += c;
+      for (int q = 0; q < kWaves; ++q) {
+        const uint32_t c2 = whist[q][d];
+        whist[q][d] = run;
+        run += c2;
       }
-      cnt_d = run;
+      cd[j] = d < nd ? run : 0u;
     }
-    uint32_t tot;
-    uint32_t lex = block_excl_sum<kSortThreads>(cnt_d, scratch, &tot);
-    if ((uint32_t)tid < nd) {
-      s_ldig[tid] = lex;
-      s_gadj[tid] = s_dbase[tid] + a.hist[tid * a.stride + t] - lex;
+    s_ldig[tid] = cd[0];
+    s_ldig[tid + kThreads] = cd[1];
+    __syncthreads();
+    {
+      const uint32_t v0 = s_ldig[2 * tid], v1 = s_ldig[2 * tid + 1];
+      __syncthreads();
+      uint32_t t2;
+      const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, scratch, &t2);
+      s_ldig[2 * tid] = ex;
+      s_ldig[2 * tid + 1] = ex + v0;
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kSortIpt; ++r) {
-      uint32_t i = wbase + r * kWave + lane;
+    for (int j = 0; j < kRadix / kThreads; ++j) {
+      const uint32_t d = tid + j * kThreads;
+      if (d < nd) s_gadj[d] = s_dbase[d] + a.hist[(size_t)d * a.stride + t] - s_ldig[d];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kIpt; ++r) {
+      const uint32_t i = wbase + r * kWave + lane;
       if (i < n) {
-        uint32_t d = (k[r] >> a.shift) & mask;
-        uint32_t lp = s_ldig[d] + whist[w][d] + rk[r];
+        const uint32_t d = (k[r] >> a.shift) & mask;
+        const uint32_t lp = s_ldig[d] + whist[w][d] + rk[r];
         s_key[lp] = k[r];
         s_src[lp] = s[r];
         s_pay[lp] = p[r];
       }
     }
     __syncthreads();
-    const uint32_t cnt_tile = min((uint32_t)kSortTile, n - base);
-    for (uint32_t lp = tid; lp < cnt_tile; lp += kSortThreads) {
-      uint32_t kk = s_key[lp];
-      uint32_t g = s_gadj[(kk >> a.shift) & mask] + lp;
+    const uint32_t cnt_tile = min((uint32_t)kTile, n - base);
+    for (uint32_t lp = tid; lp < cnt_tile; lp += kThreads) {
+      const uint32_t kk = s_key[lp];
+      const uint32_t g = s_gadj[(kk >> a.shift) & mask] + lp;
       a.out.key[g] = kk;
       a.out.src[g] = s_src[lp];
       a.out.pay[g] = s_pay[lp];
@@ -349,44 +456,8 @@ __global__ void __launch_bounds__(kSortThreads) k_sort_downsweep(SortArgs a) {
 }
 
 // =========================================================================
-// Segmented drain + behaviour-apply.
-// Input: envelopes sorted by key (stable).  For item i of actor a's segment,
-// p = position in the segment (backlog first, then arrivals in canonical
-// order).  Classification (Mailbox.scala:260-277, 551-565):
-//   !alive               -> dead letter
-//   p <  T               -> drained: invoked in order by the segment head thread
-//   T <= p < C (or C=0)  -> stays queued (backlog chunk)
-//   p >= C               -> dead letter (bounded tail-drop)
+// Bucket apply: in-bucket sort + segmented drain + behaviour + emission
 // =========================================================================
-struct ApplyArgs {
-  DevParams P;
-  CMsgs in;
-  const uint32_t* d_n;
-  Msgs bl;    // backlog chunks (tile * kApplyTile)
-  Msgs em;    // emission chunks, bump-allocated: chunk t at base_em[t]
-  uint32_t* cnt_bl;
-  uint32_t* cnt_em;
-  uint32_t* base_em;
-  uint32_t* d_bump;
-  uint64_t cap_em;   // capacity of the emission buffer
-  uint64_t* stats;
-};
-
-// first index of the run of `kb` that ends at `hi` (keys sorted; keys[hi] == kb)
-__device__ __forceinline__ uint32_t run_start(const uint32_t* keys, uint32_t hi, uint32_t kb) {
-  uint32_t step = 1;
-  while (hi >= step && keys[hi - step] == kb) {
-    hi -= step;
-    step <<= 1;
-  }
-  uint32_t lo = hi >= step ? hi - step + 1 : 0;  // keys[lo-1] != kb (or lo == 0)
-  while (lo < hi) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (keys[mid] == kb) hi = mid; else lo = mid + 1;
-  }
-  return hi;
-}
-
 template <bool kWrite>
 struct Emitter {
   const DevParams* P;
@@ -395,212 +466,543 @@ struct Emitter {
   uint32_t self;      // sender id (global)
   uint32_t n_valid;   // tells to a known actor
   uint32_t n_all;     // all tells
+  uint32_t* nh;       // next-pass digit histogram (LDS)
+  uint32_t nh_shift, nh_mask;
   __device__ __forceinline__ void operator()(uint32_t dst, uint32_t pay) {
     ++n_all;
     if (dst >= P->n_global) return;  // unknown ref -> deadLetters
     ++n_valid;
     if (kWrite) {
-      uint32_t key = (P->R > 1) ? P->route[dst] : dst;
+      const uint32_t key = (P->R > 1) ? P->route[dst] : dst;
       out.key[pos] = key;
       out.src[pos] = self;
       out.pay[pos] = pay;
       ++pos;
+      atomicAdd(&nh[((key & kLocalMask) >> nh_shift) & nh_mask], 1u);
     }
   }
 };
 
-__global__ void __launch_bounds__(kApplyThreads) k_apply(ApplyArgs a) {
-  __shared__ uint32_t s_lastkey[kApplyThreads];
-  __shared__ int s_maxscratch[kApplyThreads / kWave + 1];
-  __shared__ uint32_t s_scratch[kApplyThreads / kWave + 1];
-  __shared__ uint32_t s_carry;
-  __shared__ uint32_t s_ebase;
-  __shared__ unsigned long long s_stat[5];
+constexpr int kBThreads = 512;                 // bucket_apply block: 8 waves
+constexpr int kBWaves = kBThreads / kWave;
+constexpr int kBIpt = kBucket / kBThreads;      // items per thread per sub-tile (4)
+constexpr int kBAct = kBucket / kBThreads;      // actors per thread (4)
+constexpr int kStagedChunks = 256;              // host-staged tells are split over this many chunks
 
+struct BucketArgs {
+  DevParams P;
+  CMsgs in;                // mail sorted by bucket (local key >> kBucketBits)
+  const uint32_t* d_n;
+  const uint32_t* bstart;  // single_pass: bucket starts [nb + 1]
+  Msgs scr;                // general path: bucket-local sorted copy (index space of `in`)
+  Msgs bl, em;             // chunk arenas: backlog of bucket b at [lo, lo+cnt), tells at [lo*kmax, (lo+cnt)*kmax)
+  uint32_t* chunk_off;
+  uint32_t* chunk_cnt;
+  uint32_t* nhist;         // next step's first-pass histogram, digit-major [nbins][nhist_stride]
+  uint32_t nhist_stride, nx_shift, nx_bits;
+  uint32_t nb, single_pass, kmax;
+  uint64_t* stats;
+};
+
+// 64-ary lower bound by one wave: first index i in [0, n) with ((key[i] & local) >> sh) >= target
+__device__ __forceinline__ uint32_t wave_lower_bound(const uint32_t* key, uint32_t n, uint32_t sh, uint32_t target) {
+  uint32_t lo = 0, hi = n;  // answer in [lo, hi]
+  const uint32_t lane = lane_id();
+  while (hi - lo > 64) {
+    const uint32_t step = div_up(hi - lo, 64);
+    const uint32_t probe = lo + lane * step;  // lane 0 probes lo
+    const bool ge = probe < hi ? (((key[probe] & kLocalMask) >> sh) >= target) : true;
+    const uint64_t m = __ballot(ge);
+    const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;  // first lane with key >= target
+    const uint32_t nlo = first == 0 ? lo : lo + (first - 1) * step;
+    const uint32_t nhi = first >= 64 ? hi : min(hi, lo + first * step);
+    lo = nlo;
+    hi = nhi;
+  }
+  const uint32_t probe = lo + lane;
+  const bool ge = probe < hi ? (((key[probe] & kLocalMask) >> sh) >= target) : true;
+  const uint64_t m = __ballot(ge);
+  return m ? lo + (uint32_t)__builtin_ctzll(m) : hi;
+}
+
+struct BucketLds {
+  uint32_t* key;   // fast path: sorted items (LDS); general path: run / tmp scratch
+  uint32_t* src;
+  uint32_t* pay;
+  uint64_t* U;     // time-shared: whist (u16 [kBWaves][kBucket]) / blpre (u32) / w0,w1 (u64)
+  uint32_t* seg;   // [kBucket + 4] segment starts
+  uint32_t* ecnt;  // [kBucket] emission counts -> offsets
+  uint8_t* alive;
+  uint8_t* kind;
+  uint32_t* nh;    // [kRadix]
+  uint32_t* scratch;
+  unsigned long long* stat;
+};
+
+// After the in-bucket sort: classification, queued copy, behaviour apply, emission.
+// kLds: sorted items are in LDS (fast path) or in the global scratch copy.
+template <bool kLds>
+__device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t lo,
+                                              uint32_t cnt, uint32_t a0, uint32_t na) {
   const DevParams& P = a.P;
-  const uint32_t n = *a.d_n, nt = div_up(n, kApplyTile);
   const int tid = threadIdx.x;
   const uint32_t T = P.T, C = P.C;
-  if (blockIdx.x == 0 && tid == 0 && n > 0) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
+  const uint32_t nhmask = (1u << a.nx_bits) - 1u;
+  auto ikey = [&](uint32_t q) -> uint32_t { return kLds ? L.key[q] : a.scr.key[lo + q]; };
+  auto isrc = [&](uint32_t q) -> uint32_t { return kLds ? L.src[q] : a.scr.src[lo + q]; };
+  auto ipay = [&](uint32_t q) -> uint32_t { return kLds ? L.pay[q] : a.scr.pay[lo + q]; };
+  uint32_t* blpre = reinterpret_cast<uint32_t*>(L.U);
+  uint64_t* w0s = L.U;
+  uint64_t* w1s = L.U + kBucket;
 
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    const uint32_t base = t * kApplyTile;
-    const uint32_t i0 = base + tid * kApplyIpt;
-    if (tid < 5) s_stat[tid] = 0;
-    uint32_t k[kApplyIpt];
-    if (i0 + kApplyIpt <= n) {
-      const uint4* k4 = reinterpret_cast<const uint4*>(a.in.key + i0);
-      uint4 v0 = k4[0], v1 = k4[1];
-      k[0] = v0.x; k[1] = v0.y; k[2] = v0.z; k[3] = v0.w;
-      k[4] = v1.x; k[5] = v1.y; k[6] = v1.z; k[7] = v1.w;
-    } else {
+  // ---- classification per actor (blocked): drained / queued (backlog) / dead letters
+  uint32_t nbl_t = 0, ndead = 0, blc[kBAct];
 #pragma unroll
-      for (int j = 0; j < kApplyIpt; ++j) k[j] = (i0 + j < n) ? a.in.key[i0 + j] : 0xFFFFFFFFu;
+  for (int j = 0; j < kBAct; ++j) {
+    const uint32_t la = tid * kBAct + j;
+    const uint32_t len = L.seg[la + 1] - L.seg[la];
+    uint32_t q = 0;
+    if (len) {
+      if (!L.alive[la]) {
+        ndead += len;
+      } else {
+        const uint32_t keep = (C == 0 || len < C) ? len : C;  // admitted (tail-drop beyond C)
+        ndead += len - keep;
+        q = keep > T ? keep - T : 0u;
+      }
     }
-    s_lastkey[tid] = k[kApplyIpt - 1];
-    if (tid == 0) {
-      // segment start carried into this tile (galloping search backwards)
-      uint32_t kb = a.in.key[base];
-      s_carry = (base > 0 && a.in.key[base - 1] == kb) ? run_start(a.in.key, base, kb) : base;
+    blc[j] = q;
+    nbl_t += q;
+  }
+  uint32_t bltot;
+  uint32_t blex = block_excl_sum<kBThreads>(nbl_t, L.scratch, &bltot);
+  if (tid == 0) {
+    a.chunk_off[b] = lo;
+    a.chunk_cnt[b] = bltot;
+  }
+  if (bltot) {
+#pragma unroll
+    for (int j = 0; j < kBAct; ++j) {
+      blpre[tid * kBAct + j] = blex;
+      blex += blc[j];
     }
     __syncthreads();
-    uint32_t prevk = tid > 0 ? s_lastkey[tid - 1] : (base > 0 ? a.in.key[base - 1] : 0xFFFFFFFEu);
-    // head flags + running last-head index inside the thread
-    int hs[kApplyIpt];
-    int lh = -1;
-    uint32_t headmask = 0;
-#pragma unroll
-    for (int j = 0; j < kApplyIpt; ++j) {
-      uint32_t i = i0 + j;
-      bool head = i < n && (i == 0 || k[j] != (j == 0 ? prevk : k[j - 1]));
-      if (head) { lh = (int)i; headmask |= 1u << j; }
-      hs[j] = lh;
+    for (uint32_t q = tid; q < cnt; q += kBThreads) {  // queued messages, in actor order
+      const uint32_t key = ikey(q);
+      const uint32_t la = key & (kBucket - 1);
+      const uint32_t p = q - L.seg[la];
+      const uint32_t len = L.seg[la + 1] - L.seg[la];
+      const uint32_t keep = (C == 0 || len < C) ? len : C;
+      if (L.alive[la] && p >= T && p < keep) {
+        const uint32_t o = lo + blpre[la] + (p - T);
+        a.bl.key[o] = key;
+        a.bl.src[o] = isrc(q);
+        a.bl.pay[o] = ipay(q);
+      }
     }
-    int carry = block_excl_max<kApplyThreads>(lh, s_maxscratch);
-    if (carry < 0) carry = (int)s_carry;
+    if (tid == 0) {  // all queued mail is in this bucket: one bin of the next first-pass histogram
+      const uint32_t d = ((b << kBucketBits) >> a.nx_shift) & nhmask;
+      a.nhist[(size_t)d * a.nhist_stride + b] = bltot;
+    }
+  }
+  __syncthreads();
 
-    // classify items; backlog compaction
-    uint32_t nbl = 0, ndead = 0;
-    uint32_t blmask = 0;
-    uint8_t al[kApplyIpt];
+  // ---- prefetch kind + state words 0/1 of actors with mail (striped: coalesced)
 #pragma unroll
-    for (int j = 0; j < kApplyIpt; ++j) {
-      uint32_t i = i0 + j;
-      al[j] = 0;
-      if (i >= n) continue;
-      uint32_t ss = hs[j] >= 0 ? (uint32_t)hs[j] : (uint32_t)carry;
-      uint32_t p = i - ss;
-      uint32_t l = k[j] & kLocalMask;
-      al[j] = P.alive[l];
-      if (!al[j]) { ++ndead; continue; }
-      if (p < T) continue;  // drained by the head thread
-      if (C == 0 || p < C) { blmask |= 1u << j; ++nbl; } else ++ndead;
+  for (int j = 0; j < kBAct; ++j) {
+    const uint32_t la = j * kBThreads + tid;
+    L.ecnt[la] = 0;
+    if (la < na && L.alive[la] && L.seg[la + 1] != L.seg[la]) {
+      const uint32_t l = a0 + la;
+      L.kind[la] = P.kind[l];
+      w0s[la] = P.state[l];
+      w1s[la] = P.W > 1 ? P.state[(size_t)P.n_local + l] : 0ull;
     }
-    uint32_t bltot;
-    uint32_t bloff = block_excl_sum<kApplyThreads>(nbl, s_scratch, &bltot);
-    if (blmask) {
-      const size_t ob = (size_t)t * kApplyTile + bloff;
-      uint32_t q = 0;
-#pragma unroll
-      for (int j = 0; j < kApplyIpt; ++j)
-        if (blmask & (1u << j)) {
-          uint32_t i = i0 + j;
-          a.bl.key[ob + q] = k[j];
-          a.bl.src[ob + q] = a.in.src[i];
-          a.bl.pay[ob + q] = a.in.pay[i];
-          ++q;
-        }
-    }
-    if (tid == 0) a.cnt_bl[t] = bltot;
-
-    // ---- phase A: count emissions of the segments headed in this thread
-    uint32_t nem = 0;
+  }
+  // ---- phase A: emissions per actor (drain min(len, T) messages in order)
+#pragma unroll 1
+  for (int j = 0; j < kBAct; ++j) {
+    const uint32_t la = j * kBThreads + tid;
+    const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
+    if (la >= na || !len || !L.alive[la]) continue;
+    const uint32_t l = a0 + la;
+    const uint32_t self = P.R > 1 ? P.gid[l] : l;
+    Emitter<false> em{&P, {}, 0, self, 0, 0, L.nh, a.nx_shift, nhmask};
     uint64_t wv[AGX_MAX_WORDS];
-    if (headmask) {
+    wv[0] = w0s[la];
+    wv[1] = w1s[la];
 #pragma unroll
-      for (int j = 0; j < kApplyIpt; ++j) {
-        if (!(headmask & (1u << j)) || !al[j]) continue;
-        const uint32_t i = i0 + j, kb = k[j], l = kb & kLocalMask;
-        const uint32_t self = P.R > 1 ? P.gid[l] : l;
-        const uint32_t kind = P.kind[l];
+    for (int q = 2; q < (int)AGX_MAX_WORDS; ++q) wv[q] = (q < (int)P.W) ? P.state[(size_t)q * P.n_local + l] : 0ull;
+    const uint32_t nd = min(len, T);
+    for (uint32_t q = 0; q < nd; ++q) {
+      const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, isrc(s0 + q), ipay(s0 + q), em);
+      if (r == AGX_RES_STOPPED) break;
+    }
+    L.ecnt[la] = em.n_valid;
+  }
+  __syncthreads();
+  // ---- exclusive scan of emission counts in actor (= sender) order
+  uint32_t emtot;
+  {
+    uint32_t ec[kBAct], run = 0;
+    const uint4 v = reinterpret_cast<const uint4*>(L.ecnt)[tid];
+    ec[0] = v.x; ec[1] = v.y; ec[2] = v.z; ec[3] = v.w;
 #pragma unroll
-        for (int q = 0; q < (int)AGX_MAX_WORDS; ++q) wv[q] = (q < (int)P.W) ? P.state[(size_t)q * P.n_local + l] : 0ull;
-        Emitter<false> em{&P, {}, 0, self, 0, 0};
-        for (uint32_t q = 0; q < T; ++q) {
-          uint32_t ii = i + q;
-          if (ii >= n || (q > 0 && a.in.key[ii] != kb)) break;
-          uint32_t r = apply_msg(P, kind, self, l, wv, a.in.src[ii], a.in.pay[ii], em);
-          if (r == AGX_RES_STOPPED) break;
-        }
-        nem += em.n_valid;
-      }
+    for (int j = 0; j < kBAct; ++j) run += ec[j];
+    uint32_t ex = block_excl_sum<kBThreads>(run, L.scratch, &emtot);
+    uint32_t o[kBAct];
+#pragma unroll
+    for (int j = 0; j < kBAct; ++j) {
+      o[j] = ex;
+      ex += ec[j];
     }
-    uint32_t emtot;
-    uint32_t emoff = block_excl_sum<kApplyThreads>(nem, s_scratch, &emtot);
-    if (tid == 0) {
-      uint32_t b = emtot ? atomicAdd(a.d_bump, emtot) : 0u;
-      if ((uint64_t)b + emtot > a.cap_em) {  // out of emission capacity: abort the run
-        atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
-        emtot = 0;
-        b = 0xFFFFFFFFu;
-      }
-      a.cnt_em[t] = emtot;
-      a.base_em[t] = b;
-      s_ebase = b;
-    }
-    __syncthreads();
-    const uint32_t ebase = s_ebase;
+    reinterpret_cast<uint4*>(L.ecnt)[tid] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  const uint64_t embase = (uint64_t)lo * a.kmax;  // this bucket's slice of the tell arena
+  if (tid == 0) {
+    a.chunk_off[a.nb + b] = (uint32_t)embase;
+    a.chunk_cnt[a.nb + b] = emtot;
+  }
+  __syncthreads();
 
-    // ---- phase B: apply for real, write emissions and state
-    uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0;
-    if (headmask && ebase != 0xFFFFFFFFu) {
-      Emitter<true> em{&P, a.em, (uint64_t)ebase + emoff, 0, 0, 0};
+  // ---- phase B: apply for real, write tells (sender order) and state
+  uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0;
+#pragma unroll 1
+  for (int j = 0; j < kBAct; ++j) {
+    const uint32_t la = j * kBThreads + tid;
+    const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
+    if (la >= na || !len || !L.alive[la]) continue;
+    const uint32_t l = a0 + la;
+    const uint32_t self = P.R > 1 ? P.gid[l] : l;
+    Emitter<true> em{&P, a.em, embase + L.ecnt[la], self, 0, 0, L.nh, a.nx_shift, nhmask};
+    uint64_t wv[AGX_MAX_WORDS];
+    wv[0] = w0s[la];
+    wv[1] = w1s[la];
 #pragma unroll
-      for (int j = 0; j < kApplyIpt; ++j) {
-        if (!(headmask & (1u << j)) || !al[j]) continue;
-        const uint32_t i = i0 + j, kb = k[j], l = kb & kLocalMask;
-        const uint32_t self = P.R > 1 ? P.gid[l] : l;
-        const uint32_t kind = P.kind[l];
-        em.self = self;
-        ++nact;
+    for (int q = 2; q < (int)AGX_MAX_WORDS; ++q) wv[q] = (q < (int)P.W) ? P.state[(size_t)q * P.n_local + l] : 0ull;
+    const uint32_t nd = min(len, T);
+    ++nact;
+    for (uint32_t q = 0; q < nd; ++q) {
+      const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, isrc(s0 + q), ipay(s0 + q), em);
+      ++ndel;
+      if (r == AGX_RES_UNHANDLED) ++nunh;
+      if (r == AGX_RES_STOPPED) {
+        P.stopq[atomicAdd(P.nstop, 1u)] = l;
+        ndead += nd - q - 1;  // drained-but-unprocessed after the stop
+        break;
+      }
+    }
 #pragma unroll
-        for (int q = 0; q < (int)AGX_MAX_WORDS; ++q) wv[q] = (q < (int)P.W) ? P.state[(size_t)q * P.n_local + l] : 0ull;
-        uint32_t nd = 0;
-        for (uint32_t q = 0; q < T; ++q) {
-          uint32_t ii = i + q;
-          if (ii >= n || (q > 0 && a.in.key[ii] != kb)) break;
-          ++nd;
+    for (int q = 0; q < (int)AGX_MAX_WORDS; ++q)
+      if (q < (int)P.W) P.state[(size_t)q * P.n_local + l] = wv[q];
+    nall += em.n_all;
+    ndead += em.n_all - em.n_valid;
+  }
+  __syncthreads();
+  // next first-pass histogram column of this bucket's tell chunk (zeroed by the host memset)
+  for (uint32_t d = tid; d < (1u << a.nx_bits); d += kBThreads)
+    if (L.nh[d]) a.nhist[(size_t)d * a.nhist_stride + a.nb + b] = L.nh[d];
+  // block stats -> global
+  const uint32_t lane = lane_id();
+  uint32_t v0 = wave_incl_sum(ndel), v1 = wave_incl_sum(ndead), v2 = wave_incl_sum(nunh), v3 = wave_incl_sum(nall),
+           v4 = wave_incl_sum(nact);
+  if (lane == kWave - 1) {
+    atomicAdd(&L.stat[0], (unsigned long long)v0);
+    atomicAdd(&L.stat[1], (unsigned long long)v1);
+    atomicAdd(&L.stat[2], (unsigned long long)v2);
+    atomicAdd(&L.stat[3], (unsigned long long)v3);
+    atomicAdd(&L.stat[4], (unsigned long long)v4);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (L.stat[0]) atomicAdd((unsigned long long*)&a.stats[ST_DELIVERED], L.stat[0]);
+    if (L.stat[1]) atomicAdd((unsigned long long*)&a.stats[ST_DEAD], L.stat[1]);
+    if (L.stat[2]) atomicAdd((unsigned long long*)&a.stats[ST_UNHANDLED], L.stat[2]);
+    if (L.stat[3]) atomicAdd((unsigned long long*)&a.stats[ST_EMITTED], L.stat[3]);
+    if (L.stat[4]) atomicAdd((unsigned long long*)&a.stats[ST_ACTIVE], L.stat[4]);
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_key[kBucket];
+  __shared__ __attribute__((aligned(16))) uint32_t s_src[kBucket];
+  __shared__ __attribute__((aligned(16))) uint32_t s_pay[kBucket];
+  __shared__ __attribute__((aligned(16))) uint64_t U[2 * kBucket];  // 32 KB
+  __shared__ __attribute__((aligned(16))) uint32_t s_seg[kBucket + 4];
+  __shared__ __attribute__((aligned(16))) uint32_t s_ecnt[kBucket];
+  __shared__ uint8_t s_alive[kBucket];
+  __shared__ uint8_t s_kind[kBucket];
+  __shared__ uint32_t s_nh[kRadix];
+  __shared__ uint32_t scratch[kBWaves + 1];
+  __shared__ uint32_t s_lo, s_hi;
+  __shared__ unsigned long long s_stat[5];
+  const BucketLds L{s_key, s_src, s_pay, U, s_seg, s_ecnt, s_alive, s_kind, s_nh, scratch, s_stat};
+  uint16_t* whist = reinterpret_cast<uint16_t*>(U);  // [kBWaves][kBucket]
+
+  const DevParams& P = a.P;
+  const int tid = threadIdx.x, w = tid / kWave;
+  const uint32_t lane = lane_id();
+  const uint64_t ltm = lanemask_lt();
+  const uint32_t n = *a.d_n;
+  if (blockIdx.x == 0) {
+    if (tid == 0 && n > 0) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
+    for (uint32_t i = tid; i < kStagedChunks; i += kBThreads) a.chunk_cnt[2 * a.nb + i] = 0;  // staged consumed
+  }
+
+  for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x) {
+    const uint32_t a0 = b << kBucketBits;
+    const uint32_t na = min((uint32_t)kBucket, P.n_local - a0);
+    if (tid < 5) s_stat[tid] = 0;
+    for (uint32_t d = tid; d < kRadix; d += kBThreads) s_nh[d] = 0;
+    if (a.single_pass) {
+      if (tid == 0) {
+        s_lo = a.bstart[b];
+        s_hi = a.bstart[b + 1];
+      }
+    } else if (w == 0) {
+      const uint32_t lo = wave_lower_bound(a.in.key, n, kBucketBits, b);
+      const uint32_t hi = wave_lower_bound(a.in.key, n, kBucketBits, b + 1);
+      if (lane == 0) {
+        s_lo = lo;
+        s_hi = hi;
+      }
+    }
+    for (uint32_t la = tid; la < kBucket; la += kBThreads) s_alive[la] = la < na ? P.alive[a0 + la] : 0;
+    __syncthreads();
+    const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
+
+    if (cnt <= (uint32_t)kBucket) {
+      // ---- fast path: the whole bucket in one LDS tile
+      uint32_t k[kBIpt], sv[kBIpt], pv[kBIpt], rk[kBIpt];
+      const uint32_t wbase = w * (kBIpt * kWave);
+#pragma unroll
+      for (int r = 0; r < kBIpt; ++r) {
+        const uint32_t q = wbase + r * kWave + lane;
+        if (q < cnt) {
+          k[r] = a.in.key[lo + q];
+          sv[r] = a.in.src[lo + q];
+          pv[r] = a.in.pay[lo + q];
+        } else {
+          k[r] = 0xFFFFFFFFu;
         }
-        for (uint32_t q = 0; q < nd; ++q) {
-          uint32_t ii = i + q;
-          uint32_t r = apply_msg(P, kind, self, l, wv, a.in.src[ii], a.in.pay[ii], em);
-          ++ndel;
-          if (r == AGX_RES_UNHANDLED) ++nunh;
-          if (r == AGX_RES_STOPPED) {
-            P.stopq[atomicAdd(P.nstop, 1u)] = l;
-            ndead += nd - q - 1;
-            break;
+      }
+      for (uint32_t i = tid; i < kBWaves * kBucket / 2; i += kBThreads) reinterpret_cast<uint32_t*>(whist)[i] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kBIpt; ++r) {
+        const uint32_t q = wbase + r * kWave + lane;
+        rk[r] = wave_rank(q < cnt, k[r] & (kBucket - 1), kBucketBits, whist + w * kBucket, ltm);
+      }
+      __syncthreads();
+      // per actor: wave prefixes in place, segment length
+      uint32_t tl[kBAct];
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        const uint32_t la = tid * kBAct + j;  // blocked (for the scan below)
+        uint32_t run = 0;
+#pragma unroll
+        for (int q = 0; q < kBWaves; ++q) {
+          const uint32_t c2 = whist[q * kBucket + la];
+          whist[q * kBucket + la] = (uint16_t)run;
+          run += c2;
+        }
+        tl[j] = run;
+      }
+      {
+        uint32_t run = 0;
+#pragma unroll
+        for (int j = 0; j < kBAct; ++j) run += tl[j];
+        uint32_t t;
+        uint32_t ex = block_excl_sum<kBThreads>(run, scratch, &t);
+#pragma unroll
+        for (int j = 0; j < kBAct; ++j) {
+          s_seg[tid * kBAct + j] = ex;
+          ex += tl[j];
+        }
+        if (tid == 0) s_seg[kBucket] = t;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kBIpt; ++r) {
+        const uint32_t q = wbase + r * kWave + lane;
+        if (q < cnt) {
+          const uint32_t la = k[r] & (kBucket - 1);
+          const uint32_t pos = s_seg[la] + whist[w * kBucket + la] + rk[r];
+          s_key[pos] = k[r];
+          s_src[pos] = sv[r];
+          s_pay[pos] = pv[r];
+        }
+      }
+      __syncthreads();
+      bucket_finish<true>(a, L, b, lo, cnt, a0, na);
+    } else {
+      // ---- general path (skewed bucket): counting sort into the global scratch copy
+      uint32_t* s_run = s_key;  // LDS items are unused on this path
+      uint32_t* s_tmp = s_src;
+      for (uint32_t i = tid; i < kBucket + 4; i += kBThreads) s_seg[i] = 0;
+      for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] = 0;
+      __syncthreads();
+      for (uint32_t q = tid; q < cnt; q += kBThreads) atomicAdd(&s_seg[a.in.key[lo + q] & (kBucket - 1)], 1u);
+      __syncthreads();
+      {
+        uint32_t v[kBAct], run = 0;
+#pragma unroll
+        for (int j = 0; j < kBAct; ++j) {
+          v[j] = s_seg[tid * kBAct + j];
+          run += v[j];
+        }
+        uint32_t t;
+        uint32_t ex = block_excl_sum<kBThreads>(run, scratch, &t);
+#pragma unroll
+        for (int j = 0; j < kBAct; ++j) {
+          s_seg[tid * kBAct + j] = ex;
+          ex += v[j];
+        }
+        if (tid == 0) s_seg[kBucket] = t;
+      }
+      for (uint32_t sub = 0; sub < cnt; sub += kBucket) {
+        for (uint32_t i = tid; i < kBWaves * kBucket / 2; i += kBThreads) reinterpret_cast<uint32_t*>(whist)[i] = 0;
+        __syncthreads();
+        const uint32_t wbase = sub + w * (kBIpt * kWave);
+        uint32_t k[kBIpt], sv[kBIpt], pv[kBIpt], rk[kBIpt];
+#pragma unroll
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t q = wbase + r * kWave + lane;
+          if (q < cnt) {
+            k[r] = a.in.key[lo + q];
+            sv[r] = a.in.src[lo + q];
+            pv[r] = a.in.pay[lo + q];
+          } else {
+            k[r] = 0xFFFFFFFFu;
           }
         }
 #pragma unroll
-        for (int q = 0; q < (int)AGX_MAX_WORDS; ++q)
-          if (q < (int)P.W) P.state[(size_t)q * P.n_local + l] = wv[q];
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t q = wbase + r * kWave + lane;
+          rk[r] = wave_rank(q < cnt, k[r] & (kBucket - 1), kBucketBits, whist + w * kBucket, ltm);
+        }
+        __syncthreads();
+        for (uint32_t la = tid; la < kBucket; la += kBThreads) {
+          uint32_t run = 0;
+#pragma unroll
+          for (int q = 0; q < kBWaves; ++q) {
+            const uint32_t c2 = whist[q * kBucket + la];
+            whist[q * kBucket + la] = (uint16_t)run;
+            run += c2;
+          }
+          s_tmp[la] = run;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t q = wbase + r * kWave + lane;
+          if (q < cnt) {
+            const uint32_t la = k[r] & (kBucket - 1);
+            const uint32_t pos = lo + s_seg[la] + s_run[la] + whist[w * kBucket + la] + rk[r];
+            a.scr.key[pos] = k[r];
+            a.scr.src[pos] = sv[r];
+            a.scr.pay[pos] = pv[r];
+          }
+        }
+        __syncthreads();
+        for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] += s_tmp[la];
+        __syncthreads();
       }
-      nall = em.n_all;
-      ndead += em.n_all - em.n_valid;
+      bucket_finish<false>(a, L, b, lo, cnt, a0, na);
     }
-    // tile stats -> global
-    uint32_t v0 = ndel, v1 = ndead, v2 = nunh, v3 = nall, v4 = nact;
-    v0 = wave_incl_sum(v0); v1 = wave_incl_sum(v1); v2 = wave_incl_sum(v2); v3 = wave_incl_sum(v3);
-    v4 = wave_incl_sum(v4);
-    if (lane_id() == kWave - 1) {
-      atomicAdd(&s_stat[0], (unsigned long long)v0);
-      atomicAdd(&s_stat[1], (unsigned long long)v1);
-      atomicAdd(&s_stat[2], (unsigned long long)v2);
-      atomicAdd(&s_stat[3], (unsigned long long)v3);
-      atomicAdd(&s_stat[4], (unsigned long long)v4);
-    }
-    __syncthreads();
-    if (tid == 0) {
-      if (s_stat[0]) atomicAdd((unsigned long long*)&a.stats[ST_DELIVERED], s_stat[0]);
-      if (s_stat[1]) atomicAdd((unsigned long long*)&a.stats[ST_DEAD], s_stat[1]);
-      if (s_stat[2]) atomicAdd((unsigned long long*)&a.stats[ST_UNHANDLED], s_stat[2]);
-      if (s_stat[3]) atomicAdd((unsigned long long*)&a.stats[ST_EMITTED], s_stat[3]);
-      if (s_stat[4]) atomicAdd((unsigned long long*)&a.stats[ST_ACTIVE], s_stat[4]);
-    }
-    __syncthreads();
   }
 }
 
-// messages still in flight after the last apply (backlog + emitted chunks)
-__global__ void __launch_bounds__(kScanThreads) k_inflight(const uint32_t* d_n, const uint32_t* cnt_bl,
-                                                           const uint32_t* cnt_em, unsigned long long* out) {
+// Histogram columns of the host-staged chunks (one block per staged chunk).
+__global__ void __launch_bounds__(kThreads) k_chunk_hist(const uint32_t* key, uint32_t n, uint32_t* hist,
+                                                         uint32_t stride, uint32_t col0, uint32_t shift, uint32_t bits,
+                                                         uint32_t* chunk_off, uint32_t* chunk_cnt) {
+  __shared__ uint32_t h[kRadix];
+  const uint32_t mask = (1u << bits) - 1u;
+  const uint32_t per = div_up(n, kStagedChunks);
+  const uint32_t c = blockIdx.x;
+  const uint32_t b0 = min(n, c * per), b1 = min(n, b0 + per);
+  for (uint32_t d = threadIdx.x; d < kRadix; d += kThreads) h[d] = 0;
+  __syncthreads();
+  for (uint32_t i = b0 + threadIdx.x; i < b1; i += kThreads) atomicAdd(&h[((key[i] & kLocalMask) >> shift) & mask], 1u);
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < (1u << bits); d += kThreads)
+    if (h[d]) hist[(size_t)d * stride + col0 + c] = h[d];
+  if (threadIdx.x == 0) {
+    chunk_off[col0 + c] = b0;
+    chunk_cnt[col0 + c] = b1 - b0;
+  }
+}
+
+// =========================================================================
+// Multi-GPU helpers: chunk list -> [backlog -> sort input front, tells -> send buffer]
+// =========================================================================
+struct McompactArgs {
+  Chunks ch;
+  Msgs out0, out1;
+  uint32_t* off0;   // [nb] destination offsets of backlog chunks
+  uint32_t* off1;   // [nb] destination offsets of tell chunks
+  uint32_t* d_total;  // [0] backlog total, [1] tell total
+  uint8_t* alive;
+  const uint32_t* stopq;
+  uint32_t* nstop;
+  uint64_t* stats;
+  uint64_t cap0, cap1;
+};
+
+__global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactArgs a) {
+  __shared__ uint32_t scratch[kScanThreads / kWave + 1];
+  __shared__ uint64_t s_run[2];
+  commit_stops(a.alive, a.stopq, a.nstop);
+  const int tid = threadIdx.x;
+  if (tid == 0) s_run[0] = s_run[1] = 0;
+  __syncthreads();
+  for (int sdx = 0; sdx < 2; ++sdx) {
+    uint32_t* off = sdx == 0 ? a.off0 : a.off1;
+    for (uint32_t base = 0; base < a.ch.nb; base += kScanThreads) {
+      const uint32_t i = base + tid;
+      uint32_t v = i < a.ch.nb ? a.ch.cnt[sdx * a.ch.nb + i] : 0u, t;
+      const uint32_t ex = block_excl_sum<kScanThreads>(v, scratch, &t);
+      if (i < a.ch.nb) off[i] = (uint32_t)(s_run[sdx] + ex);
+      __syncthreads();
+      if (tid == 0) s_run[sdx] += t;
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    const bool over = s_run[0] > a.cap0 || s_run[1] > a.cap1;
+    if (over) atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
+    a.d_total[0] = over ? 0u : (uint32_t)s_run[0];
+    a.d_total[1] = over ? 0u : (uint32_t)s_run[1];
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) k_mcompact_copy(McompactArgs a) {
+  if (a.d_total[0] == 0 && a.d_total[1] == 0) return;
+  for (uint32_t c = blockIdx.x; c < 2 * a.ch.nb; c += gridDim.x) {
+    const uint32_t n = a.ch.cnt[c];
+    if (!n) continue;
+    const CMsgs& s = a.ch.arena(c);
+    const uint32_t so = a.ch.off[c];
+    const Msgs& d = c < a.ch.nb ? a.out0 : a.out1;
+    const uint32_t dof = c < a.ch.nb ? a.off0[c] : a.off1[c - a.ch.nb];
+    for (uint32_t i = threadIdx.x; i < n; i += kThreads) {
+      d.key[dof + i] = s.key[so + i];
+      d.src[dof + i] = s.src[so + i];
+      d.pay[dof + i] = s.pay[so + i];
+    }
+  }
+}
+
+// messages in flight after the last apply = all chunk counts
+__global__ void __launch_bounds__(kScanThreads) k_inflight(const uint32_t* chunk_cnt, uint32_t nchunks,
+                                                           unsigned long long* out) {
   __shared__ unsigned long long s;
   if (threadIdx.x == 0) s = 0;
   __syncthreads();
-  const uint32_t nt = div_up(*d_n, kApplyTile);
   unsigned long long v = 0;
-  for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) v += (unsigned long long)cnt_bl[i] + cnt_em[i];
+  for (uint32_t i = threadIdx.x; i < nchunks; i += blockDim.x) v += chunk_cnt[i];
   atomicAdd(&s, v);
   __syncthreads();
   if (threadIdx.x == 0) *out = s;
@@ -610,7 +1012,7 @@ __global__ void __launch_bounds__(kScanThreads) k_inflight(const uint32_t* d_n, 
 __global__ void k_pack_counts(const uint32_t* tot, const uint32_t* d_total, uint64_t* vec, uint32_t R,
                               uint32_t n_staged) {
   uint32_t i = threadIdx.x;
-  if (i < R) vec[i] = tot[i];
+  if (i < R) vec[i] = d_total[1] ? tot[i] : 0u;
   if (i == 0) {
     vec[R] = d_total[0];  // backlog kept locally
     vec[R + 1] = n_staged;

@@ -46,11 +46,11 @@ def parse():
 def kernel_bytes_per_msg(W: int) -> dict:
     """Algorithmic HBM bytes per message for each kernel class."""
     return {
-        "apply": 12 + 12 + (16 * W + 2),      # read envelope, write emitted tell, state r/w + kind/alive
-        "sort_downsweep": 24,                # read + write one 12 B envelope (per pass)
-        "sort_upsweep": 4,                   # read key (per pass)
-        "compact_copy": 24,                  # read chunk + write dense
-        "sort_rowscan": 0, "compact_scan": 0, "exchange": 12,
+        "bucket_apply": 12 + 12 + (16 * W + 2),  # read inbox envelope, write emitted tell, state r/w + kind/alive
+        "chunk_downsweep": 24,                  # read + write one 12 B envelope (first radix pass)
+        "sort_downsweep": 24,                   # read + write one 12 B envelope (later passes)
+        "sort_upsweep": 4,                      # read key
+        "chunk_rowscan": 0, "sort_rowscan": 0, "mcompact": 24, "exchange": 12,
     }
 
 
@@ -103,7 +103,8 @@ def main():
     from akka_amd import workloads as wl
     from akka_amd.engine import EngineConfig, GpuEngine
 
-    hops = max(args.hops, args.warmup + args.steps + 1)
+    prof_steps = min(args.steps, 64)
+    hops = max(args.hops, args.warmup + args.steps + prof_steps + 1)
     n_total = args.actors_per_gpu * world
     w = wl.token_ring(n_total, hops)
     cfg = EngineConfig(device=local, n_ranks=world, rank=rank, **w.engine_kwargs())
@@ -115,11 +116,9 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(uid[0])
 
-    # warmup (includes the upload of actor state and the initial tells)
+    # warmup (includes the upload of actor state, the initial tells and the graph capture)
     s0 = eng.run(args.warmup)
     torch.cuda.synchronize()
-    eng.profile(True)
-    eng.profile_reset()
 
     if world > 1:
         dist.barrier()
@@ -131,9 +130,16 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    prof = eng.profile_read()
     delivered = s1.delivered - s0.delivered
     steps_done = s1.supersteps - s0.supersteps
+
+    # per-kernel HIP-event timing on the engine's stream (eager launches: the
+    # event pairs bracket every kernel); kernel durations are launch-mode independent
+    eng.profile(True)
+    eng.profile_reset()
+    eng.run(prof_steps)
+    prof = eng.profile_read()
+    eng.profile(False)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -178,7 +184,8 @@ def main():
                                "unbounded mailbox" + (", hash-sharded (ShardRegion extractShardId), RCCL exchange"
                                                       if world > 1 else ""),
                    "actors": n_total, "actors_per_gpu": args.actors_per_gpu, "hop_budget": hops,
-                   "supersteps_timed": int(steps_done), "parallelism": f"shard{world}"},
+                   "supersteps_timed": int(steps_done), "profiled_supersteps": prof_steps,
+                   "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms,
