@@ -145,6 +145,7 @@ struct agx_engine {
   static constexpr uint32_t kGraphSteps = 8;
   bool graphs_enabled = true;
   hipGraphExec_t g1 = nullptr, gG = nullptr;
+  unsigned long long* d_dbg = nullptr;  // AGX_STAMPS diagnostic build only
 
   // profiling
   bool prof = false;
@@ -341,8 +342,8 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
 }
 
 agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
-  // the chunk histograms consumed by this step's first pass are free again
-  HIP_TRY(hipMemsetAsync(e->d_hist_c, 0, (size_t)kRadix * e->nchunks * 4, e->stream));
+  // the chunk histograms consumed by this step's first pass were zeroed by k_chunk_downsweep;
+  // on the multi-rank path (no chunk pass) they are never read, so stale columns are harmless
   BucketArgs ba{};
   ba.P = make_params(e);
   ba.in = sorted.c();
@@ -361,6 +362,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.single_pass = e->plan.npass == 1;
   ba.kmax = e->kmax;
   ba.stats = e->d_stats;
+  ba.dbg = e->d_dbg;
   {
     Scope s(e, K_APPLY);
     hipLaunchKernelGGL(k_bucket_apply, dim3(grid_for(e->nb, 4096)), dim3(kBThreads), 0, e->stream, ba);
@@ -691,7 +693,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->R = cfg->n_ranks ? cfg->n_ranks : 1;
   e->rank = cfg->rank;
   e->num_shards = cfg->num_shards ? cfg->num_shards : 1000;
-  e->graphs_enabled = getenv("AGX_NO_GRAPH") == nullptr;
+  e->graphs_enabled = getenv("AGX_NO_GRAPH") == nullptr && getenv("AGX_STAMPS") == nullptr;
   agx_status st = ensure_dev(e);
   if (st) { delete e; return st; }
 
@@ -777,6 +779,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(dalloc(&e->d_hist_c, (uint64_t)kRadix * e->nchunks));
   CREATE_TRY(hipMemset(e->d_hist_c, 0, (uint64_t)kRadix * e->nchunks * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_bstart, kRadix + 1));
+  if (getenv("AGX_STAMPS")) CREATE_TRY(dalloc(&e->d_dbg, (uint64_t)std::min<uint64_t>(e->nb, 4096) * 16));
   CREATE_TRY(dalloc(&e->d_hist_d, (uint64_t)kRadix * e->max_tiles));
   CREATE_TRY(dalloc(&e->d_tot, kRadix));
   CREATE_TRY(dalloc(&e->d_n, 4));
@@ -810,7 +813,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_row); hipFree(e->d_col);
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
   free_msgs(e->s1); free_msgs(e->s2);
-  hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart);
+  hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);
   if (e->h_pin) hipHostFree(e->h_pin);
@@ -937,6 +940,22 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
     AGX_TRY(run_single(e, max_supersteps));
   }
   prof_collect(e);
+  if (e->d_dbg) {  // diagnostic: mean phase durations of k_bucket_apply blocks (last superstep)
+    const uint64_t nbk = std::min<uint64_t>(e->nb, 4096);
+    std::vector<unsigned long long> h(nbk * 16);
+    HIP_TRY(hipMemcpy(h.data(), e->d_dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    double acc[8] = {0};
+    unsigned long long t0min = ~0ull, t8max = 0;
+    for (uint64_t b = 0; b < nbk; ++b) {
+      for (int k = 0; k < 8; ++k) acc[k] += (double)(h[b * 16 + k + 1] - h[b * 16 + k]);
+      t0min = std::min(t0min, h[b * 16]);
+      t8max = std::max(t8max, h[b * 16 + 8]);
+    }
+    fprintf(stderr, "[agx stamps] mean cycles per phase:");
+    const char* nm[8] = {"range+alive", "sort", "->finish", "classify+backlog", "prefetch+phaseA", "scan", "phaseB", "hist+stats"};
+    for (int k = 0; k < 8; ++k) fprintf(stderr, " %s=%.0f", nm[k], acc[k] / nbk);
+    fprintf(stderr, " | kernel span=%llu cycles\n", t8max - t0min);
+  }
   AGX_TRY(check_error(e));
   return agx_get_stats(e, out);
 }

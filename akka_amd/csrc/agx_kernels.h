@@ -193,10 +193,16 @@ __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
 
   for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
     const uint32_t cnt = a.ch.cnt[c];
+    // this chunk's per-digit prefix (from the rowscan), cached; the column is then zeroed so that
+    // the next k_bucket_apply can write fresh histograms without a separate memset
+    for (uint32_t d = tid; d < nd; d += kThreads) {
+      uint32_t* hp = a.hist + (size_t)d * a.stride + c;
+      s_run[d] = cnt ? *hp : 0u;  // s_run = chunk prefix + items placed so far
+      *hp = 0u;
+    }
     if (cnt == 0) continue;
     const CMsgs& src = a.ch.arena(c);
     const uint32_t off = a.ch.off[c];
-    for (uint32_t d = tid; d < nd; d += kThreads) s_run[d] = 0;
     for (uint32_t sub = 0; sub < cnt; sub += kTile) {
       for (int i = tid; i < kWaves * kRadix; i += kThreads) (&whist[0][0])[i] = 0;
       __syncthreads();
@@ -250,7 +256,7 @@ __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
       for (int j = 0; j < kRadix / kThreads; ++j) {
         const uint32_t d = tid + j * kThreads;
         if (d < nd) {
-          s_gadj[d] = s_dbase[d] + a.hist[(size_t)d * a.stride + c] + s_run[d] - s_ldig[d];
+          s_gadj[d] = s_dbase[d] + s_run[d] - s_ldig[d];
           s_run[d] += cd[j];
         }
       }
@@ -489,6 +495,30 @@ constexpr int kBIpt = kBucket / kBThreads;      // items per thread per sub-tile
 constexpr int kBAct = kBucket / kBThreads;      // actors per thread (4)
 constexpr int kStagedChunks = 256;              // host-staged tells are split over this many chunks
 
+// Tell staging in LDS (single-pass path): tells overwrite consumed inbox slots of the same actor.
+struct EmitterLds {
+  const DevParams* P;
+  uint32_t* key;
+  uint32_t* src;
+  uint32_t* pay;
+  uint32_t slot;      // next LDS slot
+  uint32_t self;
+  uint32_t n_valid, n_all;
+  uint32_t* nh;
+  uint32_t nh_shift, nh_mask;
+  __device__ __forceinline__ void operator()(uint32_t dst, uint32_t p) {
+    ++n_all;
+    if (dst >= P->n_global) return;  // unknown ref -> deadLetters
+    ++n_valid;
+    const uint32_t k = (P->R > 1) ? P->route[dst] : dst;
+    key[slot] = k;
+    src[slot] = self;
+    pay[slot] = p;
+    ++slot;
+    atomicAdd(&nh[((k & kLocalMask) >> nh_shift) & nh_mask], 1u);
+  }
+};
+
 struct BucketArgs {
   DevParams P;
   CMsgs in;                // mail sorted by bucket (local key >> kBucketBits)
@@ -502,7 +532,13 @@ struct BucketArgs {
   uint32_t nhist_stride, nx_shift, nx_bits;
   uint32_t nb, single_pass, kmax;
   uint64_t* stats;
+  unsigned long long* dbg;  // diagnostic build only (AGX_STAMPS): per-block phase timestamps
 };
+
+#define AGX_STAMP(a, idx)                                                                         \
+  do {                                                                                            \
+    if ((a).dbg && threadIdx.x == 0) (a).dbg[blockIdx.x * 16 + (idx)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 
 // 64-ary lower bound by one wave: first index i in [0, n) with ((key[i] & local) >> sh) >= target
 __device__ __forceinline__ uint32_t wave_lower_bound(const uint32_t* key, uint32_t n, uint32_t sh, uint32_t target) {
@@ -555,6 +591,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   uint64_t* w0s = L.U;
   uint64_t* w1s = L.U + kBucket;
 
+  AGX_STAMP(a, 3);
   // ---- classification per actor (blocked): drained / queued (backlog) / dead letters
   uint32_t nbl_t = 0, ndead = 0, blc[kBAct];
 #pragma unroll
@@ -607,6 +644,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   }
   __syncthreads();
 
+  AGX_STAMP(a, 4);
   // ---- prefetch kind + state words 0/1 of actors with mail (striped: coalesced)
 #pragma unroll
   for (int j = 0; j < kBAct; ++j) {
@@ -619,87 +657,146 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       w1s[la] = P.W > 1 ? P.state[(size_t)P.n_local + l] : 0ull;
     }
   }
-  // ---- phase A: emissions per actor (drain min(len, T) messages in order)
-#pragma unroll 1
-  for (int j = 0; j < kBAct; ++j) {
-    const uint32_t la = j * kBThreads + tid;
-    const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
-    if (la >= na || !len || !L.alive[la]) continue;
-    const uint32_t l = a0 + la;
-    const uint32_t self = P.R > 1 ? P.gid[l] : l;
-    Emitter<false> em{&P, {}, 0, self, 0, 0, L.nh, a.nx_shift, nhmask};
-    uint64_t wv[AGX_MAX_WORDS];
-    wv[0] = w0s[la];
-    wv[1] = w1s[la];
-#pragma unroll
-    for (int q = 2; q < (int)AGX_MAX_WORDS; ++q) wv[q] = (q < (int)P.W) ? P.state[(size_t)q * P.n_local + l] : 0ull;
-    const uint32_t nd = min(len, T);
-    for (uint32_t q = 0; q < nd; ++q) {
-      const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, isrc(s0 + q), ipay(s0 + q), em);
-      if (r == AGX_RES_STOPPED) break;
-    }
-    L.ecnt[la] = em.n_valid;
-  }
-  __syncthreads();
-  // ---- exclusive scan of emission counts in actor (= sender) order
-  uint32_t emtot;
-  {
-    uint32_t ec[kBAct], run = 0;
-    const uint4 v = reinterpret_cast<const uint4*>(L.ecnt)[tid];
-    ec[0] = v.x; ec[1] = v.y; ec[2] = v.z; ec[3] = v.w;
-#pragma unroll
-    for (int j = 0; j < kBAct; ++j) run += ec[j];
-    uint32_t ex = block_excl_sum<kBThreads>(run, L.scratch, &emtot);
-    uint32_t o[kBAct];
-#pragma unroll
-    for (int j = 0; j < kBAct; ++j) {
-      o[j] = ex;
-      ex += ec[j];
-    }
-    reinterpret_cast<uint4*>(L.ecnt)[tid] = make_uint4(o[0], o[1], o[2], o[3]);
-  }
+  uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0, emtot = 0;
   const uint64_t embase = (uint64_t)lo * a.kmax;  // this bucket's slice of the tell arena
+  if (kLds && a.kmax == 1) {
+    // ---- single pass (each message emits <= 1 tell): drain + apply; tells are staged in LDS over the
+    // actor's own, already consumed, inbox slots (tell e of an actor <= message index q that made it)
+    uint32_t ecl[kBAct];
+#pragma unroll 1
+    for (int j = 0; j < kBAct; ++j) {
+      const uint32_t la = j * kBThreads + tid;
+      const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
+      ecl[j] = 0;
+      if (la >= na || !len || !L.alive[la]) continue;
+      const uint32_t l = a0 + la;
+      const uint32_t self = P.R > 1 ? P.gid[l] : l;
+      EmitterLds em{&P, L.key, L.src, L.pay, s0, self, 0, 0, L.nh, a.nx_shift, nhmask};
+      uint64_t wv[2] = {w0s[la], w1s[la]};
+      const uint32_t nd = min(len, T);
+      ++nact;
+      for (uint32_t q = 0; q < nd; ++q) {
+        const uint32_t sv = L.src[s0 + q], pv = L.pay[s0 + q];
+        const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, sv, pv, em);
+        ++ndel;
+        if (r == AGX_RES_UNHANDLED) ++nunh;
+        if (r == AGX_RES_STOPPED) {
+          P.stopq[atomicAdd(P.nstop, 1u)] = l;
+          ndead += nd - q - 1;  // drained-but-unprocessed after the stop
+          break;
+        }
+      }
+      P.state[l] = wv[0];
+      if (P.W > 1) P.state[(size_t)P.n_local + l] = wv[1];
+      nall += em.n_all;
+      ndead += em.n_all - em.n_valid;
+      ecl[j] = em.n_valid;
+      L.ecnt[la] = em.n_valid;
+    }
+    __syncthreads();
+    AGX_STAMP(a, 5);
+    {  // exclusive scan of tell counts in actor (= sender) order
+      uint32_t ec[kBAct], run = 0;
+      const uint4 v = reinterpret_cast<const uint4*>(L.ecnt)[tid];
+      ec[0] = v.x; ec[1] = v.y; ec[2] = v.z; ec[3] = v.w;
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) run += ec[j];
+      uint32_t ex = block_excl_sum<kBThreads>(run, L.scratch, &emtot);
+      uint32_t o[kBAct];
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        o[j] = ex;
+        ex += ec[j];
+      }
+      reinterpret_cast<uint4*>(L.ecnt)[tid] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();
+    AGX_STAMP(a, 6);
+    // compact the staged tells into the bucket's tell chunk (lane-consecutive actors: coalesced)
+#pragma unroll 1
+    for (int j = 0; j < kBAct; ++j) {
+      const uint32_t la = j * kBThreads + tid;
+      const uint32_t s0 = L.seg[la], o = L.ecnt[la];
+      for (uint32_t e = 0; e < ecl[j]; ++e) {
+        a.em.key[embase + o + e] = L.key[s0 + e];
+        a.em.src[embase + o + e] = L.src[s0 + e];
+        a.em.pay[embase + o + e] = L.pay[s0 + e];
+      }
+    }
+  } else {
+  // ---- phase A: emissions per actor (drain min(len, T) messages in order)
+  #pragma unroll 1
+    for (int j = 0; j < kBAct; ++j) {
+      const uint32_t la = j * kBThreads + tid;
+      const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
+      if (la >= na || !len || !L.alive[la]) continue;
+      const uint32_t l = a0 + la;
+      const uint32_t self = P.R > 1 ? P.gid[l] : l;
+      Emitter<false> em{&P, {}, 0, self, 0, 0, L.nh, a.nx_shift, nhmask};
+      uint64_t wv[2] = {w0s[la], w1s[la]};  // behaviours read/write state words 0-1 only
+      const uint32_t nd = min(len, T);
+      for (uint32_t q = 0; q < nd; ++q) {
+        const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, isrc(s0 + q), ipay(s0 + q), em);
+        if (r == AGX_RES_STOPPED) break;
+      }
+      L.ecnt[la] = em.n_valid;
+    }
+    __syncthreads();
+    AGX_STAMP(a, 5);
+    // ---- exclusive scan of emission counts in actor (= sender) order
+      {
+      uint32_t ec[kBAct], run = 0;
+      const uint4 v = reinterpret_cast<const uint4*>(L.ecnt)[tid];
+      ec[0] = v.x; ec[1] = v.y; ec[2] = v.z; ec[3] = v.w;
+  #pragma unroll
+      for (int j = 0; j < kBAct; ++j) run += ec[j];
+      uint32_t ex = block_excl_sum<kBThreads>(run, L.scratch, &emtot);
+      uint32_t o[kBAct];
+  #pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        o[j] = ex;
+        ex += ec[j];
+      }
+      reinterpret_cast<uint4*>(L.ecnt)[tid] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();
+  
+    AGX_STAMP(a, 6);
+    // ---- phase B: apply for real, write tells (sender order) and state
+  #pragma unroll 1
+    for (int j = 0; j < kBAct; ++j) {
+      const uint32_t la = j * kBThreads + tid;
+      const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
+      if (la >= na || !len || !L.alive[la]) continue;
+      const uint32_t l = a0 + la;
+      const uint32_t self = P.R > 1 ? P.gid[l] : l;
+      Emitter<true> em{&P, a.em, embase + L.ecnt[la], self, 0, 0, L.nh, a.nx_shift, nhmask};
+      uint64_t wv[2] = {w0s[la], w1s[la]};  // behaviours read/write state words 0-1 only
+      const uint32_t nd = min(len, T);
+      ++nact;
+      for (uint32_t q = 0; q < nd; ++q) {
+        const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, isrc(s0 + q), ipay(s0 + q), em);
+        ++ndel;
+        if (r == AGX_RES_UNHANDLED) ++nunh;
+        if (r == AGX_RES_STOPPED) {
+          P.stopq[atomicAdd(P.nstop, 1u)] = l;
+          ndead += nd - q - 1;  // drained-but-unprocessed after the stop
+          break;
+        }
+      }
+      P.state[l] = wv[0];
+      if (P.W > 1) P.state[(size_t)P.n_local + l] = wv[1];
+      nall += em.n_all;
+      ndead += em.n_all - em.n_valid;
+    }
+  }
   if (tid == 0) {
     a.chunk_off[a.nb + b] = (uint32_t)embase;
     a.chunk_cnt[a.nb + b] = emtot;
   }
   __syncthreads();
-
-  // ---- phase B: apply for real, write tells (sender order) and state
-  uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0;
-#pragma unroll 1
-  for (int j = 0; j < kBAct; ++j) {
-    const uint32_t la = j * kBThreads + tid;
-    const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
-    if (la >= na || !len || !L.alive[la]) continue;
-    const uint32_t l = a0 + la;
-    const uint32_t self = P.R > 1 ? P.gid[l] : l;
-    Emitter<true> em{&P, a.em, embase + L.ecnt[la], self, 0, 0, L.nh, a.nx_shift, nhmask};
-    uint64_t wv[AGX_MAX_WORDS];
-    wv[0] = w0s[la];
-    wv[1] = w1s[la];
-#pragma unroll
-    for (int q = 2; q < (int)AGX_MAX_WORDS; ++q) wv[q] = (q < (int)P.W) ? P.state[(size_t)q * P.n_local + l] : 0ull;
-    const uint32_t nd = min(len, T);
-    ++nact;
-    for (uint32_t q = 0; q < nd; ++q) {
-      const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, isrc(s0 + q), ipay(s0 + q), em);
-      ++ndel;
-      if (r == AGX_RES_UNHANDLED) ++nunh;
-      if (r == AGX_RES_STOPPED) {
-        P.stopq[atomicAdd(P.nstop, 1u)] = l;
-        ndead += nd - q - 1;  // drained-but-unprocessed after the stop
-        break;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < (int)AGX_MAX_WORDS; ++q)
-      if (q < (int)P.W) P.state[(size_t)q * P.n_local + l] = wv[q];
-    nall += em.n_all;
-    ndead += em.n_all - em.n_valid;
-  }
-  __syncthreads();
-  // next first-pass histogram column of this bucket's tell chunk (zeroed by the host memset)
+  AGX_STAMP(a, 7);
+  // next first-pass histogram column of this bucket's tell chunk (zeroed by the chunk downsweep)
   for (uint32_t d = tid; d < (1u << a.nx_bits); d += kBThreads)
     if (L.nh[d]) a.nhist[(size_t)d * a.nhist_stride + a.nb + b] = L.nh[d];
   // block stats -> global
@@ -722,6 +819,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     if (L.stat[4]) atomicAdd((unsigned long long*)&a.stats[ST_ACTIVE], L.stat[4]);
   }
   __syncthreads();
+  AGX_STAMP(a, 8);
 }
 
 __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
@@ -751,6 +849,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   }
 
   for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x) {
+    AGX_STAMP(a, 0);
     const uint32_t a0 = b << kBucketBits;
     const uint32_t na = min((uint32_t)kBucket, P.n_local - a0);
     if (tid < 5) s_stat[tid] = 0;
@@ -770,6 +869,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     }
     for (uint32_t la = tid; la < kBucket; la += kBThreads) s_alive[la] = la < na ? P.alive[a0 + la] : 0;
     __syncthreads();
+    AGX_STAMP(a, 1);
     const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
 
     if (cnt <= (uint32_t)kBucket) {
@@ -787,29 +887,60 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
           k[r] = 0xFFFFFFFFu;
         }
       }
-      for (uint32_t i = tid; i < kBWaves * kBucket / 2; i += kBThreads) reinterpret_cast<uint32_t*>(whist)[i] = 0;
-      __syncthreads();
+      // in-order copy + sortedness check: local topologies (rings, stencils) arrive already in
+      // actor order, and then the wave multisplit ranking is unnecessary (same result)
+      for (uint32_t i = tid; i < kBucket + 4; i += kBThreads) s_seg[i] = 0;
 #pragma unroll
       for (int r = 0; r < kBIpt; ++r) {
         const uint32_t q = wbase + r * kWave + lane;
-        rk[r] = wave_rank(q < cnt, k[r] & (kBucket - 1), kBucketBits, whist + w * kBucket, ltm);
+        if (q < cnt) {
+          s_key[q] = k[r];
+          s_src[q] = sv[r];
+          s_pay[q] = pv[r];
+        }
       }
       __syncthreads();
-      // per actor: wave prefixes in place, segment length
-      uint32_t tl[kBAct];
+      int ok = 1;
 #pragma unroll
-      for (int j = 0; j < kBAct; ++j) {
-        const uint32_t la = tid * kBAct + j;  // blocked (for the scan below)
-        uint32_t run = 0;
-#pragma unroll
-        for (int q = 0; q < kBWaves; ++q) {
-          const uint32_t c2 = whist[q * kBucket + la];
-          whist[q * kBucket + la] = (uint16_t)run;
-          run += c2;
-        }
-        tl[j] = run;
+      for (int r = 0; r < kBIpt; ++r) {
+        const uint32_t q = wbase + r * kWave + lane;
+        if (q < cnt && q > 0) ok &= (s_key[q - 1] & (kBucket - 1)) <= (k[r] & (kBucket - 1));
       }
-      {
+      const bool presorted = __syncthreads_and(ok) != 0;
+      uint32_t tl[kBAct];
+      if (presorted) {
+#pragma unroll
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t q = wbase + r * kWave + lane;
+          if (q < cnt) atomicAdd(&s_seg[k[r] & (kBucket - 1)], 1u);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kBAct; ++j) tl[j] = s_seg[tid * kBAct + j];
+      } else {
+        for (uint32_t i = tid; i < kBWaves * kBucket / 2; i += kBThreads) reinterpret_cast<uint32_t*>(whist)[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t q = wbase + r * kWave + lane;
+          rk[r] = wave_rank(q < cnt, k[r] & (kBucket - 1), kBucketBits, whist + w * kBucket, ltm);
+        }
+        __syncthreads();
+        // per actor: wave prefixes in place, segment length
+#pragma unroll
+        for (int j = 0; j < kBAct; ++j) {
+          const uint32_t la = tid * kBAct + j;  // blocked (for the scan below)
+          uint32_t run = 0;
+#pragma unroll
+          for (int q = 0; q < kBWaves; ++q) {
+            const uint32_t c2 = whist[q * kBucket + la];
+            whist[q * kBucket + la] = (uint16_t)run;
+            run += c2;
+          }
+          tl[j] = run;
+        }
+      }
+      {  // segment starts: exclusive scan of per-actor counts (blocked)
         uint32_t run = 0;
 #pragma unroll
         for (int j = 0; j < kBAct; ++j) run += tl[j];
@@ -823,18 +954,21 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         if (tid == 0) s_seg[kBucket] = t;
       }
       __syncthreads();
+      if (!presorted) {  // stable scatter into actor order (items come from registers)
 #pragma unroll
-      for (int r = 0; r < kBIpt; ++r) {
-        const uint32_t q = wbase + r * kWave + lane;
-        if (q < cnt) {
-          const uint32_t la = k[r] & (kBucket - 1);
-          const uint32_t pos = s_seg[la] + whist[w * kBucket + la] + rk[r];
-          s_key[pos] = k[r];
-          s_src[pos] = sv[r];
-          s_pay[pos] = pv[r];
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t q = wbase + r * kWave + lane;
+          if (q < cnt) {
+            const uint32_t la = k[r] & (kBucket - 1);
+            const uint32_t pos = s_seg[la] + whist[w * kBucket + la] + rk[r];
+            s_key[pos] = k[r];
+            s_src[pos] = sv[r];
+            s_pay[pos] = pv[r];
+          }
         }
+        __syncthreads();
       }
-      __syncthreads();
+      AGX_STAMP(a, 2);
       bucket_finish<true>(a, L, b, lo, cnt, a0, na);
     } else {
       // ---- general path (skewed bucket): counting sort into the global scratch copy
