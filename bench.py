@@ -37,6 +37,10 @@ def parse():
     ap.add_argument("--actors-per-gpu", type=int, default=N_PER_GPU)
     ap.add_argument("--hops", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--large-actors", type=int, default=100_000_000,
+                    help="whole-job actor count of the second operating point (0 = skip)")
+    ap.add_argument("--large-steps", type=int, default=24)
+    ap.add_argument("--large-warmup", type=int, default=4)
     ap.add_argument("--cpu-hops", type=int, default=96, help="hop budget of the bounded CPU sample")
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_r01.json"),
                     help="PMC traffic summary written by profiles/collect_pmc.py")
@@ -79,16 +83,65 @@ def cpu_baseline(hops: int) -> dict:
             "bsp_ref_1thread_msg_s": sb["delivered"] / bsp_s}
 
 
+def timed_ring(n_total: int, hops: int, warmup: int, steps: int, world: int, rank: int, local: int,
+               msg_capacity: int = 0, keep: bool = False):
+    """Build the C2 ring over n_total actors (this rank keeps the ones it owns),
+    run `warmup` untimed supersteps, then time exactly `steps` supersteps
+    bracketed by barrier + device sync.  Returns (engine|None, s, delivered, supersteps)."""
+    import torch
+    import torch.distributed as dist
+    from akka_amd import workloads as wl
+    from akka_amd.engine import EngineConfig, GpuEngine
+
+    w = wl.token_ring(n_total, hops)
+    cfg = EngineConfig(device=local, n_ranks=world, rank=rank, **w.engine_kwargs())
+    cfg.msg_capacity = msg_capacity
+    eng = GpuEngine(cfg)
+    w.apply_to(eng)
+    del w
+    if world > 1:
+        uid = [GpuEngine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0])
+    # warmup (includes the upload of actor state, the initial tells and the graph capture)
+    s0 = eng.run(warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s1 = eng.run(steps)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    if not keep:
+        eng.close()
+        eng = None
+    return eng, t1 - t0, s1.delivered - s0.delivered, s1.supersteps - s0.supersteps
+
+
+def reduce_ranks(elapsed: float, delivered: int, world: int):
+    """MAX elapsed and SUM delivered over ranks."""
+    if world == 1:
+        return elapsed, delivered
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    d = torch.tensor([delivered], dtype=torch.float64)
+    dist.all_reduce(d, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(d.item())
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    n_gpus = max(args.gpus, world)
-    if world != args.gpus and world > 1:
-        n_gpus = world
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N>1 needs one process per GPU: torchrun --nproc-per-node N bench.py --gpus N")
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -100,38 +153,12 @@ def main():
         dist.barrier()
     torch.cuda.set_device(local)
 
-    from akka_amd import workloads as wl
-    from akka_amd.engine import EngineConfig, GpuEngine
-
     prof_steps = min(args.steps, 64)
     hops = max(args.hops, args.warmup + args.steps + prof_steps + 1)
     n_total = args.actors_per_gpu * world
-    w = wl.token_ring(n_total, hops)
-    cfg = EngineConfig(device=local, n_ranks=world, rank=rank, **w.engine_kwargs())
-    cfg.msg_capacity = int(2 * args.actors_per_gpu * 1.25) if world > 1 else 0
-    eng = GpuEngine(cfg)
-    w.apply_to(eng)  # each rank keeps the actors / tells it owns
-    if world > 1:
-        uid = [GpuEngine.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.comm_init(uid[0])
-
-    # warmup (includes the upload of actor state, the initial tells and the graph capture)
-    s0 = eng.run(args.warmup)
-    torch.cuda.synchronize()
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    s1 = eng.run(args.steps)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    delivered = s1.delivered - s0.delivered
-    steps_done = s1.supersteps - s0.supersteps
+    eng, elapsed, delivered, steps_done = timed_ring(n_total, hops, args.warmup, args.steps, world, rank, local,
+                                                     msg_capacity=int(2 * args.actors_per_gpu * 1.25) if world > 1 else 0,
+                                                     keep=True)
 
     # per-kernel HIP-event timing on the engine's stream (eager launches: the
     # event pairs bracket every kernel); kernel durations are launch-mode independent
@@ -140,18 +167,29 @@ def main():
     eng.run(prof_steps)
     prof = eng.profile_read()
     eng.profile(False)
+    cfg_words = eng.cfg.n_words
+    eng.close()
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        d = torch.tensor([delivered], dtype=torch.float64)
-        dist.all_reduce(d, op=dist.ReduceOp.SUM)
-        delivered = int(d.item())
+    elapsed, delivered = reduce_ranks(elapsed, delivered, world)
+
+    # the metric's second operating point: 100M actors over the whole job
+    # (strong-scaled: 100M/N actors per GPU), same ring, shorter timed region
+    large = None
+    if args.large_actors > 0:
+        n_l = args.large_actors
+        per = (n_l + world - 1) // world
+        steps_l = args.large_steps
+        _, el_l, dl_l, sd_l = timed_ring(n_l, args.large_warmup + steps_l + 1, args.large_warmup, steps_l, world,
+                                         rank, local, msg_capacity=int(per * (2.5 if world > 1 else 1.25)) + 4096)
+        el_l, dl_l = reduce_ranks(el_l, dl_l, world)
+        large = {"actors": n_l, "actors_per_gpu": per, "steps": steps_l, "warmup": args.large_warmup,
+                 "supersteps_timed": int(sd_l), "value": dl_l / el_l, "unit": "msg/s",
+                 "ms_per_step": el_l / steps_l * 1e3, "scaling": "strong",
+                 "superstep_frac": (12 + 12 + 16 * cfg_words + 2) * per / (el_l / steps_l) / 1e9 / PEAK_HBM_GBS}
 
     value = delivered / elapsed
     # roofline of the dominant kernel (largest total time in the timed region)
-    per_msg = kernel_bytes_per_msg(cfg.n_words)
+    per_msg = kernel_bytes_per_msg(cfg_words)
     local_msgs_per_step = args.actors_per_gpu
     dom = max((k for k in prof if prof[k]["launches"]), key=lambda k: prof[k]["total_ms"])
     avg_ms = prof[dom]["total_ms"] / prof[dom]["launches"]
@@ -166,7 +204,7 @@ def main():
         except Exception:
             traffic = None
     step_time = elapsed / max(args.steps, 1)
-    superstep_bytes = (12 + 12 + 16 * cfg.n_words + 2) * local_msgs_per_step
+    superstep_bytes = (12 + 12 + 16 * cfg_words + 2) * local_msgs_per_step
     out = {
         "metric": "messages delivered/sec (whole node) at 1M and 100M actors; % HBM roofline",
         "value": value,
@@ -190,6 +228,7 @@ def main():
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms,
                      "superstep_frac": superstep_bytes / step_time / 1e9 / PEAK_HBM_GBS * (1 if world == 1 else 1)},
+        "at_100M_actors": large,
         "kernel_ms": {k: {"total_ms": round(v["total_ms"], 4), "launches": v["launches"]} for k, v in prof.items()},
     }
     if rank == 0:
@@ -199,7 +238,6 @@ def main():
             except Exception as ex:  # the baseline must never hide the GPU number
                 out["cpu_baseline"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(built):
 def test_gfx950_code_object_present(built):
     from akka_amd import _lib
     data = _lib.LIB_PATH.read_bytes()
-    assert b"gfx950" in data and b"k_apply" in data and b"k_sort_downsweep" in data
+    assert b"gfx950" in data and b"k_bucket_apply" in data and b"k_chunk_downsweep" in data
 
 
 def test_host_shard_helpers_match_golden(built):

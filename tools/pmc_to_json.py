@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Fold separate rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) into the
+per-kernel HBM traffic summary bench.py reads (roofline.traffic).
+
+Corrections (MI355X_MICROARCH.md, HBM section): both counters are in KiB;
+on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced streaming
+reads, so it is doubled; WRITE_SIZE is taken as is.  The engine's reads are
+4-12 B per lane, a width the guide lists as uncalibrated: the raw values are
+kept beside the corrected total.
+
+    python tools/pmc_to_json.py OUT.json FETCH_DIR WRITE_DIR [--note TEXT]
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+
+def load(d: str, counter: str) -> dict:
+    vals = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0]
+            if not name.startswith("agx::k_"):
+                continue
+            vals[name[len("agx::k_"):]].append(float(r["Counter_Value"]))
+    return {k: (sum(v) / len(v), len(v)) for k, v in vals.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--note", default="")
+    a = ap.parse_args()
+    fe = load(a.fetch_dir, "FETCH_SIZE")
+    wr = load(a.write_dir, "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fe) | set(wr)):
+        f_kib, nf = fe.get(k, (0.0, 0))
+        w_kib, nw = wr.get(k, (0.0, 0))
+        kernels[k] = {"fetch_kib_raw": round(f_kib, 1), "write_kib_raw": round(w_kib, 1),
+                      "dispatches": [nf, nw],
+                      "hbm_bytes_per_launch": int(2 * f_kib * 1024 + w_kib * 1024)}
+    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes)",
+               "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), KiB -> bytes",
+               "note": a.note, "kernels": kernels}, open(a.out, "w"), indent=1)
+    print(json.dumps(kernels, indent=1))
+
+
+if __name__ == "__main__":
+    main()
