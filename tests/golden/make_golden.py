@@ -82,6 +82,99 @@ def gcounter_kats():
     }
 
 
+def pncounter_kats():
+    # node1, node2 = UniqueAddress(akka://Sys@localhost:2551/2552, uid 1/2) (PNCounterSpec.scala:15-16) -> slots 0, 1.
+    # ops: ["inc"|"dec", slot, n]; state = (increments slots, decrements slots).
+    a_ops = [["inc", 0, 3], ["dec", 0, 2], ["inc", 1, 5], ["dec", 1, 2], ["inc", 1, 1]]
+    b_ops = [["inc", 0, 2], ["dec", 0, 3], ["inc", 1, 3], ["dec", 1, 2], ["inc", 1, 1]]
+    return {
+        "source": "akka-distributed-data/src/test/scala/akka/cluster/ddata/PNCounterSpec.scala",
+        "slots": 2,
+        "cases": [
+            {"name": "increment each node's record by one (:20-40)",
+             "ops": [["inc", 0, 1], ["inc", 0, 1], ["inc", 1, 1], ["inc", 1, 1], ["inc", 1, 1]],
+             "increments": [2, 3], "decrements": [0, 0]},
+            {"name": "decrement each node's record by one (:42-60)",
+             "ops": [["dec", 0, 1], ["dec", 0, 1], ["dec", 1, 1], ["dec", 1, 1], ["dec", 1, 1]],
+             "increments": [0, 0], "decrements": [2, 3]},
+            {"name": "increment by arbitrary delta (:62-75)",
+             "ops": [["inc", 0, 3], ["inc", 0, 4], ["inc", 1, 2], ["inc", 1, 7], ["inc", 1, 1]],
+             "increments": [7, 10], "decrements": [0, 0]},
+            {"name": "decrement by arbitrary delta (:91-104)",
+             "ops": [["dec", 0, 3], ["dec", 0, 4], ["dec", 1, 2], ["dec", 1, 7], ["dec", 1, 1]],
+             "increments": [0, 0], "decrements": [7, 10]},
+            {"name": "increment and decrement by arbitrary delta (:106-118,119-131)",
+             "ops": a_ops, "increments_value": 9, "decrements_value": 4, "value": 5},
+        ],
+        "merges": [
+            {"name": "history correctly merged with another counter (:133-167), both ways",
+             "a_ops": a_ops, "b_ops": b_ops,
+             "a_value": 5, "b_value": 1, "b_increments_value": 6, "b_decrements_value": 5,
+             "merged_increments_value": 9, "merged_decrements_value": 5, "merged_value": 4},
+        ],
+    }
+
+
+def orset_kats():
+    """ORSetSpec 'ORSet unit test' vectors.  Nodes nodeA..nodeH (ORSetSpec.scala:22-29) -> 0..7,
+    node1..node3 (:18-20) -> 0..2 (UniqueAddress order).  Elements are numbered in order of
+    first appearance.  Dots/vvectors are {node: version}."""
+    A, B, C, D, E, F, G = range(7)
+    return {
+        "source": "akka-distributed-data/src/test/scala/akka/cluster/ddata/ORSetSpec.scala",
+        "subtract_dots": [
+            {"name": "verify subtractDots (:489-495)",
+             "dot": {A: 3, B: 2, D: 14, G: 22}, "vvector": {A: 4, B: 1, C: 1, D: 14, E: 5, F: 2},
+             "expected": {B: 2, G: 22}},
+        ],
+        "merges": [
+            {"name": "verify mergeCommonKeys (:497-511)",
+             "this": {"elements": {"K1": {A: 3, D: 7}, "K2": {B: 5, C: 2}}, "vvector": {A: 3, B: 5, C: 2, D: 7}},
+             "that": {"elements": {"K1": {A: 3}, "K2": {B: 6}}, "vvector": {A: 3, B: 6, C: 1, D: 8}},
+             "expected_elements": {"K1": {A: 3}, "K2": {B: 6, C: 2}}},
+            {"name": "verify mergeDisjointKeys (:513-524): keys only in `this`, against that.vvector",
+             "this": {"elements": {"K3": {A: 4}, "K4": {A: 3, D: 8}, "K5": {A: 2}}, "vvector": {A: 4, D: 8}},
+             "that": {"elements": {}, "vvector": {A: 3, D: 7}},
+             "expected_elements": {"K3": {A: 4}, "K4": {D: 8}}},
+        ],
+        # replica scripts: ["new", r] | ["add", r, node, elem] | ["remove", r, elem] | ["copy", dst, src]
+        # | ["merge", dst, x, y] (dst := x.merge(y)); checks: ["elements", r, [elems...]]
+        "scripts": [
+            {"name": "verify disjoint merge (:526-533)",
+             "ops": [["new", "a1"], ["add", "a1", 0, "bar"], ["new", "b1"], ["add", "b1", 1, "baz"],
+                     ["merge", "c", "a1", "b1"], ["copy", "a2", "a1"], ["remove", "a2", "bar"],
+                     ["merge", "d", "a2", "c"]],
+             "checks": [["elements", "d", ["baz"]]]},
+            {"name": "verify removed after merge (:535-568)",
+             "ops": [["new", "a"], ["add", "a", 0, "Z"], ["copy", "c", "a"], ["copy", "a2", "a"],
+                     ["remove", "a2", "Z"], ["new", "b"], ["add", "b", 1, "Z"], ["merge", "a3", "b", "a2"],
+                     ["copy", "b2", "b"], ["remove", "b2", "Z"],
+                     ["merge", "t1", "a3", "c"], ["merge", "t1", "t1", "b2"],
+                     ["merge", "t2", "a3", "b2"], ["merge", "t2", "t2", "c"],
+                     ["merge", "t3", "c", "b2"], ["merge", "t3", "t3", "a3"],
+                     ["merge", "t4", "c", "a3"], ["merge", "t4", "t4", "b2"],
+                     ["merge", "t5", "b2", "c"], ["merge", "t5", "t5", "a3"],
+                     ["merge", "t6", "b2", "a3"], ["merge", "t6", "t6", "c"]],
+             "checks": [["elements", "a3", ["Z"]], ["elements", "c", ["Z"]], ["elements", "b2", []],
+                        ["elements", "t1", []], ["elements", "t2", []], ["elements", "t3", []],
+                        ["elements", "t4", []], ["elements", "t5", []], ["elements", "t6", []]]},
+            {"name": "verify removed after merge 2 (:570-591)",
+             "ops": [["new", "a"], ["add", "a", 0, "Z"], ["new", "b"], ["add", "b", 1, "Z"], ["copy", "c", "a"],
+                     ["copy", "a2", "a"], ["remove", "a2", "Z"], ["merge", "a3", "a2", "b"],
+                     ["copy", "b2", "b"], ["remove", "b2", "Z"], ["merge", "b3", "b2", "c"],
+                     ["merge", "t1", "a3", "c"], ["merge", "t1", "t1", "b3"],
+                     ["merge", "t2", "a3", "b3"], ["merge", "t2", "t2", "c"],
+                     ["merge", "t3", "c", "b3"], ["merge", "t3", "t3", "a3"],
+                     ["merge", "t4", "c", "a3"], ["merge", "t4", "t4", "b3"],
+                     ["merge", "t5", "b3", "c"], ["merge", "t5", "t5", "a3"],
+                     ["merge", "t6", "b3", "a3"], ["merge", "t6", "t6", "c"]],
+             "checks": [["elements", "a3", ["Z"]], ["elements", "b3", ["Z"]],
+                        ["elements", "t1", []], ["elements", "t2", []], ["elements", "t3", []],
+                        ["elements", "t4", []], ["elements", "t5", []], ["elements", "t6", []]]},
+        ],
+    }
+
+
 def mailbox_kats():
     """Queue semantics as engine runs on one receiver (COUNTER behaviour:
     w0 = messages invoked, w1 = sum of payloads)."""
@@ -131,6 +224,8 @@ def main():
     files = {
         "shard_ids.json": shard_vectors(),
         "gcounter_kat.json": gcounter_kats(),
+        "pncounter_kat.json": pncounter_kats(),
+        "orset_kat.json": orset_kats(),
         "mailbox_kat.json": mailbox_kats(),
         "pingpong_kat.json": pingpong_kats(),
         "ring_kat.json": ring_kats(),
