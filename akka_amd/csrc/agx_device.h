@@ -29,6 +29,15 @@ struct DevParams {
   uint32_t* stopq;          // actors that returned Behaviors.stopped this step
   uint32_t* nstop;
   uint64_t* state;          // word-major SoA: state[w * n_local + l]
+  // CRDT state gossips (agx_crdt.h): snapshot rows, row-major, `pw` u32 each.
+  // heap = 2 x heap_rows rows (ping-pong by superstep parity); rx = rows
+  // received from other ranks this superstep (handle - heap_rows).
+  uint32_t* heap;
+  const uint32_t* rx;
+  uint32_t* heap_top;       // [2] rows allocated in heap[parity]
+  const uint32_t* step;     // superstep counter (bumped by the first kernel of a step)
+  uint32_t heap_rows, pw, gossip_f;
+  uint64_t gossip_seed;
 };
 
 // ------------------------------------------------------------------ RNG

@@ -121,6 +121,11 @@ struct agx_engine {
   uint32_t *d_zcdf = nullptr, *d_zperm = nullptr;
   uint64_t* d_row = nullptr;
   uint32_t* d_col = nullptr;
+  // CRDT state gossips (agx_crdt.h): snapshot heap, 2 x cap rows of pw u32
+  uint32_t pw = 0, gossip_f = 0;
+  uint64_t gossip_seed = 0;
+  uint32_t *d_heap = nullptr, *d_heap_top = nullptr, *d_step = nullptr;
+  uint32_t *d_rx = nullptr, *d_s2rows = nullptr;  // multi-rank: received rows / rows packed for sending
 
   DevMsgs A, B, scr, bl, em, stg, s1, s2;
   uint64_t stg_cap = 0;
@@ -251,6 +256,14 @@ DevParams make_params(agx_engine* e) {
   P.state = e->d_state;
   P.stopq = e->d_stopq;
   P.nstop = e->d_nstop;
+  P.heap = e->d_heap;
+  P.rx = e->d_rx;
+  P.heap_top = e->d_heap_top;
+  P.step = e->d_step;
+  P.heap_rows = (uint32_t)e->cap;
+  P.pw = e->pw;
+  P.gossip_f = e->gossip_f;
+  P.gossip_seed = e->gossip_seed;
   return P;
 }
 
@@ -317,6 +330,8 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     ca.alive = e->d_alive;
     ca.stopq = e->d_stopq;
     ca.nstop = e->d_nstop;
+    ca.step = e->pw ? e->d_step : nullptr;
+    ca.heap_top = e->d_heap_top;
     ca.cap = e->cap;
     ca.stride = e->nchunks;
     ca.nchunks = e->nchunks;
@@ -365,7 +380,10 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.dbg = e->d_dbg;
   {
     Scope s(e, K_APPLY);
-    hipLaunchKernelGGL(k_bucket_apply, dim3(grid_for(e->nb, 4096)), dim3(kBThreads), 0, e->stream, ba);
+    if (e->pw)  // CRDT kinds registered: the variant with state gossips
+      hipLaunchKernelGGL(k_bucket_apply<true>, dim3(grid_for(e->nb, 4096)), dim3(kBThreads), 0, e->stream, ba);
+    else
+      hipLaunchKernelGGL(k_bucket_apply<false>, dim3(grid_for(e->nb, 4096)), dim3(kBThreads), 0, e->stream, ba);
   }
   HIP_TRY(hipGetLastError());
   return AGX_OK;
@@ -425,6 +443,8 @@ agx_status phase1(agx_engine* e) {
   m.stopq = e->d_stopq;
   m.nstop = e->d_nstop;
   m.stats = e->d_stats;
+  m.step = e->pw ? e->d_step : nullptr;
+  m.heap_top = e->d_heap_top;
   m.cap0 = e->cap;
   m.cap1 = e->cap_emit;
   {
@@ -433,6 +453,11 @@ agx_status phase1(agx_engine* e) {
     hipLaunchKernelGGL(k_mcompact_copy, dim3(grid_for(2 * e->nb, 4096)), dim3(kThreads), 0, e->stream, m);
   }
   AGX_TRY(launch_dense_pass(e, e->s1, e->s2, e->d_total + 1, kOwnerShift, std::max<uint32_t>(1, ceil_log2(e->R))));
+  if (e->pw) {
+    Scope s(e, K_MCOMPACT);
+    hipLaunchKernelGGL(k_pack_rows, dim3(grid_for(e->cap_emit / kThreads + 1, 2048)), dim3(kThreads), 0, e->stream,
+                       e->s2.c(), e->d_total, make_params(e), e->d_s2rows);
+  }
   hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(64), 0, e->stream, e->d_tot, e->d_total, e->d_cvec, e->R,
                      e->n_staged_dev);
   HIP_TRY(hipGetLastError());
@@ -600,6 +625,17 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
   return st;
 }
 
+// received state gossips -> rx rows (single kernel over the received range)
+agx_status fix_rx(agx_engine* e, const Plan& p) {
+  if (!e->pw || !p.n_recv) return AGX_OK;
+  const uint32_t lo = (uint32_t)p.n_bl, hi = (uint32_t)(p.n_bl + p.n_recv);
+  const uint32_t slo = (uint32_t)p.recv_off[e->rank], shi = (uint32_t)(p.recv_off[e->rank] + p.recv_cnt[e->rank]);
+  hipLaunchKernelGGL(k_fix_rx, dim3(grid_for(p.n_recv / kThreads + 1, 2048)), dim3(kThreads), 0, e->stream, e->A.m(),
+                     lo, hi, slo, shi, (uint32_t)e->cap);
+  HIP_TRY(hipGetLastError());
+  return AGX_OK;
+}
+
 agx_status exchange_rccl(agx_engine* e, Plan& p) {
   NCCL_TRY(ncclGroupStart());
   for (uint32_t q = 0; q < e->R; ++q) {
@@ -608,12 +644,16 @@ agx_status exchange_rccl(agx_engine* e, Plan& p) {
       NCCL_TRY(ncclSend(e->s2.key + o, n, ncclUint32, (int)q, e->comm, e->stream));
       NCCL_TRY(ncclSend(e->s2.src + o, n, ncclUint32, (int)q, e->comm, e->stream));
       NCCL_TRY(ncclSend(e->s2.pay + o, n, ncclUint32, (int)q, e->comm, e->stream));
+      if (e->pw && q != e->rank)
+        NCCL_TRY(ncclSend(e->d_s2rows + o * e->pw, n * e->pw, ncclUint32, (int)q, e->comm, e->stream));
     }
     if (p.recv_cnt[q]) {
       const uint64_t o = p.recv_off[q], n = p.recv_cnt[q];
       NCCL_TRY(ncclRecv(e->A.key + o, n, ncclUint32, (int)q, e->comm, e->stream));
       NCCL_TRY(ncclRecv(e->A.src + o, n, ncclUint32, (int)q, e->comm, e->stream));
       NCCL_TRY(ncclRecv(e->A.pay + o, n, ncclUint32, (int)q, e->comm, e->stream));
+      if (e->pw && q != e->rank)
+        NCCL_TRY(ncclRecv(e->d_rx + o * e->pw, n * e->pw, ncclUint32, (int)q, e->comm, e->stream));
     }
   }
   NCCL_TRY(ncclGroupEnd());
@@ -640,9 +680,40 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
       Scope sc(e, K_EXCHANGE);
       AGX_TRY(exchange_rccl(e, p));
     }
+    AGX_TRY(fix_rx(e, p));
     AGX_TRY(phase2(e, p.n_bl + p.n_recv + p.n_staged, p.n_bl + p.n_recv));
   }
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return AGX_OK;
+}
+
+void drop_graphs(agx_engine* e) {
+  if (e->g1) hipGraphExecDestroy(e->g1);
+  if (e->gG) hipGraphExecDestroy(e->gG);
+  e->g1 = e->gG = nullptr;
+}
+
+// First CRDT kind (or a wider one): size the snapshot heap for `kind`'s rows.
+agx_status enable_crdt(agx_engine* e, uint32_t kind) {
+  const uint32_t words = kind == AGX_KIND_GCOUNTER ? AGX_GCOUNTER_WORDS
+                         : kind == AGX_KIND_PNCOUNTER ? AGX_PNCOUNTER_WORDS : AGX_ORSET_WORDS;
+  if (e->W < words) return set_err(AGX_EINVAL, "behaviour kind %u needs n_words >= %u", kind, words);
+  const uint32_t pw = 2 * words;
+  if (pw <= e->pw) return AGX_OK;
+  if (e->started) return set_err(AGX_ESTATE, "register CRDT kinds before the first agx_run");
+  if (2 * e->cap >= (1ull << 30)) return set_err(AGX_EINVAL, "CRDT kinds need msg_capacity < 2^29");
+  hipFree(e->d_heap);
+  hipFree(e->d_rx);
+  hipFree(e->d_s2rows);
+  e->d_heap = e->d_rx = e->d_s2rows = nullptr;
+  e->pw = 0;
+  AGX_TRY(dalloc(&e->d_heap, 2 * e->cap * pw));
+  if (e->R > 1) {
+    AGX_TRY(dalloc(&e->d_rx, e->cap * pw));
+    AGX_TRY(dalloc(&e->d_s2rows, e->cap_emit * pw));
+  }
+  e->pw = pw;
+  drop_graphs(e);
   return AGX_OK;
 }
 
@@ -785,6 +856,10 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(dalloc(&e->d_n, 4));
   CREATE_TRY(dalloc(&e->d_total, 4));
   CREATE_TRY(dalloc(&e->d_stats, ST_N));
+  CREATE_TRY(dalloc(&e->d_heap_top, 2));
+  CREATE_TRY(dalloc(&e->d_step, 1));
+  CREATE_TRY(hipMemset(e->d_heap_top, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipMemset(e->d_step, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_inflight, 1));
   CREATE_TRY(dalloc(&e->d_cvec, AGX_MAX_RANKS + 2));
   CREATE_TRY(dalloc(&e->d_cmat, (uint64_t)AGX_MAX_RANKS * (AGX_MAX_RANKS + 2)));
@@ -816,6 +891,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);
+  hipFree(e->d_heap); hipFree(e->d_heap_top); hipFree(e->d_step); hipFree(e->d_rx); hipFree(e->d_s2rows);
   if (e->h_pin) hipHostFree(e->h_pin);
   if (e->h_pin64) hipHostFree(e->h_pin64);
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
@@ -833,6 +909,7 @@ agx_status agx_register_range(agx_engine* e, uint64_t first_id, uint64_t count, 
   if ((kind == AGX_KIND_FORWARD_RR || kind == AGX_KIND_STOP_AFTER) && e->W < 2)
     return set_err(AGX_EINVAL, "behaviour kind %u needs n_words >= 2", kind);
   if (init && stride < e->W * 8ull) return set_err(AGX_EINVAL, "state_stride smaller than n_words*8");
+  if (kind >= AGX_KIND_GCOUNTER && kind <= AGX_KIND_ORSET) AGX_TRY(enable_crdt(e, kind));
   const uint8_t* ib = (const uint8_t*)init;
   for (uint64_t i = 0; i < count; ++i) {
     uint64_t id = first_id + i, l;
@@ -855,9 +932,19 @@ agx_status agx_register_range(agx_engine* e, uint64_t first_id, uint64_t count, 
   return AGX_OK;
 }
 
+agx_status agx_set_gossip(agx_engine* e, uint32_t fanout, uint64_t seed) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  if (fanout + 1 > e->kmax) return set_err(AGX_EINVAL, "gossip fanout %u needs max_emit >= %u", fanout, fanout + 1);
+  e->gossip_f = fanout;
+  e->gossip_seed = seed;
+  drop_graphs(e);  // behaviour parameters are captured in the superstep graphs
+  return AGX_OK;
+}
+
 agx_status agx_set_ring(agx_engine* e, uint32_t stride) {
   if (!e) return set_err(AGX_EINVAL, "null engine");
   e->ring_stride = stride;
+  drop_graphs(e);
   return AGX_OK;
 }
 
@@ -878,6 +965,7 @@ agx_status agx_set_fanout(agx_engine* e, uint32_t k, uint64_t seed, const uint32
   e->fan_k = k;
   e->fan_seed = seed;
   e->zipf_n = n;
+  drop_graphs(e);
   return AGX_OK;
 }
 
@@ -903,6 +991,7 @@ agx_status agx_set_graph(agx_engine* e, const uint64_t* row_ptr, const uint32_t*
   HIP_TRY(hipMemcpy(e->d_row, row.data(), row.size() * 8, hipMemcpyHostToDevice));
   if (!c.empty()) HIP_TRY(hipMemcpy(e->d_col, c.data(), c.size() * 4, hipMemcpyHostToDevice));
   e->graph_set = true;
+  drop_graphs(e);
   return AGX_OK;
 }
 
@@ -920,9 +1009,12 @@ agx_status agx_stage_tells(agx_engine* e, const uint32_t* dst, const uint32_t* s
       if ((r >> kOwnerShift) != e->rank) continue;
       key = r;
     }
+    const uint32_t sv = src ? src[i] : AGX_NO_SENDER;
+    if ((sv & AGX_WIDE_BIT) && sv != AGX_NO_SENDER)
+      return set_err(AGX_EINVAL, "tell %zu: sender %u is not an actor id (bit 31 tags CRDT state gossips)", i, sv);
     e->staged_total++;
     e->hs_key.push_back(key);
-    e->hs_src.push_back(src ? src[i] : AGX_NO_SENDER);
+    e->hs_src.push_back(sv);
     e->hs_pay.push_back(payload[i]);
   }
   if (e->hs_key.size() + e->n_staged_dev > e->cap) return set_err(AGX_ECAPACITY, "too many staged tells");
@@ -934,6 +1026,7 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
   AGX_TRY(ensure_dev(e));
   if (e->R > 1 && !e->comm) return set_err(AGX_ESTATE, "n_ranks > 1 needs agx_comm_init (or agx_group_run)");
   AGX_TRY(prepare_run(e));
+  e->started = true;
   if (e->R > 1) {
     AGX_TRY(run_multi_rccl(e, max_supersteps));
   } else {
@@ -1016,6 +1109,7 @@ agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_steps, agx_
       return set_err(AGX_EINVAL, "group engines must be ranks 0..n-1 of one population");
     AGX_TRY(ensure_dev(engs[i]));
     AGX_TRY(prepare_run(engs[i]));
+    engs[i]->started = true;
   }
   const uint32_t S = n + 2;
   std::vector<uint64_t> mat((size_t)n * S);
@@ -1046,7 +1140,11 @@ agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_steps, agx_
         HIP_TRY(hipMemcpyAsync(r->A.key + ro, snd->s2.key + so, cnt * 4, hipMemcpyDeviceToDevice, r->stream));
         HIP_TRY(hipMemcpyAsync(r->A.src + ro, snd->s2.src + so, cnt * 4, hipMemcpyDeviceToDevice, r->stream));
         HIP_TRY(hipMemcpyAsync(r->A.pay + ro, snd->s2.pay + so, cnt * 4, hipMemcpyDeviceToDevice, r->stream));
+        if (r->pw && q != i)
+          HIP_TRY(hipMemcpyAsync(r->d_rx + ro * r->pw, snd->d_s2rows + so * snd->pw, cnt * r->pw * 4ull,
+                                 hipMemcpyDeviceToDevice, r->stream));
       }
+      AGX_TRY(fix_rx(r, plans[i]));
     }
     for (uint32_t i = 0; i < n; ++i) {
       Plan& p = plans[i];

@@ -20,6 +20,7 @@
 //
 // Envelopes are SoA u32 {key, src, payload} = 12 B.
 #pragma once
+#include "agx_crdt.h"
 #include "agx_device.h"
 
 namespace agx {
@@ -55,6 +56,16 @@ struct CMsgs {
 };
 
 __device__ __forceinline__ uint32_t div_up(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+// A new superstep begins: bump the step counter and reset the snapshot rows of
+// heap[step & 1] (their gossips were consumed or copied forward two steps ago).
+__device__ __forceinline__ void begin_step(uint32_t* step, uint32_t* heap_top) {
+  if (threadIdx.x == 0 && step) {
+    const uint32_t s = *step + 1u;
+    *step = s;
+    heap_top[s & 1u] = 0u;
+  }
+}
 
 // Commit Behaviors.stopped results of the previous apply: alive[l] = 0.
 // (k_bucket_apply never writes `alive`, so every block classifies against the
@@ -123,6 +134,8 @@ struct ChunkSortArgs {
   uint8_t* alive;      // stop commit
   const uint32_t* stopq;
   uint32_t* nstop;
+  uint32_t* step;      // CRDT heap parity (null when no CRDT kind is registered)
+  uint32_t* heap_top;
   uint64_t cap;
   uint32_t stride, nchunks, shift, bits;
 };
@@ -132,7 +145,10 @@ struct ChunkSortArgs {
 __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs a) {
   __shared__ uint32_t scratch[kWaves + 1];
   __shared__ uint32_t s_run;
-  if (blockIdx.x == 0) commit_stops(a.alive, a.stopq, a.nstop);
+  if (blockIdx.x == 0) {
+    begin_step(a.step, a.heap_top);
+    commit_stops(a.alive, a.stopq, a.nstop);
+  }
   const uint32_t d = blockIdx.x;
   if (d >= (1u << a.bits)) return;
   uint32_t* row = a.hist + (size_t)d * a.stride;
@@ -487,6 +503,23 @@ struct Emitter {
       atomicAdd(&nh[((key & kLocalMask) >> nh_shift) & nh_mask], 1u);
     }
   }
+  // CRDT state gossip to a known actor: the sender field carries the wide tag, payload = row handle
+  __device__ __forceinline__ void wide(uint32_t dst, uint32_t h) {
+    ++n_all;
+    ++n_valid;
+    if (kWrite) {
+      const uint32_t key = (P->R > 1) ? P->route[dst] : dst;
+      out.key[pos] = key;
+      out.src[pos] = self | AGX_WIDE_BIT;
+      out.pay[pos] = h;
+      ++pos;
+      atomicAdd(&nh[((key & kLocalMask) >> nh_shift) & nh_mask], 1u);
+    }
+  }
+  __device__ __forceinline__ void count(uint32_t k) {
+    n_all += k;
+    n_valid += k;
+  }
 };
 
 constexpr int kBThreads = 512;                 // bucket_apply block: 8 waves
@@ -577,7 +610,7 @@ struct BucketLds {
 
 // After the in-bucket sort: classification, queued copy, behaviour apply, emission.
 // kLds: sorted items are in LDS (fast path) or in the global scratch copy.
-template <bool kLds>
+template <bool kLds, bool kWide>
 __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t lo,
                                               uint32_t cnt, uint32_t a0, uint32_t na) {
   const DevParams& P = a.P;
@@ -590,6 +623,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   uint32_t* blpre = reinterpret_cast<uint32_t*>(L.U);
   uint64_t* w0s = L.U;
   uint64_t* w1s = L.U + kBucket;
+  CrdtHeap H{};
+  if (kWide) H = crdt_heap(P);
 
   AGX_STAMP(a, 3);
   // ---- classification per actor (blocked): drained / queued (backlog) / dead letters
@@ -630,11 +665,30 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       const uint32_t p = q - L.seg[la];
       const uint32_t len = L.seg[la + 1] - L.seg[la];
       const uint32_t keep = (C == 0 || len < C) ? len : C;
-      if (L.alive[la] && p >= T && p < keep) {
+      const bool queued = L.alive[la] && p >= T && p < keep;
+      const uint32_t sv = isrc(q);
+      uint32_t pv = ipay(q);
+      if (kWide) {  // a queued state gossip outlives its row's superstep: copy the row forward
+        const bool need = queued && is_wide(sv);
+        const uint64_t m = __ballot(need);
+        if (m) {
+          const uint32_t lane = lane_id(), leader = (uint32_t)__builtin_ctzll(m);
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(H.top, (uint32_t)__popcll(m));
+          base = __shfl(base, (int)leader, kWave);
+          if (need) {
+            const uint32_t h = base + (uint32_t)__popcll(m & lanemask_lt());
+            if (h < H.rows) copy_row(H.wrow(h), H.row(pv & kHandleMask), H.pw);
+            else atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
+            pv = (pv & ~kHandleMask) | h;
+          }
+        }
+      }
+      if (queued) {
         const uint32_t o = lo + blpre[la] + (p - T);
         a.bl.key[o] = key;
-        a.bl.src[o] = isrc(q);
-        a.bl.pay[o] = ipay(q);
+        a.bl.src[o] = sv;
+        a.bl.pay[o] = pv;
       }
     }
     if (tid == 0) {  // all queued mail is in this bucket: one bin of the next first-pass histogram
@@ -659,7 +713,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   }
   uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0, emtot = 0;
   const uint64_t embase = (uint64_t)lo * a.kmax;  // this bucket's slice of the tell arena
-  if (kLds && a.kmax == 1) {
+  if (kLds && !kWide && a.kmax == 1) {
     // ---- single pass (each message emits <= 1 tell): drain + apply; tells are staged in LDS over the
     // actor's own, already consumed, inbox slots (tell e of an actor <= message index q that made it)
     uint32_t ecl[kBAct];
@@ -724,6 +778,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       }
     }
   } else {
+  uint32_t nrows_t = 0;  // snapshot rows this thread's actors will write (kWide)
   // ---- phase A: emissions per actor (drain min(len, T) messages in order)
   #pragma unroll 1
     for (int j = 0; j < kBAct; ++j) {
@@ -735,9 +790,16 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       Emitter<false> em{&P, {}, 0, self, 0, 0, L.nh, a.nx_shift, nhmask};
       uint64_t wv[2] = {w0s[la], w1s[la]};  // behaviours read/write state words 0-1 only
       const uint32_t nd = min(len, T);
-      for (uint32_t q = 0; q < nd; ++q) {
-        const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, isrc(s0 + q), ipay(s0 + q), em);
-        if (r == AGX_RES_STOPPED) break;
+      const uint32_t kd = L.kind[la];
+      if (kWide && is_crdt(kd)) {
+        for (uint32_t q = 0; q < nd; ++q) em.count(crdt_count(P, isrc(s0 + q), ipay(s0 + q), &nrows_t));
+      } else {
+        for (uint32_t q = 0; q < nd; ++q) {
+          const uint32_t sv = isrc(s0 + q);
+          if (kWide && is_wide(sv)) continue;  // not in this behaviour's protocol: unhandled, no tells
+          const uint32_t r = apply_msg(P, kd, self, l, wv, sv, ipay(s0 + q), em);
+          if (r == AGX_RES_STOPPED) break;
+        }
       }
       L.ecnt[la] = em.n_valid;
     }
@@ -759,6 +821,18 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       }
       reinterpret_cast<uint4*>(L.ecnt)[tid] = make_uint4(o[0], o[1], o[2], o[3]);
     }
+    uint32_t row_cursor = 0;
+    if (kWide) {  // this block's snapshot rows: one heap allocation, thread ranges by scan
+      uint32_t rtot;
+      const uint32_t rex = block_excl_sum<kBThreads>(nrows_t, L.scratch, &rtot);
+      if (tid == 0) {
+        const uint32_t base = rtot ? atomicAdd(H.top, rtot) : 0u;
+        if (base + rtot > H.rows) atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
+        L.scratch[kBWaves] = base;
+      }
+      __syncthreads();
+      row_cursor = L.scratch[kBWaves] + rex;
+    }
     __syncthreads();
   
     AGX_STAMP(a, 6);
@@ -773,19 +847,33 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       Emitter<true> em{&P, a.em, embase + L.ecnt[la], self, 0, 0, L.nh, a.nx_shift, nhmask};
       uint64_t wv[2] = {w0s[la], w1s[la]};  // behaviours read/write state words 0-1 only
       const uint32_t nd = min(len, T);
+      const uint32_t kd = L.kind[la];
       ++nact;
-      for (uint32_t q = 0; q < nd; ++q) {
-        const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, isrc(s0 + q), ipay(s0 + q), em);
-        ++ndel;
-        if (r == AGX_RES_UNHANDLED) ++nunh;
-        if (r == AGX_RES_STOPPED) {
-          P.stopq[atomicAdd(P.nstop, 1u)] = l;
-          ndead += nd - q - 1;  // drained-but-unprocessed after the stop
-          break;
+      if (kWide && is_crdt(kd)) {
+        for (uint32_t q = 0; q < nd; ++q) {
+          const uint32_t r = crdt_apply(P, H, kd, self, l, isrc(s0 + q), ipay(s0 + q), row_cursor, em);
+          ++ndel;
+          if (r == AGX_RES_UNHANDLED) ++nunh;
         }
+      } else {
+        for (uint32_t q = 0; q < nd; ++q) {
+          const uint32_t sv = isrc(s0 + q);
+          ++ndel;
+          if (kWide && is_wide(sv)) {
+            ++nunh;
+            continue;
+          }
+          const uint32_t r = apply_msg(P, kd, self, l, wv, sv, ipay(s0 + q), em);
+          if (r == AGX_RES_UNHANDLED) ++nunh;
+          if (r == AGX_RES_STOPPED) {
+            P.stopq[atomicAdd(P.nstop, 1u)] = l;
+            ndead += nd - q - 1;  // drained-but-unprocessed after the stop
+            break;
+          }
+        }
+        P.state[l] = wv[0];
+        if (P.W > 1) P.state[(size_t)P.n_local + l] = wv[1];
       }
-      P.state[l] = wv[0];
-      if (P.W > 1) P.state[(size_t)P.n_local + l] = wv[1];
       nall += em.n_all;
       ndead += em.n_all - em.n_valid;
     }
@@ -822,6 +910,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   AGX_STAMP(a, 8);
 }
 
+template <bool kWide>
 __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_key[kBucket];
   __shared__ __attribute__((aligned(16))) uint32_t s_src[kBucket];
@@ -969,7 +1058,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         __syncthreads();
       }
       AGX_STAMP(a, 2);
-      bucket_finish<true>(a, L, b, lo, cnt, a0, na);
+      bucket_finish<true, kWide>(a, L, b, lo, cnt, a0, na);
     } else {
       // ---- general path (skewed bucket): counting sort into the global scratch copy
       uint32_t* s_run = s_key;  // LDS items are unused on this path
@@ -1043,7 +1132,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] += s_tmp[la];
         __syncthreads();
       }
-      bucket_finish<false>(a, L, b, lo, cnt, a0, na);
+      bucket_finish<false, kWide>(a, L, b, lo, cnt, a0, na);
     }
   }
 }
@@ -1082,12 +1171,15 @@ struct McompactArgs {
   const uint32_t* stopq;
   uint32_t* nstop;
   uint64_t* stats;
+  uint32_t* step;
+  uint32_t* heap_top;
   uint64_t cap0, cap1;
 };
 
 __global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactArgs a) {
   __shared__ uint32_t scratch[kScanThreads / kWave + 1];
   __shared__ uint64_t s_run[2];
+  begin_step(a.step, a.heap_top);
   commit_stops(a.alive, a.stopq, a.nstop);
   const int tid = threadIdx.x;
   if (tid == 0) s_run[0] = s_run[1] = 0;
@@ -1151,6 +1243,30 @@ __global__ void k_pack_counts(const uint32_t* tot, const uint32_t* d_total, uint
     vec[R] = d_total[0];  // backlog kept locally
     vec[R + 1] = n_staged;
   }
+}
+
+}  // namespace agx
+
+namespace agx {
+
+// Multi-rank CRDT rows.  After the owner partition, the rows of state gossips that
+// leave this rank are packed in the order of the partitioned tells (row i <-> tell i);
+// they travel beside the envelopes and land in `rx` at the receiver's sort-input index.
+__global__ void __launch_bounds__(kThreads) k_pack_rows(CMsgs s2, const uint32_t* d_total, DevParams P,
+                                                        uint32_t* out) {
+  const uint32_t n = d_total[1];
+  const CrdtHeap H = crdt_heap(P);
+  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads)
+    if (is_wide(s2.src[i]) && (s2.key[i] >> kOwnerShift) != P.rank)
+      copy_row(out + (size_t)i * H.pw, H.row(s2.pay[i] & kHandleMask), H.pw);
+}
+
+// Received gossips from other ranks [lo, hi) minus this rank's own segment: point
+// their handles at the rx rows (handle = heap_rows + sort-input index).
+__global__ void __launch_bounds__(kThreads) k_fix_rx(Msgs a, uint32_t lo, uint32_t hi, uint32_t self_lo,
+                                                     uint32_t self_hi, uint32_t heap_rows) {
+  for (uint32_t i = lo + blockIdx.x * kThreads + threadIdx.x; i < hi; i += gridDim.x * kThreads)
+    if ((i < self_lo || i >= self_hi) && is_wide(a.src[i])) a.pay[i] = (a.pay[i] & ~kHandleMask) | (heap_rows + i);
 }
 
 }  // namespace agx

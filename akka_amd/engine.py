@@ -26,6 +26,29 @@ class Kind:
     STOP_AFTER = 5
     PINGPONG = 6
     EVEN = 7
+    GCOUNTER = 8      # Replicator-style replicas (akka-distributed-data), include/akka_gpu.h "CRDT behaviours"
+    PNCOUNTER = 9
+    ORSET = 10
+
+
+CRDT_NODES = 8
+ORSET_ELEMS = 64
+CRDT_WORDS = {Kind.GCOUNTER: 8, Kind.PNCOUNTER: 16, Kind.ORSET: 260}
+WIDE_BIT = 0x80000000
+
+
+class Op:
+    """Control-tell opcodes of the CRDT kinds: payload = (op << 24) | arg."""
+    INCREMENT = 1
+    DECREMENT = 2
+    ADD = 3
+    REMOVE = 4
+    CLEAR = 5
+    GOSSIP = 6
+
+    @staticmethod
+    def make(op: int, arg: int = 0) -> int:
+        return ((op & 0xFF) << 24) | (arg & 0xFFFFFF)
 
 
 @dataclass
@@ -129,6 +152,9 @@ class GpuEngine:
 
     def set_ring(self, stride: int = 1) -> None:
         check(self.lib.agx_set_ring(self._h, stride))
+
+    def set_gossip(self, fanout: int, seed: int) -> None:
+        check(self.lib.agx_set_gossip(self._h, fanout, seed))
 
     def set_fanout(self, k: int, seed: int, cdf, perm) -> None:
         cdf = _u32(cdf)

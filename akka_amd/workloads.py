@@ -12,7 +12,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .engine import Kind, NO_SENDER
+from .engine import CRDT_NODES, CRDT_WORDS, Kind, NO_SENDER, Op
 
 SEED = 0x5EED
 M64 = (1 << 64) - 1
@@ -36,6 +36,7 @@ class Workload:
     capacity: int
     ranges: list = field(default_factory=list)  # (first, count, kind, init_state or None)
     ring_stride: int | None = None
+    gossip: tuple | None = None  # (fanout, seed)
     fanout: tuple | None = None  # (k, seed, cdf, perm)
     graph: tuple | None = None   # (row_ptr, col)
     tells: tuple | None = None   # (dst, src, payload)
@@ -49,6 +50,8 @@ class Workload:
             target.register_range(first, count, kind, init)
         if self.ring_stride is not None:
             target.set_ring(self.ring_stride)
+        if self.gossip is not None:
+            target.set_gossip(*self.gossip)
         if self.fanout is not None:
             target.set_fanout(*self.fanout)
         if self.graph is not None:
@@ -102,6 +105,75 @@ def zipf_fanout(n: int = 10_000_000, k: int = 4, ttl: int = 3, root_every: int =
     src = np.full(roots.size, NO_SENDER, np.uint32)
     return Workload("zipf_fanout", n, 2, k, throughput, capacity, [(0, n, Kind.FANOUT, None)],
                     fanout=(k, seed, cdf, perm), tells=(roots, src, pay.astype(np.uint32)))
+
+
+# ------------------------------------------------------------------ C4
+def crdt_ops(n: int, kind: int, ops_per_actor: int, seed: int = SEED):
+    """Round-0 local updates, one row per actor: INCREMENT (GCounter), INCREMENT/DECREMENT
+    (PNCounter), ADD/REMOVE of one of the 64 elements, 3:1 (ORSet)."""
+    a = np.arange(n, dtype=np.uint64)
+    out = np.zeros((n, ops_per_actor), np.uint32)
+    for j in range(ops_per_actor):
+        r = splitmix64_np((a << np.uint64(8)) ^ np.uint64(j) ^ np.uint64(seed * 11))
+        lo = (r & np.uint64(0xFFFF)).astype(np.uint32)
+        hi = ((r >> np.uint64(32)) & np.uint64(0xFF)).astype(np.uint32)
+        if kind == Kind.GCOUNTER:
+            op, arg = np.full(n, Op.INCREMENT, np.uint32), lo % 100 + 1
+        elif kind == Kind.PNCOUNTER:
+            op = np.where(hi % 3 == 0, Op.DECREMENT, Op.INCREMENT).astype(np.uint32)
+            arg = lo % 100 + 1
+        else:
+            op = np.where(hi % 4 == 0, Op.REMOVE, Op.ADD).astype(np.uint32)
+            arg = lo % 64
+        out[:, j] = (op << np.uint32(24)) | arg
+    return out
+
+
+def crdt_gossip(n: int = 1_000_000, kind: int = Kind.GCOUNTER, rounds: int = 32, fanout: int = 2,
+                ops_per_writer: int = 16, throughput: int = 5, seed: int = SEED, capacity: int = 0) -> Workload:
+    """C4: Replicator-style replicas.  Actors 0..7 are the writers of node slots 0..7
+    (one writer per UniqueAddress, as the CRDTs require) and first apply `ops_per_writer`
+    local updates (host tells); then every actor runs `rounds` GossipTicks: each tick sends
+    its full state to `fanout` random peers, which merge it
+    (DD/Replicator.scala:2029-2064,2118-2133).  The population converges to the merge
+    of the 8 writers' values."""
+    nw = min(n, CRDT_NODES)
+    ops = crdt_ops(nw, kind, ops_per_writer, seed).reshape(-1)
+    odst = np.repeat(np.arange(nw, dtype=np.uint32), ops_per_writer)
+    tdst = np.arange(n, dtype=np.uint32)
+    tick = np.full(n, Op.make(Op.GOSSIP, rounds - 1), np.uint32)
+    dst = np.concatenate([odst, tdst])
+    pay = np.concatenate([ops, tick])
+    src = np.full(dst.size, NO_SENDER, np.uint32)
+    return Workload(f"crdt_gossip_{kind}", n, CRDT_WORDS[kind], fanout + 1, throughput, capacity,
+                    [(0, n, kind, None)], gossip=(fanout, seed), tells=(dst, src, pay))
+
+
+def crdt_mixed(n: int = 4096, rounds: int = 4, seed: int = 3, throughput: int = 3, capacity: int = 0) -> Workload:
+    """GCounter / PNCounter / ORSet replicas beside COUNTER and EVEN actors: gossips that
+    land on a non-CRDT actor (or an ORSet op on a counter) are Behaviors.unhandled."""
+    kinds = [Kind.GCOUNTER, Kind.PNCOUNTER, Kind.ORSET, Kind.COUNTER, Kind.EVEN]
+    per = n // len(kinds)
+    ranges, dsts, pays = [], [], []
+    rng = np.random.default_rng(seed)
+    for i, kd in enumerate(kinds):
+        first = i * per
+        count = per if i < len(kinds) - 1 else n - first
+        ranges.append((first, count, kd, None))
+        ids = np.arange(first, first + count, dtype=np.uint32)
+        if kd in CRDT_WORDS:
+            ops = crdt_ops(count, kd, 3, seed + i)
+            tick = np.full((count, 1), Op.make(Op.GOSSIP, rounds - 1), np.uint32)
+            dsts.append(np.repeat(ids, 4))
+            pays.append(np.concatenate([ops, tick], axis=1).reshape(-1))
+    m = n
+    dsts.append(rng.integers(0, n, m).astype(np.uint32))  # random control ops everywhere
+    pays.append(((rng.integers(1, 8, m).astype(np.uint32) << 24) | rng.integers(0, 70, m).astype(np.uint32)))
+    dst = np.concatenate(dsts)
+    pay = np.concatenate(pays)
+    src = np.full(dst.size, NO_SENDER, np.uint32)
+    return Workload("crdt_mixed", n, CRDT_WORDS[Kind.ORSET], 3, throughput, capacity, ranges, gossip=(2, seed),
+                    tells=(dst, src, pay))
 
 
 # ------------------------------------------------------------------ C5

@@ -70,7 +70,11 @@ enum agx_behavior_kind {
   AGX_KIND_STOP_AFTER = 5, /* w0 += 1; w0 >= w1 -> Behaviors.stopped                  */
   AGX_KIND_PINGPONG = 6,   /* BenchmarkActors.PingPong: reply to sender, stop at 0    */
   AGX_KIND_EVEN = 7,       /* odd payload -> Behaviors.unhandled; else w0 += 1         */
-  AGX_KIND_MAX = 8
+  /* Replicator-style CRDT replicas (akka-distributed-data), see "CRDT behaviours" below */
+  AGX_KIND_GCOUNTER = 8,   /* w[0..7]  = GCounter slots                                 */
+  AGX_KIND_PNCOUNTER = 9,  /* w[0..7]  = increments, w[8..15] = decrements              */
+  AGX_KIND_ORSET = 10,     /* w[0..259] = 64 x 8 u32 dots + 8 u32 version vector        */
+  AGX_KIND_MAX = 11
 };
 
 /* Behaviour results (ActorAdapter.next, TY/internal/adapter/ActorAdapter.scala:152-168) */
@@ -78,8 +82,44 @@ enum agx_behavior_kind {
 #define AGX_RES_STOPPED 1u
 #define AGX_RES_UNHANDLED 2u
 
-#define AGX_MAX_WORDS 8u
+#define AGX_MAX_WORDS 260u
 #define AGX_MAX_RANKS 16u
+
+/* --- CRDT behaviours ---------------------------------------------------------
+ * Each actor of a CRDT kind is one replica holding one data value; its node
+ * index (the UniqueAddress slot, akka-cluster/.../Member.scala:307-311) is
+ * id % AGX_CRDT_NODES.  Two message shapes:
+ *  - control tells: payload = (op << 24) | arg, from the host or from itself
+ *      AGX_OP_INCREMENT  arg = n    GCounter.increment / PNCounter.increment
+ *                                   (DD/GCounter.scala:97-111, DD/PNCounter.scala:161-176)
+ *      AGX_OP_DECREMENT  arg = n    PNCounter.decrement (:167-176)
+ *      AGX_OP_ADD        arg = e    ORSet.add (DD/ORSet.scala:339-351), e < 64
+ *      AGX_OP_REMOVE     arg = e    ORSet.remove (:380-387)
+ *      AGX_OP_CLEAR                 ORSet.clear (:404-412)
+ *      AGX_OP_GOSSIP     arg = k    Replicator GossipTick (DD/Replicator.scala:1316,2029-2061):
+ *                                   send the full state to `fanout` random peers
+ *                                   and, if k > 0, GOSSIP(k-1) to itself
+ *  - state gossip: a full-state snapshot; the receiver merges it
+ *    (GCounter.merge :113-125, PNCounter.merge :178, ORSet.merge :427-452).
+ *    On the wire the sender field carries AGX_WIDE_BIT and the payload is
+ *    (data type << 30) | an engine-internal handle to the snapshot (type =
+ *    kind - AGX_KIND_GCOUNTER).  A gossip of another data type, and any state
+ *    gossip reaching a non-CRDT behaviour, is Behaviors.unhandled.  Host
+ *    tells are always control tells.
+ * Unknown ops are Behaviors.unhandled.                                       */
+#define AGX_CRDT_NODES 8u
+#define AGX_ORSET_ELEMS 64u
+#define AGX_GCOUNTER_WORDS 8u
+#define AGX_PNCOUNTER_WORDS 16u
+#define AGX_ORSET_WORDS 260u /* (64 * 8 + 8) u32 */
+#define AGX_WIDE_BIT 0x80000000u
+#define AGX_OP_INCREMENT 1u
+#define AGX_OP_DECREMENT 2u
+#define AGX_OP_ADD 3u
+#define AGX_OP_REMOVE 4u
+#define AGX_OP_CLEAR 5u
+#define AGX_OP_GOSSIP 6u
+#define AGX_OP(op, arg) (((uint32_t)(op) << 24) | ((uint32_t)(arg) & 0xFFFFFFu))
 
 typedef struct agx_cfg {
   uint32_t abi_version;   /* must be AGX_ABI_VERSION                                   */
@@ -127,6 +167,10 @@ agx_status agx_set_ring(agx_engine* eng, uint32_t stride);
  * (non-decreasing, cdf[n-1] = 0xFFFFFFFF); perm maps rank -> actor id.      */
 agx_status agx_set_fanout(agx_engine* eng, uint32_t k, uint64_t seed, const uint32_t* cdf,
                           const uint32_t* perm, uint64_t n);
+/* CRDT gossip: each GOSSIP tick sends the replica's state to `fanout` peers
+ * drawn uniformly from the other actors with the counter RNG (seed, self,
+ * countdown, j) — Replicator.selectRandomNode (DD/Replicator.scala:2063-2064). */
+agx_status agx_set_gossip(agx_engine* eng, uint32_t fanout, uint64_t seed);
 /* Out-edge lists in CSR over GLOBAL ids: row_ptr[n_actors+1], col[row_ptr[n]].  */
 agx_status agx_set_graph(agx_engine* eng, const uint64_t* row_ptr, const uint32_t* col);
 

@@ -29,9 +29,14 @@ typedef struct {
   uint64_t zipf_n;
   const uint64_t* row_ptr; /* global CSR */
   const uint32_t* col;
+  uint32_t gossip_f;       /* CRDT gossip fan-out */
+  uint64_t gossip_seed;
 } ref_params;
 
-typedef void (*ref_emit_fn)(void* ctx, uint32_t dst, uint32_t self, uint32_t payload);
+/* tell(dst, payload) from `self`; row != NULL = a CRDT state gossip carrying
+ * `row_words` u64 of snapshot (copied by the callee). */
+typedef void (*ref_emit_fn)(void* ctx, uint32_t dst, uint32_t self, uint32_t payload, const uint64_t* row,
+                            uint32_t row_words);
 
 static inline uint64_t ref_splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -57,8 +62,61 @@ static inline uint32_t ref_zipf_index(const uint32_t* cdf, uint64_t n, uint64_t 
   return (uint32_t)lo;
 }
 
+#include "crdt_ref.h"
+
+static inline int ref_is_wide(uint32_t src) { return (src & AGX_WIDE_BIT) && src != AGX_NO_SENDER; }
+
+static inline uint32_t ref_crdt_words(uint32_t kind) {
+  return kind == AGX_KIND_GCOUNTER ? AGX_GCOUNTER_WORDS
+         : kind == AGX_KIND_PNCOUNTER ? AGX_PNCOUNTER_WORDS
+         : kind == AGX_KIND_ORSET ? AGX_ORSET_WORDS : 0u;
+}
+
+/* One invoke of a CRDT replica (include/akka_gpu.h "CRDT behaviours"). */
+static inline uint32_t ref_apply_crdt(const ref_params* P, uint32_t kind, uint32_t a, uint64_t* w, uint32_t src,
+                                      uint32_t payload, const uint64_t* row, ref_emit_fn emit, void* ctx) {
+  const uint32_t node = a % AGX_CRDT_NODES;
+  if (ref_is_wide(src)) { /* state gossip: merge (Replicator.receiveGossip -> write, DD/Replicator.scala:2118-2133) */
+    if ((payload >> 30) != kind - AGX_KIND_GCOUNTER) return AGX_RES_UNHANDLED; /* another data type */
+    if (kind == AGX_KIND_ORSET) orset_merge(w, row);
+    else crdt_counter_merge(w, row, ref_crdt_words(kind));
+    return AGX_RES_SAME;
+  }
+  const uint32_t op = payload >> 24, arg = payload & 0xFFFFFFu;
+  switch (op) {
+    case AGX_OP_INCREMENT:
+      if (kind == AGX_KIND_ORSET) return AGX_RES_UNHANDLED;
+      w[node] += arg;
+      return AGX_RES_SAME;
+    case AGX_OP_DECREMENT:
+      if (kind != AGX_KIND_PNCOUNTER) return AGX_RES_UNHANDLED;
+      w[AGX_CRDT_NODES + node] += arg;
+      return AGX_RES_SAME;
+    case AGX_OP_ADD:
+    case AGX_OP_REMOVE:
+    case AGX_OP_CLEAR:
+      if (kind != AGX_KIND_ORSET || (op != AGX_OP_CLEAR && arg >= AGX_ORSET_ELEMS)) return AGX_RES_UNHANDLED;
+      if (op == AGX_OP_ADD) orset_add(w, node, arg);
+      else if (op == AGX_OP_REMOVE) orset_remove(w, arg);
+      else orset_clear(w);
+      return AGX_RES_SAME;
+    case AGX_OP_GOSSIP:
+      if (P->n > 1)
+        for (uint32_t j = 0; j < P->gossip_f; ++j)
+          emit(ctx, crdt_peer(P->gossip_seed, a, arg, j, P->n), a, (kind - AGX_KIND_GCOUNTER) << 30, w,
+               ref_crdt_words(kind));
+      if (arg > 0) emit(ctx, a, a, AGX_OP(AGX_OP_GOSSIP, arg - 1u), (const uint64_t*)0, 0u);
+      return AGX_RES_SAME;
+    default:
+      return AGX_RES_UNHANDLED;
+  }
+}
+
 static inline uint32_t ref_apply(const ref_params* P, uint32_t kind, uint32_t a, uint64_t* w, uint32_t src,
-                                 uint32_t payload, ref_emit_fn emit, void* ctx) {
+                                 uint32_t payload, const uint64_t* row, ref_emit_fn emit, void* ctx) {
+  if (kind >= AGX_KIND_GCOUNTER && kind <= AGX_KIND_ORSET)
+    return ref_apply_crdt(P, kind, a, w, src, payload, row, emit, ctx);
+  if (ref_is_wide(src)) return AGX_RES_UNHANDLED; /* a state gossip is not in this behaviour's protocol */
   switch (kind) {
     case AGX_KIND_COUNTER:
       w[0] += 1;
@@ -66,7 +124,7 @@ static inline uint32_t ref_apply(const ref_params* P, uint32_t kind, uint32_t a,
       return AGX_RES_SAME;
     case AGX_KIND_RING:
       w[0] += 1;
-      if (payload > 0) emit(ctx, (uint32_t)(((uint64_t)a + P->ring_stride) % P->n), a, payload - 1);
+      if (payload > 0) emit(ctx, (uint32_t)(((uint64_t)a + P->ring_stride) % P->n), a, payload - 1, 0, 0);
       return AGX_RES_SAME;
     case AGX_KIND_FANOUT: {
       w[0] += 1;
@@ -76,7 +134,7 @@ static inline uint32_t ref_apply(const ref_params* P, uint32_t kind, uint32_t a,
         for (uint32_t j = 0; j < P->fan_k; ++j) {
           uint64_t r = ref_fanout_rand(P->fan_seed, a, h, j);
           uint32_t d = P->zipf_perm[ref_zipf_index(P->zipf_cdf, P->zipf_n, r)];
-          emit(ctx, d, a, ((ttl - 1) << 28) | ((uint32_t)r & 0x0FFFFFFFu));
+          emit(ctx, d, a, ((ttl - 1) << 28) | ((uint32_t)r & 0x0FFFFFFFu), 0, 0);
         }
       return AGX_RES_SAME;
     }
@@ -87,7 +145,7 @@ static inline uint32_t ref_apply(const ref_params* P, uint32_t kind, uint32_t a,
         if (deg) {
           uint64_t e = b + (w[1] % deg);
           w[1] += 1;
-          emit(ctx, P->col[e], a, payload - 1);
+          emit(ctx, P->col[e], a, payload - 1, 0, 0);
         }
       }
       return AGX_RES_SAME;
@@ -100,7 +158,7 @@ static inline uint32_t ref_apply(const ref_params* P, uint32_t kind, uint32_t a,
        *   sender() ! Message; left -= 1                                       */
       uint32_t res = (w[0] == 0) ? AGX_RES_STOPPED : AGX_RES_SAME;
       if (P->W > 1) w[1] += 1;
-      emit(ctx, src, a, payload);
+      emit(ctx, src, a, payload, 0, 0);
       w[0] -= 1;
       return res;
     }

@@ -92,23 +92,49 @@ typedef struct {
   uint32_t dst, src, payload;
 } env_t;
 
+/* Envelopes; CRDT state gossips carry their snapshot inline (`rw` u64 per
+ * envelope in `rows`, allocated once a CRDT kind is registered). */
 typedef struct {
   env_t* v;
+  uint64_t* rows;
   uint64_t n, cap;
+  uint32_t rw;
 } envvec;
 
-static int ev_push(envvec* e, uint32_t d, uint32_t s, uint32_t p) {
+static int ev_push(envvec* e, uint32_t d, uint32_t s, uint32_t p, const uint64_t* row, uint32_t row_words) {
   if (e->n == e->cap) {
     uint64_t nc = e->cap ? e->cap * 2 : 1024;
     env_t* nv = (env_t*)realloc(e->v, nc * sizeof(env_t));
     if (!nv) return -1;
     e->v = nv;
+    if (e->rw) {
+      uint64_t* nr = (uint64_t*)realloc(e->rows, nc * e->rw * 8);
+      if (!nr) return -1;
+      e->rows = nr;
+    }
     e->cap = nc;
   }
   e->v[e->n].dst = d;
   e->v[e->n].src = s;
   e->v[e->n].payload = p;
+  if (e->rw) {
+    uint64_t* r = e->rows + e->n * e->rw;
+    uint32_t k = row ? (row_words < e->rw ? row_words : e->rw) : 0;
+    if (k) memcpy(r, row, (size_t)k * 8);
+    if (k < e->rw) memset(r + k, 0, (size_t)(e->rw - k) * 8);
+  }
   e->n++;
+  return 0;
+}
+
+/* enable inline snapshots of `rw` u64 per envelope (only before any mail exists) */
+static int ev_set_rw(envvec* e, uint32_t rw) {
+  if (rw <= e->rw) return 0;
+  if (e->n) return -1;
+  free(e->rows);
+  e->rows = e->cap ? (uint64_t*)calloc(e->cap * rw, 8) : (uint64_t*)0;
+  if (e->cap && !e->rows) return -1;
+  e->rw = rw;
   return 0;
 }
 
@@ -175,6 +201,7 @@ void bsp_destroy(bsp_sim* s) {
   free(s->kind); free(s->alive); free(s->state); free(s->order);
   free(s->zipf_cdf); free(s->zipf_perm); free(s->row_ptr); free(s->col);
   free(s->backlog.v); free(s->emitted.v); free(s->staged.v);
+  free(s->backlog.rows); free(s->emitted.rows); free(s->staged.rows);
   free(s);
 }
 
@@ -182,6 +209,11 @@ int bsp_register_range(bsp_sim* s, uint64_t first, uint64_t count, uint32_t kind
                        uint64_t stride_words) {
   if (first + count > s->n || kind >= AGX_KIND_MAX) return 1;
   if ((kind == AGX_KIND_FORWARD_RR || kind == AGX_KIND_STOP_AFTER) && s->W < 2) return 1;
+  uint32_t rw = ref_crdt_words(kind);
+  if (rw) {
+    if (s->W < rw) return 1;
+    if (ev_set_rw(&s->backlog, rw) || ev_set_rw(&s->emitted, rw) || ev_set_rw(&s->staged, rw)) return 1;
+  }
   for (uint64_t i = 0; i < count; ++i) {
     uint64_t a = first + i;
     s->kind[a] = (uint8_t)kind;
@@ -192,6 +224,11 @@ int bsp_register_range(bsp_sim* s, uint64_t first, uint64_t count, uint32_t kind
 }
 
 void bsp_set_ring(bsp_sim* s, uint32_t stride) { s->P.ring_stride = stride; }
+
+void bsp_set_gossip(bsp_sim* s, uint32_t fanout, uint64_t seed) {
+  s->P.gossip_f = fanout;
+  s->P.gossip_seed = seed;
+}
 
 int bsp_set_fanout(bsp_sim* s, uint32_t k, uint64_t seed, const uint32_t* cdf, const uint32_t* perm, uint64_t n) {
   s->P.fan_k = k;
@@ -224,18 +261,20 @@ int bsp_set_graph(bsp_sim* s, const uint64_t* row_ptr, const uint32_t* col) {
 int bsp_stage(bsp_sim* s, const uint32_t* dst, const uint32_t* src, const uint32_t* payload, uint64_t n) {
   for (uint64_t i = 0; i < n; ++i) {
     s->st.staged++;
+    uint32_t sv = src ? src[i] : AGX_NO_SENDER;
+    if (ref_is_wide(sv)) return 1; /* host tells are never state gossips */
     if (dst[i] >= s->n) { s->st.dead_letters++; continue; }
-    if (ev_push(&s->staged, dst[i], src ? src[i] : AGX_NO_SENDER, payload[i])) return 2;
+    if (ev_push(&s->staged, dst[i], sv, payload[i], 0, 0)) return 2;
   }
   return 0;
 }
 
 /* emit: tell(dst, payload) from `self`; unknown dst -> deadLetters now. */
-static void emit_cb(void* ctx, uint32_t dst, uint32_t self, uint32_t payload) {
+static void emit_cb(void* ctx, uint32_t dst, uint32_t self, uint32_t payload, const uint64_t* row, uint32_t rw) {
   bsp_sim* s = (bsp_sim*)ctx;
   s->st.emitted++;
   if (dst >= s->n) { s->st.dead_letters++; return; }
-  ev_push(&s->emitted, dst, self, payload);
+  ev_push(&s->emitted, dst, row ? (self | AGX_WIDE_BIT) : self, payload, row, rw);
 }
 
 /* One BSP superstep.  Returns 1 if any message was in flight. */
@@ -243,17 +282,22 @@ static int bsp_step(bsp_sim* s) {
   uint64_t total = s->backlog.n + s->emitted.n + s->staged.n;
   if (total == 0) return 0;
   /* inbox formation: stable counting sort of [backlog ++ emitted ++ staged] by dst */
+  const uint32_t rw = s->backlog.rw;
   env_t* in = (env_t*)malloc(total * sizeof(env_t));
+  uint64_t* inrows = rw ? (uint64_t*)malloc(total * rw * 8) : (uint64_t*)0;
   uint64_t* off = (uint64_t*)calloc(s->n + 1, 8);
-  env_t* srcs[3] = {s->backlog.v, s->emitted.v, s->staged.v};
-  uint64_t ns[3] = {s->backlog.n, s->emitted.n, s->staged.n};
+  envvec* srcs[3] = {&s->backlog, &s->emitted, &s->staged};
   for (int k = 0; k < 3; ++k)
-    for (uint64_t i = 0; i < ns[k]; ++i) off[srcs[k][i].dst + 1]++;
+    for (uint64_t i = 0; i < srcs[k]->n; ++i) off[srcs[k]->v[i].dst + 1]++;
   for (uint64_t a = 0; a < s->n; ++a) off[a + 1] += off[a];
   uint64_t* cur = (uint64_t*)malloc((s->n) * 8);
   memcpy(cur, off, s->n * 8);
   for (int k = 0; k < 3; ++k)
-    for (uint64_t i = 0; i < ns[k]; ++i) in[cur[srcs[k][i].dst]++] = srcs[k][i];
+    for (uint64_t i = 0; i < srcs[k]->n; ++i) {
+      uint64_t q = cur[srcs[k]->v[i].dst]++;
+      in[q] = srcs[k]->v[i];
+      if (rw) memcpy(inrows + q * rw, srcs[k]->rows + i * rw, (size_t)rw * 8);
+    }
   free(cur);
   s->backlog.n = 0;
   s->emitted.n = 0;
@@ -268,7 +312,8 @@ static int bsp_step(bsp_sim* s) {
     if (!s->alive[a]) { s->st.dead_letters += L; continue; }
     uint64_t nd = L < s->T ? L : s->T;
     for (uint64_t p = 0; p < nd; ++p) {
-      uint32_t r = ref_apply(&s->P, s->kind[a], a, &s->state[(uint64_t)a * s->W], in[b + p].src, in[b + p].payload, emit_cb, s);
+      uint32_t r = ref_apply(&s->P, s->kind[a], a, &s->state[(uint64_t)a * s->W], in[b + p].src, in[b + p].payload,
+                             rw ? inrows + (b + p) * rw : (const uint64_t*)0, emit_cb, s);
       s->st.delivered++;
       if (r == AGX_RES_UNHANDLED) s->st.unhandled++;
       if (r == AGX_RES_STOPPED) {
@@ -278,11 +323,13 @@ static int bsp_step(bsp_sim* s) {
       }
     }
     for (uint64_t p = nd; p < L; ++p) {
-      if (s->C == 0 || p < s->C) ev_push(&s->backlog, in[b + p].dst, in[b + p].src, in[b + p].payload);
+      if (s->C == 0 || p < s->C)
+        ev_push(&s->backlog, in[b + p].dst, in[b + p].src, in[b + p].payload, rw ? inrows + (b + p) * rw : 0, rw);
       else s->st.dead_letters++;
     }
   }
   free(in);
+  free(inrows);
   free(off);
   s->st.supersteps++;
   return 1;
@@ -319,6 +366,15 @@ uint64_t bsp_gcounter_value(const uint64_t* c, uint32_t r) {
   for (uint32_t i = 0; i < r; ++i) v += c[i];
   return v;
 }
+/* ORSet restatement on the engine layout (crdt_ref.h), for the ORSetSpec KATs. */
+void bsp_orset_merge(uint64_t* self, const uint64_t* that) { orset_merge(self, that); }
+void bsp_orset_add(uint64_t* w, uint32_t node, uint32_t e) { orset_add(w, node, e); }
+void bsp_orset_remove(uint64_t* w, uint32_t e) { orset_remove(w, e); }
+void bsp_orset_subtract_dots(uint32_t* out, const uint32_t* dot, const uint32_t* vv) { orset_subtract_dots(out, dot, vv); }
+uint32_t bsp_crdt_peer(uint64_t seed, uint32_t self, uint32_t round, uint32_t j, uint64_t n) {
+  return crdt_peer(seed, self, round, j, n);
+}
+
 /* PNCounter = (increments, decrements) GCounters; merge each (PNCounter.scala:178). */
 void bsp_pncounter_merge(uint64_t* out_p, uint64_t* out_n, const uint64_t* ap, const uint64_t* an,
                          const uint64_t* bp, const uint64_t* bn, uint32_t r) {

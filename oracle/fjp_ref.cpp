@@ -171,7 +171,7 @@ struct EmitCtx {
   Sim* s;
   Worker* w;
 };
-void emit_cb(void* ctx, uint32_t dst, uint32_t self, uint32_t payload) {
+void emit_cb(void* ctx, uint32_t dst, uint32_t self, uint32_t payload, const uint64_t*, uint32_t) {
   EmitCtx* c = (EmitCtx*)ctx;
   c->w->emitted++;
   tell(c->s, dst, self, payload, c->w);
@@ -190,7 +190,7 @@ void run_mailbox(Sim* s, uint32_t a, Worker* w) {
     if (ac.status.load(std::memory_order_acquire) & kClosed) {
       w->dead++;  // cleanUp -> deadLetters
     } else {
-      uint32_t r = ref_apply(&s->P, ac.kind, a, &s->state[(uint64_t)a * s->W], src, pay, emit_cb, &ctx);
+      uint32_t r = ref_apply(&s->P, ac.kind, a, &s->state[(uint64_t)a * s->W], src, pay, nullptr, emit_cb, &ctx);
       w->delivered++;
       if (r == AGX_RES_UNHANDLED) w->unhandled++;
       if (r == AGX_RES_STOPPED) ac.status.fetch_or(kClosed, std::memory_order_acq_rel);
@@ -285,6 +285,7 @@ int fjp_register_range(void* h, uint64_t first, uint64_t count, uint32_t kind, c
                        uint64_t stride_words) {
   Sim* s = (Sim*)h;
   if (first + count > s->n || kind >= AGX_KIND_MAX) return 1;
+  if (ref_crdt_words(kind)) return 1; /* CRDT replicas are checked by the BSP oracle only */
   for (uint64_t i = 0; i < count; ++i) {
     uint64_t a = first + i;
     s->actors[a].kind = kind;

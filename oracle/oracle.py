@@ -20,7 +20,7 @@ _lock = threading.Lock()
 _bsp = None
 _fjp = None
 
-W_MAX = 8
+W_MAX = 260
 NO_SENDER = 0xFFFFFFFF
 
 
@@ -60,6 +60,12 @@ def _load_bsp():
             "bsp_destroy": (None, [vp]),
             "bsp_register_range": (ctypes.c_int, [vp, u64, u64, u32, P64, u64]),
             "bsp_set_ring": (None, [vp, u32]),
+            "bsp_set_gossip": (None, [vp, u32, u64]),
+            "bsp_orset_merge": (None, [P64, P64]),
+            "bsp_orset_add": (None, [P64, u32, u32]),
+            "bsp_orset_remove": (None, [P64, u32]),
+            "bsp_orset_subtract_dots": (None, [P32, P32, P32]),
+            "bsp_crdt_peer": (u32, [u64, u32, u32, u32, u64]),
             "bsp_set_fanout": (ctypes.c_int, [vp, u32, u64, P32, P32, u64]),
             "bsp_set_graph": (ctypes.c_int, [vp, P64, P32]),
             "bsp_stage": (ctypes.c_int, [vp, P32, P32, P32, u64]),
@@ -143,6 +149,9 @@ class BspOracle(_Base):
     def set_ring(self, stride):
         self.lib.bsp_set_ring(self.h, stride)
 
+    def set_gossip(self, fanout, seed):
+        self.lib.bsp_set_gossip(self.h, fanout, seed)
+
     def set_fanout(self, k, seed, cdf, perm):
         cdf, perm = _u32(cdf), _u32(perm)
         self.lib.bsp_set_fanout(self.h, k, seed, _p(cdf, ctypes.c_uint32), _p(perm, ctypes.c_uint32), cdf.size)
@@ -155,8 +164,9 @@ class BspOracle(_Base):
     def tell(self, dst, payload, src=None):
         dst, pay = _u32(dst), _u32(payload)
         s = _u32(np.broadcast_to(np.asarray(NO_SENDER if src is None else src, dtype=np.uint32), dst.shape))
-        self.lib.bsp_stage(self.h, _p(dst, ctypes.c_uint32), _p(s, ctypes.c_uint32), _p(pay, ctypes.c_uint32),
-                           dst.size)
+        if self.lib.bsp_stage(self.h, _p(dst, ctypes.c_uint32), _p(s, ctypes.c_uint32), _p(pay, ctypes.c_uint32),
+                              dst.size):
+            raise ValueError("bsp_stage rejected the tells")
 
     def run(self, max_supersteps=1 << 30):
         st = Stats()
@@ -258,3 +268,78 @@ class crdt:
         a = np.ascontiguousarray(np.asarray(a, dtype=np.uint64)).copy()
         _load_bsp().bsp_gcounter_increment(_p(a, ctypes.c_uint64), slot, n)
         return a
+
+
+class orset:
+    """ORSet restatement on the engine layout (crdt_ref.h; DD/ORSet.scala).  A value is a
+    u64[260] array: u32 dots[64][8] then u32 vvector[8] (node index = UniqueAddress order)."""
+    WORDS = 260
+    ELEMS = 64
+    NODES = 8
+
+    @staticmethod
+    def empty():
+        return np.zeros(orset.WORDS, np.uint64)
+
+    @staticmethod
+    def from_dict(elements: dict, vvector: dict, index: dict):
+        """elements {name: {node: version}}, vvector {node: version}; index maps name -> element slot."""
+        w = orset.empty()
+        u = w.view(np.uint32)
+        for name, dot in elements.items():
+            for n, v in dot.items():
+                u[index[name] * orset.NODES + int(n)] = v
+        for n, v in vvector.items():
+            u[orset.ELEMS * orset.NODES + int(n)] = v
+        return w
+
+    @staticmethod
+    def dots(w, e):
+        u = np.asarray(w, np.uint64).view(np.uint32)
+        d = u[e * orset.NODES:(e + 1) * orset.NODES]
+        return {n: int(v) for n, v in enumerate(d) if v}
+
+    @staticmethod
+    def vvector(w):
+        u = np.asarray(w, np.uint64).view(np.uint32)[orset.ELEMS * orset.NODES:]
+        return {n: int(v) for n, v in enumerate(u) if v}
+
+    @staticmethod
+    def elements(w):
+        u = np.asarray(w, np.uint64).view(np.uint32)[:orset.ELEMS * orset.NODES].reshape(orset.ELEMS, orset.NODES)
+        return set(np.nonzero(u.any(axis=1))[0].tolist())
+
+    @staticmethod
+    def merge(a, b):
+        out = np.ascontiguousarray(np.asarray(a, np.uint64)).copy()
+        b = np.ascontiguousarray(np.asarray(b, np.uint64))
+        _load_bsp().bsp_orset_merge(_p(out, ctypes.c_uint64), _p(b, ctypes.c_uint64))
+        return out
+
+    @staticmethod
+    def add(a, node, e):
+        out = np.ascontiguousarray(np.asarray(a, np.uint64)).copy()
+        _load_bsp().bsp_orset_add(_p(out, ctypes.c_uint64), node, e)
+        return out
+
+    @staticmethod
+    def remove(a, e):
+        out = np.ascontiguousarray(np.asarray(a, np.uint64)).copy()
+        _load_bsp().bsp_orset_remove(_p(out, ctypes.c_uint64), e)
+        return out
+
+    @staticmethod
+    def subtract_dots(dot: dict, vv: dict) -> dict:
+        d = np.zeros(orset.NODES, np.uint32)
+        v = np.zeros(orset.NODES, np.uint32)
+        for n, x in dot.items():
+            d[int(n)] = x
+        for n, x in vv.items():
+            v[int(n)] = x
+        out = np.zeros(orset.NODES, np.uint32)
+        _load_bsp().bsp_orset_subtract_dots(_p(out, ctypes.c_uint32), _p(d, ctypes.c_uint32), _p(v, ctypes.c_uint32))
+        return {n: int(x) for n, x in enumerate(out) if x}
+
+
+def crdt_peer(seed: int, self_id: int, round_: int, j: int, n: int) -> int:
+    return int(_load_bsp().bsp_crdt_peer(seed, self_id, round_, j, n))

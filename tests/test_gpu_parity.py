@@ -154,3 +154,70 @@ def test_ring_1m_properties(built):
     assert st.delivered == n * (hops + 1) and st.dead_letters == 0 and st.supersteps == hops + 1
     assert (words[:, 0] == hops + 1).all() and alive.all()
     eng.close()
+
+
+# ------------------------------------------------------------------ CRDT replicas (C4; rows a9, a10)
+@pytest.mark.parametrize("kind", [Kind.GCOUNTER, Kind.PNCOUNTER, Kind.ORSET])
+@pytest.mark.parametrize("T,C", [(5, 0), (1, 0), (2, 3)])
+def test_crdt_gossip(built, kind, T, C):
+    """Full-state gossip rounds: merges, snapshot rows, rows forwarded for queued
+    gossips (T=1), tail-dropped gossips (C=3) — bit-exact vs the oracle."""
+    w = wl.crdt_gossip(3000, kind, rounds=12, throughput=T, capacity=C)
+    sg, so, a, b = run_both(w)
+    assert_same(sg, so, a, b, f"crdt kind={kind} T={T} C={C}")
+
+
+@pytest.mark.parametrize("T,C", [(3, 0), (1, 4)])
+def test_crdt_mixed_protocols(built, T, C):
+    """CRDT replicas beside classic kinds: gossips to a non-CRDT actor and ops of the
+    wrong data type are Behaviors.unhandled."""
+    w = wl.crdt_mixed(5000, rounds=5, throughput=T, capacity=C)
+    sg, so, a, b = run_both(w)
+    assert_same(sg, so, a, b, f"crdt_mixed T={T} C={C}")
+    assert sg.unhandled > 0
+
+
+def test_crdt_gcounter_1m_converges(built):
+    """C4 size (1M replicas): every replica converges to the join of the 8 writers."""
+    n, rounds = 1_000_000, 40
+    w = wl.crdt_gossip(n, Kind.GCOUNTER, rounds=rounds)
+    eng = GpuEngine(EngineConfig(**w.engine_kwargs()))
+    w.apply_to(eng)
+    st = eng.run()
+    words, _ = eng.read_state()
+    eng.close()
+    ops = wl.crdt_ops(8, Kind.GCOUNTER, 16)
+    exp = (ops & 0xFFFFFF).astype(np.uint64).sum(axis=1)
+    assert st.in_flight == 0 and st.unhandled == 0 and st.delivered == 8 * 16 + 3 * n * rounds
+    assert (words == exp[None, :]).all()
+
+
+@pytest.mark.parametrize("ranks", [2, 5])
+@pytest.mark.parametrize("workload", ["orset", "mixed"])
+def test_crdt_loopback_sharded(built, ranks, workload):
+    """C4 hash-sharded: snapshot rows travel with the gossips between ranks."""
+    from oracle import BspOracle
+    from akka_amd.engine import owner
+    if workload == "orset":
+        w = wl.crdt_gossip(2000, Kind.ORSET, rounds=8, throughput=2, capacity=0)
+    else:
+        w = wl.crdt_mixed(3000, rounds=4, throughput=2, capacity=5)
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.engine_kwargs())) for r in range(ranks)]
+    for e in engs:
+        w.apply_to(e)
+    sg = GpuEngine.group_run(engs)
+    ref = BspOracle(n_ranks=ranks, **w.engine_kwargs())
+    w.apply_to(ref)
+    so = ref.run()
+    for k in ("delivered", "dead_letters", "unhandled", "emitted", "staged", "in_flight"):
+        assert getattr(sg, k) == so[k], (k, getattr(sg, k), so[k])
+    wo, ao = ref.read_state()
+    wg = np.zeros_like(wo)
+    own_of = np.array([owner(i, 1000, ranks) for i in range(w.n_actors)])
+    for e in engs:
+        a, _ = e.read_state()
+        own = own_of == e.cfg.rank
+        wg[own] = a[own]
+        e.close()
+    diff = np.nonzero((wg != wo).any(axis=1))[0]
+    assert diff.size == 0, diff[:10]

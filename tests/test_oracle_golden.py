@@ -146,3 +146,117 @@ def test_sharded_order_is_rank_major():
         o.run()
         outs.append(o.read_state()[0])
     assert all(np.array_equal(outs[0], x) for x in outs[1:])  # confluent: same for any R
+
+
+# ------------------------------------------------------------------ CRDT KATs (a9, a10)
+def _pn_apply(ops, slots):
+    inc = np.zeros(slots, np.uint64)
+    dec = np.zeros(slots, np.uint64)
+    for op, slot, n in ops:
+        if op == "inc":
+            inc = crdt.gcounter_increment(inc, slot, n)
+        else:
+            dec = crdt.gcounter_increment(dec, slot, n)
+    return inc, dec
+
+
+def test_pncounter_kats():
+    g = load("pncounter_kat.json")
+    for case in g["cases"]:
+        inc, dec = _pn_apply(case["ops"], g["slots"])
+        if "increments" in case:
+            assert inc.tolist() == case["increments"] and dec.tolist() == case["decrements"], case["name"]
+        if "value" in case:
+            assert crdt.gcounter_value(inc) == case["increments_value"], case["name"]
+            assert crdt.gcounter_value(dec) == case["decrements_value"], case["name"]
+            assert crdt.gcounter_value(inc) - crdt.gcounter_value(dec) == case["value"], case["name"]
+    for m in g["merges"]:
+        a = _pn_apply(m["a_ops"], g["slots"])
+        b = _pn_apply(m["b_ops"], g["slots"])
+        assert crdt.gcounter_value(b[0]) == m["b_increments_value"]
+        assert crdt.gcounter_value(b[1]) == m["b_decrements_value"]
+        for x, y in ((a, b), (b, a)):  # PNCounter.merge = GCounter.merge of each half (PNCounter.scala:178)
+            mi, md = crdt.gcounter_merge(x[0], y[0]), crdt.gcounter_merge(x[1], y[1])
+            assert crdt.gcounter_value(mi) == m["merged_increments_value"], m["name"]
+            assert crdt.gcounter_value(md) == m["merged_decrements_value"], m["name"]
+            assert crdt.gcounter_value(mi) - crdt.gcounter_value(md) == m["merged_value"], m["name"]
+
+
+def _ikeys(d):
+    return {int(k): v for k, v in d.items()}
+
+
+def test_orset_subtract_dots_kat():
+    from oracle.oracle import orset
+    for c in load("orset_kat.json")["subtract_dots"]:
+        assert orset.subtract_dots(_ikeys(c["dot"]), _ikeys(c["vvector"])) == _ikeys(c["expected"]), c["name"]
+
+
+def test_orset_merge_kats():
+    from oracle.oracle import orset
+    for c in load("orset_kat.json")["merges"]:
+        names = sorted(set(c["this"]["elements"]) | set(c["that"]["elements"]) | set(c["expected_elements"]))
+        idx = {k: i for i, k in enumerate(names)}
+        a = orset.from_dict({k: _ikeys(v) for k, v in c["this"]["elements"].items()}, _ikeys(c["this"]["vvector"]), idx)
+        b = orset.from_dict({k: _ikeys(v) for k, v in c["that"]["elements"].items()}, _ikeys(c["that"]["vvector"]), idx)
+        m = orset.merge(a, b)
+        got = {k: orset.dots(m, idx[k]) for k in names if orset.dots(m, idx[k])}
+        assert got == {k: _ikeys(v) for k, v in c["expected_elements"].items()}, c["name"]
+        # vvector = VersionVector.merge (pointwise max)
+        vv = {**_ikeys(c["this"]["vvector"])}
+        for n, v in _ikeys(c["that"]["vvector"]).items():
+            vv[n] = max(vv.get(n, 0), v)
+        assert orset.vvector(m) == vv
+
+
+def test_orset_replica_scripts():
+    """ORSetSpec 'verify disjoint merge' / 'removed after merge' (1, 2): add/remove/merge
+    sequences on named replicas, checked on the element sets."""
+    from oracle.oracle import orset
+    for c in load("orset_kat.json")["scripts"]:
+        reps, idx = {}, {}
+        for op in c["ops"]:
+            if op[0] == "new":
+                reps[op[1]] = orset.empty()
+            elif op[0] == "add":
+                reps[op[1]] = orset.add(reps[op[1]], op[2], idx.setdefault(op[3], len(idx)))
+            elif op[0] == "remove":
+                reps[op[1]] = orset.remove(reps[op[1]], idx.setdefault(op[2], len(idx)))
+            elif op[0] == "copy":
+                reps[op[1]] = reps[op[2]].copy()
+            elif op[0] == "merge":
+                reps[op[1]] = orset.merge(reps[op[2]], reps[op[3]])
+        inv = {v: k for k, v in idx.items()}
+        for chk in c["checks"]:
+            assert {inv[e] for e in orset.elements(reps[chk[1]])} == set(chk[2]), (c["name"], chk)
+
+
+@pytest.mark.parametrize("kind", [Kind.GCOUNTER, Kind.PNCOUNTER, Kind.ORSET])
+def test_crdt_gossip_converges_to_writers_merge(kind):
+    """C4 on the oracle: after enough GossipTicks every replica holds the join of the
+    8 writers' values (computed here from the ops with the KAT-pinned functions)."""
+    from oracle.oracle import orset
+    n, rounds, opw = 384, 24, 16
+    w = wl.crdt_gossip(n, kind, rounds=rounds, ops_per_writer=opw)
+    o = BspOracle(**w.engine_kwargs())
+    w.apply_to(o)
+    st = o.run()
+    assert st["in_flight"] == 0 and st["unhandled"] == 0
+    assert st["delivered"] == 8 * opw + n * rounds * 3  # ops + ticks + 2 gossips per tick
+    ws, _ = o.read_state()
+    ops = wl.crdt_ops(8, kind, opw)
+    if kind == Kind.ORSET:
+        exp = orset.empty()
+        for k in range(8):
+            r = orset.empty()
+            for p in ops[k]:
+                op, arg = int(p) >> 24, int(p) & 0xFFFFFF
+                r = orset.add(r, k, arg) if op == 3 else orset.remove(r, arg)
+            exp = orset.merge(exp, r)
+    else:
+        exp = np.zeros(w.n_words, np.uint64)
+        for k in range(8):
+            for p in ops[k]:
+                op, arg = int(p) >> 24, int(p) & 0xFFFFFF
+                exp[k if op == 1 else 8 + k] += arg
+    assert all(np.array_equal(r, exp) for r in ws)
