@@ -135,6 +135,7 @@ struct agx_engine {
   uint32_t* d_hist_c = nullptr;  // [kRadix][nchunks] first-pass chunk histograms, then bump[2]
   uint32_t* d_hist_d = nullptr;  // [kRadix][max_tiles] dense-pass histograms
   uint32_t *d_tot = nullptr, *d_bstart = nullptr, *d_n = nullptr, *d_total = nullptr, *d_moff0 = nullptr, *d_moff1 = nullptr;
+  unsigned long long *d_bstats = nullptr, *d_sred = nullptr;  // per-block apply counters, their sum
   uint64_t *d_stats = nullptr, *d_cvec = nullptr, *d_cmat = nullptr, *d_inflight = nullptr;
   uint32_t* h_pin = nullptr;     // pinned ring of per-step totals
   uint64_t* h_pin64 = nullptr;   // pinned scratch (count matrix, stats)
@@ -352,6 +353,12 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     AGX_TRY(launch_dense_pass(e, *src, *dst, e->d_n, e->plan.shift[p], e->plan.bits[p]));
     std::swap(src, dst);
   }
+  if (e->plan.npass > 1) {  // digits of the last pass are not buckets: find the bucket starts
+    Scope s(e, K_ROWSCAN);
+    hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((e->nb + kThreads) / kThreads, 4096)), dim3(kThreads), 0,
+                       e->stream, src->key, e->d_n, e->nb, e->d_bstart);
+    HIP_TRY(hipGetLastError());
+  }
   *result = src;
   return AGX_OK;
 }
@@ -374,16 +381,16 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.nx_shift = e->plan.shift[0];
   ba.nx_bits = e->plan.bits[0];
   ba.nb = e->nb;
-  ba.single_pass = e->plan.npass == 1;
   ba.kmax = e->kmax;
   ba.stats = e->d_stats;
+  ba.bstats = e->d_bstats;
   ba.dbg = e->d_dbg;
   {
     Scope s(e, K_APPLY);
     if (e->pw)  // CRDT kinds registered: the variant with state gossips
-      hipLaunchKernelGGL(k_bucket_apply<true>, dim3(grid_for(e->nb, 4096)), dim3(kBThreads), 0, e->stream, ba);
+      hipLaunchKernelGGL(k_bucket_apply<true>, dim3(grid_for(e->nb, kMaxApplyGrid)), dim3(kBThreads), 0, e->stream, ba);
     else
-      hipLaunchKernelGGL(k_bucket_apply<false>, dim3(grid_for(e->nb, 4096)), dim3(kBThreads), 0, e->stream, ba);
+      hipLaunchKernelGGL(k_bucket_apply<false>, dim3(grid_for(e->nb, kMaxApplyGrid)), dim3(kBThreads), 0, e->stream, ba);
   }
   HIP_TRY(hipGetLastError());
   return AGX_OK;
@@ -531,8 +538,17 @@ agx_status check_error(agx_engine* e) {
 }
 
 agx_status fill_stats(agx_engine* e, agx_stats* out, uint64_t inflight) {
-  uint64_t s[ST_N];
+  uint64_t s[ST_N], bs[kBStats];
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_bstats, kMaxApplyGrid, e->d_sred);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(s, e->d_stats, sizeof s, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(bs, e->d_sred, sizeof bs, hipMemcpyDeviceToHost));
+  s[ST_DELIVERED] = bs[0];
+  s[ST_DEAD] += bs[1];
+  s[ST_UNHANDLED] = bs[2];
+  s[ST_EMITTED] = bs[3];
+  s[ST_ACTIVE] = bs[4];
   agx_stats st{};
   st.delivered = s[ST_DELIVERED];
   st.dead_letters = s[ST_DEAD] + e->staged_dead;
@@ -799,7 +815,11 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->nchunks = 2 * e->nb + kStagedChunks;
   {
     const uint32_t lo = kBucketBits, hi = std::max<uint32_t>(e->key_bits, kBucketBits + 1);
-    e->plan.npass = (hi - lo + kRadixBits - 1) / kRadixBits;
+    // AGX_RADIX_BITS (test knob): narrower digits, so that small populations take the multi-pass path
+    uint32_t rb = kRadixBits;
+    if (const char* s = getenv("AGX_RADIX_BITS")) rb = std::min<uint32_t>(kRadixBits, std::max(1, atoi(s)));
+    e->plan.npass = (hi - lo + rb - 1) / rb;
+    if (e->plan.npass > 4) { delete e; return set_err(AGX_EINVAL, "AGX_RADIX_BITS=%u needs more than 4 passes", rb); }
     for (uint32_t p = 0, sh = lo; p < e->plan.npass; ++p) {
       const uint32_t b = (hi - sh + (e->plan.npass - p) - 1) / (e->plan.npass - p);  // spread bits evenly
       e->plan.shift[p] = sh;
@@ -849,13 +869,16 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(hipMemset(e->d_chunk_cnt, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_hist_c, (uint64_t)kRadix * e->nchunks));
   CREATE_TRY(hipMemset(e->d_hist_c, 0, (uint64_t)kRadix * e->nchunks * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-  CREATE_TRY(dalloc(&e->d_bstart, kRadix + 1));
+  CREATE_TRY(dalloc(&e->d_bstart, std::max<uint64_t>(kRadix, e->nb) + 1));
   if (getenv("AGX_STAMPS")) CREATE_TRY(dalloc(&e->d_dbg, (uint64_t)std::min<uint64_t>(e->nb, 4096) * 16));
   CREATE_TRY(dalloc(&e->d_hist_d, (uint64_t)kRadix * e->max_tiles));
   CREATE_TRY(dalloc(&e->d_tot, kRadix));
   CREATE_TRY(dalloc(&e->d_n, 4));
   CREATE_TRY(dalloc(&e->d_total, 4));
   CREATE_TRY(dalloc(&e->d_stats, ST_N));
+  CREATE_TRY(dalloc(&e->d_bstats, (uint64_t)kMaxApplyGrid * kBStats));
+  CREATE_TRY(dalloc(&e->d_sred, kBStats));
+  CREATE_TRY(hipMemset(e->d_bstats, 0, (uint64_t)kMaxApplyGrid * kBStats * 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_heap_top, 2));
   CREATE_TRY(dalloc(&e->d_step, 1));
   CREATE_TRY(hipMemset(e->d_heap_top, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
@@ -890,7 +913,7 @@ agx_status agx_destroy(agx_engine* e) {
   free_msgs(e->s1); free_msgs(e->s2);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_n); hipFree(e->d_total);
-  hipFree(e->d_stats); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);
+  hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_sred); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);
   hipFree(e->d_heap); hipFree(e->d_heap_top); hipFree(e->d_step); hipFree(e->d_rx); hipFree(e->d_s2rows);
   if (e->h_pin) hipHostFree(e->h_pin);
   if (e->h_pin64) hipHostFree(e->h_pin64);

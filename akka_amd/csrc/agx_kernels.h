@@ -43,6 +43,9 @@ constexpr int kScanThreads = 1024;
 // stats slots (u64) on device
 enum { ST_DELIVERED = 0, ST_DEAD = 1, ST_UNHANDLED = 2, ST_EMITTED = 3, ST_STEPS = 4, ST_ERROR = 5, ST_ACTIVE = 6, ST_N = 8 };
 constexpr uint64_t kErrCapacity = 1;
+// per-block counters of k_bucket_apply: delivered, dead, unhandled, emitted, active
+constexpr int kBStats = 5;
+constexpr uint32_t kMaxApplyGrid = 4096;
 
 struct Msgs {
   uint32_t* key;
@@ -118,6 +121,19 @@ __device__ __forceinline__ uint32_t wave_rank(bool valid, uint32_t d, uint32_t b
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const uint32_t lane = lane_id();
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// h[d] += 1 from every active lane.  When all active lanes share the digit (local
+// topologies: a whole wave's tells go to one destination bucket) one lane adds the
+// popcount instead of 64 serialised LDS atomics on one address.
+__device__ __forceinline__ void lds_hist_inc(uint32_t* h, uint32_t d) {
+  const uint64_t act = __ballot(1);
+  const uint32_t first = __builtin_amdgcn_readfirstlane(d);
+  if (__ballot(d == first) == act) {
+    if (lane_id() == (uint32_t)__builtin_ctzll(act)) atomicAdd(&h[first], (uint32_t)__popcll(act));
+  } else {
+    atomicAdd(&h[d], 1u);
+  }
 }
 
 // =========================================================================
@@ -500,7 +516,7 @@ struct Emitter {
       out.src[pos] = self;
       out.pay[pos] = pay;
       ++pos;
-      atomicAdd(&nh[((key & kLocalMask) >> nh_shift) & nh_mask], 1u);
+      lds_hist_inc(nh, ((key & kLocalMask) >> nh_shift) & nh_mask);
     }
   }
   // CRDT state gossip to a known actor: the sender field carries the wide tag, payload = row handle
@@ -513,7 +529,7 @@ struct Emitter {
       out.src[pos] = self | AGX_WIDE_BIT;
       out.pay[pos] = h;
       ++pos;
-      atomicAdd(&nh[((key & kLocalMask) >> nh_shift) & nh_mask], 1u);
+      lds_hist_inc(nh, ((key & kLocalMask) >> nh_shift) & nh_mask);
     }
   }
   __device__ __forceinline__ void count(uint32_t k) {
@@ -548,7 +564,7 @@ struct EmitterLds {
     src[slot] = self;
     pay[slot] = p;
     ++slot;
-    atomicAdd(&nh[((k & kLocalMask) >> nh_shift) & nh_mask], 1u);
+    lds_hist_inc(nh, ((k & kLocalMask) >> nh_shift) & nh_mask);
   }
 };
 
@@ -556,15 +572,16 @@ struct BucketArgs {
   DevParams P;
   CMsgs in;                // mail sorted by bucket (local key >> kBucketBits)
   const uint32_t* d_n;
-  const uint32_t* bstart;  // single_pass: bucket starts [nb + 1]
+  const uint32_t* bstart;  // bucket starts [nb + 1]
   Msgs scr;                // general path: bucket-local sorted copy (index space of `in`)
   Msgs bl, em;             // chunk arenas: backlog of bucket b at [lo, lo+cnt), tells at [lo*kmax, (lo+cnt)*kmax)
   uint32_t* chunk_off;
   uint32_t* chunk_cnt;
   uint32_t* nhist;         // next step's first-pass histogram, digit-major [nbins][nhist_stride]
   uint32_t nhist_stride, nx_shift, nx_bits;
-  uint32_t nb, single_pass, kmax;
+  uint32_t nb, kmax;
   uint64_t* stats;
+  unsigned long long* bstats;  // [gridDim][kBStats] per-block counters (summed by k_stats_reduce)
   unsigned long long* dbg;  // diagnostic build only (AGX_STAMPS): per-block phase timestamps
 };
 
@@ -572,27 +589,6 @@ struct BucketArgs {
   do {                                                                                            \
     if ((a).dbg && threadIdx.x == 0) (a).dbg[blockIdx.x * 16 + (idx)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
-
-// 64-ary lower bound by one wave: first index i in [0, n) with ((key[i] & local) >> sh) >= target
-__device__ __forceinline__ uint32_t wave_lower_bound(const uint32_t* key, uint32_t n, uint32_t sh, uint32_t target) {
-  uint32_t lo = 0, hi = n;  // answer in [lo, hi]
-  const uint32_t lane = lane_id();
-  while (hi - lo > 64) {
-    const uint32_t step = div_up(hi - lo, 64);
-    const uint32_t probe = lo + lane * step;  // lane 0 probes lo
-    const bool ge = probe < hi ? (((key[probe] & kLocalMask) >> sh) >= target) : true;
-    const uint64_t m = __ballot(ge);
-    const uint32_t first = m ? (uint32_t)__builtin_ctzll(m) : 64u;  // first lane with key >= target
-    const uint32_t nlo = first == 0 ? lo : lo + (first - 1) * step;
-    const uint32_t nhi = first >= 64 ? hi : min(hi, lo + first * step);
-    lo = nlo;
-    hi = nhi;
-  }
-  const uint32_t probe = lo + lane;
-  const bool ge = probe < hi ? (((key[probe] & kLocalMask) >> sh) >= target) : true;
-  const uint64_t m = __ballot(ge);
-  return m ? lo + (uint32_t)__builtin_ctzll(m) : hi;
-}
 
 struct BucketLds {
   uint32_t* key;   // fast path: sorted items (LDS); general path: run / tmp scratch
@@ -899,13 +895,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     atomicAdd(&L.stat[4], (unsigned long long)v4);
   }
   __syncthreads();
-  if (tid == 0) {
-    if (L.stat[0]) atomicAdd((unsigned long long*)&a.stats[ST_DELIVERED], L.stat[0]);
-    if (L.stat[1]) atomicAdd((unsigned long long*)&a.stats[ST_DEAD], L.stat[1]);
-    if (L.stat[2]) atomicAdd((unsigned long long*)&a.stats[ST_UNHANDLED], L.stat[2]);
-    if (L.stat[3]) atomicAdd((unsigned long long*)&a.stats[ST_EMITTED], L.stat[3]);
-    if (L.stat[4]) atomicAdd((unsigned long long*)&a.stats[ST_ACTIVE], L.stat[4]);
-  }
+  if (tid < kBStats) a.bstats[(size_t)blockIdx.x * kBStats + tid] += L.stat[tid];  // this block's own slot
   __syncthreads();
   AGX_STAMP(a, 8);
 }
@@ -943,18 +933,9 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     const uint32_t na = min((uint32_t)kBucket, P.n_local - a0);
     if (tid < 5) s_stat[tid] = 0;
     for (uint32_t d = tid; d < kRadix; d += kBThreads) s_nh[d] = 0;
-    if (a.single_pass) {
-      if (tid == 0) {
-        s_lo = a.bstart[b];
-        s_hi = a.bstart[b + 1];
-      }
-    } else if (w == 0) {
-      const uint32_t lo = wave_lower_bound(a.in.key, n, kBucketBits, b);
-      const uint32_t hi = wave_lower_bound(a.in.key, n, kBucketBits, b + 1);
-      if (lane == 0) {
-        s_lo = lo;
-        s_hi = hi;
-      }
+    if (tid == 0) {
+      s_lo = a.bstart[b];
+      s_hi = a.bstart[b + 1];
     }
     for (uint32_t la = tid; la < kBucket; la += kBThreads) s_alive[la] = la < na ? P.alive[a0 + la] : 0;
     __syncthreads();
@@ -1135,6 +1116,38 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       bucket_finish<false, kWide>(a, L, b, lo, cnt, a0, na);
     }
   }
+}
+
+// Bucket starts after a multi-pass sort: bstart[x] = first index with bucket >= x
+// (one thread per bucket, binary search over the sorted keys; the top levels of every
+// search hit the same cached lines).
+__global__ void __launch_bounds__(kThreads) k_bucket_bounds(const uint32_t* key, const uint32_t* d_n, uint32_t nb,
+                                                            uint32_t* bstart) {
+  const uint32_t n = *d_n;
+  for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x <= nb; x += gridDim.x * kThreads) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (((key[mid] & kLocalMask) >> kBucketBits) < x) lo = mid + 1; else hi = mid;
+    }
+    bstart[x] = lo;
+  }
+}
+
+// Sum the per-block counters of k_bucket_apply into out[0..kBStats).
+__global__ void __launch_bounds__(kScanThreads) k_stats_reduce(const unsigned long long* bstats, uint32_t nslots,
+                                                               unsigned long long* out) {
+  __shared__ unsigned long long s[kBStats];
+  if (threadIdx.x < kBStats) s[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long v[kBStats] = {0, 0, 0, 0, 0};
+  for (uint32_t i = threadIdx.x; i < nslots; i += blockDim.x)
+#pragma unroll
+    for (int k = 0; k < kBStats; ++k) v[k] += bstats[(size_t)i * kBStats + k];
+#pragma unroll
+  for (int k = 0; k < kBStats; ++k) atomicAdd(&s[k], v[k]);
+  __syncthreads();
+  if (threadIdx.x < kBStats) out[threadIdx.x] = s[threadIdx.x];
 }
 
 // Histogram columns of the host-staged chunks (one block per staged chunk).

@@ -221,3 +221,58 @@ def test_crdt_loopback_sharded(built, ranks, workload):
         e.close()
     diff = np.nonzero((wg != wo).any(axis=1))[0]
     assert diff.size == 0, diff[:10]
+
+
+# ------------------------------------------------------------------ multi-pass bucket grouping
+# Populations above 2^20 actors per rank group mail by bucket with more than one radix
+# pass (and find bucket starts with k_bucket_bounds).  AGX_RADIX_BITS narrows the digits
+# so that the same code path runs at oracle-friendly sizes.
+MULTIPASS_CASES = {
+    "ring": lambda: wl.token_ring(100_000, 9),
+    "mixed": lambda: wl.mixed(30_000, seed=4, throughput=2, capacity=5),
+    "zipf": lambda: wl.zipf_fanout(40_000, k=4, ttl=3, root_every=32, throughput=1000),
+    "power_law": lambda: wl.power_law_forward(50_000, ttl=5, capacity=8, throughput=5),
+    "crdt": lambda: wl.crdt_mixed(20_000, rounds=4, throughput=2, capacity=5),
+}
+
+
+@pytest.mark.parametrize("bits", [2, 3])
+@pytest.mark.parametrize("case", sorted(MULTIPASS_CASES))
+def test_multipass_grouping(built, monkeypatch, bits, case):
+    monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
+    w = MULTIPASS_CASES[case]()
+    sg, so, a, b = run_both(w)
+    assert_same(sg, so, a, b, f"multipass {case} bits={bits}")
+
+
+def test_multipass_loopback_sharded(built, monkeypatch):
+    from oracle import BspOracle
+    from akka_amd.engine import owner
+    monkeypatch.setenv("AGX_RADIX_BITS", "2")
+    ranks = 3
+    w = wl.mixed(30_000, seed=11, throughput=2, capacity=6)
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.engine_kwargs())) for r in range(ranks)]
+    for e in engs:
+        w.apply_to(e)
+    sg = GpuEngine.group_run(engs)
+    ref = BspOracle(n_ranks=ranks, **w.engine_kwargs())
+    w.apply_to(ref)
+    so = ref.run()
+    for k in ("delivered", "dead_letters", "unhandled", "emitted", "staged", "in_flight"):
+        assert getattr(sg, k) == so[k], (k, getattr(sg, k), so[k])
+    wo, _ = ref.read_state()
+    wg = np.zeros_like(wo)
+    own_of = np.array([owner(i, 1000, ranks) for i in range(w.n_actors)])
+    for e in engs:
+        a, _ = e.read_state()
+        own = own_of == e.cfg.rank
+        wg[own] = a[own]
+        e.close()
+    assert np.array_equal(wg, wo)
+
+
+def test_ring_2m_multipass_native(built):
+    """2.1M actors: the real (9-bit digit) multi-pass path, bit-exact vs the oracle."""
+    w = wl.token_ring(2_100_000, 6)
+    sg, so, a, b = run_both(w)
+    assert_same(sg, so, a, b, "ring 2.1M")

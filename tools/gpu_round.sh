@@ -10,7 +10,7 @@ B1M="--no-cpu-baseline --large-actors 0"
 fail() { echo "$1 failed"; tail -30 "$2"; exit 1; }
 
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/${TAG}_pytest.log 2>&1 || fail pytest gpurun_out/${TAG}_pytest.log
+  timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 || fail pytest gpurun_out/${TAG}_pytest.log
   tail -2 gpurun_out/${TAG}_pytest.log
 fi
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch -o run -- python3 bench.py $B1M --steps 40 --warmup 4 > gpurun_out/${TAG}_pmc_fetch.log 2>&1 || fail pmc_fetch gpurun_out/${TAG}_pmc_fetch.log
