@@ -128,62 +128,87 @@ __device__ __forceinline__ int block_excl_max(int v, int* scratch) {
 // One ActorCell.invoke of one message (akka-actor/.../ActorCell.scala:539-555)
 // through the typed ActorAdapter (TY/internal/adapter/ActorAdapter.scala:77-168).
 // `Emit` is called for each tell: emit(dst_global, payload).
-template <typename Emit>
+//
+// KM is the set of behaviour kinds compiled in (bit k = kind k).  The engine
+// launches the narrowest specialisation that covers every registered kind, so a
+// population of one behaviour runs a small, branch-free apply kernel.
+constexpr uint32_t kb(uint32_t k) { return 1u << k; }
+constexpr uint32_t KM_ALL = kb(AGX_KIND_COUNTER) | kb(AGX_KIND_RING) | kb(AGX_KIND_FANOUT) | kb(AGX_KIND_FORWARD_RR) |
+                            kb(AGX_KIND_STOP_AFTER) | kb(AGX_KIND_PINGPONG) | kb(AGX_KIND_EVEN);
+
+template <uint32_t KM, typename Emit>
 __device__ __forceinline__ uint32_t apply_msg(const DevParams& P, uint32_t kind, uint32_t self, uint32_t local,
                                               uint64_t* w, uint32_t src, uint32_t pay, Emit&& emit) {
+  if constexpr (KM == kb(AGX_KIND_RING)) kind = AGX_KIND_RING;  // single-kind specialisations: no dispatch
+  if constexpr (KM == kb(AGX_KIND_FORWARD_RR)) kind = AGX_KIND_FORWARD_RR;
+  if constexpr (KM == kb(AGX_KIND_FANOUT)) kind = AGX_KIND_FANOUT;
+  if constexpr (KM == kb(AGX_KIND_COUNTER)) kind = AGX_KIND_COUNTER;
   switch (kind) {
     case AGX_KIND_COUNTER:
-      w[0] += 1;
-      w[1] += pay;  // w[1] exists (array of AGX_MAX_WORDS); only stored back if W > 1
+      if constexpr ((KM & kb(AGX_KIND_COUNTER)) != 0) {
+        w[0] += 1;
+        w[1] += pay;  // w[1] exists (array of AGX_MAX_WORDS); only stored back if W > 1
+      }
       return AGX_RES_SAME;
     case AGX_KIND_RING:
-      w[0] += 1;
-      if (pay > 0) {
-        uint32_t d = self + P.ring_stride;  // both < n_global < 2^31: no overflow, one conditional subtract
-        emit(d >= P.n_global ? d - P.n_global : d, pay - 1);
-      }
-      return AGX_RES_SAME;
-    case AGX_KIND_FANOUT: {
-      w[0] += 1;
-      w[1] += pay;
-      const uint32_t ttl = pay >> 28, h = pay & 0x0FFFFFFFu;
-      if (ttl > 0)
-        for (uint32_t j = 0; j < P.fan_k; ++j) {
-          uint64_t r = fanout_rand(P.fan_seed, self, h, j);
-          uint32_t d = P.zipf_perm[zipf_index(P.zipf_cdf, P.zipf_n, r)];
-          emit(d, ((ttl - 1) << 28) | ((uint32_t)r & 0x0FFFFFFFu));
-        }
-      return AGX_RES_SAME;
-    }
-    case AGX_KIND_FORWARD_RR: {
-      w[0] += 1;
-      if (pay > 0) {
-        uint64_t b = P.row_ptr[local], deg = P.row_ptr[local + 1] - b;
-        if (deg) {
-          // cursor mod degree; 32-bit remainder when both fit (the common case)
-          uint64_t r = (w[1] <= 0xFFFFFFFFull && deg <= 0xFFFFFFFFull) ? (uint64_t)((uint32_t)w[1] % (uint32_t)deg)
-                                                                       : w[1] % deg;
-          uint64_t e = b + r;
-          w[1] += 1;
-          emit(P.col[e], pay - 1);
+      if constexpr ((KM & kb(AGX_KIND_RING)) != 0) {
+        w[0] += 1;
+        if (pay > 0) {
+          uint32_t d = self + P.ring_stride;  // both < n_global < 2^31: no overflow, one conditional subtract
+          emit(d >= P.n_global ? d - P.n_global : d, pay - 1);
         }
       }
       return AGX_RES_SAME;
-    }
+    case AGX_KIND_FANOUT:
+      if constexpr ((KM & kb(AGX_KIND_FANOUT)) != 0) {
+        w[0] += 1;
+        w[1] += pay;
+        const uint32_t ttl = pay >> 28, h = pay & 0x0FFFFFFFu;
+        if (ttl > 0)
+          for (uint32_t j = 0; j < P.fan_k; ++j) {
+            uint64_t r = fanout_rand(P.fan_seed, self, h, j);
+            uint32_t d = P.zipf_perm[zipf_index(P.zipf_cdf, P.zipf_n, r)];
+            emit(d, ((ttl - 1) << 28) | ((uint32_t)r & 0x0FFFFFFFu));
+          }
+      }
+      return AGX_RES_SAME;
+    case AGX_KIND_FORWARD_RR:
+      if constexpr ((KM & kb(AGX_KIND_FORWARD_RR)) != 0) {
+        w[0] += 1;
+        if (pay > 0) {
+          uint64_t b = P.row_ptr[local], deg = P.row_ptr[local + 1] - b;
+          if (deg) {
+            // cursor mod degree; 32-bit remainder when both fit (the common case)
+            uint64_t r = (w[1] <= 0xFFFFFFFFull && deg <= 0xFFFFFFFFull) ? (uint64_t)((uint32_t)w[1] % (uint32_t)deg)
+                                                                         : w[1] % deg;
+            uint64_t e = b + r;
+            w[1] += 1;
+            emit(P.col[e], pay - 1);
+          }
+        }
+      }
+      return AGX_RES_SAME;
     case AGX_KIND_STOP_AFTER:
-      w[0] += 1;
-      return (w[0] >= w[1]) ? AGX_RES_STOPPED : AGX_RES_SAME;
-    case AGX_KIND_PINGPONG: {
-      // BenchmarkActors.PingPong (akka-bench-jmh/.../actor/BenchmarkActors.scala:20-32)
-      uint32_t res = (w[0] == 0) ? AGX_RES_STOPPED : AGX_RES_SAME;
-      w[1] += 1;
-      emit(src, pay);
-      w[0] -= 1;
-      return res;
-    }
+      if constexpr ((KM & kb(AGX_KIND_STOP_AFTER)) != 0) {
+        w[0] += 1;
+        return (w[0] >= w[1]) ? AGX_RES_STOPPED : AGX_RES_SAME;
+      }
+      return AGX_RES_SAME;
+    case AGX_KIND_PINGPONG:
+      if constexpr ((KM & kb(AGX_KIND_PINGPONG)) != 0) {
+        // BenchmarkActors.PingPong (akka-bench-jmh/.../actor/BenchmarkActors.scala:20-32)
+        uint32_t res = (w[0] == 0) ? AGX_RES_STOPPED : AGX_RES_SAME;
+        w[1] += 1;
+        emit(src, pay);
+        w[0] -= 1;
+        return res;
+      }
+      return AGX_RES_SAME;
     case AGX_KIND_EVEN:
-      if (pay & 1u) return AGX_RES_UNHANDLED;
-      w[0] += 1;
+      if constexpr ((KM & kb(AGX_KIND_EVEN)) != 0) {
+        if (pay & 1u) return AGX_RES_UNHANDLED;
+        w[0] += 1;
+      }
       return AGX_RES_SAME;
     default:
       return AGX_RES_SAME;

@@ -99,7 +99,8 @@ struct SortPlan {  // LSD passes over key bits [kBucketBits, key_bits)
 struct agx_engine {
   agx_cfg cfg{};
   hipStream_t stream = nullptr;
-  uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0, max_tiles = 0;
+  uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0;
+  uint32_t max_supers = 1, dstride = 4;  // dense passes: super-tiles, table row stride
   uint32_t T = 1, C = 0, W = 1, kmax = 1, R = 1, rank = 0, num_shards = 1000, key_bits = 1;
 
   // sharding tables (R > 1)
@@ -108,6 +109,7 @@ struct agx_engine {
   std::vector<uint8_t> h_kind, h_alive;
   std::vector<uint64_t> h_state;  // word-major
   bool actors_dirty = true;
+  uint32_t kinds_mask = 0;  // bit k set when some local actor has behaviour kind k (selects the apply variant)
   std::vector<uint64_t> h_row;  // local CSR rows (graph)
   std::vector<uint32_t> h_col;
   bool graph_set = false;
@@ -129,11 +131,12 @@ struct agx_engine {
 
   DevMsgs A, B, scr, bl, em, stg, s1, s2;
   uint64_t stg_cap = 0;
-  uint32_t nb = 1, nchunks = 3;                // buckets; chunks = 2 nb + 1
+  uint32_t nb = 1, nchunks = 3;                // buckets; chunks = 2 nb + kStagedChunks
+  uint32_t G = 1, ng = 1, nunits = 3, cstride = 4;  // first-pass histogram units (G buckets each)
   SortPlan plan;
   uint32_t *d_chunk_off = nullptr, *d_chunk_cnt = nullptr;
-  uint32_t* d_hist_c = nullptr;  // [kRadix][nchunks] first-pass chunk histograms, then bump[2]
-  uint32_t* d_hist_d = nullptr;  // [kRadix][max_tiles] dense-pass histograms
+  uint32_t* d_hist_c = nullptr;  // [kRadix][cstride] first-pass histograms per unit
+  uint32_t* d_hist_d = nullptr;  // [kRadix][dstride] dense-pass histograms per super-tile
   uint32_t *d_tot = nullptr, *d_bstart = nullptr, *d_n = nullptr, *d_total = nullptr, *d_moff0 = nullptr, *d_moff1 = nullptr;
   unsigned long long *d_bstats = nullptr, *d_sred = nullptr;  // per-block apply counters, their sum
   uint64_t *d_stats = nullptr, *d_cvec = nullptr, *d_cmat = nullptr, *d_inflight = nullptr;
@@ -292,10 +295,10 @@ agx_status launch_dense_pass(agx_engine* e, const DevMsgs& in, const DevMsgs& ou
   sa.hist = e->d_hist_d;
   sa.tot = e->d_tot;
   sa.bstart = e->d_bstart;
-  sa.stride = (uint32_t)e->max_tiles;
+  sa.stride = e->dstride;
   sa.shift = shift;
   sa.bits = bits;
-  const uint32_t g = grid_for(e->max_tiles, 2048);
+  const uint32_t g = grid_for(e->max_supers, 4096);
   {
     Scope s(e, K_UPSWEEP);
     hipLaunchKernelGGL(k_sort_upsweep, dim3(g), dim3(kThreads), 0, e->stream, sa);
@@ -334,8 +337,10 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     ca.step = e->pw ? e->d_step : nullptr;
     ca.heap_top = e->d_heap_top;
     ca.cap = e->cap;
-    ca.stride = e->nchunks;
-    ca.nchunks = e->nchunks;
+    ca.stride = e->cstride;
+    ca.nunits = e->nunits;
+    ca.ng = e->ng;
+    ca.G = e->G;
     ca.shift = e->plan.shift[0];
     ca.bits = e->plan.bits[0];
     {
@@ -344,7 +349,7 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     }
     {
       Scope s(e, K_CDOWN);
-      hipLaunchKernelGGL(k_chunk_downsweep, dim3(grid_for(e->nchunks, 4096)), dim3(kThreads), 0, e->stream, ca);
+      hipLaunchKernelGGL(k_chunk_downsweep, dim3(grid_for(e->nunits, 4096)), dim3(kThreads), 0, e->stream, ca);
     }
     HIP_TRY(hipGetLastError());
     p0 = 1;
@@ -377,7 +382,9 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.chunk_off = e->d_chunk_off;
   ba.chunk_cnt = e->d_chunk_cnt;
   ba.nhist = e->d_hist_c;
-  ba.nhist_stride = e->nchunks;
+  ba.nhist_stride = e->cstride;
+  ba.G = e->G;
+  ba.ng = e->ng;
   ba.nx_shift = e->plan.shift[0];
   ba.nx_bits = e->plan.bits[0];
   ba.nb = e->nb;
@@ -387,10 +394,20 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.dbg = e->d_dbg;
   {
     Scope s(e, K_APPLY);
+    const dim3 g(grid_for(e->nb, kMaxApplyGrid)), blk(kBThreads);
+    const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
     if (e->pw)  // CRDT kinds registered: the variant with state gossips
-      hipLaunchKernelGGL(k_bucket_apply<true>, dim3(grid_for(e->nb, kMaxApplyGrid)), dim3(kBThreads), 0, e->stream, ba);
+      hipLaunchKernelGGL((k_bucket_apply<true, KM_ALL>), g, blk, 0, e->stream, ba);
+    else if (km == kb(AGX_KIND_RING))  // behaviour-specialised variants (see apply_msg)
+      hipLaunchKernelGGL((k_bucket_apply<false, kb(AGX_KIND_RING)>), g, blk, 0, e->stream, ba);
+    else if (km == kb(AGX_KIND_FORWARD_RR))
+      hipLaunchKernelGGL((k_bucket_apply<false, kb(AGX_KIND_FORWARD_RR)>), g, blk, 0, e->stream, ba);
+    else if (km == kb(AGX_KIND_FANOUT))
+      hipLaunchKernelGGL((k_bucket_apply<false, kb(AGX_KIND_FANOUT)>), g, blk, 0, e->stream, ba);
+    else if (km == kb(AGX_KIND_COUNTER))
+      hipLaunchKernelGGL((k_bucket_apply<false, kb(AGX_KIND_COUNTER)>), g, blk, 0, e->stream, ba);
     else
-      hipLaunchKernelGGL(k_bucket_apply<false>, dim3(grid_for(e->nb, kMaxApplyGrid)), dim3(kBThreads), 0, e->stream, ba);
+      hipLaunchKernelGGL((k_bucket_apply<false, KM_ALL>), g, blk, 0, e->stream, ba);
   }
   HIP_TRY(hipGetLastError());
   return AGX_OK;
@@ -399,9 +416,9 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
 // host-staged tells enter as chunk 2nb of the next single-rank step
 agx_status launch_staged_chunk(agx_engine* e) {
   if (!e->n_staged_dev) return AGX_OK;
-  hipLaunchKernelGGL(k_chunk_hist, dim3(kStagedChunks), dim3(kThreads), 0,
-                     e->stream, e->stg.key, e->n_staged_dev, e->d_hist_c, e->nchunks, 2 * e->nb, e->plan.shift[0],
-                     e->plan.bits[0], e->d_chunk_off, e->d_chunk_cnt);
+  hipLaunchKernelGGL(k_chunk_hist, dim3(kStagedChunks), dim3(kThreads), 0, e->stream, e->stg.key, e->n_staged_dev,
+                     e->d_hist_c, e->cstride, 2 * e->ng, e->plan.shift[0], e->plan.bits[0], e->d_chunk_off,
+                     e->d_chunk_cnt, 2 * e->nb);
   HIP_TRY(hipGetLastError());
   e->n_staged_dev = 0;
   return AGX_OK;
@@ -809,10 +826,17 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   if (e->cap >= (1ull << 32) - kTile) { delete e; return set_err(AGX_EINVAL, "msg_capacity too large"); }
   e->cap_emit = e->cap * e->kmax;  // bucket b's tells live at [lo*kmax, (lo+cnt)*kmax)
   if (e->cap_emit >= (1ull << 32)) { delete e; return set_err(AGX_EINVAL, "msg_capacity * max_emit must be < 2^32"); }
-  e->max_tiles = (std::max(e->cap, e->cap_emit) + kTile - 1) / kTile + 1;
+  e->max_supers = (uint32_t)((std::max(e->cap, e->cap_emit) + kSuper - 1) / kSuper + 1);
+  e->dstride = (e->max_supers + 3) & ~3u;
   // buckets of 2^kBucketBits actors; LSD passes over key bits [kBucketBits, key_bits), <= kRadixBits each
   e->nb = (uint32_t)((nl + kBucket - 1) / kBucket);
   e->nchunks = 2 * e->nb + kStagedChunks;
+  // first-pass histogram columns: ~2048 units per arena at most (G buckets per unit)
+  e->G = (e->nb + 2047) / 2048;
+  if (const char* s = getenv("AGX_UNIT_G")) e->G = (uint32_t)std::max(1, atoi(s));  // test knob
+  e->ng = (e->nb + e->G - 1) / e->G;
+  e->nunits = 2 * e->ng + kStagedChunks;
+  e->cstride = (e->nunits + 3) & ~3u;
   {
     const uint32_t lo = kBucketBits, hi = std::max<uint32_t>(e->key_bits, kBucketBits + 1);
     // AGX_RADIX_BITS (test knob): narrower digits, so that small populations take the multi-pass path
@@ -867,11 +891,11 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(dalloc(&e->d_chunk_cnt, e->nchunks));
   CREATE_TRY(hipMemset(e->d_chunk_off, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(hipMemset(e->d_chunk_cnt, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-  CREATE_TRY(dalloc(&e->d_hist_c, (uint64_t)kRadix * e->nchunks));
-  CREATE_TRY(hipMemset(e->d_hist_c, 0, (uint64_t)kRadix * e->nchunks * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(dalloc(&e->d_hist_c, (uint64_t)kRadix * e->cstride));
+  CREATE_TRY(hipMemset(e->d_hist_c, 0, (uint64_t)kRadix * e->cstride * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_bstart, std::max<uint64_t>(kRadix, e->nb) + 1));
   if (getenv("AGX_STAMPS")) CREATE_TRY(dalloc(&e->d_dbg, (uint64_t)std::min<uint64_t>(e->nb, 4096) * 16));
-  CREATE_TRY(dalloc(&e->d_hist_d, (uint64_t)kRadix * e->max_tiles));
+  CREATE_TRY(dalloc(&e->d_hist_d, (uint64_t)kRadix * e->dstride));
   CREATE_TRY(dalloc(&e->d_tot, kRadix));
   CREATE_TRY(dalloc(&e->d_n, 4));
   CREATE_TRY(dalloc(&e->d_total, 4));
@@ -933,6 +957,10 @@ agx_status agx_register_range(agx_engine* e, uint64_t first_id, uint64_t count, 
     return set_err(AGX_EINVAL, "behaviour kind %u needs n_words >= 2", kind);
   if (init && stride < e->W * 8ull) return set_err(AGX_EINVAL, "state_stride smaller than n_words*8");
   if (kind >= AGX_KIND_GCOUNTER && kind <= AGX_KIND_ORSET) AGX_TRY(enable_crdt(e, kind));
+  if (count && !(e->kinds_mask & kb(kind))) {  // the apply variant is captured in the superstep graphs
+    e->kinds_mask |= kb(kind);
+    drop_graphs(e);
+  }
   const uint8_t* ib = (const uint8_t*)init;
   for (uint64_t i = 0; i < count; ++i) {
     uint64_t id = first_id + i, l;

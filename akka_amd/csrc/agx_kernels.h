@@ -137,12 +137,161 @@ __device__ __forceinline__ void lds_hist_inc(uint32_t* h, uint32_t d) {
 }
 
 // =========================================================================
-// Chunked first radix pass
+// Stable multisplit of one tile (<= kTile items) by a radix digit: wave ballot
+// ranks, LDS staging, coalesced scatter.  `S.base[d]` is the output position of
+// the next item of digit d and is advanced by this tile's digit counts.
+// =========================================================================
+struct SplitLds {
+  uint32_t (*whist)[kRadix];  // [kWaves][kRadix]
+  uint32_t* base;             // [kRadix] running output position per digit
+  uint32_t* ldig;             // [kRadix] tile-local digit starts
+  uint32_t* gadj;             // [kRadix] base - ldig
+  uint32_t* scratch;          // kWaves + 1
+  uint32_t *key, *src, *pay;  // [kTile]
+};
+
+__device__ __forceinline__ void split_tile(const CMsgs& in, uint32_t base, uint32_t cnt, const Msgs& out,
+                                           uint32_t shift, uint32_t bits, const SplitLds& S) {
+  const int tid = threadIdx.x, w = tid / kWave;
+  const uint32_t lane = lane_id();
+  const uint32_t mask = (1u << bits) - 1u, nd = 1u << bits;
+  const uint64_t ltm = lanemask_lt();
+  for (int i = tid; i < kWaves * kRadix; i += kThreads) (&S.whist[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t wbase = w * (kIpt * kWave);
+  uint32_t k[kIpt], sv[kIpt], pv[kIpt], rk[kIpt];
+#pragma unroll
+  for (int r = 0; r < kIpt; ++r) {
+    const uint32_t q = wbase + r * kWave + lane;
+    if (q < cnt) {
+      k[r] = in.key[base + q];
+      sv[r] = in.src[base + q];
+      pv[r] = in.pay[base + q];
+    } else {
+      k[r] = 0xFFFFFFFFu;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kIpt; ++r) {
+    const uint32_t q = wbase + r * kWave + lane;
+    rk[r] = wave_rank(q < cnt, (k[r] >> shift) & mask, bits, S.whist[w], ltm);
+  }
+  __syncthreads();
+  uint32_t cd[kRadix / kThreads];
+#pragma unroll
+  for (int j = 0; j < kRadix / kThreads; ++j) {
+    const uint32_t d = tid + j * kThreads;
+    uint32_t run = 0;
+#pragma unroll
+    for (int q = 0; q < kWaves; ++q) {
+      const uint32_t c2 = S.whist[q][d];
+      S.whist[q][d] = run;
+      run += c2;
+    }
+    cd[j] = d < nd ? run : 0u;
+  }
+  {  // tile-local digit starts: exclusive scan over 512 digits, 2 per thread (blocked)
+    S.ldig[tid] = cd[0];
+    S.ldig[tid + kThreads] = cd[1];
+    __syncthreads();
+    const uint32_t v0 = S.ldig[2 * tid], v1 = S.ldig[2 * tid + 1];
+    __syncthreads();
+    uint32_t t2;
+    const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, S.scratch, &t2);
+    S.ldig[2 * tid] = ex;
+    S.ldig[2 * tid + 1] = ex + v0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRadix / kThreads; ++j) {
+    const uint32_t d = tid + j * kThreads;
+    if (d < nd) {
+      S.gadj[d] = S.base[d] - S.ldig[d];
+      S.base[d] += cd[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kIpt; ++r) {
+    const uint32_t q = wbase + r * kWave + lane;
+    if (q < cnt) {
+      const uint32_t d = (k[r] >> shift) & mask;
+      const uint32_t lp = S.ldig[d] + S.whist[w][d] + rk[r];
+      S.key[lp] = k[r];
+      S.src[lp] = sv[r];
+      S.pay[lp] = pv[r];
+    }
+  }
+  __syncthreads();
+  for (uint32_t lp = tid; lp < cnt; lp += kThreads) {
+    const uint32_t kk = S.key[lp];
+    const uint32_t g = S.gadj[(kk >> shift) & mask] + lp;
+    out.key[g] = kk;
+    out.src[g] = S.src[lp];
+    out.pay[g] = S.pay[lp];
+  }
+  __syncthreads();
+}
+
+// digit bases: s_dbase[d] = exclusive scan of tot[d] over digits; returns the total
+__device__ __forceinline__ uint32_t digit_bases(const uint32_t* tot, uint32_t nd, uint32_t* s_dbase, uint32_t* scratch) {
+  const int tid = threadIdx.x;
+  for (uint32_t d = tid; d < kRadix; d += kThreads) s_dbase[d] = d < nd ? tot[d] : 0u;
+  __syncthreads();
+  const uint32_t v0 = s_dbase[2 * tid], v1 = s_dbase[2 * tid + 1];
+  __syncthreads();
+  uint32_t t;
+  const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, scratch, &t);
+  s_dbase[2 * tid] = ex;
+  s_dbase[2 * tid + 1] = ex + v0;
+  __syncthreads();
+  return t;
+}
+
+// Exclusive prefix, in place, of one digit row of a histogram table (len entries,
+// row 16-byte aligned): 4 consecutive entries per thread.  Returns the row total.
+__device__ __forceinline__ uint32_t scan_row(uint32_t* row, uint32_t len, uint32_t* scratch) {
+  const int tid = threadIdx.x;
+  uint32_t run = 0;
+  for (uint32_t base = 0; base < len; base += 4 * kThreads) {
+    const uint32_t i0 = base + 4 * tid;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (i0 + 3 < len) {
+      v = reinterpret_cast<const uint4*>(row)[i0 / 4];
+    } else if (i0 < len) {
+      v.x = row[i0];
+      if (i0 + 1 < len) v.y = row[i0 + 1];
+      if (i0 + 2 < len) v.z = row[i0 + 2];
+    }
+    uint32_t t;
+    const uint32_t ex = run + block_excl_sum<kThreads>(v.x + v.y + v.z + v.w, scratch, &t);
+    const uint4 o = make_uint4(ex, ex + v.x, ex + v.x + v.y, ex + v.x + v.y + v.z);
+    if (i0 + 3 < len) {
+      reinterpret_cast<uint4*>(row)[i0 / 4] = o;
+    } else if (i0 < len) {
+      row[i0] = o.x;
+      if (i0 + 1 < len) row[i0 + 1] = o.y;
+      if (i0 + 2 < len) row[i0 + 2] = o.z;
+    }
+    run += t;
+  }
+  return run;
+}
+
+// =========================================================================
+// First radix pass, reading the chunk list left by k_bucket_apply.
+// Histogram columns ("units") group G consecutive buckets' chunks:
+//   unit u <  ng        backlog chunks of buckets [uG, uG+G)
+//   unit ng + u         tell chunks of buckets [uG, uG+G)
+//   unit 2ng + c        host-staged chunk c
+// k_bucket_apply adds its digit counts into its unit's column; the rowscan turns
+// each digit row into an exclusive prefix over units; the downsweep block of unit
+// u places that unit's chunks in order (canonical order preserved).
 // =========================================================================
 struct ChunkSortArgs {
   Chunks ch;
   Msgs out;
-  uint32_t* hist;      // digit-major [nbins][stride]: per-chunk digit counts -> exclusive prefix
+  uint32_t* hist;      // digit-major [nbins][stride]: per-unit digit counts -> exclusive prefix
   uint32_t* tot;       // [nbins] digit totals
   uint32_t* d_n;       // out: total messages
   uint32_t* bstart;    // out: exclusive scan of digit totals (bucket starts when one pass)
@@ -153,65 +302,32 @@ struct ChunkSortArgs {
   uint32_t* step;      // CRDT heap parity (null when no CRDT kind is registered)
   uint32_t* heap_top;
   uint64_t cap;
-  uint32_t stride, nchunks, shift, bits;
+  uint32_t stride, nunits, ng, G, shift, bits;
 };
 
-// one block per digit: exclusive prefix over chunks (in place) + digit total;
+// one block per digit: exclusive prefix over units (in place) + digit total;
 // block 0 also commits the previous step's stops.
 __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs a) {
   __shared__ uint32_t scratch[kWaves + 1];
-  __shared__ uint32_t s_run;
   if (blockIdx.x == 0) {
     begin_step(a.step, a.heap_top);
     commit_stops(a.alive, a.stopq, a.nstop);
   }
   const uint32_t d = blockIdx.x;
   if (d >= (1u << a.bits)) return;
-  uint32_t* row = a.hist + (size_t)d * a.stride;
-  if (threadIdx.x == 0) s_run = 0;
-  __syncthreads();
-  for (uint32_t base = 0; base < a.nchunks; base += kThreads) {
-    const uint32_t i = base + threadIdx.x;
-    uint32_t v = i < a.nchunks ? row[i] : 0u, t;
-    const uint32_t ex = block_excl_sum<kThreads>(v, scratch, &t);
-    if (i < a.nchunks) row[i] = s_run + ex;
-    __syncthreads();
-    if (threadIdx.x == 0) s_run += t;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) a.tot[d] = s_run;
+  const uint32_t t = scan_row(a.hist + (size_t)d * a.stride, a.nunits, scratch);
+  if (threadIdx.x == 0) a.tot[d] = t;
 }
 
 __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
   __shared__ uint32_t whist[kWaves][kRadix];
-  __shared__ uint32_t s_dbase[kRadix];  // exclusive scan of digit totals
-  __shared__ uint32_t s_run[kRadix];    // items of each digit already placed from this chunk
-  __shared__ uint32_t s_ldig[kRadix];
-  __shared__ uint32_t s_gadj[kRadix];
+  __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
   __shared__ uint32_t scratch[kWaves + 1];
-  __shared__ uint32_t s_total;
   __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
-
-  const int tid = threadIdx.x, w = tid / kWave;
-  const uint32_t lane = lane_id();
-  const uint32_t mask = (1u << a.bits) - 1u, nd = 1u << a.bits;
-  const uint64_t ltm = lanemask_lt();
-  for (uint32_t d = tid; d < kRadix; d += kThreads) {
-    uint32_t v = d < nd ? a.tot[d] : 0u;
-    s_dbase[d] = v;
-  }
-  __syncthreads();
-  {  // exclusive scan over (up to 512) digit totals: 2 per thread
-    const uint32_t v0 = s_dbase[2 * tid], v1 = s_dbase[2 * tid + 1];
-    uint32_t t;
-    __syncthreads();
-    const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, scratch, &t);
-    s_dbase[2 * tid] = ex;
-    s_dbase[2 * tid + 1] = ex + v0;
-    if (tid == 0) s_total = t;
-  }
-  __syncthreads();
-  const uint32_t total = s_total;
+  const SplitLds S{whist, s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
+  const int tid = threadIdx.x;
+  const uint32_t nd = 1u << a.bits;
+  const uint32_t total = digit_bases(a.tot, nd, s_dbase, scratch);
   const bool over = total > a.cap;
   if (blockIdx.x == 0) {
     for (uint32_t d = tid; d < nd; d += kThreads) a.bstart[d] = s_dbase[d];
@@ -223,104 +339,45 @@ __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
   }
   if (over) return;
 
-  for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
-    const uint32_t cnt = a.ch.cnt[c];
-    // this chunk's per-digit prefix (from the rowscan), cached; the column is then zeroed so that
-    // the next k_bucket_apply can write fresh histograms without a separate memset
+  for (uint32_t u = blockIdx.x; u < a.nunits; u += gridDim.x) {
+    // chunk range of this unit
+    uint32_t c0, c1;
+    if (u < a.ng) {
+      c0 = u * a.G;
+      c1 = min(a.ch.nb, c0 + a.G);
+    } else if (u < 2 * a.ng) {
+      c0 = a.ch.nb + (u - a.ng) * a.G;
+      c1 = a.ch.nb + min(a.ch.nb, (u - a.ng + 1) * a.G);
+    } else {
+      c0 = 2 * a.ch.nb + (u - 2 * a.ng);
+      c1 = c0 + 1;
+    }
+    // this unit's per-digit prefix (from the rowscan); the column is then zeroed so
+    // that the next k_bucket_apply can accumulate fresh counts without a memset
     for (uint32_t d = tid; d < nd; d += kThreads) {
-      uint32_t* hp = a.hist + (size_t)d * a.stride + c;
-      s_run[d] = cnt ? *hp : 0u;  // s_run = chunk prefix + items placed so far
+      uint32_t* hp = a.hist + (size_t)d * a.stride + u;
+      s_base[d] = s_dbase[d] + *hp;
       *hp = 0u;
     }
-    if (cnt == 0) continue;
-    const CMsgs& src = a.ch.arena(c);
-    const uint32_t off = a.ch.off[c];
-    for (uint32_t sub = 0; sub < cnt; sub += kTile) {
-      for (int i = tid; i < kWaves * kRadix; i += kThreads) (&whist[0][0])[i] = 0;
-      __syncthreads();
-      const uint32_t wbase = sub + w * (kIpt * kWave);
-      uint32_t k[kIpt], sv[kIpt], pv[kIpt], rk[kIpt];
-#pragma unroll
-      for (int r = 0; r < kIpt; ++r) {
-        const uint32_t q = wbase + r * kWave + lane;
-        if (q < cnt) {
-          k[r] = src.key[off + q];
-          sv[r] = src.src[off + q];
-          pv[r] = src.pay[off + q];
-        } else {
-          k[r] = 0xFFFFFFFFu;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < kIpt; ++r) {
-        const uint32_t q = wbase + r * kWave + lane;
-        rk[r] = wave_rank(q < cnt, (k[r] >> a.shift) & mask, a.bits, whist[w], ltm);
-      }
-      __syncthreads();
-      uint32_t cd[kRadix / kThreads];
-#pragma unroll
-      for (int j = 0; j < kRadix / kThreads; ++j) {
-        const uint32_t d = tid + j * kThreads;
-        uint32_t run = 0;
-#pragma unroll
-        for (int q = 0; q < kWaves; ++q) {
-          const uint32_t c2 = whist[q][d];
-          whist[q][d] = run;
-          run += c2;
-        }
-        cd[j] = d < nd ? run : 0u;
-      }
-      // tile-local digit bases (scan over 512 digits: 2 per thread, blocked)
-      uint32_t t2;
-      {  // digits tid and tid+256 are in cd[0], cd[1]; exclusive scan over digits, 2 per thread (blocked)
-        const uint32_t e0 = tid * 2, e1 = tid * 2 + 1;
-        s_ldig[tid] = cd[0];
-        s_ldig[tid + kThreads] = cd[1];
-        __syncthreads();
-        const uint32_t v0 = s_ldig[e0], v1 = s_ldig[e1];
-        __syncthreads();
-        const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, scratch, &t2);
-        s_ldig[e0] = ex;
-        s_ldig[e1] = ex + v0;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < kRadix / kThreads; ++j) {
-        const uint32_t d = tid + j * kThreads;
-        if (d < nd) {
-          s_gadj[d] = s_dbase[d] + s_run[d] - s_ldig[d];
-          s_run[d] += cd[j];
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < kIpt; ++r) {
-        const uint32_t q = wbase + r * kWave + lane;
-        if (q < cnt) {
-          const uint32_t d = (k[r] >> a.shift) & mask;
-          const uint32_t lp = s_ldig[d] + whist[w][d] + rk[r];
-          s_key[lp] = k[r];
-          s_src[lp] = sv[r];
-          s_pay[lp] = pv[r];
-        }
-      }
-      __syncthreads();
-      const uint32_t nsub = min((uint32_t)kTile, cnt - sub);
-      for (uint32_t lp = tid; lp < nsub; lp += kThreads) {
-        const uint32_t kk = s_key[lp];
-        const uint32_t g = s_gadj[(kk >> a.shift) & mask] + lp;
-        a.out.key[g] = kk;
-        a.out.src[g] = s_src[lp];
-        a.out.pay[g] = s_pay[lp];
-      }
-      __syncthreads();
+    __syncthreads();
+    for (uint32_t c = c0; c < c1; ++c) {
+      const uint32_t cnt = a.ch.cnt[c];
+      if (cnt == 0) continue;
+      const CMsgs& src = a.ch.arena(c);
+      const uint32_t off = a.ch.off[c];
+      for (uint32_t sub = 0; sub < cnt; sub += kTile)
+        split_tile(src, off + sub, min((uint32_t)kTile, cnt - sub), a.out, a.shift, a.bits, S);
     }
   }
 }
 
 // =========================================================================
-// Dense radix pass (reduce-then-scan): upsweep / rowscan / downsweep
+// Dense radix pass (reduce-then-scan) over "super-tiles" of kSub tiles: one
+// histogram column per super-tile keeps the digit-major tables small.
 // =========================================================================
+constexpr int kSub = 8;
+constexpr uint32_t kSuper = (uint32_t)kTile * kSub;
+
 struct SortArgs {
   CMsgs in;
   Msgs out;
@@ -332,28 +389,50 @@ struct SortArgs {
   uint32_t shift, bits;
 };
 
+// Digit counts of four keys into a wave's LDS histogram.  Sorted-by-lower-bits input
+// (the ring after the first pass) gives whole waves of one digit: those cost one LDS
+// atomic instead of 256 conflicting ones.
+__device__ __forceinline__ void count4(uint32_t* h, const uint4& v, uint32_t shift, uint32_t mask) {
+  const uint32_t d0 = (v.x >> shift) & mask, d1 = (v.y >> shift) & mask, d2 = (v.z >> shift) & mask,
+                 d3 = (v.w >> shift) & mask;
+  const bool same4 = d0 == d1 && d0 == d2 && d0 == d3;
+  const uint32_t first = __builtin_amdgcn_readfirstlane(d0);
+  const uint64_t act = __ballot(1);
+  if (__ballot(same4 && d0 == first) == act) {
+    if (lane_id() == (uint32_t)__builtin_ctzll(act)) atomicAdd(&h[first], 4u * (uint32_t)__popcll(act));
+  } else if (same4) {
+    atomicAdd(&h[d0], 4u);
+  } else {
+    atomicAdd(&h[d0], 1u);
+    atomicAdd(&h[d1], 1u);
+    atomicAdd(&h[d2], 1u);
+    atomicAdd(&h[d3], 1u);
+  }
+}
+
 __global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
   __shared__ uint32_t h[kWaves][kRadix];
-  const uint32_t n = *a.d_n, nt = div_up(n, kTile);
+  const uint32_t n = *a.d_n, nt = div_up(n, kSuper);
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t mask = (1u << a.bits) - 1u, nd = 1u << a.bits;
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     for (int i = tid; i < kWaves * kRadix; i += kThreads) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t base = t * kTile;
-    if (base + kTile <= n) {
-      const uint4* k4 = reinterpret_cast<const uint4*>(a.in.key + base);
+    const uint32_t b0 = t * kSuper, b1 = min(n, b0 + kSuper);
+    const uint32_t nfull = (b1 - b0) / (4 * kThreads);  // full rounds of one uint4 per thread
+    const uint4* k4 = reinterpret_cast<const uint4*>(a.in.key + b0);
+    uint32_t j = 0;
+    for (; j + 8 <= nfull; j += 8) {  // eight loads in flight per thread before the LDS updates
+      uint4 v[8];
 #pragma unroll
-      for (int j = 0; j < kIpt / 4; ++j) {
-        uint4 v = k4[j * kThreads + tid];
-        atomicAdd(&h[w][(v.x >> a.shift) & mask], 1u);
-        atomicAdd(&h[w][(v.y >> a.shift) & mask], 1u);
-        atomicAdd(&h[w][(v.z >> a.shift) & mask], 1u);
-        atomicAdd(&h[w][(v.w >> a.shift) & mask], 1u);
-      }
-    } else {
-      for (uint32_t i = base + tid; i < n; i += kThreads) atomicAdd(&h[w][(a.in.key[i] >> a.shift) & mask], 1u);
+      for (int u = 0; u < 8; ++u) v[u] = k4[(j + u) * kThreads + tid];
+      asm volatile("" ::: "memory");  // keep the loads ahead of the LDS atomics (issued together)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) count4(h[w], v[u], a.shift, mask);
     }
+    for (; j < nfull; ++j) count4(h[w], k4[j * kThreads + tid], a.shift, mask);
+    for (uint32_t i = b0 + nfull * 4 * kThreads + tid; i < b1; i += kThreads)
+      atomicAdd(&h[w][(a.in.key[i] >> a.shift) & mask], 1u);
     __syncthreads();
     for (uint32_t d = tid; d < nd; d += kThreads) {
       uint32_t s = 0;
@@ -367,129 +446,32 @@ __global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
 
 __global__ void __launch_bounds__(kThreads) k_sort_rowscan(SortArgs a) {
   __shared__ uint32_t scratch[kWaves + 1];
-  __shared__ uint32_t s_run;
-  const uint32_t n = *a.d_n, nt = div_up(n, kTile);
   const uint32_t d = blockIdx.x;
   if (d >= (1u << a.bits)) return;
-  uint32_t* row = a.hist + (size_t)d * a.stride;
-  if (threadIdx.x == 0) s_run = 0;
-  __syncthreads();
-  for (uint32_t base = 0; base < nt; base += kThreads) {
-    uint32_t i = base + threadIdx.x;
-    uint32_t v = i < nt ? row[i] : 0u, t;
-    uint32_t ex = block_excl_sum<kThreads>(v, scratch, &t);
-    if (i < nt) row[i] = s_run + ex;
-    __syncthreads();
-    if (threadIdx.x == 0) s_run += t;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) a.tot[d] = s_run;
+  const uint32_t t = scan_row(a.hist + (size_t)d * a.stride, div_up(*a.d_n, kSuper), scratch);
+  if (threadIdx.x == 0) a.tot[d] = t;
 }
 
 __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) {
   __shared__ uint32_t whist[kWaves][kRadix];
-  __shared__ uint32_t s_dbase[kRadix];
-  __shared__ uint32_t s_ldig[kRadix];
-  __shared__ uint32_t s_gadj[kRadix];
+  __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
   __shared__ uint32_t scratch[kWaves + 1];
   __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
-
-  const uint32_t n = *a.d_n, nt = div_up(n, kTile);
-  const int tid = threadIdx.x, w = tid / kWave;
-  const uint32_t lane = lane_id();
-  const uint32_t mask = (1u << a.bits) - 1u, nd = 1u << a.bits;
-  const uint64_t ltm = lanemask_lt();
-  for (uint32_t d = tid; d < kRadix; d += kThreads) s_dbase[d] = d < nd ? a.tot[d] : 0u;
-  __syncthreads();
-  {
-    const uint32_t v0 = s_dbase[2 * tid], v1 = s_dbase[2 * tid + 1];
-    uint32_t t;
-    __syncthreads();
-    const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, scratch, &t);
-    s_dbase[2 * tid] = ex;
-    s_dbase[2 * tid + 1] = ex + v0;
-    if (blockIdx.x == 0 && tid == 0) a.bstart[nd] = t;
-  }
-  __syncthreads();
-  if (blockIdx.x == 0)
+  const SplitLds S{whist, s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
+  const int tid = threadIdx.x;
+  const uint32_t n = *a.d_n, nt = div_up(n, kSuper);
+  const uint32_t nd = 1u << a.bits;
+  const uint32_t total = digit_bases(a.tot, nd, s_dbase, scratch);
+  if (blockIdx.x == 0) {
     for (uint32_t d = tid; d < nd; d += kThreads) a.bstart[d] = s_dbase[d];
-  if (nt == 0) return;  // (bucket starts above are still published for an empty rank)
-
+    if (tid == 0) a.bstart[nd] = total;
+  }
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    for (int i = tid; i < kWaves * kRadix; i += kThreads) (&whist[0][0])[i] = 0;
+    for (uint32_t d = tid; d < nd; d += kThreads) s_base[d] = s_dbase[d] + a.hist[(size_t)d * a.stride + t];
     __syncthreads();
-    const uint32_t base = t * kTile;
-    const uint32_t wbase = base + w * (kIpt * kWave);
-    uint32_t k[kIpt], s[kIpt], p[kIpt], rk[kIpt];
-#pragma unroll
-    for (int r = 0; r < kIpt; ++r) {
-      const uint32_t i = wbase + r * kWave + lane;
-      if (i < n) {
-        k[r] = a.in.key[i];
-        s[r] = a.in.src[i];
-        p[r] = a.in.pay[i];
-      } else {
-        k[r] = 0xFFFFFFFFu;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < kIpt; ++r) {
-      const uint32_t i = wbase + r * kWave + lane;
-      rk[r] = wave_rank(i < n, (k[r] >> a.shift) & mask, a.bits, whist[w], ltm);
-    }
-    __syncthreads();
-    uint32_t cd[kRadix / kThreads];
-#pragma unroll
-    for (int j = 0; j < kRadix / kThreads; ++j) {
-      const uint32_t d = tid + j * kThreads;
-      uint32_t run = 0;
-#pragma unroll
-      for (int q = 0; q < kWaves; ++q) {
-        const uint32_t c2 = whist[q][d];
-        whist[q][d] = run;
-        run += c2;
-      }
-      cd[j] = d < nd ? run : 0u;
-    }
-    s_ldig[tid] = cd[0];
-    s_ldig[tid + kThreads] = cd[1];
-    __syncthreads();
-    {
-      const uint32_t v0 = s_ldig[2 * tid], v1 = s_ldig[2 * tid + 1];
-      __syncthreads();
-      uint32_t t2;
-      const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, scratch, &t2);
-      s_ldig[2 * tid] = ex;
-      s_ldig[2 * tid + 1] = ex + v0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kRadix / kThreads; ++j) {
-      const uint32_t d = tid + j * kThreads;
-      if (d < nd) s_gadj[d] = s_dbase[d] + a.hist[(size_t)d * a.stride + t] - s_ldig[d];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kIpt; ++r) {
-      const uint32_t i = wbase + r * kWave + lane;
-      if (i < n) {
-        const uint32_t d = (k[r] >> a.shift) & mask;
-        const uint32_t lp = s_ldig[d] + whist[w][d] + rk[r];
-        s_key[lp] = k[r];
-        s_src[lp] = s[r];
-        s_pay[lp] = p[r];
-      }
-    }
-    __syncthreads();
-    const uint32_t cnt_tile = min((uint32_t)kTile, n - base);
-    for (uint32_t lp = tid; lp < cnt_tile; lp += kThreads) {
-      const uint32_t kk = s_key[lp];
-      const uint32_t g = s_gadj[(kk >> a.shift) & mask] + lp;
-      a.out.key[g] = kk;
-      a.out.src[g] = s_src[lp];
-      a.out.pay[g] = s_pay[lp];
-    }
-    __syncthreads();
+    const uint32_t b0 = t * kSuper, b1 = min(n, b0 + kSuper);
+    for (uint32_t base = b0; base < b1; base += kTile)
+      split_tile(a.in, base, min((uint32_t)kTile, b1 - base), a.out, a.shift, a.bits, S);
   }
 }
 
@@ -542,6 +524,7 @@ constexpr int kBThreads = 512;                 // bucket_apply block: 8 waves
 constexpr int kBWaves = kBThreads / kWave;
 constexpr int kBIpt = kBucket / kBThreads;      // items per thread per sub-tile (4)
 constexpr int kBAct = kBucket / kBThreads;      // actors per thread (4)
+static_assert(kBAct == 4 && kBIpt == 4, "bucket_apply assumes 4 actors and 4 inbox items per thread");
 constexpr int kStagedChunks = 256;              // host-staged tells are split over this many chunks
 
 // Tell staging in LDS (single-pass path): tells overwrite consumed inbox slots of the same actor.
@@ -579,6 +562,7 @@ struct BucketArgs {
   uint32_t* chunk_cnt;
   uint32_t* nhist;         // next step's first-pass histogram, digit-major [nbins][nhist_stride]
   uint32_t nhist_stride, nx_shift, nx_bits;
+  uint32_t G, ng;          // histogram units: G buckets per column, ng units per arena
   uint32_t nb, kmax;
   uint64_t* stats;
   unsigned long long* bstats;  // [gridDim][kBStats] per-block counters (summed by k_stats_reduce)
@@ -606,7 +590,7 @@ struct BucketLds {
 
 // After the in-bucket sort: classification, queued copy, behaviour apply, emission.
 // kLds: sorted items are in LDS (fast path) or in the global scratch copy.
-template <bool kLds, bool kWide>
+template <bool kLds, bool kWide, uint32_t KM>
 __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t lo,
                                               uint32_t cnt, uint32_t a0, uint32_t na) {
   const DevParams& P = a.P;
@@ -689,22 +673,33 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     }
     if (tid == 0) {  // all queued mail is in this bucket: one bin of the next first-pass histogram
       const uint32_t d = ((b << kBucketBits) >> a.nx_shift) & nhmask;
-      a.nhist[(size_t)d * a.nhist_stride + b] = bltot;
+      atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + b / a.G], bltot);
     }
   }
   __syncthreads();
 
   AGX_STAMP(a, 4);
-  // ---- prefetch kind + state words 0/1 of actors with mail (striped: coalesced)
+  // ---- prefetch kind + state words 0/1 of actors with mail (striped: coalesced).  All loads
+  // are issued before the LDS stores (the stores go through generic pointers).
+  {
+    uint32_t kd[kBAct];
+    uint64_t x0[kBAct], x1[kBAct];
 #pragma unroll
-  for (int j = 0; j < kBAct; ++j) {
-    const uint32_t la = j * kBThreads + tid;
-    L.ecnt[la] = 0;
-    if (la < na && L.alive[la] && L.seg[la + 1] != L.seg[la]) {
+    for (int j = 0; j < kBAct; ++j) {
+      const uint32_t la = j * kBThreads + tid;
+      const bool has = la < na && L.alive[la] && L.seg[la + 1] != L.seg[la];
       const uint32_t l = a0 + la;
-      L.kind[la] = P.kind[l];
-      w0s[la] = P.state[l];
-      w1s[la] = P.W > 1 ? P.state[(size_t)P.n_local + l] : 0ull;
+      kd[j] = has && (KM & (KM - 1)) != 0 ? P.kind[l] : 0u;  // single-kind variants never read it
+      x0[j] = has ? P.state[l] : 0ull;
+      x1[j] = has && P.W > 1 ? P.state[(size_t)P.n_local + l] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kBAct; ++j) {
+      const uint32_t la = j * kBThreads + tid;
+      L.ecnt[la] = 0;
+      L.kind[la] = (uint8_t)kd[j];
+      w0s[la] = x0[j];
+      w1s[la] = x1[j];
     }
   }
   uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0, emtot = 0;
@@ -727,7 +722,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       ++nact;
       for (uint32_t q = 0; q < nd; ++q) {
         const uint32_t sv = L.src[s0 + q], pv = L.pay[s0 + q];
-        const uint32_t r = apply_msg(P, L.kind[la], self, l, wv, sv, pv, em);
+        const uint32_t r = apply_msg<KM>(P, L.kind[la], self, l, wv, sv, pv, em);
         ++ndel;
         if (r == AGX_RES_UNHANDLED) ++nunh;
         if (r == AGX_RES_STOPPED) {
@@ -793,7 +788,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         for (uint32_t q = 0; q < nd; ++q) {
           const uint32_t sv = isrc(s0 + q);
           if (kWide && is_wide(sv)) continue;  // not in this behaviour's protocol: unhandled, no tells
-          const uint32_t r = apply_msg(P, kd, self, l, wv, sv, ipay(s0 + q), em);
+          const uint32_t r = apply_msg<KM>(P, kd, self, l, wv, sv, ipay(s0 + q), em);
           if (r == AGX_RES_STOPPED) break;
         }
       }
@@ -859,7 +854,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
             ++nunh;
             continue;
           }
-          const uint32_t r = apply_msg(P, kd, self, l, wv, sv, ipay(s0 + q), em);
+          const uint32_t r = apply_msg<KM>(P, kd, self, l, wv, sv, ipay(s0 + q), em);
           if (r == AGX_RES_UNHANDLED) ++nunh;
           if (r == AGX_RES_STOPPED) {
             P.stopq[atomicAdd(P.nstop, 1u)] = l;
@@ -882,7 +877,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   AGX_STAMP(a, 7);
   // next first-pass histogram column of this bucket's tell chunk (zeroed by the chunk downsweep)
   for (uint32_t d = tid; d < (1u << a.nx_bits); d += kBThreads)
-    if (L.nh[d]) a.nhist[(size_t)d * a.nhist_stride + a.nb + b] = L.nh[d];
+    if (L.nh[d]) atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + a.ng + b / a.G], L.nh[d]);
   // block stats -> global
   const uint32_t lane = lane_id();
   uint32_t v0 = wave_incl_sum(ndel), v1 = wave_incl_sum(ndead), v2 = wave_incl_sum(nunh), v3 = wave_incl_sum(nall),
@@ -900,7 +895,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   AGX_STAMP(a, 8);
 }
 
-template <bool kWide>
+template <bool kWide, uint32_t KM>
 __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_key[kBucket];
   __shared__ __attribute__((aligned(16))) uint32_t s_src[kBucket];
@@ -937,7 +932,14 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       s_lo = a.bstart[b];
       s_hi = a.bstart[b + 1];
     }
-    for (uint32_t la = tid; la < kBucket; la += kBThreads) s_alive[la] = la < na ? P.alive[a0 + la] : 0;
+    {  // alive flags of the bucket, 4 per thread (a0 is a multiple of kBucket: 4-aligned)
+      const uint32_t la0 = tid * 4;
+      uint32_t v = 0;
+      if (la0 + 4 <= na) v = *reinterpret_cast<const uint32_t*>(P.alive + a0 + la0);
+      else
+        for (uint32_t j = 0; j < 4; ++j) v |= (la0 + j < na ? (uint32_t)P.alive[a0 + la0 + j] : 0u) << (8 * j);
+      reinterpret_cast<uint32_t*>(s_alive)[tid] = v;
+    }
     __syncthreads();
     AGX_STAMP(a, 1);
     const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
@@ -1039,7 +1041,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         __syncthreads();
       }
       AGX_STAMP(a, 2);
-      bucket_finish<true, kWide>(a, L, b, lo, cnt, a0, na);
+      bucket_finish<true, kWide, KM>(a, L, b, lo, cnt, a0, na);
     } else {
       // ---- general path (skewed bucket): counting sort into the global scratch copy
       uint32_t* s_run = s_key;  // LDS items are unused on this path
@@ -1113,7 +1115,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] += s_tmp[la];
         __syncthreads();
       }
-      bucket_finish<false, kWide>(a, L, b, lo, cnt, a0, na);
+      bucket_finish<false, kWide, KM>(a, L, b, lo, cnt, a0, na);
     }
   }
 }
@@ -1153,7 +1155,7 @@ __global__ void __launch_bounds__(kScanThreads) k_stats_reduce(const unsigned lo
 // Histogram columns of the host-staged chunks (one block per staged chunk).
 __global__ void __launch_bounds__(kThreads) k_chunk_hist(const uint32_t* key, uint32_t n, uint32_t* hist,
                                                          uint32_t stride, uint32_t col0, uint32_t shift, uint32_t bits,
-                                                         uint32_t* chunk_off, uint32_t* chunk_cnt) {
+                                                         uint32_t* chunk_off, uint32_t* chunk_cnt, uint32_t chunk0) {
   __shared__ uint32_t h[kRadix];
   const uint32_t mask = (1u << bits) - 1u;
   const uint32_t per = div_up(n, kStagedChunks);
@@ -1166,8 +1168,8 @@ __global__ void __launch_bounds__(kThreads) k_chunk_hist(const uint32_t* key, ui
   for (uint32_t d = threadIdx.x; d < (1u << bits); d += kThreads)
     if (h[d]) hist[(size_t)d * stride + col0 + c] = h[d];
   if (threadIdx.x == 0) {
-    chunk_off[col0 + c] = b0;
-    chunk_cnt[col0 + c] = b1 - b0;
+    chunk_off[chunk0 + c] = b0;
+    chunk_cnt[chunk0 + c] = b1 - b0;
   }
 }
 

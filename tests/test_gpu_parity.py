@@ -236,10 +236,12 @@ MULTIPASS_CASES = {
 }
 
 
-@pytest.mark.parametrize("bits", [2, 3])
+@pytest.mark.parametrize("bits,G", [(2, 1), (3, 5), (9, 3)])
 @pytest.mark.parametrize("case", sorted(MULTIPASS_CASES))
-def test_multipass_grouping(built, monkeypatch, bits, case):
+def test_multipass_grouping(built, monkeypatch, bits, G, case):
+    """AGX_UNIT_G groups G buckets per first-pass histogram column (as at 100M actors)."""
     monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
+    monkeypatch.setenv("AGX_UNIT_G", str(G))
     w = MULTIPASS_CASES[case]()
     sg, so, a, b = run_both(w)
     assert_same(sg, so, a, b, f"multipass {case} bits={bits}")
