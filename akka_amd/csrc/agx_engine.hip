@@ -143,6 +143,17 @@ struct agx_engine {
   uint32_t* h_pin = nullptr;     // pinned ring of per-step totals
   uint64_t* h_pin64 = nullptr;   // pinned scratch (count matrix, stats)
 
+  // fused superstep (single rank, one radix pass): gather-apply, parity-double-buffered arenas
+  bool fused = false;
+  DevMsgs bl2, eg0, eg1;
+  uint32_t *d_tcnt[2] = {nullptr, nullptr}, *d_toff[2] = {nullptr, nullptr};
+  uint32_t *d_blo[2] = {nullptr, nullptr}, *d_blc[2] = {nullptr, nullptr}, *d_emc[2] = {nullptr, nullptr};
+  uint32_t *d_stg_off = nullptr, *d_stg_cnt = nullptr, *d_ovf = nullptr, *d_cntb = nullptr;
+  uint32_t tstride = 4, region = 0;
+  uint64_t acap = 0;  // arena capacity (fused: regions + overflow area)
+  std::vector<uint32_t> hd_key, hd_src, hd_pay;  // staged tells on the device, not yet consumed (fused)
+  bool stg_pending = false;
+
   // host-staged tells (consumed by the next superstep)
   std::vector<uint32_t> hs_key, hs_src, hs_pay;
   uint32_t n_staged_dev = 0;  // staged tells uploaded for the next step
@@ -234,6 +245,8 @@ struct Scope {
   Scope(agx_engine* e_, int cls) : e(e_) { prof_begin(e, cls, &b); }
   ~Scope() { prof_end(e, b); }
 };
+
+void drop_graphs(agx_engine* e);
 
 DevParams make_params(agx_engine* e) {
   DevParams P{};
@@ -391,24 +404,57 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.kmax = e->kmax;
   ba.stats = e->d_stats;
   ba.bstats = e->d_bstats;
+  if (e->fused) {
+    GatherArgs& g = ba.g;
+    g.bl[0] = e->bl.m();
+    g.bl[1] = e->bl2.m();
+    g.eg[0] = e->eg0.m();
+    g.eg[1] = e->eg1.m();
+    g.stg = e->stg.c();
+    for (int q = 0; q < 2; ++q) {
+      g.tcnt[q] = e->d_tcnt[q];
+      g.toff[q] = e->d_toff[q];
+      g.blo[q] = e->d_blo[q];
+      g.blc[q] = e->d_blc[q];
+      g.emc[q] = e->d_emc[q];
+    }
+    g.stg_off = e->d_stg_off;
+    g.stg_cnt = e->d_stg_cnt;
+    g.inb = e->A.m();
+    g.step = e->d_step;
+    g.ovf = e->d_ovf;
+    g.cntb = e->d_cntb;
+    g.cap = e->acap;
+    g.tstride = e->tstride;
+    g.region = e->region;
+  }
   ba.dbg = e->d_dbg;
   {
     Scope s(e, K_APPLY);
     const dim3 g(grid_for(e->nb, kMaxApplyGrid)), blk(kBThreads);
     const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
+#define AGX_APPLY(W, M)                                                                  \
+  do {                                                                                   \
+    if (e->fused) hipLaunchKernelGGL((k_bucket_apply<W, M, true>), g, blk, 0, e->stream, ba);  \
+    else hipLaunchKernelGGL((k_bucket_apply<W, M, false>), g, blk, 0, e->stream, ba);         \
+  } while (0)
     if (e->pw)  // CRDT kinds registered: the variant with state gossips
-      hipLaunchKernelGGL((k_bucket_apply<true, KM_ALL>), g, blk, 0, e->stream, ba);
+      AGX_APPLY(true, KM_ALL);
     else if (km == kb(AGX_KIND_RING))  // behaviour-specialised variants (see apply_msg)
-      hipLaunchKernelGGL((k_bucket_apply<false, kb(AGX_KIND_RING)>), g, blk, 0, e->stream, ba);
+      AGX_APPLY(false, kb(AGX_KIND_RING));
     else if (km == kb(AGX_KIND_FORWARD_RR))
-      hipLaunchKernelGGL((k_bucket_apply<false, kb(AGX_KIND_FORWARD_RR)>), g, blk, 0, e->stream, ba);
+      AGX_APPLY(false, kb(AGX_KIND_FORWARD_RR));
     else if (km == kb(AGX_KIND_FANOUT))
-      hipLaunchKernelGGL((k_bucket_apply<false, kb(AGX_KIND_FANOUT)>), g, blk, 0, e->stream, ba);
+      AGX_APPLY(false, kb(AGX_KIND_FANOUT));
     else if (km == kb(AGX_KIND_COUNTER))
-      hipLaunchKernelGGL((k_bucket_apply<false, kb(AGX_KIND_COUNTER)>), g, blk, 0, e->stream, ba);
+      AGX_APPLY(false, kb(AGX_KIND_COUNTER));
     else
-      hipLaunchKernelGGL((k_bucket_apply<false, KM_ALL>), g, blk, 0, e->stream, ba);
+      AGX_APPLY(false, KM_ALL);
+#undef AGX_APPLY
   }
+  if (e->fused)
+    hipLaunchKernelGGL(k_fused_tick, dim3(1), dim3(kBThreads), 0, e->stream, e->d_step, e->d_cntb, e->nb, e->d_stg_cnt,
+                       e->d_ovf, e->pw ? e->d_heap_top : nullptr, e->d_n, e->d_stats);
   HIP_TRY(hipGetLastError());
   return AGX_OK;
 }
@@ -432,6 +478,45 @@ agx_status prepare_run(agx_engine* e) {
     HIP_TRY(hipMemcpyAsync(e->d_state, e->h_state.data(), e->n_local * e->W * 8, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->actors_dirty = false;
+  }
+  if (e->fused && !e->hs_key.empty()) {
+    // staged tells still on the device (a run of 0 supersteps) come first: staging order
+    if (e->stg_pending) {
+      e->hs_key.insert(e->hs_key.begin(), e->hd_key.begin(), e->hd_key.end());
+      e->hs_src.insert(e->hs_src.begin(), e->hd_src.begin(), e->hd_src.end());
+      e->hs_pay.insert(e->hs_pay.begin(), e->hd_pay.begin(), e->hd_pay.end());
+    }
+    const uint64_t n = e->hs_key.size();
+    if (n > e->stg_cap) {
+      free_msgs(e->stg);
+      AGX_TRY(alloc_msgs(e->stg, n));
+      e->stg_cap = n;
+      drop_graphs(e);  // the staging arena is a kernel argument of the captured supersteps
+    }
+    // stable counting sort by destination bucket: each bucket's staged tells are one run
+    std::vector<uint32_t> off(e->nb + 1, 0), cnt(e->nb, 0);
+    for (uint64_t i = 0; i < n; ++i) cnt[e->hs_key[i] >> kBucketBits]++;
+    for (uint32_t b = 0; b < e->nb; ++b) off[b + 1] = off[b] + cnt[b];
+    std::vector<uint32_t> k(n), sv(n), pv(n), pos(off.begin(), off.end() - 1);
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint32_t o = pos[e->hs_key[i] >> kBucketBits]++;
+      k[o] = e->hs_key[i];
+      sv[o] = e->hs_src[i];
+      pv[o] = e->hs_pay[i];
+    }
+    HIP_TRY(hipMemcpyAsync(e->stg.key, k.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->stg.src, sv.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->stg.pay, pv.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_stg_off, off.data(), e->nb * 4ull, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->d_stg_cnt, cnt.data(), e->nb * 4ull, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->hd_key.swap(e->hs_key);
+    e->hd_src.swap(e->hs_src);
+    e->hd_pay.swap(e->hs_pay);
+    e->hs_key.clear();
+    e->hs_src.clear();
+    e->hs_pay.clear();
+    e->stg_pending = true;
   }
   if (!e->hs_key.empty()) {
     uint64_t n = e->hs_key.size();
@@ -581,8 +666,12 @@ agx_status fill_stats(agx_engine* e, agx_stats* out, uint64_t inflight) {
 }
 
 agx_status chunk_inflight(agx_engine* e, uint64_t* out) {
-  hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_chunk_cnt, e->nchunks,
-                     (unsigned long long*)e->d_inflight);
+  if (e->fused)
+    hipLaunchKernelGGL(k_inflight_fused, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_blc[0], e->d_blc[1],
+                       e->d_emc[0], e->d_emc[1], e->d_stg_cnt, e->d_step, e->nb, (unsigned long long*)e->d_inflight);
+  else
+    hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_chunk_cnt, e->nchunks,
+                       (unsigned long long*)e->d_inflight);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_inflight, 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -592,6 +681,7 @@ agx_status chunk_inflight(agx_engine* e, uint64_t* out) {
 
 // one superstep on one rank: [chunks] -> group by bucket -> in-bucket sort + drain + apply -> [chunks]
 agx_status launch_step_single(agx_engine* e) {
+  if (e->fused) return launch_apply(e, e->A);  // one kernel per superstep
   AGX_TRY(launch_staged_chunk(e));
   DevMsgs* sorted = nullptr;
   AGX_TRY(launch_bucket_sort(e, true, &sorted));
@@ -625,6 +715,12 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
   agx_status st = AGX_OK;
   uint32_t left = max_steps;
   // staged host tells enter through an eager step (the graphs assume none)
+  if (left && e->fused && e->stg_pending) {  // the next superstep consumes the staged tells
+    e->stg_pending = false;
+    e->hd_key.clear();
+    e->hd_src.clear();
+    e->hd_pay.clear();
+  }
   if (left && e->n_staged_dev) {
     st = launch_step_single(e);
     --left;
@@ -852,6 +948,16 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     }
   }
 
+  // fused superstep when one radix digit covers every bucket of a single rank
+  e->fused = e->R == 1 && e->plan.npass == 1 && getenv("AGX_NO_FUSED") == nullptr;
+  e->tstride = (e->nb + 3) & ~3u;
+  // fused: bucket b's inbox (and its backlog / tell slices) live at [b*region, ...) of the
+  // arenas; an inbox larger than the region (skew) takes a slot of the overflow area that
+  // follows, sized like the whole message capacity — no shared counter on the common path
+  e->region = kBucket;
+  e->acap = e->fused ? (uint64_t)e->nb * e->region + e->cap : e->cap;
+  if (e->acap * e->kmax >= (1ull << 32)) { delete e; return set_err(AGX_EINVAL, "msg_capacity * max_emit too large"); }
+
   e->h_kind.assign(e->n_local, 0);
   e->h_alive.assign(e->n_local, 0);
   e->h_state.assign(e->n_local * e->W, 0);
@@ -876,16 +982,39 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(hipMemcpy(e->d_gid, e->h_gid.data(), e->n_local * 4, hipMemcpyHostToDevice) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "upload gid"));
     CREATE_TRY(hipMemcpy(e->d_route, e->h_route.data(), e->n_global * 4, hipMemcpyHostToDevice) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "upload route"));
   }
-  CREATE_TRY(alloc_msgs(e->A, e->cap));
-  CREATE_TRY(alloc_msgs(e->B, e->cap));
-  CREATE_TRY(alloc_msgs(e->scr, e->cap));
-  CREATE_TRY(alloc_msgs(e->bl, e->cap));
-  CREATE_TRY(alloc_msgs(e->em, e->cap_emit));
+  CREATE_TRY(alloc_msgs(e->A, e->acap));
+  CREATE_TRY(alloc_msgs(e->B, e->fused ? 1 : e->cap));
+  CREATE_TRY(alloc_msgs(e->scr, e->acap));
+  CREATE_TRY(alloc_msgs(e->bl, e->acap));
+  CREATE_TRY(alloc_msgs(e->em, e->acap * e->kmax));
   if (e->R > 1) {
     CREATE_TRY(alloc_msgs(e->s1, e->cap_emit));
     CREATE_TRY(alloc_msgs(e->s2, e->cap_emit));
     CREATE_TRY(dalloc(&e->d_moff0, e->nb));
     CREATE_TRY(dalloc(&e->d_moff1, e->nb));
+  }
+  if (e->fused) {
+    const uint64_t tsz = (uint64_t)kRadix * e->tstride;
+    CREATE_TRY(alloc_msgs(e->bl2, e->acap));
+    CREATE_TRY(alloc_msgs(e->eg0, e->acap * e->kmax));
+    CREATE_TRY(alloc_msgs(e->eg1, e->acap * e->kmax));
+    for (int q = 0; q < 2; ++q) {
+      CREATE_TRY(dalloc(&e->d_tcnt[q], tsz));
+      CREATE_TRY(dalloc(&e->d_toff[q], tsz));
+      CREATE_TRY(dalloc(&e->d_blo[q], e->nb));
+      CREATE_TRY(dalloc(&e->d_blc[q], e->nb));
+      CREATE_TRY(dalloc(&e->d_emc[q], e->nb));
+      CREATE_TRY(hipMemset(e->d_tcnt[q], 0, tsz * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+      CREATE_TRY(hipMemset(e->d_blc[q], 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+      CREATE_TRY(hipMemset(e->d_emc[q], 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    }
+    CREATE_TRY(dalloc(&e->d_stg_off, e->nb));
+    CREATE_TRY(dalloc(&e->d_stg_cnt, e->nb));
+    CREATE_TRY(dalloc(&e->d_ovf, 1));
+    CREATE_TRY(dalloc(&e->d_cntb, e->nb));
+    CREATE_TRY(hipMemset(e->d_stg_cnt, 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    CREATE_TRY(hipMemset(e->d_ovf, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    CREATE_TRY(hipMemset(e->d_cntb, 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   }
   CREATE_TRY(dalloc(&e->d_chunk_off, e->nchunks));
   CREATE_TRY(dalloc(&e->d_chunk_cnt, e->nchunks));
@@ -934,7 +1063,11 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_kind); hipFree(e->d_alive); hipFree(e->d_stopq); hipFree(e->d_nstop); hipFree(e->d_state); hipFree(e->d_gid); hipFree(e->d_route);
   hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_row); hipFree(e->d_col);
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
-  free_msgs(e->s1); free_msgs(e->s2);
+  free_msgs(e->s1); free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1);
+  for (int q = 0; q < 2; ++q) {
+    hipFree(e->d_tcnt[q]); hipFree(e->d_toff[q]); hipFree(e->d_blo[q]); hipFree(e->d_blc[q]); hipFree(e->d_emc[q]);
+  }
+  hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_cntb);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_sred); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);

@@ -102,12 +102,17 @@ struct Chunks {
 // =========================================================================
 template <typename HT>
 __device__ __forceinline__ uint32_t wave_rank(bool valid, uint32_t d, uint32_t bits, HT* hist, uint64_t lt_mask) {
-  uint64_t m = __ballot(valid);
-  for (uint32_t b = 0; b < bits; ++b) {
-    const uint32_t bit = (d >> b) & 1u;
-    const uint64_t bal = __ballot(bit);
-    m &= bit ? bal : ~bal;
-  }
+  const uint64_t vm = __ballot(valid);
+  // lowest valid lane's digit; when every valid lane has it (local topologies), the match
+  // mask is the valid mask and the per-bit ballots are skipped
+  const uint32_t first = __builtin_amdgcn_readlane(d, vm ? (int)__builtin_ctzll(vm) : 0);
+  uint64_t m = vm;
+  if (__ballot(valid && d != first) != 0)
+    for (uint32_t b = 0; b < bits; ++b) {
+      const uint32_t bit = (d >> b) & 1u;
+      const uint64_t bal = __ballot(bit);
+      m &= bit ? bal : ~bal;
+    }
   const uint32_t before = (uint32_t)__popcll(m & lt_mask);
   const uint32_t c = (uint32_t)__popcll(m);
   uint32_t old = 0;
@@ -142,26 +147,28 @@ __device__ __forceinline__ void lds_hist_inc(uint32_t* h, uint32_t d) {
 // the next item of digit d and is advanced by this tile's digit counts.
 // =========================================================================
 struct SplitLds {
-  uint32_t (*whist)[kRadix];  // [kWaves][kRadix]
+  uint32_t* whist;            // [NT/64][kRadix] per-wave digit counts
   uint32_t* base;             // [kRadix] running output position per digit
   uint32_t* ldig;             // [kRadix] tile-local digit starts
   uint32_t* gadj;             // [kRadix] base - ldig
-  uint32_t* scratch;          // kWaves + 1
+  uint32_t* scratch;          // NT/64 + 1
   uint32_t *key, *src, *pay;  // [kTile]
 };
 
+template <int NT>
 __device__ __forceinline__ void split_tile(const CMsgs& in, uint32_t base, uint32_t cnt, const Msgs& out,
                                            uint32_t shift, uint32_t bits, const SplitLds& S) {
+  constexpr int NW = NT / kWave, IPT = kTile / NT, DPT = kRadix / NT;
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t lane = lane_id();
   const uint32_t mask = (1u << bits) - 1u, nd = 1u << bits;
   const uint64_t ltm = lanemask_lt();
-  for (int i = tid; i < kWaves * kRadix; i += kThreads) (&S.whist[0][0])[i] = 0;
+  for (int i = tid; i < NW * kRadix; i += NT) S.whist[i] = 0;
   __syncthreads();
-  const uint32_t wbase = w * (kIpt * kWave);
-  uint32_t k[kIpt], sv[kIpt], pv[kIpt], rk[kIpt];
+  const uint32_t wbase = w * (IPT * kWave);
+  uint32_t k[IPT], sv[IPT], pv[IPT], rk[IPT];
 #pragma unroll
-  for (int r = 0; r < kIpt; ++r) {
+  for (int r = 0; r < IPT; ++r) {
     const uint32_t q = wbase + r * kWave + lane;
     if (q < cnt) {
       k[r] = in.key[base + q];
@@ -172,39 +179,46 @@ __device__ __forceinline__ void split_tile(const CMsgs& in, uint32_t base, uint3
     }
   }
 #pragma unroll
-  for (int r = 0; r < kIpt; ++r) {
+  for (int r = 0; r < IPT; ++r) {
     const uint32_t q = wbase + r * kWave + lane;
-    rk[r] = wave_rank(q < cnt, (k[r] >> shift) & mask, bits, S.whist[w], ltm);
+    rk[r] = wave_rank(q < cnt, (k[r] >> shift) & mask, bits, S.whist + w * kRadix, ltm);
   }
   __syncthreads();
-  uint32_t cd[kRadix / kThreads];
+  uint32_t cd[DPT];
 #pragma unroll
-  for (int j = 0; j < kRadix / kThreads; ++j) {
-    const uint32_t d = tid + j * kThreads;
+  for (int j = 0; j < DPT; ++j) {
+    const uint32_t d = tid + j * NT;
     uint32_t run = 0;
 #pragma unroll
-    for (int q = 0; q < kWaves; ++q) {
-      const uint32_t c2 = S.whist[q][d];
-      S.whist[q][d] = run;
+    for (int q = 0; q < NW; ++q) {
+      const uint32_t c2 = S.whist[q * kRadix + d];
+      S.whist[q * kRadix + d] = run;
       run += c2;
     }
     cd[j] = d < nd ? run : 0u;
+    S.ldig[d] = cd[j];
   }
-  {  // tile-local digit starts: exclusive scan over 512 digits, 2 per thread (blocked)
-    S.ldig[tid] = cd[0];
-    S.ldig[tid + kThreads] = cd[1];
-    __syncthreads();
-    const uint32_t v0 = S.ldig[2 * tid], v1 = S.ldig[2 * tid + 1];
+  __syncthreads();
+  {  // tile-local digit starts: exclusive scan over kRadix digits, DPT per thread (blocked)
+    uint32_t v[DPT], tot = 0;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      v[j] = S.ldig[tid * DPT + j];
+      tot += v[j];
+    }
     __syncthreads();
     uint32_t t2;
-    const uint32_t ex = block_excl_sum<kThreads>(v0 + v1, S.scratch, &t2);
-    S.ldig[2 * tid] = ex;
-    S.ldig[2 * tid + 1] = ex + v0;
+    uint32_t ex = block_excl_sum<NT>(tot, S.scratch, &t2);
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      S.ldig[tid * DPT + j] = ex;
+      ex += v[j];
+    }
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kRadix / kThreads; ++j) {
-    const uint32_t d = tid + j * kThreads;
+  for (int j = 0; j < DPT; ++j) {
+    const uint32_t d = tid + j * NT;
     if (d < nd) {
       S.gadj[d] = S.base[d] - S.ldig[d];
       S.base[d] += cd[j];
@@ -212,18 +226,18 @@ __device__ __forceinline__ void split_tile(const CMsgs& in, uint32_t base, uint3
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kIpt; ++r) {
+  for (int r = 0; r < IPT; ++r) {
     const uint32_t q = wbase + r * kWave + lane;
     if (q < cnt) {
       const uint32_t d = (k[r] >> shift) & mask;
-      const uint32_t lp = S.ldig[d] + S.whist[w][d] + rk[r];
+      const uint32_t lp = S.ldig[d] + S.whist[w * kRadix + d] + rk[r];
       S.key[lp] = k[r];
       S.src[lp] = sv[r];
       S.pay[lp] = pv[r];
     }
   }
   __syncthreads();
-  for (uint32_t lp = tid; lp < cnt; lp += kThreads) {
+  for (uint32_t lp = tid; lp < cnt; lp += NT) {
     const uint32_t kk = S.key[lp];
     const uint32_t g = S.gadj[(kk >> shift) & mask] + lp;
     out.key[g] = kk;
@@ -324,7 +338,7 @@ __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
   __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
   __shared__ uint32_t scratch[kWaves + 1];
   __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
-  const SplitLds S{whist, s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
+  const SplitLds S{&whist[0][0], s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
   const int tid = threadIdx.x;
   const uint32_t nd = 1u << a.bits;
   const uint32_t total = digit_bases(a.tot, nd, s_dbase, scratch);
@@ -366,7 +380,7 @@ __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
       const CMsgs& src = a.ch.arena(c);
       const uint32_t off = a.ch.off[c];
       for (uint32_t sub = 0; sub < cnt; sub += kTile)
-        split_tile(src, off + sub, min((uint32_t)kTile, cnt - sub), a.out, a.shift, a.bits, S);
+        split_tile<kThreads>(src, off + sub, min((uint32_t)kTile, cnt - sub), a.out, a.shift, a.bits, S);
     }
   }
 }
@@ -457,7 +471,7 @@ __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) {
   __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
   __shared__ uint32_t scratch[kWaves + 1];
   __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
-  const SplitLds S{whist, s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
+  const SplitLds S{&whist[0][0], s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
   const int tid = threadIdx.x;
   const uint32_t n = *a.d_n, nt = div_up(n, kSuper);
   const uint32_t nd = 1u << a.bits;
@@ -471,7 +485,7 @@ __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) {
     __syncthreads();
     const uint32_t b0 = t * kSuper, b1 = min(n, b0 + kSuper);
     for (uint32_t base = b0; base < b1; base += kTile)
-      split_tile(a.in, base, min((uint32_t)kTile, b1 - base), a.out, a.shift, a.bits, S);
+      split_tile<kThreads>(a.in, base, min((uint32_t)kTile, b1 - base), a.out, a.shift, a.bits, S);
   }
 }
 
@@ -551,8 +565,33 @@ struct EmitterLds {
   }
 };
 
+// Fused superstep (single rank, one radix digit covers every bucket): k_bucket_apply
+// gathers its inbox straight from the tell chunks of the previous superstep, which
+// were written grouped by destination bucket, so no separate sort kernel runs.
+// Arenas and tables are double-buffered by superstep parity (step & 1).
+struct GatherArgs {
+  Msgs bl[2];              // backlog of bucket b at [lo_b, +blc) (parity)
+  Msgs eg[2];              // tells grouped by destination bucket (parity)
+  CMsgs stg;               // host-staged tells, grouped by bucket on the host
+  uint32_t* tcnt[2];       // [nd][tstride]: tells from chunk c to bucket d (zeroed by the reader)
+  uint32_t* toff[2];       // [nd][tstride]: their offset in eg[parity]
+  uint32_t* blo[2];        // [nb] backlog offset / count per bucket
+  uint32_t* blc[2];
+  uint32_t* emc[2];        // [nb] tells emitted per bucket (in-flight accounting)
+  uint32_t* stg_off;       // [nb] staged tells per bucket (count zeroed by the reader)
+  uint32_t* stg_cnt;
+  Msgs inb;                // skewed buckets: gathered inbox copy at [lo, lo+cnt)
+  uint32_t* step;          // superstep counter (parity = step & 1), advanced by k_fused_tick
+  uint32_t* ovf;           // overflow-region cursor (inboxes larger than `region`), reset by the tick
+  uint32_t* cntb;          // [nb] inbox size per bucket this superstep (summed by the tick)
+  uint64_t cap;
+  uint32_t tstride;
+  uint32_t region;         // bucket b's inbox lives at [b*region, ...) unless larger (overflow region)
+};
+
 struct BucketArgs {
   DevParams P;
+  GatherArgs g;
   CMsgs in;                // mail sorted by bucket (local key >> kBucketBits)
   const uint32_t* d_n;
   const uint32_t* bstart;  // bucket starts [nb + 1]
@@ -590,9 +629,84 @@ struct BucketLds {
 
 // After the in-bucket sort: classification, queued copy, behaviour apply, emission.
 // kLds: sorted items are in LDS (fast path) or in the global scratch copy.
-template <bool kLds, bool kWide, uint32_t KM>
+// Tells of one bucket in sender order -> grouped by destination bucket in eg[w] at
+// [embase, embase+emtot), plus this chunk's column of the parity-w tables.  Every
+// destination's run is contiguous and in sender order (stable multisplit).
+template <bool kFromLds>
+__device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t w,
+                                            uint64_t embase, uint32_t emtot, const Msgs& src) {
+  const GatherArgs& g = a.g;
+  const int tid = threadIdx.x;
+  const uint32_t nd = 1u << a.nx_bits;
+  uint32_t* whist = L.key;             // [kBWaves][kRadix] u32 = 16 KB over key+src (free now)
+  uint32_t* dbase = L.ecnt;            // [kRadix]
+  uint32_t* base = L.ecnt + kRadix;    // [kRadix] running positions (multi-tile)
+  uint32_t* ldig = L.ecnt + 2 * kRadix;
+  uint32_t* gadj = L.ecnt + 3 * kRadix;
+  {  // destination bases inside the chunk: exclusive scan of the per-destination counts
+    const uint32_t v = (uint32_t)tid < nd ? L.nh[tid] : 0u;
+    uint32_t t;
+    const uint32_t ex = block_excl_sum<kBThreads>(v, L.scratch, &t);
+    dbase[tid] = (uint32_t)embase + ex;
+    base[tid] = (uint32_t)embase + ex;
+    if ((uint32_t)tid < nd && v) {
+      g.tcnt[w][(size_t)tid * g.tstride + b] = v;
+      g.toff[w][(size_t)tid * g.tstride + b] = (uint32_t)embase + ex;
+    }
+  }
+  __syncthreads();
+  if (kFromLds) {  // <= kBucket tells, compacted in sender order in U: ranks + direct scatter
+    const uint32_t* ukey = reinterpret_cast<const uint32_t*>(L.U);
+    const uint32_t* usrc = ukey + kBucket;
+    const uint32_t* upay = usrc + kBucket;
+    const int wv = tid / kWave;
+    const uint32_t lane = lane_id();
+    const uint64_t ltm = lanemask_lt();
+    for (int i = tid; i < kBWaves * kRadix; i += kBThreads) whist[i] = 0;
+    __syncthreads();
+    uint32_t k[kBIpt], d[kBIpt], rk[kBIpt];
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r) {
+      const uint32_t i = wv * (kBIpt * kWave) + r * kWave + lane;
+      k[r] = i < emtot ? ukey[i] : 0u;
+      d[r] = ((k[r] & kLocalMask) >> kBucketBits) & (nd - 1);
+      rk[r] = wave_rank(i < emtot, d[r], a.nx_bits, whist + wv * kRadix, ltm);
+    }
+    __syncthreads();
+    if ((uint32_t)tid < nd) {  // per destination: prefix over waves
+      uint32_t run = 0;
+#pragma unroll
+      for (int q = 0; q < kBWaves; ++q) {
+        const uint32_t c2 = whist[q * kRadix + tid];
+        whist[q * kRadix + tid] = run;
+        run += c2;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r) {
+      const uint32_t i = wv * (kBIpt * kWave) + r * kWave + lane;
+      if (i < emtot) {
+        const uint32_t o = dbase[d[r]] + whist[wv * kRadix + d[r]] + rk[r];
+        g.eg[w].key[o] = k[r];
+        g.eg[w].src[o] = usrc[i];
+        g.eg[w].pay[o] = upay[i];
+      }
+    }
+  } else {  // tells in sender order in the em scratch arena: tile-wise stable multisplit
+    uint32_t* U32 = reinterpret_cast<uint32_t*>(L.U);
+    const SplitLds S{whist, base, ldig, gadj, L.scratch, U32, U32 + kTile, U32 + 2 * kTile};
+    const CMsgs in{src.key, src.src, src.pay};
+    for (uint32_t sub = 0; sub < emtot; sub += kTile)
+      split_tile<kBThreads>(in, (uint32_t)embase + sub, min((uint32_t)kTile, emtot - sub), g.eg[w], kBucketBits,
+                            a.nx_bits, S);
+  }
+  if (tid == 0) g.emc[w][b] = emtot;
+}
+
+template <bool kLds, bool kWide, uint32_t KM, bool kGather>
 __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t lo,
-                                              uint32_t cnt, uint32_t a0, uint32_t na) {
+                                              uint32_t cnt, uint32_t a0, uint32_t na, uint32_t w) {
   const DevParams& P = a.P;
   const int tid = threadIdx.x;
   const uint32_t T = P.T, C = P.C;
@@ -628,9 +742,15 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   }
   uint32_t bltot;
   uint32_t blex = block_excl_sum<kBThreads>(nbl_t, L.scratch, &bltot);
+  const Msgs blw = kGather ? a.g.bl[w] : a.bl;  // backlog arena written by this superstep
   if (tid == 0) {
-    a.chunk_off[b] = lo;
-    a.chunk_cnt[b] = bltot;
+    if constexpr (kGather) {
+      a.g.blo[w][b] = lo;
+      a.g.blc[w][b] = bltot;
+    } else {
+      a.chunk_off[b] = lo;
+      a.chunk_cnt[b] = bltot;
+    }
   }
   if (bltot) {
 #pragma unroll
@@ -666,12 +786,12 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       }
       if (queued) {
         const uint32_t o = lo + blpre[la] + (p - T);
-        a.bl.key[o] = key;
-        a.bl.src[o] = sv;
-        a.bl.pay[o] = pv;
+        blw.key[o] = key;
+        blw.src[o] = sv;
+        blw.pay[o] = pv;
       }
     }
-    if (tid == 0) {  // all queued mail is in this bucket: one bin of the next first-pass histogram
+    if (!kGather && tid == 0) {  // all queued mail is in this bucket: one bin of the next first-pass histogram
       const uint32_t d = ((b << kBucketBits) >> a.nx_shift) & nhmask;
       atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + b / a.G], bltot);
     }
@@ -726,7 +846,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         ++ndel;
         if (r == AGX_RES_UNHANDLED) ++nunh;
         if (r == AGX_RES_STOPPED) {
-          P.stopq[atomicAdd(P.nstop, 1u)] = l;
+          if constexpr (kGather) P.alive[l] = 0;  // fused: only this block reads this bucket's flags
+          else P.stopq[atomicAdd(P.nstop, 1u)] = l;
           ndead += nd - q - 1;  // drained-but-unprocessed after the stop
           break;
         }
@@ -757,15 +878,33 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     }
     __syncthreads();
     AGX_STAMP(a, 6);
-    // compact the staged tells into the bucket's tell chunk (lane-consecutive actors: coalesced)
+    if constexpr (kGather) {
+      // compact the staged tells in sender order into U (free: state was written back), then
+      // group them by destination straight into this superstep's tell arena
+      uint32_t* ukey = reinterpret_cast<uint32_t*>(L.U);
 #pragma unroll 1
-    for (int j = 0; j < kBAct; ++j) {
-      const uint32_t la = j * kBThreads + tid;
-      const uint32_t s0 = L.seg[la], o = L.ecnt[la];
-      for (uint32_t e = 0; e < ecl[j]; ++e) {
-        a.em.key[embase + o + e] = L.key[s0 + e];
-        a.em.src[embase + o + e] = L.src[s0 + e];
-        a.em.pay[embase + o + e] = L.pay[s0 + e];
+      for (int j = 0; j < kBAct; ++j) {
+        const uint32_t la = j * kBThreads + tid;
+        const uint32_t s0 = L.seg[la], o = L.ecnt[la];
+        for (uint32_t e = 0; e < ecl[j]; ++e) {
+          ukey[o + e] = L.key[s0 + e];
+          ukey[kBucket + o + e] = L.src[s0 + e];
+          ukey[2 * kBucket + o + e] = L.pay[s0 + e];
+        }
+      }
+      __syncthreads();
+      group_tells<true>(a, L, b, w, embase, emtot, a.em);
+    } else {
+      // compact the staged tells into the bucket's tell chunk (lane-consecutive actors: coalesced)
+#pragma unroll 1
+      for (int j = 0; j < kBAct; ++j) {
+        const uint32_t la = j * kBThreads + tid;
+        const uint32_t s0 = L.seg[la], o = L.ecnt[la];
+        for (uint32_t e = 0; e < ecl[j]; ++e) {
+          a.em.key[embase + o + e] = L.key[s0 + e];
+          a.em.src[embase + o + e] = L.src[s0 + e];
+          a.em.pay[embase + o + e] = L.pay[s0 + e];
+        }
       }
     }
   } else {
@@ -857,7 +996,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           const uint32_t r = apply_msg<KM>(P, kd, self, l, wv, sv, ipay(s0 + q), em);
           if (r == AGX_RES_UNHANDLED) ++nunh;
           if (r == AGX_RES_STOPPED) {
-            P.stopq[atomicAdd(P.nstop, 1u)] = l;
+            if constexpr (kGather) P.alive[l] = 0;  // fused: only this block reads this bucket's flags
+            else P.stopq[atomicAdd(P.nstop, 1u)] = l;
             ndead += nd - q - 1;  // drained-but-unprocessed after the stop
             break;
           }
@@ -868,16 +1008,21 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       nall += em.n_all;
       ndead += em.n_all - em.n_valid;
     }
+    if constexpr (kGather) {
+      __syncthreads();  // phase B's tells are in the em scratch arena (sender order)
+      group_tells<false>(a, L, b, w, embase, emtot, a.em);
+    }
   }
-  if (tid == 0) {
+  if (!kGather && tid == 0) {
     a.chunk_off[a.nb + b] = (uint32_t)embase;
     a.chunk_cnt[a.nb + b] = emtot;
   }
   __syncthreads();
   AGX_STAMP(a, 7);
   // next first-pass histogram column of this bucket's tell chunk (zeroed by the chunk downsweep)
-  for (uint32_t d = tid; d < (1u << a.nx_bits); d += kBThreads)
-    if (L.nh[d]) atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + a.ng + b / a.G], L.nh[d]);
+  if (!kGather)
+    for (uint32_t d = tid; d < (1u << a.nx_bits); d += kBThreads)
+      if (L.nh[d]) atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + a.ng + b / a.G], L.nh[d]);
   // block stats -> global
   const uint32_t lane = lane_id();
   uint32_t v0 = wave_incl_sum(ndel), v1 = wave_incl_sum(ndead), v2 = wave_incl_sum(nunh), v3 = wave_incl_sum(nall),
@@ -890,16 +1035,54 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     atomicAdd(&L.stat[4], (unsigned long long)v4);
   }
   __syncthreads();
-  if (tid < kBStats) a.bstats[(size_t)blockIdx.x * kBStats + tid] += L.stat[tid];  // this block's own slot
+  if (tid < kBStats && L.stat[tid])  // this block's own slot (no contention; no load round trip)
+    atomicAdd(&a.bstats[(size_t)blockIdx.x * kBStats + tid], L.stat[tid]);
   __syncthreads();
   AGX_STAMP(a, 8);
 }
 
-template <bool kWide, uint32_t KM>
+// Inbox of one bucket in fused mode: [backlog][tell segments, sender-bucket order][staged].
+struct GatherView {
+  const uint32_t* segp;  // [nseg + 1] inbox position of each non-empty tell segment; [nseg] = staged start
+  const uint32_t* sego;  // [nseg] its offset in eg[r]
+  uint32_t nseg, blc, blo, sto;
+  // arena pointers are re-read from the kernel arguments at each use (scalar loads): holding
+  // them here would pin 18 VGPRs across the whole bucket
+  __device__ __forceinline__ void load(const GatherArgs& g, uint32_t r, uint32_t q, uint32_t& k, uint32_t& sv,
+                                       uint32_t& pv) const {
+    if (q < blc) {
+      const uint32_t i = blo + q;
+      k = g.bl[r].key[i];
+      sv = g.bl[r].src[i];
+      pv = g.bl[r].pay[i];
+      return;
+    }
+    uint32_t lo = 0, hi = nseg;  // last segment start <= q
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (segp[mid] <= q) lo = mid; else hi = mid - 1;
+    }
+    if (lo < nseg) {
+      const uint32_t i = sego[lo] + (q - segp[lo]);
+      k = g.eg[r].key[i];
+      sv = g.eg[r].src[i];
+      pv = g.eg[r].pay[i];
+    } else {
+      const uint32_t i = sto + (q - segp[nseg]);
+      k = g.stg.key[i];
+      sv = g.stg.src[i];
+      pv = g.stg.pay[i];
+    }
+  }
+};
+
+template <bool kWide, uint32_t KM, bool kGather>
 __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_key[kBucket];
-  __shared__ __attribute__((aligned(16))) uint32_t s_src[kBucket];
-  __shared__ __attribute__((aligned(16))) uint32_t s_pay[kBucket];
+  // key/src/pay carved from one array: group_tells reuses key+src as a 16 KB histogram
+  __shared__ __attribute__((aligned(16))) uint32_t s_ksp[3 * kBucket];
+  uint32_t* const s_key = s_ksp;
+  uint32_t* const s_src = s_ksp + kBucket;
+  uint32_t* const s_pay = s_ksp + 2 * kBucket;
   __shared__ __attribute__((aligned(16))) uint64_t U[2 * kBucket];  // 32 KB
   __shared__ __attribute__((aligned(16))) uint32_t s_seg[kBucket + 4];
   __shared__ __attribute__((aligned(16))) uint32_t s_ecnt[kBucket];
@@ -907,7 +1090,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   __shared__ uint8_t s_kind[kBucket];
   __shared__ uint32_t s_nh[kRadix];
   __shared__ uint32_t scratch[kBWaves + 1];
-  __shared__ uint32_t s_lo, s_hi;
+  __shared__ uint32_t s_lo, s_hi, s_g[6];
   __shared__ unsigned long long s_stat[5];
   const BucketLds L{s_key, s_src, s_pay, U, s_seg, s_ecnt, s_alive, s_kind, s_nh, scratch, s_stat};
   uint16_t* whist = reinterpret_cast<uint16_t*>(U);  // [kBWaves][kBucket]
@@ -916,9 +1099,11 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t lane = lane_id();
   const uint64_t ltm = lanemask_lt();
-  const uint32_t n = *a.d_n;
-  if (blockIdx.x == 0) {
-    if (tid == 0 && n > 0) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
+  const GatherArgs& g = a.g;
+  const uint32_t step0 = kGather ? *g.step : 0u;  // fused: write parity w, read parity w ^ 1 (the tick advances it)
+  const uint32_t wpar = step0 & 1u, rpar = wpar ^ 1u;
+  if (!kGather && blockIdx.x == 0) {
+    if (tid == 0 && *a.d_n > 0) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
     for (uint32_t i = tid; i < kStagedChunks; i += kBThreads) a.chunk_cnt[2 * a.nb + i] = 0;  // staged consumed
   }
 
@@ -928,9 +1113,57 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     const uint32_t na = min((uint32_t)kBucket, P.n_local - a0);
     if (tid < 5) s_stat[tid] = 0;
     for (uint32_t d = tid; d < kRadix; d += kBThreads) s_nh[d] = 0;
-    if (tid == 0) {
-      s_lo = a.bstart[b];
-      s_hi = a.bstart[b + 1];
+    if (!kGather) {
+      if (tid == 0) {
+        s_lo = a.bstart[b];
+        s_hi = a.bstart[b + 1];
+      }
+    } else {
+      // fused: this bucket's row of the tell tables (chunk c = sender bucket c), its backlog,
+      // its host-staged tells; rows are zeroed once read (the writers only set non-zero entries)
+      uint32_t* segp = reinterpret_cast<uint32_t*>(U);
+      uint32_t* sego = segp + kRadix + 2;
+      const uint32_t c = tid;
+      uint32_t v = 0, o = 0;
+      if (c < a.nb) {  // count and offset in one round trip (the offset is stale when the count is 0)
+        uint32_t* tc = g.tcnt[rpar] + (size_t)b * g.tstride + c;
+        v = *tc;
+        o = g.toff[rpar][(size_t)b * g.tstride + c];
+        if (v) *tc = 0u;
+      }
+      if (tid == 0) {
+        s_g[0] = g.blc[rpar][b];
+        s_g[1] = g.blo[rpar][b];
+        s_g[2] = g.stg_cnt[b];
+        s_g[3] = g.stg_off[b];
+        if (s_g[2]) g.stg_cnt[b] = 0u;
+      }
+      uint32_t tt, ns;
+      const uint32_t ex = block_excl_sum<kBThreads>(v, scratch, &tt);   // (syncs: s_g visible after)
+      const uint32_t ix = block_excl_sum<kBThreads>(v ? 1u : 0u, scratch, &ns);
+      const uint32_t blc = s_g[0];
+      if (v) {
+        segp[ix] = blc + ex;
+        sego[ix] = o;
+      }
+      if (tid == 0) {
+        segp[ns] = blc + tt;  // staged segment
+        s_g[4] = ns;
+        const uint32_t cnt = blc + tt + s_g[2];
+        // inbox slot: the bucket's own region (no shared counter), else the overflow region
+        uint64_t lo = (uint64_t)b * g.region;
+        if (cnt > g.region) lo = (uint64_t)a.nb * g.region + atomicAdd(g.ovf, cnt);
+        if (lo + cnt > g.cap) {  // arena overflow: report, drop this bucket's mail
+          atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
+          s_lo = 0;
+          s_hi = 0;
+          g.cntb[b] = 0;
+        } else {
+          s_lo = (uint32_t)lo;
+          s_hi = (uint32_t)lo + cnt;
+          g.cntb[b] = cnt;
+        }
+      }
     }
     {  // alive flags of the bucket, 4 per thread (a0 is a multiple of kBucket: 4-aligned)
       const uint32_t la0 = tid * 4;
@@ -943,6 +1176,15 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     __syncthreads();
     AGX_STAMP(a, 1);
     const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
+    GatherView gv{};
+    if (kGather) {
+      gv.segp = reinterpret_cast<const uint32_t*>(U);
+      gv.sego = gv.segp + kRadix + 2;
+      gv.nseg = s_g[4];
+      gv.blc = s_g[0];
+      gv.blo = s_g[1];
+      gv.sto = s_g[3];
+    }
 
     if (cnt <= (uint32_t)kBucket) {
       // ---- fast path: the whole bucket in one LDS tile
@@ -952,13 +1194,18 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       for (int r = 0; r < kBIpt; ++r) {
         const uint32_t q = wbase + r * kWave + lane;
         if (q < cnt) {
-          k[r] = a.in.key[lo + q];
-          sv[r] = a.in.src[lo + q];
-          pv[r] = a.in.pay[lo + q];
+          if (kGather) {
+            gv.load(g, rpar, q, k[r], sv[r], pv[r]);
+          } else {
+            k[r] = a.in.key[lo + q];
+            sv[r] = a.in.src[lo + q];
+            pv[r] = a.in.pay[lo + q];
+          }
         } else {
           k[r] = 0xFFFFFFFFu;
         }
       }
+      __syncthreads();  // (fused) the segment list in U is read before whist reuses U
       // in-order copy + sortedness check: local topologies (rings, stencils) arrive already in
       // actor order, and then the wave multisplit ranking is unnecessary (same result)
       for (uint32_t i = tid; i < kBucket + 4; i += kBThreads) s_seg[i] = 0;
@@ -1041,15 +1288,28 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         __syncthreads();
       }
       AGX_STAMP(a, 2);
-      bucket_finish<true, kWide, KM>(a, L, b, lo, cnt, a0, na);
+      bucket_finish<true, kWide, KM, kGather>(a, L, b, lo, cnt, a0, na, wpar);
     } else {
       // ---- general path (skewed bucket): counting sort into the global scratch copy
+      CMsgs in = a.in;
+      if (kGather) {  // materialise the gathered inbox at [lo, lo+cnt) of the inbox arena
+        for (uint32_t q = tid; q < cnt; q += kBThreads) {
+          uint32_t k0, s0, p0;
+          gv.load(g, rpar, q, k0, s0, p0);
+          g.inb.key[lo + q] = k0;
+          g.inb.src[lo + q] = s0;
+          g.inb.pay[lo + q] = p0;
+        }
+        __threadfence_block();
+        __syncthreads();
+        in = {g.inb.key, g.inb.src, g.inb.pay};
+      }
       uint32_t* s_run = s_key;  // LDS items are unused on this path
       uint32_t* s_tmp = s_src;
       for (uint32_t i = tid; i < kBucket + 4; i += kBThreads) s_seg[i] = 0;
       for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] = 0;
       __syncthreads();
-      for (uint32_t q = tid; q < cnt; q += kBThreads) atomicAdd(&s_seg[a.in.key[lo + q] & (kBucket - 1)], 1u);
+      for (uint32_t q = tid; q < cnt; q += kBThreads) atomicAdd(&s_seg[in.key[lo + q] & (kBucket - 1)], 1u);
       __syncthreads();
       {
         uint32_t v[kBAct], run = 0;
@@ -1076,9 +1336,9 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         for (int r = 0; r < kBIpt; ++r) {
           const uint32_t q = wbase + r * kWave + lane;
           if (q < cnt) {
-            k[r] = a.in.key[lo + q];
-            sv[r] = a.in.src[lo + q];
-            pv[r] = a.in.pay[lo + q];
+            k[r] = in.key[lo + q];
+            sv[r] = in.src[lo + q];
+            pv[r] = in.pay[lo + q];
           } else {
             k[r] = 0xFFFFFFFFu;
           }
@@ -1115,7 +1375,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] += s_tmp[la];
         __syncthreads();
       }
-      bucket_finish<false, kWide, KM>(a, L, b, lo, cnt, a0, na);
+      bucket_finish<false, kWide, KM, kGather>(a, L, b, lo, cnt, a0, na, wpar);
     }
   }
 }
@@ -1244,6 +1504,47 @@ __global__ void __launch_bounds__(kScanThreads) k_inflight(const uint32_t* chunk
   __syncthreads();
   unsigned long long v = 0;
   for (uint32_t i = threadIdx.x; i < nchunks; i += blockDim.x) v += chunk_cnt[i];
+  atomicAdd(&s, v);
+  __syncthreads();
+  if (threadIdx.x == 0) *out = s;
+}
+
+// Fused mode, after each superstep: publish the inbox total (quiescence poll, step count),
+// zero what the superstep consumed, advance the parity.  One block.
+__global__ void __launch_bounds__(kBThreads) k_fused_tick(uint32_t* step, const uint32_t* cntb, uint32_t nb,
+                                                          uint32_t* stg_cnt, uint32_t* ovf, uint32_t* heap_top,
+                                                          uint32_t* d_n, uint64_t* stats) {
+  __shared__ uint32_t scratch[kBWaves + 1];
+  uint32_t v = 0;
+  for (uint32_t i = threadIdx.x; i < nb; i += kBThreads) {
+    v += cntb[i];
+    stg_cnt[i] = 0;  // staged tells are consumed by the superstep that just ran
+  }
+  uint32_t t;
+  block_excl_sum<kBThreads>(v, scratch, &t);
+  if (threadIdx.x == 0) {
+    *d_n = t;
+    if (t) stats[ST_STEPS] += 1;
+    const uint32_t s1 = *step + 1u;
+    *step = s1;
+    *ovf = 0u;
+    if (heap_top) heap_top[s1 & 1u] = 0u;
+  }
+}
+
+// fused mode: messages in flight after the last superstep = its backlog + tells + staged
+__global__ void __launch_bounds__(kScanThreads) k_inflight_fused(const uint32_t* blc0, const uint32_t* blc1,
+                                                                 const uint32_t* emc0, const uint32_t* emc1,
+                                                                 const uint32_t* stg_cnt, const uint32_t* step,
+                                                                 uint32_t nb, unsigned long long* out) {
+  __shared__ unsigned long long s;
+  const bool p1 = ((*step + 1u) & 1u) != 0;  // parity written by the last superstep
+  const uint32_t* blc = p1 ? blc1 : blc0;
+  const uint32_t* emc = p1 ? emc1 : emc0;
+  if (threadIdx.x == 0) s = 0;
+  __syncthreads();
+  unsigned long long v = 0;
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) v += (unsigned long long)blc[i] + emc[i] + stg_cnt[i];
   atomicAdd(&s, v);
   __syncthreads();
   if (threadIdx.x == 0) *out = s;

@@ -278,3 +278,13 @@ def test_ring_2m_multipass_native(built):
     w = wl.token_ring(2_100_000, 6)
     sg, so, a, b = run_both(w)
     assert_same(sg, so, a, b, "ring 2.1M")
+
+
+@pytest.mark.parametrize("case", sorted(MULTIPASS_CASES))
+def test_unfused_single_pass(built, monkeypatch, case):
+    """AGX_NO_FUSED: the chunk-pass + apply pipeline at one radix pass (the fused
+    gather-apply superstep is the default there)."""
+    monkeypatch.setenv("AGX_NO_FUSED", "1")
+    w = MULTIPASS_CASES[case]()
+    sg, so, a, b = run_both(w)
+    assert_same(sg, so, a, b, f"unfused {case}")
