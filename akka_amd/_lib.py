@@ -81,6 +81,8 @@ SIGNATURES = {
     "agx_set_fanout": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, c_u32p, c_u32p,
                                         ctypes.c_uint64]),
     "agx_set_graph": (ctypes.c_int32, [ctypes.c_void_p, c_u64p, c_u32p]),
+    "agx_set_graph_rmat": (ctypes.c_int32, [ctypes.c_void_p, c_u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint64]),
     "agx_stage_tells": (ctypes.c_int32, [ctypes.c_void_p, c_u32p, c_u32p, c_u32p, ctypes.c_size_t]),
     "agx_run": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(AgxStats)]),
     "agx_get_stats": (ctypes.c_int32, [ctypes.c_void_p, ctypes.POINTER(AgxStats)]),

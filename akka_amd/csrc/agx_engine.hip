@@ -1179,6 +1179,39 @@ agx_status agx_set_graph(agx_engine* e, const uint64_t* row_ptr, const uint32_t*
   return AGX_OK;
 }
 
+agx_status agx_set_graph_rmat(agx_engine* e, const uint64_t* row_ptr, uint32_t bits, uint32_t ta, uint32_t tb,
+                              uint32_t tc, uint64_t seed) {
+  if (!e || !row_ptr || bits == 0 || bits > 40) return set_err(AGX_EINVAL, "bad rmat graph args");
+  AGX_TRY(ensure_dev(e));
+  std::vector<uint64_t> lrow(e->n_local + 1, 0), gstart(std::max<uint64_t>(e->n_local, 1), 0);
+  for (uint64_t l = 0; l < e->n_local; ++l) {
+    const uint64_t id = e->R > 1 ? e->h_gid[l] : l;
+    const uint64_t b = row_ptr[id], en = row_ptr[id + 1];
+    if (en < b) return set_err(AGX_EINVAL, "row_ptr not monotone at %llu", (unsigned long long)id);
+    gstart[l] = b;
+    lrow[l + 1] = lrow[l] + (en - b);
+  }
+  hipFree(e->d_row);
+  hipFree(e->d_col);
+  e->d_row = nullptr;
+  e->d_col = nullptr;
+  uint64_t* d_gs = nullptr;
+  AGX_TRY(dalloc(&e->d_row, lrow.size()));
+  AGX_TRY(dalloc(&e->d_col, lrow.back()));
+  AGX_TRY(dalloc(&d_gs, gstart.size()));
+  HIP_TRY(hipMemcpy(e->d_row, lrow.data(), lrow.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(d_gs, gstart.data(), gstart.size() * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_gen_rmat, dim3(grid_for(e->n_local / kThreads + 1, 8192)), dim3(kThreads), 0, e->stream,
+                     e->d_row, d_gs, e->d_col, (uint32_t)e->n_local, bits, ta, tb, tc, seed, (uint32_t)e->n_global);
+  hipError_t le = hipGetLastError();
+  hipError_t se = hipStreamSynchronize(e->stream);
+  hipFree(d_gs);
+  if (le != hipSuccess || se != hipSuccess) return set_err(AGX_EDEVICE, "rmat generation failed");
+  e->graph_set = true;
+  drop_graphs(e);
+  return AGX_OK;
+}
+
 agx_status agx_stage_tells(agx_engine* e, const uint32_t* dst, const uint32_t* src, const uint32_t* payload, size_t n) {
   if (!e || (n && (!dst || !payload))) return set_err(AGX_EINVAL, "bad tells");
   for (size_t i = 0; i < n; ++i) {

@@ -1509,6 +1509,27 @@ __global__ void __launch_bounds__(kScanThreads) k_inflight(const uint32_t* chunk
   if (threadIdx.x == 0) *out = s;
 }
 
+// Workload setup: R-MAT destinations of the local rows' out-edges (workloads.rmat_cols).
+__device__ __forceinline__ uint32_t rmat_dst(uint64_t e, uint32_t bits, uint32_t ta, uint32_t tb, uint32_t tc,
+                                             uint64_t seed, uint32_t n) {
+  uint64_t col = 0;
+  for (uint32_t bit = 0; bit < bits; ++bit) {
+    const uint32_t q = (uint32_t)(splitmix64(e * 64ull + bit + seed) & 0xFFFFull);
+    const uint64_t db = ((q >= ta && q < tb) || q >= tc) ? 1ull : 0ull;
+    col |= db << (bits - 1 - bit);
+  }
+  return (uint32_t)(col % n);
+}
+
+__global__ void __launch_bounds__(kThreads) k_gen_rmat(const uint64_t* lrow, const uint64_t* gstart, uint32_t* col,
+                                                       uint32_t n_local, uint32_t bits, uint32_t ta, uint32_t tb,
+                                                       uint32_t tc, uint64_t seed, uint32_t n_global) {
+  for (uint32_t l = blockIdx.x * kThreads + threadIdx.x; l < n_local; l += gridDim.x * kThreads) {
+    const uint64_t b = lrow[l], deg = lrow[l + 1] - b, g0 = gstart[l];
+    for (uint64_t j = 0; j < deg; ++j) col[b + j] = rmat_dst(g0 + j, bits, ta, tb, tc, seed, n_global);
+  }
+}
+
 // Fused mode, after each superstep: publish the inbox total (quiescence poll, step count),
 // zero what the superstep consumed, advance the parity.  One block.
 __global__ void __launch_bounds__(kBThreads) k_fused_tick(uint32_t* step, const uint32_t* cntb, uint32_t nb,

@@ -167,6 +167,11 @@ class GpuEngine:
         cl = _u32(col) if len(col) else np.zeros(1, np.uint32)
         check(self.lib.agx_set_graph(self._h, _ptr(rp, ctypes.c_uint64), _ptr(cl, ctypes.c_uint32)))
 
+    def set_graph_rmat(self, row_ptr, bits: int, ta: int, tb: int, tc: int, seed: int) -> None:
+        """CSR rows from the host, R-MAT destinations generated on the device."""
+        rp = np.ascontiguousarray(np.asarray(row_ptr, dtype=np.uint64))
+        check(self.lib.agx_set_graph_rmat(self._h, _ptr(rp, ctypes.c_uint64), bits, ta, tb, tc, seed))
+
     # -- tell / run
     def tell(self, dst, payload, src=None) -> None:
         dst = _u32(dst)

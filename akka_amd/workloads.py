@@ -55,7 +55,14 @@ class Workload:
         if self.fanout is not None:
             target.set_fanout(*self.fanout)
         if self.graph is not None:
-            target.set_graph(*self.graph)
+            if len(self.graph) == 3 and isinstance(self.graph[0], str):  # ("rmat", row_ptr, params)
+                _, row, prm = self.graph
+                if hasattr(target, "set_graph_rmat"):
+                    target.set_graph_rmat(row, *prm)
+                else:
+                    target.set_graph(row, rmat_cols(int(row[-1]), self.n_actors, *prm))
+            else:
+                target.set_graph(*self.graph)
         if stage_tells and self.tells is not None:
             dst, src, pay = self.tells
             target.tell(dst, pay, src)
@@ -177,45 +184,68 @@ def crdt_mixed(n: int = 4096, rounds: int = 4, seed: int = 3, throughput: int = 
 
 
 # ------------------------------------------------------------------ C5
-def power_law_graph(n: int, alpha: float = 2.1, dmax: int = 1024, a: float = 0.57, b: float = 0.19,
-                    c: float = 0.19, seed: int = SEED):
-    """Out-degrees ~ d^-alpha on [1, dmax]; endpoints by R-MAT bit sampling.
-    Integer RNG throughout (float only to build the host-side degree table)."""
+RMAT_ABC = (0.57, 0.19, 0.19)
+
+
+def power_law_degrees(n: int, alpha: float = 2.1, dmax: int = 1024, seed: int = SEED) -> np.ndarray:
+    """CSR row pointer (u64, n+1) of out-degrees ~ d^-alpha on [1, dmax], one integer
+    draw per actor against host-built u32-scaled thresholds."""
     d = np.arange(1, dmax + 1, dtype=np.float64)
     p = d ** (-alpha)
     cdf = np.cumsum(p) / p.sum()
     thr = np.floor(cdf * 4294967296.0).astype(np.uint64)
     thr[-1] = 1 << 32
-    r = splitmix64_np(np.arange(n, dtype=np.uint64) ^ np.uint64(seed * 7)) >> np.uint64(32)
-    deg = (np.searchsorted(thr, r, side="right") + 1).astype(np.uint64)
-    deg = np.minimum(deg, dmax)
     row = np.zeros(n + 1, np.uint64)
-    np.cumsum(deg, out=row[1:])
-    m = int(row[-1])
+    for lo in range(0, n, 1 << 24):  # chunked: bounded temporaries at 10^8 actors
+        hi = min(n, lo + (1 << 24))
+        r = splitmix64_np(np.arange(lo, hi, dtype=np.uint64) ^ np.uint64(seed * 7)) >> np.uint64(32)
+        deg = np.minimum(np.searchsorted(thr, r, side="right") + 1, dmax).astype(np.uint64)
+        row[lo + 1:hi + 1] = deg
+    np.cumsum(row, out=row)
+    return row
+
+
+def rmat_params(n: int, a: float = RMAT_ABC[0], b: float = RMAT_ABC[1], c: float = RMAT_ABC[2],
+                seed: int = SEED) -> tuple:
+    """(bits, ta, tb, tc, seed) of the R-MAT destination draw (agx_set_graph_rmat)."""
     bits = max(1, int(np.ceil(np.log2(max(n, 2)))))
-    ta = np.uint64(int(a * 65536))
-    tb = np.uint64(int((a + b) * 65536))
-    tc = np.uint64(int((a + b + c) * 65536))
+    return bits, int(a * 65536), int((a + b) * 65536), int((a + b + c) * 65536), seed
+
+
+def rmat_cols(m: int, n: int, bits: int, ta: int, tb: int, tc: int, seed: int) -> np.ndarray:
+    """Destination of every edge id in [0, m): `bits` quadrant draws q = splitmix64(e*64 + bit +
+    seed) & 0xFFFF, destination bit = (ta <= q < tb) | (q >= tc), reduced mod n."""
     col = np.zeros(m, np.uint64)
     eid = np.arange(m, dtype=np.uint64)
     for bit in range(bits):
         rr = splitmix64_np(eid * np.uint64(64) + np.uint64(bit) + np.uint64(seed)) & np.uint64(0xFFFF)
-        # quadrant: a -> (0,0)  b -> (0,1)  c -> (1,0)  d -> (1,1); destination bit = column bit
-        dst_bit = ((rr >= ta) & (rr < tb)) | (rr >= tc)
+        dst_bit = ((rr >= np.uint64(ta)) & (rr < np.uint64(tb))) | (rr >= np.uint64(tc))
         col |= dst_bit.astype(np.uint64) << np.uint64(bits - 1 - bit)
     col %= np.uint64(n)
-    return row, col.astype(np.uint32)
+    return col.astype(np.uint32)
+
+
+def power_law_graph(n: int, alpha: float = 2.1, dmax: int = 1024, a: float = RMAT_ABC[0], b: float = RMAT_ABC[1],
+                    c: float = RMAT_ABC[2], seed: int = SEED):
+    """Out-degrees ~ d^-alpha on [1, dmax]; endpoints by R-MAT bit sampling.
+    Integer RNG throughout (float only to build the host-side degree table)."""
+    row = power_law_degrees(n, alpha, dmax, seed)
+    return row, rmat_cols(int(row[-1]), n, *rmat_params(n, a, b, c, seed))
 
 
 def power_law_forward(n: int = 100_000_000, ttl: int = 16, capacity: int = 64, throughput: int = 5,
-                      msgs_per_actor_den: int = 1, seed: int = SEED) -> Workload:
-    """C5: FORWARD_RR over a power-law graph with BoundedMailbox(capacity)."""
-    row, col = power_law_graph(n, seed=seed)
+                      msgs_per_actor_den: int = 1, seed: int = SEED, device_graph: bool = False) -> Workload:
+    """C5: FORWARD_RR over a power-law graph with BoundedMailbox(capacity).
+    device_graph: the R-MAT destinations are generated by the engine (agx_set_graph_rmat);
+    targets without that entry point (the CPU oracle) get them from rmat_cols."""
+    row = power_law_degrees(n, seed=seed)
+    graph = ("rmat", row, rmat_params(n, seed=seed)) if device_graph else (row, rmat_cols(
+        int(row[-1]), n, *rmat_params(n, seed=seed)))
     dst = np.arange(0, n, msgs_per_actor_den, dtype=np.uint32)
     pay = np.full(dst.size, ttl, np.uint32)
     src = np.full(dst.size, NO_SENDER, np.uint32)
     return Workload("power_law_forward", n, 2, 1, throughput, capacity, [(0, n, Kind.FORWARD_RR, None)],
-                    graph=(row, col), tells=(dst, src, pay))
+                    graph=graph, tells=(dst, src, pay))
 
 
 # ------------------------------------------------------------------ C1

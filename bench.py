@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--large-steps", type=int, default=24)
     ap.add_argument("--large-warmup", type=int, default=4)
     ap.add_argument("--cpu-hops", type=int, default=96, help="hop budget of the bounded CPU sample")
+    ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (N=1 only)")
+    ap.add_argument("--quick-configs", action="store_true", help="C5 at 10M instead of 100M actors")
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_r01.json"),
                     help="PMC traffic summary written by profiles/collect_pmc.py")
     return ap.parse_args()
@@ -119,6 +121,78 @@ def timed_ring(n_total: int, hops: int, warmup: int, steps: int, world: int, ran
         eng.close()
         eng = None
     return eng, t1 - t0, s1.delivered - s0.delivered, s1.supersteps - s0.supersteps
+
+
+def timed_workload(w, warmup: int, steps: int, prof_steps: int = 8, msg_capacity: int = 0) -> dict:
+    """One BASELINE config on one GPU: install the workload, `warmup` untimed supersteps,
+    then exactly `steps` timed supersteps (inputs resident in HBM), then a short profiled
+    window (eager launches, HIP events per kernel)."""
+    import torch
+    from akka_amd.engine import EngineConfig, GpuEngine
+
+    t0 = time.perf_counter()
+    cfg = EngineConfig(**w.engine_kwargs())
+    cfg.msg_capacity = msg_capacity
+    eng = GpuEngine(cfg)
+    w.apply_to(eng)
+    setup = time.perf_counter() - t0
+    s0 = eng.run(warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s1 = eng.run(steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    eng.profile(True)
+    eng.profile_reset()
+    eng.run(prof_steps)
+    prof = eng.profile_read()
+    eng.close()
+    d = s1.delivered - s0.delivered
+    ss = s1.supersteps - s0.supersteps
+    bytes_alg = s1.bytes_alg - s0.bytes_alg
+    return {"value": d / el, "unit": "msg/s", "delivered": d, "dead_letters": s1.dead_letters - s0.dead_letters,
+            "supersteps_timed": ss, "ms_per_step": el / max(ss, 1) * 1e3, "setup_s": round(setup, 2),
+            "alg_bytes_per_msg": bytes_alg / max(d, 1),
+            "superstep_frac": bytes_alg / el / 1e9 / PEAK_HBM_GBS,
+            "kernel_ms_per_step": {k: round(v["total_ms"] / max(v["launches"], 1), 4) for k, v in prof.items()
+                                   if v["launches"]}}
+
+
+def other_configs(quick: bool) -> dict:
+    """BASELINE.json configs other than the headline ring, each measured on one GPU."""
+    from akka_amd import workloads as wl
+    from akka_amd.engine import Kind
+
+    n5 = 10_000_000 if quick else 100_000_000
+    specs = {
+        "C5_power_law_bounded": (
+            f"{n5 // 1_000_000}M actors, power-law out-degree (alpha 2.1, d<=1024) R-MAT graph, FORWARD_RR "
+            "round-robin forwarding, BoundedMailbox(64) tail-drop, throughput 5, 1 message/actor",
+            lambda: wl.power_law_forward(n5, ttl=15, capacity=64, throughput=5, device_graph=True), 2, 10, 0),
+        "C3_zipf_fanout": (
+            "10M actors, Zipf(1.1) destinations over a seeded permutation, FANOUT counter/sum behaviour, k=1 steady "
+            "state (every actor holds one message, ttl 15), BoundedMailbox(1000), throughput 5",
+            lambda: wl.zipf_fanout(10_000_000, k=1, ttl=15, root_every=1, capacity=1000), 2, 10, 0),
+        "C4_gcounter_gossip": (
+            "1M Replicator-style GCounter replicas (8 node slots), full-state gossip to 2 random peers per tick, "
+            "merge = slot-wise max (akka-distributed-data GCounter.merge)",
+            lambda: wl.crdt_gossip(1_000_000, Kind.GCOUNTER, rounds=40), 4, 24, 0),
+        "C4_orset_gossip": (
+            "1M Replicator-style ORSet replicas (64-element universe, 8 nodes, dots + version vector), full-state "
+            "gossip to 2 random peers per tick, ORSet.merge",
+            lambda: wl.crdt_gossip(1_000_000, Kind.ORSET, rounds=20), 2, 12, 0),
+        "C1_ping_pong": (
+            "akka-bench-jmh ForkJoinActorBenchmark.pingPong shape: 1000 PingPong pairs, 100 in flight per pair, "
+            "throughput 50",
+            lambda: wl.ping_pong(1000, messages_per_pair=2_000_000, throughput=50), 16, 400, 1 << 20),
+    }
+    out = {}
+    for name, (desc, make, warm, steps, mcap) in specs.items():
+        try:  # one config failing must not hide the others
+            out[name] = dict(workload=desc, **timed_workload(make(), warm, steps, msg_capacity=mcap))
+        except Exception as ex:
+            out[name] = {"workload": desc, "error": repr(ex)}
+    return out
 
 
 def reduce_ranks(elapsed: float, delivered: int, world: int):
@@ -231,6 +305,11 @@ def main():
         "at_100M_actors": large,
         "kernel_ms": {k: {"total_ms": round(v["total_ms"], 4), "launches": v["launches"]} for k, v in prof.items()},
     }
+    if world == 1 and not args.no_configs:
+        try:
+            out["configs"] = other_configs(args.quick_configs)
+        except Exception as ex:  # an auxiliary config must never hide the headline number
+            out["configs"] = {"error": repr(ex)}
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             try:

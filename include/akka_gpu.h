@@ -173,6 +173,12 @@ agx_status agx_set_fanout(agx_engine* eng, uint32_t k, uint64_t seed, const uint
 agx_status agx_set_gossip(agx_engine* eng, uint32_t fanout, uint64_t seed);
 /* Out-edge lists in CSR over GLOBAL ids: row_ptr[n_actors+1], col[row_ptr[n]].  */
 agx_status agx_set_graph(agx_engine* eng, const uint64_t* row_ptr, const uint32_t* col);
+/* The same CSR with the destinations generated on the device (workload setup for
+ * 10^8-actor graphs; not part of the dispatcher boundary): edge e gets the R-MAT
+ * destination of `bits` quadrant draws q = splitmix64(e*64 + bit + seed) & 0xFFFF,
+ * destination bit = (ta <= q < tb) | (q >= tc), reduced mod n_actors.          */
+agx_status agx_set_graph_rmat(agx_engine* eng, const uint64_t* row_ptr, uint32_t bits, uint32_t ta,
+                              uint32_t tb, uint32_t tc, uint64_t seed);
 
 /* --- tell / run ------------------------------------------------------------- */
 /* Host tells (caller-owned buffers, copied).  src may be AGX_NO_SENDER.

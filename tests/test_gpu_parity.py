@@ -288,3 +288,12 @@ def test_unfused_single_pass(built, monkeypatch, case):
     w = MULTIPASS_CASES[case]()
     sg, so, a, b = run_both(w)
     assert_same(sg, so, a, b, f"unfused {case}")
+
+
+def test_power_law_device_graph(built):
+    """agx_set_graph_rmat: device-generated R-MAT destinations equal the host generator's
+    (the oracle gets the host ones), so the whole run is bit-exact."""
+    w = wl.power_law_forward(40_000, ttl=6, capacity=8, throughput=5, device_graph=True)
+    sg, so, a, b = run_both(w)
+    assert_same(sg, so, a, b, "power_law device graph")
+    assert sg.dead_letters > 0

@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-pmc}
-ARGS="--steps 40 --warmup 4 --no-cpu-baseline ${BENCH_ARGS}"
+ARGS="--steps 40 --warmup 4 --no-cpu-baseline --no-configs ${BENCH_ARGS}"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" ${EXTRA_GROUPS}; do
   i=$((i+1))

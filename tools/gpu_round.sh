@@ -6,7 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r01}
-B1M="--no-cpu-baseline --large-actors 0"
+B1M="--no-cpu-baseline --large-actors 0 --no-configs"
 fail() { echo "$1 failed"; tail -30 "$2"; exit 1; }
 
 if [ -z "$SKIP_TESTS" ]; then
