@@ -149,8 +149,10 @@ struct agx_engine {
   uint32_t *d_tcnt[2] = {nullptr, nullptr}, *d_toff[2] = {nullptr, nullptr};
   uint32_t *d_blo[2] = {nullptr, nullptr}, *d_blc[2] = {nullptr, nullptr}, *d_emc[2] = {nullptr, nullptr};
   uint32_t *d_stg_off = nullptr, *d_stg_cnt = nullptr, *d_ovf = nullptr, *d_cntb = nullptr;
+  uint32_t *d_skew_list = nullptr, *d_skew_n = nullptr;  // buckets for the general-path launch
   uint32_t tstride = 4, region = 0;
   uint64_t acap = 0;  // arena capacity (fused: regions + overflow area)
+  uint32_t apply_grid = kMaxApplyGrid;  // AGX_APPLY_GRID test knob: fewer blocks, each looping over buckets
   std::vector<uint32_t> hd_key, hd_src, hd_pay;  // staged tells on the device, not yet consumed (fused)
   bool stg_pending = false;
 
@@ -349,6 +351,7 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     ca.nstop = e->d_nstop;
     ca.step = e->pw ? e->d_step : nullptr;
     ca.heap_top = e->d_heap_top;
+    ca.skew_n = e->d_skew_n;
     ca.cap = e->cap;
     ca.stride = e->cstride;
     ca.nunits = e->nunits;
@@ -404,6 +407,8 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.kmax = e->kmax;
   ba.stats = e->d_stats;
   ba.bstats = e->d_bstats;
+  ba.skew_list = e->d_skew_list;
+  ba.skew_n = e->d_skew_n;
   if (e->fused) {
     GatherArgs& g = ba.g;
     g.bl[0] = e->bl.m();
@@ -431,12 +436,18 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.dbg = e->d_dbg;
   {
     Scope s(e, K_APPLY);
-    const dim3 g(grid_for(e->nb, kMaxApplyGrid)), blk(kBThreads);
+    const dim3 g(grid_for(e->nb, e->apply_grid)), blk(kBThreads);
     const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
-#define AGX_APPLY(W, M)                                                                  \
-  do {                                                                                   \
-    if (e->fused) hipLaunchKernelGGL((k_bucket_apply<W, M, true>), g, blk, 0, e->stream, ba);  \
-    else hipLaunchKernelGGL((k_bucket_apply<W, M, false>), g, blk, 0, e->stream, ba);         \
+    const dim3 gs(grid_for(e->nb, e->apply_grid));  // skew list: as many blocks as there may be buckets
+#define AGX_APPLY(W, M)                                                                          \
+  do {                                                                                           \
+    if (e->fused) {                                                                              \
+      hipLaunchKernelGGL((k_bucket_apply<W, M, true, false>), g, blk, 0, e->stream, ba);         \
+      hipLaunchKernelGGL((k_bucket_apply<W, M, true, true>), gs, blk, 0, e->stream, ba);         \
+    } else {                                                                                     \
+      hipLaunchKernelGGL((k_bucket_apply<W, M, false, false>), g, blk, 0, e->stream, ba);        \
+      hipLaunchKernelGGL((k_bucket_apply<W, M, false, true>), gs, blk, 0, e->stream, ba);        \
+    }                                                                                            \
   } while (0)
     if (e->pw)  // CRDT kinds registered: the variant with state gossips
       AGX_APPLY(true, KM_ALL);
@@ -454,7 +465,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   }
   if (e->fused)
     hipLaunchKernelGGL(k_fused_tick, dim3(1), dim3(kBThreads), 0, e->stream, e->d_step, e->d_cntb, e->nb, e->d_stg_cnt,
-                       e->d_ovf, e->pw ? e->d_heap_top : nullptr, e->d_n, e->d_stats);
+                       e->d_ovf, e->pw ? e->d_heap_top : nullptr, e->d_n, e->d_stats, e->d_skew_n);
   HIP_TRY(hipGetLastError());
   return AGX_OK;
 }
@@ -554,6 +565,7 @@ agx_status phase1(agx_engine* e) {
   m.stats = e->d_stats;
   m.step = e->pw ? e->d_step : nullptr;
   m.heap_top = e->d_heap_top;
+  m.skew_n = e->d_skew_n;
   m.cap0 = e->cap;
   m.cap1 = e->cap_emit;
   {
@@ -955,6 +967,8 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   // arenas; an inbox larger than the region (skew) takes a slot of the overflow area that
   // follows, sized like the whole message capacity — no shared counter on the common path
   e->region = kBucket;
+  if (const char* s = getenv("AGX_APPLY_GRID"))
+    e->apply_grid = (uint32_t)std::min<int>(kMaxApplyGrid, std::max(1, atoi(s)));
   e->acap = e->fused ? (uint64_t)e->nb * e->region + e->cap : e->cap;
   if (e->acap * e->kmax >= (1ull << 32)) { delete e; return set_err(AGX_EINVAL, "msg_capacity * max_emit too large"); }
 
@@ -1016,6 +1030,9 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(hipMemset(e->d_ovf, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(hipMemset(e->d_cntb, 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   }
+  CREATE_TRY(dalloc(&e->d_skew_list, e->nb));
+  CREATE_TRY(dalloc(&e->d_skew_n, 1));
+  CREATE_TRY(hipMemset(e->d_skew_n, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_chunk_off, e->nchunks));
   CREATE_TRY(dalloc(&e->d_chunk_cnt, e->nchunks));
   CREATE_TRY(hipMemset(e->d_chunk_off, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
@@ -1068,6 +1085,7 @@ agx_status agx_destroy(agx_engine* e) {
     hipFree(e->d_tcnt[q]); hipFree(e->d_toff[q]); hipFree(e->d_blo[q]); hipFree(e->d_blc[q]); hipFree(e->d_emc[q]);
   }
   hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_cntb);
+  hipFree(e->d_skew_list); hipFree(e->d_skew_n);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_sred); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);
@@ -1265,6 +1283,14 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
     const char* nm[8] = {"range+alive", "sort", "->finish", "classify+backlog", "prefetch+phaseA", "scan", "phaseB", "hist+stats"};
     for (int k = 0; k < 8; ++k) fprintf(stderr, " %s=%.0f", nm[k], acc[k] / nbk);
     fprintf(stderr, " | kernel span=%llu cycles\n", t8max - t0min);
+    std::vector<std::pair<unsigned long long, uint64_t>> slow;
+    for (uint64_t b = 0; b < nbk; ++b) slow.push_back({h[b * 16 + 10], b});
+    std::sort(slow.rbegin(), slow.rend());
+    fprintf(stderr, "[agx stamps] slowest buckets (cycles bucket inbox):");
+    for (size_t i = 0; i < std::min<size_t>(6, slow.size()); ++i)
+      fprintf(stderr, " %llu:%llu:%llu", slow[i].first, h[slow[i].second * 16 + 11], h[slow[i].second * 16 + 12]);
+    fprintf(stderr, "\n");
+    HIP_TRY(hipMemset(e->d_dbg, 0, h.size() * 8));
   }
   AGX_TRY(check_error(e));
   return agx_get_stats(e, out);

@@ -103,6 +103,7 @@ struct Chunks {
 template <typename HT>
 __device__ __forceinline__ uint32_t wave_rank(bool valid, uint32_t d, uint32_t bits, HT* hist, uint64_t lt_mask) {
   const uint64_t vm = __ballot(valid);
+  if (vm == 0) return 0;  // uniform: no valid lane in this wave
   // lowest valid lane's digit; when every valid lane has it (local topologies), the match
   // mask is the valid mask and the per-bit ballots are skipped
   const uint32_t first = __builtin_amdgcn_readlane(d, vm ? (int)__builtin_ctzll(vm) : 0);
@@ -315,6 +316,7 @@ struct ChunkSortArgs {
   uint32_t* nstop;
   uint32_t* step;      // CRDT heap parity (null when no CRDT kind is registered)
   uint32_t* heap_top;
+  uint32_t* skew_n;    // skew list of the coming apply: reset here
   uint64_t cap;
   uint32_t stride, nunits, ng, G, shift, bits;
 };
@@ -326,6 +328,7 @@ __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs a) {
   if (blockIdx.x == 0) {
     begin_step(a.step, a.heap_top);
     commit_stops(a.alive, a.stopq, a.nstop);
+    if (threadIdx.x == 0) *a.skew_n = 0u;
   }
   const uint32_t d = blockIdx.x;
   if (d >= (1u << a.bits)) return;
@@ -540,6 +543,7 @@ constexpr int kBIpt = kBucket / kBThreads;      // items per thread per sub-tile
 constexpr int kBAct = kBucket / kBThreads;      // actors per thread (4)
 static_assert(kBAct == 4 && kBIpt == 4, "bucket_apply assumes 4 actors and 4 inbox items per thread");
 constexpr int kStagedChunks = 256;              // host-staged tells are split over this many chunks
+constexpr int kPF = 4;                          // apply prefetch window (messages in global scratch)
 
 // Tell staging in LDS (single-pass path): tells overwrite consumed inbox slots of the same actor.
 struct EmitterLds {
@@ -603,6 +607,8 @@ struct BucketArgs {
   uint32_t nhist_stride, nx_shift, nx_bits;
   uint32_t G, ng;          // histogram units: G buckets per column, ng units per arena
   uint32_t nb, kmax;
+  uint32_t* skew_list;     // buckets whose inbox exceeds one LDS tile (appended by the fast launch)
+  uint32_t* skew_n;        // their count (reset by the first kernel of the next superstep)
   uint64_t* stats;
   unsigned long long* bstats;  // [gridDim][kBStats] per-block counters (summed by k_stats_reduce)
   unsigned long long* dbg;  // diagnostic build only (AGX_STAMPS): per-block phase timestamps
@@ -693,6 +699,13 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
         g.eg[w].pay[o] = upay[i];
       }
     }
+  } else if (__syncthreads_or((uint32_t)tid < nd && emtot > 0 && L.nh[tid] == emtot)) {
+    // every tell goes to one destination bucket: the sender order is already grouped
+    for (uint32_t i = tid; i < emtot; i += kBThreads) {
+      g.eg[w].key[embase + i] = src.key[embase + i];
+      g.eg[w].src[embase + i] = src.src[embase + i];
+      g.eg[w].pay[embase + i] = src.pay[embase + i];
+    }
   } else {  // tells in sender order in the em scratch arena: tile-wise stable multisplit
     uint32_t* U32 = reinterpret_cast<uint32_t*>(L.U);
     const SplitLds S{whist, base, ldig, gadj, L.scratch, U32, U32 + kTile, U32 + 2 * kTile};
@@ -706,7 +719,7 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
 
 template <bool kLds, bool kWide, uint32_t KM, bool kGather>
 __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t lo,
-                                              uint32_t cnt, uint32_t a0, uint32_t na, uint32_t w) {
+                                              uint32_t cnt, uint32_t a0, uint32_t na, uint32_t w, uint32_t ndead0) {
   const DevParams& P = a.P;
   const int tid = threadIdx.x;
   const uint32_t T = P.T, C = P.C;
@@ -722,7 +735,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
 
   AGX_STAMP(a, 3);
   // ---- classification per actor (blocked): drained / queued (backlog) / dead letters
-  uint32_t nbl_t = 0, ndead = 0, blc[kBAct];
+  uint32_t nbl_t = 0, ndead = ndead0, blc[kBAct];  // ndead0: this thread's actors' arrivals dropped before the sort
 #pragma unroll
   for (int j = 0; j < kBAct; ++j) {
     const uint32_t la = tid * kBAct + j;
@@ -923,6 +936,23 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       const uint32_t kd = L.kind[la];
       if (kWide && is_crdt(kd)) {
         for (uint32_t q = 0; q < nd; ++q) em.count(crdt_count(P, isrc(s0 + q), ipay(s0 + q), &nrows_t));
+      } else if constexpr (!kLds) {  // messages in global scratch: loads issued kPF at a time
+        bool stop = false;
+        for (uint32_t q0 = 0; q0 < nd && !stop; q0 += kPF) {
+          uint32_t svb[kPF], pvb[kPF];
+#pragma unroll
+          for (int u = 0; u < kPF; ++u)
+            if (q0 + u < nd) {
+              svb[u] = isrc(s0 + q0 + u);
+              pvb[u] = ipay(s0 + q0 + u);
+            }
+#pragma unroll
+          for (int u = 0; u < kPF; ++u) {
+            if (stop || q0 + u >= nd) continue;
+            if (kWide && is_wide(svb[u])) continue;  // not in this behaviour's protocol: unhandled, no tells
+            if (apply_msg<KM>(P, kd, self, l, wv, svb[u], pvb[u], em) == AGX_RES_STOPPED) stop = true;
+          }
+        }
       } else {
         for (uint32_t q = 0; q < nd; ++q) {
           const uint32_t sv = isrc(s0 + q);
@@ -986,20 +1016,32 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           if (r == AGX_RES_UNHANDLED) ++nunh;
         }
       } else {
-        for (uint32_t q = 0; q < nd; ++q) {
-          const uint32_t sv = isrc(s0 + q);
-          ++ndel;
-          if (kWide && is_wide(sv)) {
-            ++nunh;
-            continue;
-          }
-          const uint32_t r = apply_msg<KM>(P, kd, self, l, wv, sv, ipay(s0 + q), em);
-          if (r == AGX_RES_UNHANDLED) ++nunh;
-          if (r == AGX_RES_STOPPED) {
-            if constexpr (kGather) P.alive[l] = 0;  // fused: only this block reads this bucket's flags
-            else P.stopq[atomicAdd(P.nstop, 1u)] = l;
-            ndead += nd - q - 1;  // drained-but-unprocessed after the stop
-            break;
+        bool stop = false;
+        constexpr uint32_t kW = kLds ? 1u : (uint32_t)kPF;  // global scratch: loads issued kPF at a time
+        for (uint32_t q0 = 0; q0 < nd && !stop; q0 += kW) {
+          uint32_t svb[kW], pvb[kW];
+#pragma unroll
+          for (uint32_t u = 0; u < kW; ++u)
+            if (q0 + u < nd) {
+              svb[u] = isrc(s0 + q0 + u);
+              pvb[u] = ipay(s0 + q0 + u);
+            }
+#pragma unroll
+          for (uint32_t u = 0; u < kW; ++u) {
+            if (stop || q0 + u >= nd) continue;
+            ++ndel;
+            if (kWide && is_wide(svb[u])) {
+              ++nunh;
+              continue;
+            }
+            const uint32_t r = apply_msg<KM>(P, kd, self, l, wv, svb[u], pvb[u], em);
+            if (r == AGX_RES_UNHANDLED) ++nunh;
+            if (r == AGX_RES_STOPPED) {
+              if constexpr (kGather) P.alive[l] = 0;  // fused: only this block reads this bucket's flags
+              else P.stopq[atomicAdd(P.nstop, 1u)] = l;
+              ndead += nd - (q0 + u) - 1;  // drained-but-unprocessed after the stop
+              stop = true;
+            }
           }
         }
         P.state[l] = wv[0];
@@ -1039,6 +1081,14 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     atomicAdd(&a.bstats[(size_t)blockIdx.x * kBStats + tid], L.stat[tid]);
   __syncthreads();
   AGX_STAMP(a, 8);
+  if (a.dbg && tid == 0) {  // diagnostic: slowest bucket of this block (cycles, bucket, inbox size)
+    const unsigned long long dur = a.dbg[blockIdx.x * 16 + 8] - a.dbg[blockIdx.x * 16 + 0];
+    if (dur > a.dbg[blockIdx.x * 16 + 10]) {
+      a.dbg[blockIdx.x * 16 + 10] = dur;
+      a.dbg[blockIdx.x * 16 + 11] = b;
+      a.dbg[blockIdx.x * 16 + 12] = cnt;
+    }
+  }
 }
 
 // Inbox of one bucket in fused mode: [backlog][tell segments, sender-bucket order][staged].
@@ -1048,6 +1098,15 @@ struct GatherView {
   uint32_t nseg, blc, blo, sto;
   // arena pointers are re-read from the kernel arguments at each use (scalar loads): holding
   // them here would pin 18 VGPRs across the whole bucket
+  __device__ __forceinline__ uint32_t key(const GatherArgs& g, uint32_t r, uint32_t q) const {
+    if (q < blc) return g.bl[r].key[blo + q];
+    uint32_t lo = 0, hi = nseg;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (segp[mid] <= q) lo = mid; else hi = mid - 1;
+    }
+    return lo < nseg ? g.eg[r].key[sego[lo] + (q - segp[lo])] : g.stg.key[sto + (q - segp[nseg])];
+  }
   __device__ __forceinline__ void load(const GatherArgs& g, uint32_t r, uint32_t q, uint32_t& k, uint32_t& sv,
                                        uint32_t& pv) const {
     if (q < blc) {
@@ -1076,7 +1135,11 @@ struct GatherView {
   }
 };
 
-template <bool kWide, uint32_t KM, bool kGather>
+// kSkew = false: every bucket whose inbox fits one LDS tile (<= kBucket messages); larger
+// inboxes are appended to the skew list.  kSkew = true (launched right after): the listed
+// buckets, general path — separate instantiation, so its register pressure never reaches
+// the fast path.
+template <bool kWide, uint32_t KM, bool kGather, bool kSkew>
 __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   // key/src/pay carved from one array: group_tells reuses key+src as a 16 KB histogram
   __shared__ __attribute__((aligned(16))) uint32_t s_ksp[3 * kBucket];
@@ -1102,26 +1165,31 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   const GatherArgs& g = a.g;
   const uint32_t step0 = kGather ? *g.step : 0u;  // fused: write parity w, read parity w ^ 1 (the tick advances it)
   const uint32_t wpar = step0 & 1u, rpar = wpar ^ 1u;
-  if (!kGather && blockIdx.x == 0) {
+  if (!kGather && !kSkew && blockIdx.x == 0) {
     if (tid == 0 && *a.d_n > 0) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
     for (uint32_t i = tid; i < kStagedChunks; i += kBThreads) a.chunk_cnt[2 * a.nb + i] = 0;  // staged consumed
   }
 
-  for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x) {
+  const uint32_t nwork = kSkew ? *a.skew_n : a.nb;
+  for (uint32_t it = blockIdx.x; it < nwork; it += gridDim.x) {
+    const uint32_t b = kSkew ? a.skew_list[it] : it;
     AGX_STAMP(a, 0);
     const uint32_t a0 = b << kBucketBits;
     const uint32_t na = min((uint32_t)kBucket, P.n_local - a0);
     if (tid < 5) s_stat[tid] = 0;
     for (uint32_t d = tid; d < kRadix; d += kBThreads) s_nh[d] = 0;
+    uint32_t* my_tc = nullptr;  // (fused) this thread's table entry, zeroed once the bucket is processed
     if (!kGather) {
       if (tid == 0) {
         s_lo = a.bstart[b];
         s_hi = a.bstart[b + 1];
+        s_g[5] = s_hi - s_lo > (uint32_t)kBucket;
+        if (!kSkew && s_g[5]) a.skew_list[atomicAdd(a.skew_n, 1u)] = b;
       }
     } else {
       // fused: this bucket's row of the tell tables (chunk c = sender bucket c), its backlog,
       // its host-staged tells; rows are zeroed once read (the writers only set non-zero entries)
-      uint32_t* segp = reinterpret_cast<uint32_t*>(U);
+      uint32_t* segp = s_pay;  // segment list (read by the loads; s_pay is rewritten only after a barrier)
       uint32_t* sego = segp + kRadix + 2;
       const uint32_t c = tid;
       uint32_t v = 0, o = 0;
@@ -1129,14 +1197,13 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         uint32_t* tc = g.tcnt[rpar] + (size_t)b * g.tstride + c;
         v = *tc;
         o = g.toff[rpar][(size_t)b * g.tstride + c];
-        if (v) *tc = 0u;
+        if (v) my_tc = tc;
       }
-      if (tid == 0) {
+      if (tid == 0) {  // (the tick zeroes the staged counts after the superstep)
         s_g[0] = g.blc[rpar][b];
         s_g[1] = g.blo[rpar][b];
         s_g[2] = g.stg_cnt[b];
         s_g[3] = g.stg_off[b];
-        if (s_g[2]) g.stg_cnt[b] = 0u;
       }
       uint32_t tt, ns;
       const uint32_t ex = block_excl_sum<kBThreads>(v, scratch, &tt);   // (syncs: s_g visible after)
@@ -1150,10 +1217,17 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         segp[ns] = blc + tt;  // staged segment
         s_g[4] = ns;
         const uint32_t cnt = blc + tt + s_g[2];
+        s_g[5] = cnt > (uint32_t)kBucket;
+        if (!kSkew && s_g[5]) a.skew_list[atomicAdd(a.skew_n, 1u)] = b;
         // inbox slot: the bucket's own region (no shared counter), else the overflow region
         uint64_t lo = (uint64_t)b * g.region;
-        if (cnt > g.region) lo = (uint64_t)a.nb * g.region + atomicAdd(g.ovf, cnt);
-        if (lo + cnt > g.cap) {  // arena overflow: report, drop this bucket's mail
+        if (!kSkew && s_g[5]) {
+          // deferred to the skew launch, which allocates
+        } else if (cnt > g.region) {
+          lo = (uint64_t)a.nb * g.region + atomicAdd(g.ovf, cnt);
+        }
+        if (!kSkew && s_g[5]) {
+        } else if (lo + cnt > g.cap) {  // arena overflow: report, drop this bucket's mail
           atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
           s_lo = 0;
           s_hi = 0;
@@ -1175,10 +1249,15 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     }
     __syncthreads();
     AGX_STAMP(a, 1);
+    if (!kSkew && s_g[5]) {  // large inbox: left to the skew-list launch (row kept for it)
+      __syncthreads();       // every thread has read s_g before the next bucket rewrites it
+      continue;
+    }
+    if (my_tc) *my_tc = 0u;          // fused: table row consumed
     const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
     GatherView gv{};
     if (kGather) {
-      gv.segp = reinterpret_cast<const uint32_t*>(U);
+      gv.segp = s_pay;
       gv.sego = gv.segp + kRadix + 2;
       gv.nseg = s_g[4];
       gv.blc = s_g[0];
@@ -1186,7 +1265,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       gv.sto = s_g[3];
     }
 
-    if (cnt <= (uint32_t)kBucket) {
+    if constexpr (!kSkew) {
       // ---- fast path: the whole bucket in one LDS tile
       uint32_t k[kBIpt], sv[kBIpt], pv[kBIpt], rk[kBIpt];
       const uint32_t wbase = w * (kBIpt * kWave);
@@ -1205,7 +1284,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
           k[r] = 0xFFFFFFFFu;
         }
       }
-      __syncthreads();  // (fused) the segment list in U is read before whist reuses U
+      __syncthreads();  // (fused) the segment list in s_pay is read before the items overwrite it
       // in-order copy + sortedness check: local topologies (rings, stencils) arrive already in
       // actor order, and then the wave multisplit ranking is unnecessary (same result)
       for (uint32_t i = tid; i < kBucket + 4; i += kBThreads) s_seg[i] = 0;
@@ -1288,35 +1367,41 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         __syncthreads();
       }
       AGX_STAMP(a, 2);
-      bucket_finish<true, kWide, KM, kGather>(a, L, b, lo, cnt, a0, na, wpar);
+      bucket_finish<true, kWide, KM, kGather>(a, L, b, lo, cnt, a0, na, wpar, 0u);
     } else {
-      // ---- general path (skewed bucket): counting sort into the global scratch copy
-      CMsgs in = a.in;
-      if (kGather) {  // materialise the gathered inbox at [lo, lo+cnt) of the inbox arena
-        for (uint32_t q = tid; q < cnt; q += kBThreads) {
-          uint32_t k0, s0, p0;
-          gv.load(g, rpar, q, k0, s0, p0);
-          g.inb.key[lo + q] = k0;
-          g.inb.src[lo + q] = s0;
-          g.inb.pay[lo + q] = p0;
-        }
-        __threadfence_block();
-        __syncthreads();
-        in = {g.inb.key, g.inb.src, g.inb.pay};
-      }
-      uint32_t* s_run = s_key;  // LDS items are unused on this path
+      // ---- general path (skewed bucket, > kBucket messages): admission first, then a stable
+      // counting sort of the ADMITTED messages only into the global scratch copy.  Per actor
+      // keep = alive ? min(len, C) : 0 (tail-drop: the first `keep` in canonical order are
+      // admitted); messages of an actor already at `keep` are dead letters and skip the
+      // ranking, so a hot actor of a bounded mailbox costs one key read per arrival.
+      auto gkey = [&](uint32_t q) -> uint32_t { return kGather ? gv.key(g, rpar, q) : a.in.key[lo + q]; };
+      uint32_t* s_run = s_key;   // LDS items are unused on this path
       uint32_t* s_tmp = s_src;
+      uint32_t* s_keep = s_ecnt;  // (bucket_finish re-initialises ecnt)
       for (uint32_t i = tid; i < kBucket + 4; i += kBThreads) s_seg[i] = 0;
       for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] = 0;
       __syncthreads();
-      for (uint32_t q = tid; q < cnt; q += kBThreads) atomicAdd(&s_seg[in.key[lo + q] & (kBucket - 1)], 1u);
+      for (uint32_t q0 = 0; q0 < cnt; q0 += 4 * kBThreads) {  // arrivals per actor (4 loads in flight)
+        uint32_t kk[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kk[j] = q0 + j * kBThreads + tid < cnt ? gkey(q0 + j * kBThreads + tid) : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (q0 + j * kBThreads + tid < cnt) atomicAdd(&s_seg[kk[j] & (kBucket - 1)], 1u);
+      }
       __syncthreads();
+      uint32_t ndead0 = 0;
       {
         uint32_t v[kBAct], run = 0;
 #pragma unroll
         for (int j = 0; j < kBAct; ++j) {
-          v[j] = s_seg[tid * kBAct + j];
-          run += v[j];
+          const uint32_t la = tid * kBAct + j;
+          const uint32_t len = s_seg[la];
+          const uint32_t keep = !s_alive[la] ? 0u : ((P.C == 0 || len < P.C) ? len : P.C);
+          ndead0 += len - keep;
+          v[j] = keep;
+          s_keep[la] = keep;
+          run += keep;
         }
         uint32_t t;
         uint32_t ex = block_excl_sum<kBThreads>(run, scratch, &t);
@@ -1327,27 +1412,51 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         }
         if (tid == 0) s_seg[kBucket] = t;
       }
+      __syncthreads();
+      const uint32_t cnt2 = s_seg[kBucket];  // admitted messages
+      uint32_t kn[kBIpt];  // keys of the next sub-tile, loaded one sub-tile ahead
+#pragma unroll
+      for (int r = 0; r < kBIpt; ++r) {
+        const uint32_t q = w * (kBIpt * kWave) + r * kWave + lane;
+        kn[r] = q < cnt ? gkey(q) : 0xFFFFFFFFu;
+      }
       for (uint32_t sub = 0; sub < cnt; sub += kBucket) {
-        for (uint32_t i = tid; i < kBWaves * kBucket / 2; i += kBThreads) reinterpret_cast<uint32_t*>(whist)[i] = 0;
-        __syncthreads();
         const uint32_t wbase = sub + w * (kBIpt * kWave);
         uint32_t k[kBIpt], sv[kBIpt], pv[kBIpt], rk[kBIpt];
+        bool live[kBIpt];
+        int any = 0;
+#pragma unroll
+        for (int r = 0; r < kBIpt; ++r) {
+          k[r] = kn[r];
+          const uint32_t q = wbase + r * kWave + lane;
+          const uint32_t la = k[r] & (kBucket - 1);
+          live[r] = q < cnt && s_run[la] < s_keep[la];  // actor not yet full: rank it
+          any |= live[r];
+        }
+#pragma unroll
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t q = wbase + kBucket + r * kWave + lane;
+          kn[r] = q < cnt ? gkey(q) : 0xFFFFFFFFu;
+        }
+        // every arrival of this sub-tile goes to an actor already at `keep`: all dead letters
+        if (!__syncthreads_or(any)) continue;
+        for (uint32_t i = tid; i < kBWaves * kBucket / 2; i += kBThreads) reinterpret_cast<uint32_t*>(whist)[i] = 0;
+        __syncthreads();
 #pragma unroll
         for (int r = 0; r < kBIpt; ++r) {
           const uint32_t q = wbase + r * kWave + lane;
-          if (q < cnt) {
-            k[r] = in.key[lo + q];
-            sv[r] = in.src[lo + q];
-            pv[r] = in.pay[lo + q];
-          } else {
-            k[r] = 0xFFFFFFFFu;
+          if (live[r]) {
+            if (kGather) {
+              uint32_t k2;
+              gv.load(g, rpar, q, k2, sv[r], pv[r]);
+            } else {
+              sv[r] = a.in.src[lo + q];
+              pv[r] = a.in.pay[lo + q];
+            }
           }
         }
 #pragma unroll
-        for (int r = 0; r < kBIpt; ++r) {
-          const uint32_t q = wbase + r * kWave + lane;
-          rk[r] = wave_rank(q < cnt, k[r] & (kBucket - 1), kBucketBits, whist + w * kBucket, ltm);
-        }
+        for (int r = 0; r < kBIpt; ++r) rk[r] = wave_rank(live[r], k[r] & (kBucket - 1), kBucketBits, whist + w * kBucket, ltm);
         __syncthreads();
         for (uint32_t la = tid; la < kBucket; la += kBThreads) {
           uint32_t run = 0;
@@ -1362,10 +1471,11 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < kBIpt; ++r) {
-          const uint32_t q = wbase + r * kWave + lane;
-          if (q < cnt) {
-            const uint32_t la = k[r] & (kBucket - 1);
-            const uint32_t pos = lo + s_seg[la] + s_run[la] + whist[w * kBucket + la] + rk[r];
+          if (!live[r]) continue;
+          const uint32_t la = k[r] & (kBucket - 1);
+          const uint32_t rank = s_run[la] + whist[w * kBucket + la] + rk[r];  // among this actor's arrivals
+          if (rank < s_keep[la]) {
+            const uint32_t pos = lo + s_seg[la] + rank;
             a.scr.key[pos] = k[r];
             a.scr.src[pos] = sv[r];
             a.scr.pay[pos] = pv[r];
@@ -1375,7 +1485,9 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] += s_tmp[la];
         __syncthreads();
       }
-      bucket_finish<false, kWide, KM, kGather>(a, L, b, lo, cnt, a0, na, wpar);
+      // the scratch copy holds the admitted messages in actor order; dead letters counted here
+      __threadfence_block();
+      bucket_finish<false, kWide, KM, kGather>(a, L, b, lo, cnt2, a0, na, wpar, ndead0);
     }
   }
 }
@@ -1448,6 +1560,7 @@ struct McompactArgs {
   uint64_t* stats;
   uint32_t* step;
   uint32_t* heap_top;
+  uint32_t* skew_n;
   uint64_t cap0, cap1;
 };
 
@@ -1457,7 +1570,10 @@ __global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactArgs a) 
   begin_step(a.step, a.heap_top);
   commit_stops(a.alive, a.stopq, a.nstop);
   const int tid = threadIdx.x;
-  if (tid == 0) s_run[0] = s_run[1] = 0;
+  if (tid == 0) {
+    s_run[0] = s_run[1] = 0;
+    *a.skew_n = 0u;
+  }
   __syncthreads();
   for (int sdx = 0; sdx < 2; ++sdx) {
     uint32_t* off = sdx == 0 ? a.off0 : a.off1;
@@ -1534,7 +1650,7 @@ __global__ void __launch_bounds__(kThreads) k_gen_rmat(const uint64_t* lrow, con
 // zero what the superstep consumed, advance the parity.  One block.
 __global__ void __launch_bounds__(kBThreads) k_fused_tick(uint32_t* step, const uint32_t* cntb, uint32_t nb,
                                                           uint32_t* stg_cnt, uint32_t* ovf, uint32_t* heap_top,
-                                                          uint32_t* d_n, uint64_t* stats) {
+                                                          uint32_t* d_n, uint64_t* stats, uint32_t* skew_n) {
   __shared__ uint32_t scratch[kBWaves + 1];
   uint32_t v = 0;
   for (uint32_t i = threadIdx.x; i < nb; i += kBThreads) {
@@ -1549,6 +1665,7 @@ __global__ void __launch_bounds__(kBThreads) k_fused_tick(uint32_t* step, const 
     const uint32_t s1 = *step + 1u;
     *step = s1;
     *ovf = 0u;
+    *skew_n = 0u;
     if (heap_top) heap_top[s1 & 1u] = 0u;
   }
 }

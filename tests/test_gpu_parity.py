@@ -297,3 +297,16 @@ def test_power_law_device_graph(built):
     sg, so, a, b = run_both(w)
     assert_same(sg, so, a, b, "power_law device graph")
     assert sg.dead_letters > 0
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("case", sorted(MULTIPASS_CASES))
+def test_grid_stride_apply(built, monkeypatch, fused, case):
+    """AGX_APPLY_GRID: few apply blocks, each looping over many buckets (as above 8M actors),
+    with skewed buckets deferred to the skew launch in between."""
+    monkeypatch.setenv("AGX_APPLY_GRID", "3")
+    if not fused:
+        monkeypatch.setenv("AGX_NO_FUSED", "1")
+    w = MULTIPASS_CASES[case]()
+    sg, so, a, b = run_both(w)
+    assert_same(sg, so, a, b, f"grid-stride {case} fused={fused}")

@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Diagnostic: C5 power-law bounded forwarding, eager launches with per-kernel and
+per-bucket stamps (AGX_STAMPS=1 in the environment)."""
+import sys, pathlib, time, argparse
+sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=100_000_000)
+ap.add_argument("--steps", type=int, default=4)
+ap.add_argument("--workload", default="c5")
+a = ap.parse_args()
+import torch
+from akka_amd import workloads as wl
+from akka_amd.engine import EngineConfig, GpuEngine
+if a.workload == "c5":
+    w = wl.power_law_forward(a.n, ttl=15, capacity=64, throughput=5, device_graph=True)
+elif a.workload == "c3":
+    w = wl.zipf_fanout(a.n, k=1, ttl=15, root_every=1, capacity=1000)
+else:
+    w = wl.ping_pong(1000, messages_per_pair=2_000_000, throughput=50)
+cfg = EngineConfig(**w.engine_kwargs())
+if a.workload == "c1":
+    cfg.msg_capacity = 1 << 20
+eng = GpuEngine(cfg)
+w.apply_to(eng)
+eng.run(2)
+eng.profile(True)
+for i in range(a.steps):
+    eng.profile_reset()
+    s0 = eng.stats()
+    s1 = eng.run(1)
+    p = eng.profile_read()
+    print("step", i, "delivered", s1.delivered - s0.delivered, "dead", s1.dead_letters - s0.dead_letters,
+          {k: round(v["total_ms"], 3) for k, v in p.items() if v["launches"]}, flush=True)
