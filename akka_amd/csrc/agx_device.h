@@ -104,6 +104,32 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* scratch
   return r;
 }
 
+// Two block exclusive sums at once (one set of barriers).  `scratch` needs 2 * (NT/64 + 1) u32.
+template <int NT>
+__device__ __forceinline__ uint2 block_excl_sum2(uint32_t v0, uint32_t v1, uint32_t* scratch, uint32_t* t0,
+                                                 uint32_t* t1) {
+  constexpr int NW = NT / kWave;
+  const int tid = threadIdx.x, w = tid / kWave, lane = tid % kWave;
+  const uint32_t i0 = wave_incl_sum(v0), i1 = wave_incl_sum(v1);
+  if (lane == kWave - 1) {
+    scratch[w] = i0;
+    scratch[NW + 1 + w] = i1;
+  }
+  __syncthreads();
+  if (tid < 2) {
+    uint32_t* sc = scratch + tid * (NW + 1);
+    uint32_t run = 0;
+    for (int i = 0; i < NW; ++i) { uint32_t t = sc[i]; sc[i] = run; run += t; }
+    sc[NW] = run;
+  }
+  __syncthreads();
+  const uint2 r = make_uint2(scratch[w] + i0 - v0, scratch[NW + 1 + w] + i1 - v1);
+  *t0 = scratch[NW];
+  *t1 = scratch[2 * NW + 1];
+  __syncthreads();
+  return r;
+}
+
 // Block exclusive max over NT threads; identity -1.
 template <int NT>
 __device__ __forceinline__ int block_excl_max(int v, int* scratch) {

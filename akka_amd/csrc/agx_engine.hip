@@ -85,9 +85,11 @@ struct DevMsgs {
   CMsgs c() const { return {key, src, pay}; }
 };
 
-enum KClass { K_CROWSCAN, K_CDOWN, K_UPSWEEP, K_ROWSCAN, K_DOWNSWEEP, K_APPLY, K_EXCHANGE, K_MCOMPACT, K_NCLASS };
+enum KClass { K_CROWSCAN, K_CDOWN, K_UPSWEEP, K_ROWSCAN, K_DOWNSWEEP, K_APPLY, K_EXCHANGE, K_MCOMPACT, K_SKEW, K_TICK,
+              K_BOUNDS, K_NCLASS };
 const char* kClassNames[K_NCLASS] = {"chunk_rowscan", "chunk_downsweep", "sort_upsweep", "sort_rowscan",
-                                     "sort_downsweep", "bucket_apply", "exchange", "mcompact"};
+                                     "sort_downsweep", "bucket_apply", "exchange", "mcompact", "bucket_apply_skew",
+                                     "fused_tick", "bucket_bounds"};
 
 struct SortPlan {  // LSD passes over key bits [kBucketBits, key_bits)
   uint32_t npass = 1;
@@ -148,7 +150,8 @@ struct agx_engine {
   DevMsgs bl2, eg0, eg1;
   uint32_t *d_tcnt[2] = {nullptr, nullptr}, *d_toff[2] = {nullptr, nullptr};
   uint32_t *d_blo[2] = {nullptr, nullptr}, *d_blc[2] = {nullptr, nullptr}, *d_emc[2] = {nullptr, nullptr};
-  uint32_t *d_stg_off = nullptr, *d_stg_cnt = nullptr, *d_ovf = nullptr, *d_cntb = nullptr;
+  uint32_t *d_stg_off = nullptr, *d_stg_cnt = nullptr, *d_ovf = nullptr, *d_nacc = nullptr, *d_parv = nullptr;
+  uint32_t par = 0;  // fused: parity of the next superstep (host-tracked; graphs are captured per parity)
   uint32_t *d_skew_list = nullptr, *d_skew_n = nullptr;  // buckets for the general-path launch
   uint32_t tstride = 4, region = 0;
   uint64_t acap = 0;  // arena capacity (fused: regions + overflow area)
@@ -167,6 +170,7 @@ struct agx_engine {
   static constexpr uint32_t kGraphSteps = 8;
   bool graphs_enabled = true;
   hipGraphExec_t g1 = nullptr, gG = nullptr;
+  hipGraphExec_t g1p[2] = {nullptr, nullptr}, gGp[2] = {nullptr, nullptr};  // fused: per starting parity
   unsigned long long* d_dbg = nullptr;  // AGX_STAMPS diagnostic build only
 
   // profiling
@@ -375,7 +379,7 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     std::swap(src, dst);
   }
   if (e->plan.npass > 1) {  // digits of the last pass are not buckets: find the bucket starts
-    Scope s(e, K_ROWSCAN);
+    Scope s(e, K_BOUNDS);
     hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((e->nb + kThreads) / kThreads, 4096)), dim3(kThreads), 0,
                        e->stream, src->key, e->d_n, e->nb, e->d_bstart);
     HIP_TRY(hipGetLastError());
@@ -410,6 +414,10 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.skew_list = e->d_skew_list;
   ba.skew_n = e->d_skew_n;
   if (e->fused) {
+    ba.par = e->par;
+    ba.P.step = e->d_parv + e->par;  // CRDT heap parity = superstep parity
+  }
+  if (e->fused) {
     GatherArgs& g = ba.g;
     g.bl[0] = e->bl.m();
     g.bl[1] = e->bl2.m();
@@ -426,27 +434,30 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     g.stg_off = e->d_stg_off;
     g.stg_cnt = e->d_stg_cnt;
     g.inb = e->A.m();
-    g.step = e->d_step;
     g.ovf = e->d_ovf;
-    g.cntb = e->d_cntb;
+    g.nacc = e->d_nacc;
+    g.heap_top = e->pw ? e->d_heap_top : nullptr;
     g.cap = e->acap;
     g.tstride = e->tstride;
     g.region = e->region;
   }
   ba.dbg = e->d_dbg;
   {
-    Scope s(e, K_APPLY);
     const dim3 g(grid_for(e->nb, e->apply_grid)), blk(kBThreads);
     const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
     const dim3 gs(grid_for(e->nb, e->apply_grid));  // skew list: as many blocks as there may be buckets
 #define AGX_APPLY(W, M)                                                                          \
   do {                                                                                           \
     if (e->fused) {                                                                              \
-      hipLaunchKernelGGL((k_bucket_apply<W, M, true, false>), g, blk, 0, e->stream, ba);         \
-      hipLaunchKernelGGL((k_bucket_apply<W, M, true, true>), gs, blk, 0, e->stream, ba);         \
+      { Scope s(e, K_APPLY);                                                                     \
+        hipLaunchKernelGGL((k_bucket_apply<W, M, true, false>), g, blk, 0, e->stream, ba); }     \
+      { Scope s(e, K_SKEW);                                                                      \
+        hipLaunchKernelGGL((k_bucket_apply<W, M, true, true>), gs, blk, 0, e->stream, ba); }     \
     } else {                                                                                     \
-      hipLaunchKernelGGL((k_bucket_apply<W, M, false, false>), g, blk, 0, e->stream, ba);        \
-      hipLaunchKernelGGL((k_bucket_apply<W, M, false, true>), gs, blk, 0, e->stream, ba);        \
+      { Scope s(e, K_APPLY);                                                                     \
+        hipLaunchKernelGGL((k_bucket_apply<W, M, false, false>), g, blk, 0, e->stream, ba); }    \
+      { Scope s(e, K_SKEW);                                                                      \
+        hipLaunchKernelGGL((k_bucket_apply<W, M, false, true>), gs, blk, 0, e->stream, ba); }    \
     }                                                                                            \
   } while (0)
     if (e->pw)  // CRDT kinds registered: the variant with state gossips
@@ -463,9 +474,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
       AGX_APPLY(false, KM_ALL);
 #undef AGX_APPLY
   }
-  if (e->fused)
-    hipLaunchKernelGGL(k_fused_tick, dim3(1), dim3(kBThreads), 0, e->stream, e->d_step, e->d_cntb, e->nb, e->d_stg_cnt,
-                       e->d_ovf, e->pw ? e->d_heap_top : nullptr, e->d_n, e->d_stats, e->d_skew_n);
+  if (e->fused) e->par ^= 1u;  // the next superstep writes the other parity
   HIP_TRY(hipGetLastError());
   return AGX_OK;
 }
@@ -653,6 +662,17 @@ agx_status check_error(agx_engine* e) {
 
 agx_status fill_stats(agx_engine* e, agx_stats* out, uint64_t inflight) {
   uint64_t s[ST_N], bs[kBStats];
+  if (e->fused) {  // the last superstep is counted by the next one's first block: count it now, once
+    uint32_t last = 0;
+    HIP_TRY(hipMemcpy(&last, e->d_nacc + (e->par ^ 1u), 4, hipMemcpyDeviceToHost));
+    if (last) {
+      uint64_t steps = 0;
+      HIP_TRY(hipMemcpy(&steps, e->d_stats + ST_STEPS, 8, hipMemcpyDeviceToHost));
+      ++steps;
+      HIP_TRY(hipMemcpy(e->d_stats + ST_STEPS, &steps, 8, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemset(e->d_nacc + (e->par ^ 1u), 0, 4));
+    }
+  }
   hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_bstats, kMaxApplyGrid, e->d_sred);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -680,7 +700,7 @@ agx_status fill_stats(agx_engine* e, agx_stats* out, uint64_t inflight) {
 agx_status chunk_inflight(agx_engine* e, uint64_t* out) {
   if (e->fused)
     hipLaunchKernelGGL(k_inflight_fused, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_blc[0], e->d_blc[1],
-                       e->d_emc[0], e->d_emc[1], e->d_stg_cnt, e->d_step, e->nb, (unsigned long long*)e->d_inflight);
+                       e->d_emc[0], e->d_emc[1], e->d_stg_cnt, e->par ^ 1u, e->nb, (unsigned long long*)e->d_inflight);
   else
     hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_chunk_cnt, e->nchunks,
                        (unsigned long long*)e->d_inflight);
@@ -738,10 +758,17 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     --left;
   }
   const bool use_graph = !e->prof && e->graphs_enabled;
-  if (st == AGX_OK && use_graph && !e->g1) {
-    st = capture_steps(e, 1, &e->g1);
-    if (st == AGX_OK) st = capture_steps(e, agx_engine::kGraphSteps, &e->gG);
-  }
+  auto graph1 = [&]() -> hipGraphExec_t& { return e->fused ? e->g1p[e->par] : e->g1; };
+  auto graphG = [&]() -> hipGraphExec_t& { return e->fused ? e->gGp[e->par] : e->gG; };
+  auto ensure_graphs = [&]() -> agx_status {
+    if (!use_graph || graph1()) return AGX_OK;
+    const uint32_t p0 = e->par;  // capturing advances the host parity: restore it
+    agx_status s2 = capture_steps(e, 1, &graph1());
+    e->par = p0;
+    if (s2 == AGX_OK) s2 = capture_steps(e, agx_engine::kGraphSteps, &graphG());
+    e->par = p0;
+    return s2;
+  };
   for (uint32_t it = 0; st == AGX_OK && left > 0; ++it) {
     const uint32_t slot = it % kLag;
     if (it >= kLag) {
@@ -750,15 +777,20 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     }
     uint32_t cnt;
     if (use_graph) {
+      st = ensure_graphs();
+      if (st != AGX_OK) break;
       cnt = left >= agx_engine::kGraphSteps ? agx_engine::kGraphSteps : 1;
-      hipError_t ge = hipGraphLaunch(cnt == 1 ? e->g1 : e->gG, e->stream);
+      hipError_t ge = hipGraphLaunch(cnt == 1 ? graph1() : graphG(), e->stream);
       if (ge != hipSuccess) st = set_err(AGX_EDEVICE, "hipGraphLaunch: %s", hipGetErrorString(ge));
+      if (e->fused && (cnt & 1u)) e->par ^= 1u;  // the replayed supersteps advanced the parity
     } else {
       cnt = 1;
       st = launch_step_single(e);
     }
     left -= cnt;
-    hipMemcpyAsync(&e->h_pin[slot], e->d_n, 4, hipMemcpyDeviceToHost, e->stream);
+    // inbox total of the replay's last superstep (fused: its parity's accumulator)
+    hipMemcpyAsync(&e->h_pin[slot], e->fused ? e->d_nacc + (e->par ^ 1u) : e->d_n, 4, hipMemcpyDeviceToHost,
+                   e->stream);
     hipEventRecord(ev[slot], e->stream);
   }
   hipStreamSynchronize(e->stream);
@@ -832,6 +864,11 @@ void drop_graphs(agx_engine* e) {
   if (e->g1) hipGraphExecDestroy(e->g1);
   if (e->gG) hipGraphExecDestroy(e->gG);
   e->g1 = e->gG = nullptr;
+  for (int q = 0; q < 2; ++q) {
+    if (e->g1p[q]) hipGraphExecDestroy(e->g1p[q]);
+    if (e->gGp[q]) hipGraphExecDestroy(e->gGp[q]);
+    e->g1p[q] = e->gGp[q] = nullptr;
+  }
 }
 
 // First CRDT kind (or a wider one): size the snapshot heap for `kind`'s rows.
@@ -1024,15 +1061,18 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     }
     CREATE_TRY(dalloc(&e->d_stg_off, e->nb));
     CREATE_TRY(dalloc(&e->d_stg_cnt, e->nb));
-    CREATE_TRY(dalloc(&e->d_ovf, 1));
-    CREATE_TRY(dalloc(&e->d_cntb, e->nb));
+    CREATE_TRY(dalloc(&e->d_ovf, 2));
+    CREATE_TRY(dalloc(&e->d_nacc, 2));
+    CREATE_TRY(dalloc(&e->d_parv, 2));
+    const uint32_t parv[2] = {0u, 1u};
+    CREATE_TRY(hipMemcpy(e->d_parv, parv, 8, hipMemcpyHostToDevice) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "upload"));
     CREATE_TRY(hipMemset(e->d_stg_cnt, 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-    CREATE_TRY(hipMemset(e->d_ovf, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-    CREATE_TRY(hipMemset(e->d_cntb, 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    CREATE_TRY(hipMemset(e->d_ovf, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    CREATE_TRY(hipMemset(e->d_nacc, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   }
   CREATE_TRY(dalloc(&e->d_skew_list, e->nb));
-  CREATE_TRY(dalloc(&e->d_skew_n, 1));
-  CREATE_TRY(hipMemset(e->d_skew_n, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(dalloc(&e->d_skew_n, 2));
+  CREATE_TRY(hipMemset(e->d_skew_n, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_chunk_off, e->nchunks));
   CREATE_TRY(dalloc(&e->d_chunk_cnt, e->nchunks));
   CREATE_TRY(hipMemset(e->d_chunk_off, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
@@ -1075,8 +1115,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipSetDevice((int)e->cfg.device);
   if (e->stream) hipStreamSynchronize(e->stream);
   if (e->comm) ncclCommDestroy(e->comm);
-  if (e->g1) hipGraphExecDestroy(e->g1);
-  if (e->gG) hipGraphExecDestroy(e->gG);
+  drop_graphs(e);
   hipFree(e->d_kind); hipFree(e->d_alive); hipFree(e->d_stopq); hipFree(e->d_nstop); hipFree(e->d_state); hipFree(e->d_gid); hipFree(e->d_route);
   hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_row); hipFree(e->d_col);
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
@@ -1084,7 +1123,7 @@ agx_status agx_destroy(agx_engine* e) {
   for (int q = 0; q < 2; ++q) {
     hipFree(e->d_tcnt[q]); hipFree(e->d_toff[q]); hipFree(e->d_blo[q]); hipFree(e->d_blc[q]); hipFree(e->d_emc[q]);
   }
-  hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_cntb);
+  hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_nacc); hipFree(e->d_parv);
   hipFree(e->d_skew_list); hipFree(e->d_skew_n);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_n); hipFree(e->d_total);

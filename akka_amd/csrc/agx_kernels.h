@@ -585,9 +585,9 @@ struct GatherArgs {
   uint32_t* stg_off;       // [nb] staged tells per bucket (count zeroed by the reader)
   uint32_t* stg_cnt;
   Msgs inb;                // skewed buckets: gathered inbox copy at [lo, lo+cnt)
-  uint32_t* step;          // superstep counter (parity = step & 1), advanced by k_fused_tick
-  uint32_t* ovf;           // overflow-region cursor (inboxes larger than `region`), reset by the tick
-  uint32_t* cntb;          // [nb] inbox size per bucket this superstep (summed by the tick)
+  uint32_t* ovf;           // [2] overflow-region cursor per parity (inboxes larger than `region`)
+  uint32_t* nacc;          // [2] inbox total per parity (host quiescence poll; counted as a superstep)
+  uint32_t* heap_top;      // CRDT heap tops [2] (null when no CRDT kind is registered)
   uint64_t cap;
   uint32_t tstride;
   uint32_t region;         // bucket b's inbox lives at [b*region, ...) unless larger (overflow region)
@@ -607,6 +607,7 @@ struct BucketArgs {
   uint32_t nhist_stride, nx_shift, nx_bits;
   uint32_t G, ng;          // histogram units: G buckets per column, ng units per arena
   uint32_t nb, kmax;
+  uint32_t par;            // fused: parity of this superstep (arenas/tables written; read = par ^ 1)
   uint32_t* skew_list;     // buckets whose inbox exceeds one LDS tile (appended by the fast launch)
   uint32_t* skew_n;        // their count (reset by the first kernel of the next superstep)
   uint64_t* stats;
@@ -1152,7 +1153,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   __shared__ uint8_t s_alive[kBucket];
   __shared__ uint8_t s_kind[kBucket];
   __shared__ uint32_t s_nh[kRadix];
-  __shared__ uint32_t scratch[kBWaves + 1];
+  __shared__ uint32_t scratch[2 * (kBWaves + 1)];
   __shared__ uint32_t s_lo, s_hi, s_g[6];
   __shared__ unsigned long long s_stat[5];
   const BucketLds L{s_key, s_src, s_pay, U, s_seg, s_ecnt, s_alive, s_kind, s_nh, scratch, s_stat};
@@ -1163,14 +1164,24 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   const uint32_t lane = lane_id();
   const uint64_t ltm = lanemask_lt();
   const GatherArgs& g = a.g;
-  const uint32_t step0 = kGather ? *g.step : 0u;  // fused: write parity w, read parity w ^ 1 (the tick advances it)
-  const uint32_t wpar = step0 & 1u, rpar = wpar ^ 1u;
+  const uint32_t wpar = kGather ? a.par : 0u, rpar = wpar ^ 1u;  // fused: write parity w, read parity w ^ 1
+  uint32_t* const skew_n = a.skew_n + wpar;
+  if (kGather && !kSkew && blockIdx.x == 0 && tid == 0) {
+    // close the previous superstep (its kernels are complete): count it if it had mail, and
+    // reset the per-parity cursors that the NEXT superstep (parity rpar) will use
+    const uint32_t prev = g.nacc[rpar];
+    if (prev) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
+    g.nacc[rpar] = 0u;
+    g.ovf[rpar] = 0u;
+    a.skew_n[rpar] = 0u;
+    if (g.heap_top) g.heap_top[rpar] = 0u;
+  }
   if (!kGather && !kSkew && blockIdx.x == 0) {
     if (tid == 0 && *a.d_n > 0) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
     for (uint32_t i = tid; i < kStagedChunks; i += kBThreads) a.chunk_cnt[2 * a.nb + i] = 0;  // staged consumed
   }
 
-  const uint32_t nwork = kSkew ? *a.skew_n : a.nb;
+  const uint32_t nwork = kSkew ? *skew_n : a.nb;
   for (uint32_t it = blockIdx.x; it < nwork; it += gridDim.x) {
     const uint32_t b = kSkew ? a.skew_list[it] : it;
     AGX_STAMP(a, 0);
@@ -1179,12 +1190,19 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     if (tid < 5) s_stat[tid] = 0;
     for (uint32_t d = tid; d < kRadix; d += kBThreads) s_nh[d] = 0;
     uint32_t* my_tc = nullptr;  // (fused) this thread's table entry, zeroed once the bucket is processed
+    uint32_t alive4 = 0;        // alive flags of actors 4*tid..4*tid+3, loaded first (a0 is a multiple of kBucket)
+    {
+      const uint32_t la0 = tid * 4;
+      if (la0 + 4 <= na) alive4 = *reinterpret_cast<const uint32_t*>(P.alive + a0 + la0);
+      else
+        for (uint32_t j = 0; j < 4; ++j) alive4 |= (la0 + j < na ? (uint32_t)P.alive[a0 + la0 + j] : 0u) << (8 * j);
+    }
     if (!kGather) {
       if (tid == 0) {
         s_lo = a.bstart[b];
         s_hi = a.bstart[b + 1];
         s_g[5] = s_hi - s_lo > (uint32_t)kBucket;
-        if (!kSkew && s_g[5]) a.skew_list[atomicAdd(a.skew_n, 1u)] = b;
+        if (!kSkew && s_g[5]) a.skew_list[atomicAdd(skew_n, 1u)] = b;
       }
     } else {
       // fused: this bucket's row of the tell tables (chunk c = sender bucket c), its backlog,
@@ -1199,15 +1217,15 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         o = g.toff[rpar][(size_t)b * g.tstride + c];
         if (v) my_tc = tc;
       }
-      if (tid == 0) {  // (the tick zeroes the staged counts after the superstep)
+      if (tid == 0) {  // (the staged count is zeroed once the bucket is processed)
         s_g[0] = g.blc[rpar][b];
         s_g[1] = g.blo[rpar][b];
         s_g[2] = g.stg_cnt[b];
         s_g[3] = g.stg_off[b];
       }
       uint32_t tt, ns;
-      const uint32_t ex = block_excl_sum<kBThreads>(v, scratch, &tt);   // (syncs: s_g visible after)
-      const uint32_t ix = block_excl_sum<kBThreads>(v ? 1u : 0u, scratch, &ns);
+      const uint2 exix = block_excl_sum2<kBThreads>(v, v ? 1u : 0u, scratch, &tt, &ns);  // (syncs: s_g visible after)
+      const uint32_t ex = exix.x, ix = exix.y;
       const uint32_t blc = s_g[0];
       if (v) {
         segp[ix] = blc + ex;
@@ -1218,42 +1236,37 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         s_g[4] = ns;
         const uint32_t cnt = blc + tt + s_g[2];
         s_g[5] = cnt > (uint32_t)kBucket;
-        if (!kSkew && s_g[5]) a.skew_list[atomicAdd(a.skew_n, 1u)] = b;
+        if (!kSkew && s_g[5]) a.skew_list[atomicAdd(skew_n, 1u)] = b;
         // inbox slot: the bucket's own region (no shared counter), else the overflow region
         uint64_t lo = (uint64_t)b * g.region;
         if (!kSkew && s_g[5]) {
           // deferred to the skew launch, which allocates
         } else if (cnt > g.region) {
-          lo = (uint64_t)a.nb * g.region + atomicAdd(g.ovf, cnt);
+          lo = (uint64_t)a.nb * g.region + atomicAdd(&g.ovf[wpar], cnt);
         }
         if (!kSkew && s_g[5]) {
         } else if (lo + cnt > g.cap) {  // arena overflow: report, drop this bucket's mail
           atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
           s_lo = 0;
           s_hi = 0;
-          g.cntb[b] = 0;
         } else {
           s_lo = (uint32_t)lo;
           s_hi = (uint32_t)lo + cnt;
-          g.cntb[b] = cnt;
+          if (cnt) atomicAdd(&g.nacc[wpar], cnt);  // fire-and-forget: nobody waits on it
         }
       }
     }
-    {  // alive flags of the bucket, 4 per thread (a0 is a multiple of kBucket: 4-aligned)
-      const uint32_t la0 = tid * 4;
-      uint32_t v = 0;
-      if (la0 + 4 <= na) v = *reinterpret_cast<const uint32_t*>(P.alive + a0 + la0);
-      else
-        for (uint32_t j = 0; j < 4; ++j) v |= (la0 + j < na ? (uint32_t)P.alive[a0 + la0 + j] : 0u) << (8 * j);
-      reinterpret_cast<uint32_t*>(s_alive)[tid] = v;
-    }
+    reinterpret_cast<uint32_t*>(s_alive)[tid] = alive4;
     __syncthreads();
     AGX_STAMP(a, 1);
     if (!kSkew && s_g[5]) {  // large inbox: left to the skew-list launch (row kept for it)
       __syncthreads();       // every thread has read s_g before the next bucket rewrites it
       continue;
     }
-    if (my_tc) *my_tc = 0u;          // fused: table row consumed
+    if (kGather) {                   // fused: table row and staged tells consumed
+      if (my_tc) *my_tc = 0u;
+      if (tid == 0 && s_g[2]) g.stg_cnt[b] = 0u;
+    }
     const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
     GatherView gv{};
     if (kGather) {
@@ -1646,37 +1659,13 @@ __global__ void __launch_bounds__(kThreads) k_gen_rmat(const uint64_t* lrow, con
   }
 }
 
-// Fused mode, after each superstep: publish the inbox total (quiescence poll, step count),
-// zero what the superstep consumed, advance the parity.  One block.
-__global__ void __launch_bounds__(kBThreads) k_fused_tick(uint32_t* step, const uint32_t* cntb, uint32_t nb,
-                                                          uint32_t* stg_cnt, uint32_t* ovf, uint32_t* heap_top,
-                                                          uint32_t* d_n, uint64_t* stats, uint32_t* skew_n) {
-  __shared__ uint32_t scratch[kBWaves + 1];
-  uint32_t v = 0;
-  for (uint32_t i = threadIdx.x; i < nb; i += kBThreads) {
-    v += cntb[i];
-    stg_cnt[i] = 0;  // staged tells are consumed by the superstep that just ran
-  }
-  uint32_t t;
-  block_excl_sum<kBThreads>(v, scratch, &t);
-  if (threadIdx.x == 0) {
-    *d_n = t;
-    if (t) stats[ST_STEPS] += 1;
-    const uint32_t s1 = *step + 1u;
-    *step = s1;
-    *ovf = 0u;
-    *skew_n = 0u;
-    if (heap_top) heap_top[s1 & 1u] = 0u;
-  }
-}
-
 // fused mode: messages in flight after the last superstep = its backlog + tells + staged
 __global__ void __launch_bounds__(kScanThreads) k_inflight_fused(const uint32_t* blc0, const uint32_t* blc1,
                                                                  const uint32_t* emc0, const uint32_t* emc1,
-                                                                 const uint32_t* stg_cnt, const uint32_t* step,
+                                                                 const uint32_t* stg_cnt, uint32_t last_par,
                                                                  uint32_t nb, unsigned long long* out) {
   __shared__ unsigned long long s;
-  const bool p1 = ((*step + 1u) & 1u) != 0;  // parity written by the last superstep
+  const bool p1 = last_par != 0;  // parity written by the last superstep
   const uint32_t* blc = p1 ? blc1 : blc0;
   const uint32_t* emc = p1 ? emc1 : emc0;
   if (threadIdx.x == 0) s = 0;

@@ -19,5 +19,5 @@ python3 tools/pmc_to_json.py gpurun_out/pmc_${TAG}.json gpurun_out/${TAG}_pmc_fe
   --note "bench.py $B1M --steps 40 --warmup 4 (C2 ring, 1M actors)" > /dev/null || exit 1
 timeout -k 10 900 python bench.py --pmc gpurun_out/pmc_${TAG}.json ${BENCH_ARGS} > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || fail bench gpurun_out/${TAG}_bench.err
 cat gpurun_out/${TAG}_bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py $B1M --pmc gpurun_out/pmc_${TAG}.json > gpurun_out/${TAG}_prof.log 2>&1 || fail rocprof gpurun_out/${TAG}_prof.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py $B1M --pmc gpurun_out/pmc_${TAG}.json > gpurun_out/${TAG}_prof.log 2>&1 || fail rocprof gpurun_out/${TAG}_prof.log
 cat gpurun_out/${TAG}_prof/run_kernel_stats.csv

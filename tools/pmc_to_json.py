@@ -18,16 +18,30 @@ import json
 import os
 
 
+def kernel_class(full: str):
+    """'void agx::k_bucket_apply<false, 4u, true, false>(agx::BucketArgs)' -> 'bucket_apply'
+    (the skew-list instantiation, last template argument true -> 'bucket_apply_skew')."""
+    n = full[5:] if full.startswith("void ") else full
+    base = n.split("(")[0]
+    targs = ""
+    if "<" in base:
+        base, targs = base.split("<", 1)
+    if not base.startswith("agx::k_"):
+        return None
+    k = base[len("agx::k_"):]
+    if k == "bucket_apply" and targs.rstrip(">").split(",")[-1].strip() == "true":
+        k = "bucket_apply_skew"
+    return k
+
+
 def load(d: str, counter: str) -> dict:
     vals = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            name = r["Kernel_Name"].split("(")[0]
-            if not name.startswith("agx::k_"):
-                continue
-            vals[name[len("agx::k_"):]].append(float(r["Counter_Value"]))
+            vals[kernel_class(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    vals.pop(None, None)
     return {k: (sum(v) / len(v), len(v)) for k, v in vals.items()}
 
 
