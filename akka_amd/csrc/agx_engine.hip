@@ -150,7 +150,10 @@ struct agx_engine {
   DevMsgs bl2, eg0, eg1;
   uint32_t *d_tcnt[2] = {nullptr, nullptr}, *d_toff[2] = {nullptr, nullptr};
   uint32_t *d_blo[2] = {nullptr, nullptr}, *d_blc[2] = {nullptr, nullptr}, *d_emc[2] = {nullptr, nullptr};
-  uint32_t *d_stg_off = nullptr, *d_stg_cnt = nullptr, *d_ovf = nullptr, *d_nacc = nullptr, *d_parv = nullptr;
+  uint32_t *d_stg_off = nullptr, *d_stg_cnt = nullptr, *d_ovf = nullptr, *d_cntb = nullptr, *d_parv = nullptr;
+  uint32_t* h_cntb = nullptr;  // pinned [kLag][kGraphSteps][nb]: per-superstep inbox sizes of the replays in flight
+  uint32_t cur_slot = 0;       // superstep index within the replay being captured / launched
+  uint64_t host_steps = 0;     // fused: supersteps with mail, counted on the host from h_cntb
   uint32_t par = 0;  // fused: parity of the next superstep (host-tracked; graphs are captured per parity)
   uint32_t *d_skew_list = nullptr, *d_skew_n = nullptr;  // buckets for the general-path launch
   uint32_t tstride = 4, region = 0;
@@ -415,6 +418,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.skew_n = e->d_skew_n;
   if (e->fused) {
     ba.par = e->par;
+    ba.slot = e->cur_slot;
     ba.P.step = e->d_parv + e->par;  // CRDT heap parity = superstep parity
   }
   if (e->fused) {
@@ -435,7 +439,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     g.stg_cnt = e->d_stg_cnt;
     g.inb = e->A.m();
     g.ovf = e->d_ovf;
-    g.nacc = e->d_nacc;
+    g.cntb = e->d_cntb;
     g.heap_top = e->pw ? e->d_heap_top : nullptr;
     g.cap = e->acap;
     g.tstride = e->tstride;
@@ -662,17 +666,6 @@ agx_status check_error(agx_engine* e) {
 
 agx_status fill_stats(agx_engine* e, agx_stats* out, uint64_t inflight) {
   uint64_t s[ST_N], bs[kBStats];
-  if (e->fused) {  // the last superstep is counted by the next one's first block: count it now, once
-    uint32_t last = 0;
-    HIP_TRY(hipMemcpy(&last, e->d_nacc + (e->par ^ 1u), 4, hipMemcpyDeviceToHost));
-    if (last) {
-      uint64_t steps = 0;
-      HIP_TRY(hipMemcpy(&steps, e->d_stats + ST_STEPS, 8, hipMemcpyDeviceToHost));
-      ++steps;
-      HIP_TRY(hipMemcpy(e->d_stats + ST_STEPS, &steps, 8, hipMemcpyHostToDevice));
-      HIP_TRY(hipMemset(e->d_nacc + (e->par ^ 1u), 0, 4));
-    }
-  }
   hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_bstats, kMaxApplyGrid, e->d_sred);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -689,7 +682,7 @@ agx_status fill_stats(agx_engine* e, agx_stats* out, uint64_t inflight) {
   st.unhandled = s[ST_UNHANDLED];
   st.emitted = s[ST_EMITTED];
   st.staged = e->staged_total;
-  st.supersteps = s[ST_STEPS];
+  st.supersteps = s[ST_STEPS] + e->host_steps;
   st.in_flight = inflight;
   // B = E_in + f_out*E_out + 2*S*(A/M); kind+alive bytes read per activation
   st.bytes_alg = 12ull * st.delivered + 12ull * (st.emitted) + (16ull * e->W + 2ull) * s[ST_ACTIVE];
@@ -727,7 +720,11 @@ agx_status capture_steps(agx_engine* e, uint32_t steps, hipGraphExec_t* out) {
   hipGraph_t g = nullptr;
   HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
   agx_status st = AGX_OK;
-  for (uint32_t i = 0; i < steps && st == AGX_OK; ++i) st = launch_step_single(e);
+  for (uint32_t i = 0; i < steps && st == AGX_OK; ++i) {
+    e->cur_slot = i;  // fused: the i-th superstep of the replay reports its inbox sizes in row i
+    st = launch_step_single(e);
+  }
+  e->cur_slot = 0;
   hipError_t ce = hipStreamEndCapture(e->stream, &g);
   if (st) {
     if (g) hipGraphDestroy(g);
@@ -769,11 +766,32 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     e->par = p0;
     return s2;
   };
+  // fused: per-superstep inbox sizes of each replay (pinned ring); the host counts the supersteps
+  // with mail and stops at the first replay whose last superstep had none (quiescent)
+  uint32_t rep_steps[kLag] = {0, 0, 0, 0};
+  const size_t ring_row = (size_t)agx_engine::kGraphSteps * e->nb;
+  auto fused_poll = [&](uint32_t slot) -> bool {
+    const uint32_t* h = e->h_cntb + slot * ring_row;
+    bool last_empty = rep_steps[slot] > 0;
+    for (uint32_t i = 0; i < rep_steps[slot]; ++i) {
+      uint64_t t = 0;
+      for (uint32_t b = 0; b < e->nb; ++b) t += h[(size_t)i * e->nb + b];
+      if (t) ++e->host_steps;
+      last_empty = t == 0;
+    }
+    rep_steps[slot] = 0;
+    return last_empty;
+  };
+  uint32_t launched = 0;
   for (uint32_t it = 0; st == AGX_OK && left > 0; ++it) {
     const uint32_t slot = it % kLag;
     if (it >= kLag) {
       hipEventSynchronize(ev[slot]);
-      if (e->h_pin[slot] == 0) break;  // that replay ended on a superstep with no mail: quiescent
+      if (e->fused) {
+        if (fused_poll(slot)) break;
+      } else if (e->h_pin[slot] == 0) {
+        break;  // that replay ended on a superstep with no mail: quiescent
+      }
     }
     uint32_t cnt;
     if (use_graph) {
@@ -788,12 +806,19 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
       st = launch_step_single(e);
     }
     left -= cnt;
-    // inbox total of the replay's last superstep (fused: its parity's accumulator)
-    hipMemcpyAsync(&e->h_pin[slot], e->fused ? e->d_nacc + (e->par ^ 1u) : e->d_n, 4, hipMemcpyDeviceToHost,
-                   e->stream);
+    ++launched;
+    if (e->fused) {  // per-superstep inbox sizes of this replay
+      rep_steps[slot] = cnt;
+      hipMemcpyAsync(e->h_cntb + slot * ring_row, e->d_cntb, (size_t)cnt * e->nb * 4, hipMemcpyDeviceToHost,
+                     e->stream);
+    } else {  // inbox total of the replay's last superstep
+      hipMemcpyAsync(&e->h_pin[slot], e->d_n, 4, hipMemcpyDeviceToHost, e->stream);
+    }
     hipEventRecord(ev[slot], e->stream);
   }
   hipStreamSynchronize(e->stream);
+  if (e->fused)  // replays not polled yet, in launch order
+    for (uint32_t k = launched > kLag ? launched - kLag : 0; k < launched; ++k) fused_poll(k % kLag);
   for (auto& x : ev) hipEventDestroy(x);
   return st;
 }
@@ -1062,13 +1087,14 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(dalloc(&e->d_stg_off, e->nb));
     CREATE_TRY(dalloc(&e->d_stg_cnt, e->nb));
     CREATE_TRY(dalloc(&e->d_ovf, 2));
-    CREATE_TRY(dalloc(&e->d_nacc, 2));
+    CREATE_TRY(dalloc(&e->d_cntb, (uint64_t)agx_engine::kGraphSteps * e->nb));
+    CREATE_TRY(hipHostMalloc((void**)&e->h_cntb, 4ull * agx_engine::kGraphSteps * e->nb * 4, hipHostMallocDefault) ==
+                       hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
     CREATE_TRY(dalloc(&e->d_parv, 2));
     const uint32_t parv[2] = {0u, 1u};
     CREATE_TRY(hipMemcpy(e->d_parv, parv, 8, hipMemcpyHostToDevice) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "upload"));
     CREATE_TRY(hipMemset(e->d_stg_cnt, 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(hipMemset(e->d_ovf, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-    CREATE_TRY(hipMemset(e->d_nacc, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   }
   CREATE_TRY(dalloc(&e->d_skew_list, e->nb));
   CREATE_TRY(dalloc(&e->d_skew_n, 2));
@@ -1123,7 +1149,8 @@ agx_status agx_destroy(agx_engine* e) {
   for (int q = 0; q < 2; ++q) {
     hipFree(e->d_tcnt[q]); hipFree(e->d_toff[q]); hipFree(e->d_blo[q]); hipFree(e->d_blc[q]); hipFree(e->d_emc[q]);
   }
-  hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_nacc); hipFree(e->d_parv);
+  hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_cntb);
+  if (e->h_cntb) hipHostFree(e->h_cntb); hipFree(e->d_parv);
   hipFree(e->d_skew_list); hipFree(e->d_skew_n);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_n); hipFree(e->d_total);

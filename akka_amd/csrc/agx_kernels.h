@@ -586,7 +586,8 @@ struct GatherArgs {
   uint32_t* stg_cnt;
   Msgs inb;                // skewed buckets: gathered inbox copy at [lo, lo+cnt)
   uint32_t* ovf;           // [2] overflow-region cursor per parity (inboxes larger than `region`)
-  uint32_t* nacc;          // [2] inbox total per parity (host quiescence poll; counted as a superstep)
+  uint32_t* cntb;          // [slot][nb] inbox size per bucket, one row per superstep of a replay
+                           // (the host sums them: quiescence, superstep count — no shared counter)
   uint32_t* heap_top;      // CRDT heap tops [2] (null when no CRDT kind is registered)
   uint64_t cap;
   uint32_t tstride;
@@ -608,6 +609,7 @@ struct BucketArgs {
   uint32_t G, ng;          // histogram units: G buckets per column, ng units per arena
   uint32_t nb, kmax;
   uint32_t par;            // fused: parity of this superstep (arenas/tables written; read = par ^ 1)
+  uint32_t slot;           // fused: index of this superstep within its graph replay (row of g.cntb)
   uint32_t* skew_list;     // buckets whose inbox exceeds one LDS tile (appended by the fast launch)
   uint32_t* skew_n;        // their count (reset by the first kernel of the next superstep)
   uint64_t* stats;
@@ -1167,11 +1169,8 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   const uint32_t wpar = kGather ? a.par : 0u, rpar = wpar ^ 1u;  // fused: write parity w, read parity w ^ 1
   uint32_t* const skew_n = a.skew_n + wpar;
   if (kGather && !kSkew && blockIdx.x == 0 && tid == 0) {
-    // close the previous superstep (its kernels are complete): count it if it had mail, and
-    // reset the per-parity cursors that the NEXT superstep (parity rpar) will use
-    const uint32_t prev = g.nacc[rpar];
-    if (prev) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
-    g.nacc[rpar] = 0u;
+    // reset the per-parity cursors that the NEXT superstep (parity rpar) will use (the previous
+    // superstep, which used them, is complete)
     g.ovf[rpar] = 0u;
     a.skew_n[rpar] = 0u;
     if (g.heap_top) g.heap_top[rpar] = 0u;
@@ -1249,10 +1248,11 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
           atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
           s_lo = 0;
           s_hi = 0;
+          g.cntb[(size_t)a.slot * a.nb + b] = 0u;
         } else {
           s_lo = (uint32_t)lo;
           s_hi = (uint32_t)lo + cnt;
-          if (cnt) atomicAdd(&g.nacc[wpar], cnt);  // fire-and-forget: nobody waits on it
+          g.cntb[(size_t)a.slot * a.nb + b] = cnt;
         }
       }
     }
