@@ -127,6 +127,7 @@ struct agx_engine {
   uint32_t* d_col = nullptr;
   // CRDT state gossips (agx_crdt.h): snapshot heap, 2 x cap rows of pw u32
   uint32_t pw = 0, gossip_f = 0;
+  uint64_t heap_rows = 0;  // per parity: one kBucket-row region per bucket, then an overflow area of `cap` rows
   uint64_t gossip_seed = 0;
   uint32_t *d_heap = nullptr, *d_heap_top = nullptr, *d_step = nullptr;
   uint32_t *d_rx = nullptr, *d_s2rows = nullptr;  // multi-rank: received rows / rows packed for sending
@@ -286,7 +287,7 @@ DevParams make_params(agx_engine* e) {
   P.rx = e->d_rx;
   P.heap_top = e->d_heap_top;
   P.step = e->d_step;
-  P.heap_rows = (uint32_t)e->cap;
+  P.heap_rows = (uint32_t)e->heap_rows;
   P.pw = e->pw;
   P.gossip_f = e->gossip_f;
   P.gossip_seed = e->gossip_seed;
@@ -829,7 +830,7 @@ agx_status fix_rx(agx_engine* e, const Plan& p) {
   const uint32_t lo = (uint32_t)p.n_bl, hi = (uint32_t)(p.n_bl + p.n_recv);
   const uint32_t slo = (uint32_t)p.recv_off[e->rank], shi = (uint32_t)(p.recv_off[e->rank] + p.recv_cnt[e->rank]);
   hipLaunchKernelGGL(k_fix_rx, dim3(grid_for(p.n_recv / kThreads + 1, 2048)), dim3(kThreads), 0, e->stream, e->A.m(),
-                     lo, hi, slo, shi, (uint32_t)e->cap);
+                     lo, hi, slo, shi, (uint32_t)e->heap_rows);
   HIP_TRY(hipGetLastError());
   return AGX_OK;
 }
@@ -904,13 +905,15 @@ agx_status enable_crdt(agx_engine* e, uint32_t kind) {
   const uint32_t pw = 2 * words;
   if (pw <= e->pw) return AGX_OK;
   if (e->started) return set_err(AGX_ESTATE, "register CRDT kinds before the first agx_run");
-  if (2 * e->cap >= (1ull << 30)) return set_err(AGX_EINVAL, "CRDT kinds need msg_capacity < 2^29");
+  const uint64_t rows = (uint64_t)e->nb * kBucket + e->cap;
+  if (rows + e->cap >= (1ull << 30)) return set_err(AGX_EINVAL, "CRDT kinds need msg_capacity < 2^29 - n_actors");
   hipFree(e->d_heap);
   hipFree(e->d_rx);
   hipFree(e->d_s2rows);
   e->d_heap = e->d_rx = e->d_s2rows = nullptr;
   e->pw = 0;
-  AGX_TRY(dalloc(&e->d_heap, 2 * e->cap * pw));
+  AGX_TRY(dalloc(&e->d_heap, 2 * rows * pw));
+  e->heap_rows = rows;
   if (e->R > 1) {
     AGX_TRY(dalloc(&e->d_rx, e->cap * pw));
     AGX_TRY(dalloc(&e->d_s2rows, e->cap_emit * pw));

@@ -634,6 +634,7 @@ struct BucketLds {
   uint32_t* nh;    // [kRadix]
   uint32_t* scratch;
   unsigned long long* stat;
+  uint32_t* rowtop;  // snapshot rows taken from this bucket's heap region (CRDT kinds)
 };
 
 // After the in-bucket sort: classification, queued copy, behaviour apply, emission.
@@ -735,6 +736,14 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   uint64_t* w1s = L.U + kBucket;
   CrdtHeap H{};
   if (kWide) H = crdt_heap(P);
+  // Snapshot rows of bucket b (one lane allocates for its wave / block): the bucket's own heap
+  // region [b*kBucket, (b+1)*kBucket) through an LDS cursor, then the overflow area after all
+  // regions through the shared cursor — no contended atomic for the common case.
+  auto alloc_rows = [&](uint32_t n) -> uint32_t {
+    const uint32_t r = atomicAdd(L.rowtop, n);
+    if (r + n <= (uint32_t)kBucket) return b * (uint32_t)kBucket + r;
+    return a.nb * (uint32_t)kBucket + atomicAdd(H.top, n);
+  };
 
   AGX_STAMP(a, 3);
   // ---- classification per actor (blocked): drained / queued (backlog) / dead letters
@@ -790,7 +799,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         if (m) {
           const uint32_t lane = lane_id(), leader = (uint32_t)__builtin_ctzll(m);
           uint32_t base = 0;
-          if (lane == leader) base = atomicAdd(H.top, (uint32_t)__popcll(m));
+          if (lane == leader) base = alloc_rows((uint32_t)__popcll(m));
           base = __shfl(base, (int)leader, kWave);
           if (need) {
             const uint32_t h = base + (uint32_t)__popcll(m & lanemask_lt());
@@ -989,7 +998,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       uint32_t rtot;
       const uint32_t rex = block_excl_sum<kBThreads>(nrows_t, L.scratch, &rtot);
       if (tid == 0) {
-        const uint32_t base = rtot ? atomicAdd(H.top, rtot) : 0u;
+        const uint32_t base = rtot ? alloc_rows(rtot) : 0u;
         if (base + rtot > H.rows) atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
         L.scratch[kBWaves] = base;
       }
@@ -1156,9 +1165,9 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   __shared__ uint8_t s_kind[kBucket];
   __shared__ uint32_t s_nh[kRadix];
   __shared__ uint32_t scratch[2 * (kBWaves + 1)];
-  __shared__ uint32_t s_lo, s_hi, s_g[6];
+  __shared__ uint32_t s_lo, s_hi, s_g[6], s_rowtop;
   __shared__ unsigned long long s_stat[5];
-  const BucketLds L{s_key, s_src, s_pay, U, s_seg, s_ecnt, s_alive, s_kind, s_nh, scratch, s_stat};
+  const BucketLds L{s_key, s_src, s_pay, U, s_seg, s_ecnt, s_alive, s_kind, s_nh, scratch, s_stat, &s_rowtop};
   uint16_t* whist = reinterpret_cast<uint16_t*>(U);  // [kBWaves][kBucket]
 
   const DevParams& P = a.P;
@@ -1187,6 +1196,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     const uint32_t a0 = b << kBucketBits;
     const uint32_t na = min((uint32_t)kBucket, P.n_local - a0);
     if (tid < 5) s_stat[tid] = 0;
+    if (tid == 0) s_rowtop = 0;
     for (uint32_t d = tid; d < kRadix; d += kBThreads) s_nh[d] = 0;
     uint32_t* my_tc = nullptr;  // (fused) this thread's table entry, zeroed once the bucket is processed
     uint32_t alive4 = 0;        // alive flags of actors 4*tid..4*tid+3, loaded first (a0 is a multiple of kBucket)
