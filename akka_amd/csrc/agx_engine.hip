@@ -102,7 +102,7 @@ struct agx_engine {
   agx_cfg cfg{};
   hipStream_t stream = nullptr;
   uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0;
-  uint32_t max_supers = 1, dstride = 4;  // dense passes: super-tiles, table row stride
+  uint32_t max_supers = 1, dstride = 4, dsuper = kSuper;  // dense passes: super-tiles, table row stride, tile size
   uint32_t T = 1, C = 0, W = 1, kmax = 1, R = 1, rank = 0, num_shards = 1000, key_bits = 1;
 
   // sharding tables (R > 1)
@@ -132,7 +132,7 @@ struct agx_engine {
   uint32_t *d_heap = nullptr, *d_heap_top = nullptr, *d_step = nullptr;
   uint32_t *d_rx = nullptr, *d_s2rows = nullptr;  // multi-rank: received rows / rows packed for sending
 
-  DevMsgs A, B, scr, bl, em, stg, s1, s2;
+  DevMsgs A, B, scr, bl, em, stg, s2;
   uint64_t stg_cap = 0;
   uint32_t nb = 1, nchunks = 3;                // buckets; chunks = 2 nb + kStagedChunks
   uint32_t G = 1, ng = 1, nunits = 3, cstride = 4;  // first-pass histogram units (G buckets each)
@@ -319,6 +319,7 @@ agx_status launch_dense_pass(agx_engine* e, const DevMsgs& in, const DevMsgs& ou
   sa.tot = e->d_tot;
   sa.bstart = e->d_bstart;
   sa.stride = e->dstride;
+  sa.super = e->dsuper;
   sa.shift = shift;
   sa.bits = bits;
   const uint32_t g = grid_for(e->max_supers, 4096);
@@ -446,6 +447,14 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     g.tstride = e->tstride;
     g.region = e->region;
   }
+  if (e->R > 1) {  // tells leave grouped by owner rank (phase 1 packs them for the exchange)
+    ba.nx_shift = kOwnerShift;
+    ba.nx_bits = std::max<uint32_t>(1, ceil_log2(e->R));
+    ba.g.eg[0] = e->eg0.m();
+    ba.g.tcnt[0] = e->d_tcnt[0];
+    ba.g.toff[0] = e->d_toff[0];
+    ba.g.tstride = e->tstride;
+  }
   ba.dbg = e->d_dbg;
   {
     const dim3 g(grid_for(e->nb, e->apply_grid)), blk(kBThreads);
@@ -458,6 +467,11 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
         hipLaunchKernelGGL((k_bucket_apply<W, M, true, false>), g, blk, 0, e->stream, ba); }     \
       { Scope s(e, K_SKEW);                                                                      \
         hipLaunchKernelGGL((k_bucket_apply<W, M, true, true>), gs, blk, 0, e->stream, ba); }     \
+    } else if (e->R > 1) {                                                                       \
+      { Scope s(e, K_APPLY);                                                                     \
+        hipLaunchKernelGGL((k_bucket_apply<W, M, false, false, true>), g, blk, 0, e->stream, ba); } \
+      { Scope s(e, K_SKEW);                                                                      \
+        hipLaunchKernelGGL((k_bucket_apply<W, M, false, true, true>), gs, blk, 0, e->stream, ba); } \
     } else {                                                                                     \
       { Scope s(e, K_APPLY);                                                                     \
         hipLaunchKernelGGL((k_bucket_apply<W, M, false, false>), g, blk, 0, e->stream, ba); }    \
@@ -563,16 +577,21 @@ agx_status prepare_run(agx_engine* e) {
 }
 
 // ----------------------------------------------------------- multi-rank step
-// phase 1: chunks -> [backlog at the front of A, tells dense in s1]; stable
-// partition of the tells by owner rank (s1 -> s2); pack [send counts..., n_backlog, n_staged].
+// phase 1: backlog chunks -> front of A; the apply's owner-grouped tells -> s2, owner-major
+// (the stable owner partition of the tells in chunk order); count vector
+// [send counts..., n_backlog, n_staged] for the all-gather.
 agx_status phase1(agx_engine* e) {
   McompactArgs m{};
   m.ch = make_chunks(e);
+  m.eg = e->eg0.c();
+  m.tcnt = e->d_tcnt[0];
+  m.toff = e->d_toff[0];
   m.out0 = e->A.m();
-  m.out1 = e->s1.m();
+  m.out1 = e->s2.m();
   m.off0 = e->d_moff0;
   m.off1 = e->d_moff1;
   m.d_total = e->d_total;
+  m.cvec = e->d_cvec;
   m.alive = e->d_alive;
   m.stopq = e->d_stopq;
   m.nstop = e->d_nstop;
@@ -582,19 +601,19 @@ agx_status phase1(agx_engine* e) {
   m.skew_n = e->d_skew_n;
   m.cap0 = e->cap;
   m.cap1 = e->cap_emit;
+  m.R = e->R;
+  m.tstride = e->tstride;
+  m.n_staged = e->n_staged_dev;
   {
     Scope s(e, K_MCOMPACT);
     hipLaunchKernelGGL(k_mcompact_scan, dim3(1), dim3(kScanThreads), 0, e->stream, m);
-    hipLaunchKernelGGL(k_mcompact_copy, dim3(grid_for(2 * e->nb, 4096)), dim3(kThreads), 0, e->stream, m);
+    hipLaunchKernelGGL(k_mcompact_copy, dim3(grid_for(e->nb, 4096)), dim3(kThreads), 0, e->stream, m);
   }
-  AGX_TRY(launch_dense_pass(e, e->s1, e->s2, e->d_total + 1, kOwnerShift, std::max<uint32_t>(1, ceil_log2(e->R))));
   if (e->pw) {
     Scope s(e, K_MCOMPACT);
     hipLaunchKernelGGL(k_pack_rows, dim3(grid_for(e->cap_emit / kThreads + 1, 2048)), dim3(kThreads), 0, e->stream,
                        e->s2.c(), e->d_total, make_params(e), e->d_s2rows);
   }
-  hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(64), 0, e->stream, e->d_tot, e->d_total, e->d_cvec, e->R,
-                     e->n_staged_dev);
   HIP_TRY(hipGetLastError());
   return AGX_OK;
 }
@@ -607,9 +626,7 @@ agx_status phase2(agx_engine* e, uint64_t n_sorted, uint64_t staged_at) {
     HIP_TRY(hipMemcpyAsync(e->A.pay + staged_at, e->stg.pay, e->n_staged_dev * 4ull, hipMemcpyDeviceToDevice, e->stream));
     e->n_staged_dev = 0;
   }
-  e->h_pin[0] = (uint32_t)n_sorted;
-  HIP_TRY(hipMemcpyAsync(e->d_n, e->h_pin, 4, hipMemcpyHostToDevice, e->stream));
-  // the pinned word is reused next step only after the host sync in the exchange
+  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(64), 0, e->stream, e->d_n, (uint32_t)n_sorted);  // no DMA round trip
   DevMsgs* sorted = nullptr;
   AGX_TRY(launch_bucket_sort(e, false, &sorted));
   AGX_TRY(launch_apply(e, *sorted));
@@ -999,7 +1016,12 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   if (e->cap >= (1ull << 32) - kTile) { delete e; return set_err(AGX_EINVAL, "msg_capacity too large"); }
   e->cap_emit = e->cap * e->kmax;  // bucket b's tells live at [lo*kmax, (lo+cnt)*kmax)
   if (e->cap_emit >= (1ull << 32)) { delete e; return set_err(AGX_EINVAL, "msg_capacity * max_emit must be < 2^32"); }
-  e->max_supers = (uint32_t)((std::max(e->cap, e->cap_emit) + kSuper - 1) / kSuper + 1);
+  {  // super-tile size of the dense sort passes: about 1024+ workgroups when the buffers allow it
+    const uint64_t mx = std::max(e->cap, e->cap_emit);
+    const uint64_t sub = std::min<uint64_t>(kSub, std::max<uint64_t>(1, mx / ((uint64_t)kTile * 1024)));
+    e->dsuper = (uint32_t)(kTile * sub);
+  }
+  e->max_supers = (uint32_t)((std::max(e->cap, e->cap_emit) + e->dsuper - 1) / e->dsuper + 1);
   e->dstride = (e->max_supers + 3) & ~3u;
   // buckets of 2^kBucketBits actors; LSD passes over key bits [kBucketBits, key_bits), <= kRadixBits each
   e->nb = (uint32_t)((nl + kBucket - 1) / kBucket);
@@ -1066,11 +1088,15 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(alloc_msgs(e->scr, e->acap));
   CREATE_TRY(alloc_msgs(e->bl, e->acap));
   CREATE_TRY(alloc_msgs(e->em, e->acap * e->kmax));
-  if (e->R > 1) {
-    CREATE_TRY(alloc_msgs(e->s1, e->cap_emit));
+  if (e->R > 1) {  // tells grouped by owner per bucket (eg0 + [R][tstride] tables), send buffer s2
+    const uint64_t tsz = (uint64_t)e->R * e->tstride;
+    CREATE_TRY(alloc_msgs(e->eg0, e->cap_emit));
     CREATE_TRY(alloc_msgs(e->s2, e->cap_emit));
+    CREATE_TRY(dalloc(&e->d_tcnt[0], tsz));
+    CREATE_TRY(dalloc(&e->d_toff[0], tsz));
+    CREATE_TRY(hipMemset(e->d_tcnt[0], 0, tsz * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(dalloc(&e->d_moff0, e->nb));
-    CREATE_TRY(dalloc(&e->d_moff1, e->nb));
+    CREATE_TRY(dalloc(&e->d_moff1, tsz));
   }
   if (e->fused) {
     const uint64_t tsz = (uint64_t)kRadix * e->tstride;
@@ -1148,7 +1174,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_kind); hipFree(e->d_alive); hipFree(e->d_stopq); hipFree(e->d_nstop); hipFree(e->d_state); hipFree(e->d_gid); hipFree(e->d_route);
   hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_row); hipFree(e->d_col);
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
-  free_msgs(e->s1); free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1);
+  free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1);
   for (int q = 0; q < 2; ++q) {
     hipFree(e->d_tcnt[q]); hipFree(e->d_toff[q]); hipFree(e->d_blo[q]); hipFree(e->d_blc[q]); hipFree(e->d_emc[q]);
   }

@@ -404,6 +404,7 @@ struct SortArgs {
   uint32_t* bstart;  // out (block 0 of the downsweep): exclusive scan of digit totals
   uint32_t stride;
   uint32_t shift, bits;
+  uint32_t super;  // envelopes per super-tile (kTile * 1..kSub): small inputs get more workgroups
 };
 
 // Digit counts of four keys into a wave's LDS histogram.  Sorted-by-lower-bits input
@@ -429,13 +430,13 @@ __device__ __forceinline__ void count4(uint32_t* h, const uint4& v, uint32_t shi
 
 __global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
   __shared__ uint32_t h[kWaves][kRadix];
-  const uint32_t n = *a.d_n, nt = div_up(n, kSuper);
+  const uint32_t n = *a.d_n, nt = div_up(n, a.super);
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t mask = (1u << a.bits) - 1u, nd = 1u << a.bits;
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     for (int i = tid; i < kWaves * kRadix; i += kThreads) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t b0 = t * kSuper, b1 = min(n, b0 + kSuper);
+    const uint32_t b0 = t * a.super, b1 = min(n, b0 + a.super);
     const uint32_t nfull = (b1 - b0) / (4 * kThreads);  // full rounds of one uint4 per thread
     const uint4* k4 = reinterpret_cast<const uint4*>(a.in.key + b0);
     uint32_t j = 0;
@@ -465,7 +466,7 @@ __global__ void __launch_bounds__(kThreads) k_sort_rowscan(SortArgs a) {
   __shared__ uint32_t scratch[kWaves + 1];
   const uint32_t d = blockIdx.x;
   if (d >= (1u << a.bits)) return;
-  const uint32_t t = scan_row(a.hist + (size_t)d * a.stride, div_up(*a.d_n, kSuper), scratch);
+  const uint32_t t = scan_row(a.hist + (size_t)d * a.stride, div_up(*a.d_n, a.super), scratch);
   if (threadIdx.x == 0) a.tot[d] = t;
 }
 
@@ -476,7 +477,7 @@ __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) {
   __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
   const SplitLds S{&whist[0][0], s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
   const int tid = threadIdx.x;
-  const uint32_t n = *a.d_n, nt = div_up(n, kSuper);
+  const uint32_t n = *a.d_n, nt = div_up(n, a.super);
   const uint32_t nd = 1u << a.bits;
   const uint32_t total = digit_bases(a.tot, nd, s_dbase, scratch);
   if (blockIdx.x == 0) {
@@ -486,7 +487,7 @@ __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) {
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     for (uint32_t d = tid; d < nd; d += kThreads) s_base[d] = s_dbase[d] + a.hist[(size_t)d * a.stride + t];
     __syncthreads();
-    const uint32_t b0 = t * kSuper, b1 = min(n, b0 + kSuper);
+    const uint32_t b0 = t * a.super, b1 = min(n, b0 + a.super);
     for (uint32_t base = b0; base < b1; base += kTile)
       split_tile<kThreads>(a.in, base, min((uint32_t)kTile, b1 - base), a.out, a.shift, a.bits, S);
   }
@@ -515,7 +516,7 @@ struct Emitter {
       out.src[pos] = self;
       out.pay[pos] = pay;
       ++pos;
-      lds_hist_inc(nh, ((key & kLocalMask) >> nh_shift) & nh_mask);
+      lds_hist_inc(nh, (key >> nh_shift) & nh_mask);
     }
   }
   // CRDT state gossip to a known actor: the sender field carries the wide tag, payload = row handle
@@ -528,7 +529,7 @@ struct Emitter {
       out.src[pos] = self | AGX_WIDE_BIT;
       out.pay[pos] = h;
       ++pos;
-      lds_hist_inc(nh, ((key & kLocalMask) >> nh_shift) & nh_mask);
+      lds_hist_inc(nh, (key >> nh_shift) & nh_mask);
     }
   }
   __device__ __forceinline__ void count(uint32_t k) {
@@ -565,7 +566,7 @@ struct EmitterLds {
     src[slot] = self;
     pay[slot] = p;
     ++slot;
-    lds_hist_inc(nh, ((k & kLocalMask) >> nh_shift) & nh_mask);
+    lds_hist_inc(nh, (k >> nh_shift) & nh_mask);
   }
 };
 
@@ -639,9 +640,11 @@ struct BucketLds {
 
 // After the in-bucket sort: classification, queued copy, behaviour apply, emission.
 // kLds: sorted items are in LDS (fast path) or in the global scratch copy.
-// Tells of one bucket in sender order -> grouped by destination bucket in eg[w] at
+// Tells of one bucket in sender order -> grouped by destination digit in eg[w] at
 // [embase, embase+emtot), plus this chunk's column of the parity-w tables.  Every
-// destination's run is contiguous and in sender order (stable multisplit).
+// destination's run is contiguous and in sender order (stable multisplit).  The digit is
+// (key >> nx_shift) & (2^nx_bits - 1): the destination bucket (fused, single rank) or the
+// owner rank (multi-rank: the chunk's tells leave grouped by the GPU that owns them).
 template <bool kFromLds>
 __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t w,
                                             uint64_t embase, uint32_t emtot, const Msgs& src) {
@@ -679,7 +682,7 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
     for (int r = 0; r < kBIpt; ++r) {
       const uint32_t i = wv * (kBIpt * kWave) + r * kWave + lane;
       k[r] = i < emtot ? ukey[i] : 0u;
-      d[r] = ((k[r] & kLocalMask) >> kBucketBits) & (nd - 1);
+      d[r] = (k[r] >> a.nx_shift) & (nd - 1);
       rk[r] = wave_rank(i < emtot, d[r], a.nx_bits, whist + wv * kRadix, ltm);
     }
     __syncthreads();
@@ -715,13 +718,13 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
     const SplitLds S{whist, base, ldig, gadj, L.scratch, U32, U32 + kTile, U32 + 2 * kTile};
     const CMsgs in{src.key, src.src, src.pay};
     for (uint32_t sub = 0; sub < emtot; sub += kTile)
-      split_tile<kBThreads>(in, (uint32_t)embase + sub, min((uint32_t)kTile, emtot - sub), g.eg[w], kBucketBits,
+      split_tile<kBThreads>(in, (uint32_t)embase + sub, min((uint32_t)kTile, emtot - sub), g.eg[w], a.nx_shift,
                             a.nx_bits, S);
   }
-  if (tid == 0) g.emc[w][b] = emtot;
+  if (tid == 0 && g.emc[w]) g.emc[w][b] = emtot;
 }
 
-template <bool kLds, bool kWide, uint32_t KM, bool kGather>
+template <bool kLds, bool kWide, uint32_t KM, bool kGather, bool kOwner>
 __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t lo,
                                               uint32_t cnt, uint32_t a0, uint32_t na, uint32_t w, uint32_t ndead0) {
   const DevParams& P = a.P;
@@ -816,7 +819,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         blw.pay[o] = pv;
       }
     }
-    if (!kGather && tid == 0) {  // all queued mail is in this bucket: one bin of the next first-pass histogram
+    if (!kGather && !kOwner && tid == 0) {  // all queued mail is in this bucket: one bin of the next first-pass histogram
       const uint32_t d = ((b << kBucketBits) >> a.nx_shift) & nhmask;
       atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + b / a.G], bltot);
     }
@@ -903,7 +906,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     }
     __syncthreads();
     AGX_STAMP(a, 6);
-    if constexpr (kGather) {
+    if constexpr (kGather || kOwner) {
       // compact the staged tells in sender order into U (free: state was written back), then
       // group them by destination straight into this superstep's tell arena
       uint32_t* ukey = reinterpret_cast<uint32_t*>(L.U);
@@ -1062,7 +1065,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       nall += em.n_all;
       ndead += em.n_all - em.n_valid;
     }
-    if constexpr (kGather) {
+    if constexpr (kGather || kOwner) {
       __syncthreads();  // phase B's tells are in the em scratch arena (sender order)
       group_tells<false>(a, L, b, w, embase, emtot, a.em);
     }
@@ -1074,7 +1077,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   __syncthreads();
   AGX_STAMP(a, 7);
   // next first-pass histogram column of this bucket's tell chunk (zeroed by the chunk downsweep)
-  if (!kGather)
+  if (!kGather && !kOwner)
     for (uint32_t d = tid; d < (1u << a.nx_bits); d += kBThreads)
       if (L.nh[d]) atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + a.ng + b / a.G], L.nh[d]);
   // block stats -> global
@@ -1151,7 +1154,9 @@ struct GatherView {
 // inboxes are appended to the skew list.  kSkew = true (launched right after): the listed
 // buckets, general path — separate instantiation, so its register pressure never reaches
 // the fast path.
-template <bool kWide, uint32_t KM, bool kGather, bool kSkew>
+// kOwner (multi-rank): tells leave grouped by owner rank into g.eg[0] + g.tcnt/toff[0]
+// (digit = key >> kOwnerShift) instead of the chunk arena + next-pass histogram.
+template <bool kWide, uint32_t KM, bool kGather, bool kSkew, bool kOwner = false>
 __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   // key/src/pay carved from one array: group_tells reuses key+src as a 16 KB histogram
   __shared__ __attribute__((aligned(16))) uint32_t s_ksp[3 * kBucket];
@@ -1390,7 +1395,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         __syncthreads();
       }
       AGX_STAMP(a, 2);
-      bucket_finish<true, kWide, KM, kGather>(a, L, b, lo, cnt, a0, na, wpar, 0u);
+      bucket_finish<true, kWide, KM, kGather, kOwner>(a, L, b, lo, cnt, a0, na, wpar, 0u);
     } else {
       // ---- general path (skewed bucket, > kBucket messages): admission first, then a stable
       // counting sort of the ADMITTED messages only into the global scratch copy.  Per actor
@@ -1510,7 +1515,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       }
       // the scratch copy holds the admitted messages in actor order; dead letters counted here
       __threadfence_block();
-      bucket_finish<false, kWide, KM, kGather>(a, L, b, lo, cnt2, a0, na, wpar, ndead0);
+      bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, cnt2, a0, na, wpar, ndead0);
     }
   }
 }
@@ -1569,14 +1574,21 @@ __global__ void __launch_bounds__(kThreads) k_chunk_hist(const uint32_t* key, ui
 }
 
 // =========================================================================
-// Multi-GPU helpers: chunk list -> [backlog -> sort input front, tells -> send buffer]
+// Multi-GPU helpers.  The apply left, per bucket b: its backlog chunk (bl arena) and its
+// tells grouped by owner rank q in eg at toff[q][b] (tcnt[q][b] of them, sender order).
+// Send buffer s2 = owner-major: for q, for b in order, bucket b's run for q — the stable
+// owner partition of the tells in chunk order.  Backlog chunks go to the front of A.
 // =========================================================================
 struct McompactArgs {
   Chunks ch;
+  CMsgs eg;           // owner-grouped tells
+  uint32_t* tcnt;     // [R][tstride] run lengths (zeroed by the copy)
+  const uint32_t* toff;
   Msgs out0, out1;
-  uint32_t* off0;   // [nb] destination offsets of backlog chunks
-  uint32_t* off1;   // [nb] destination offsets of tell chunks
+  uint32_t* off0;     // [nb] destination offsets of backlog chunks
+  uint32_t* off1;     // [R][tstride] destination offsets of the owner runs in s2
   uint32_t* d_total;  // [0] backlog total, [1] tell total
+  uint64_t* cvec;     // [R send counts..., backlog, staged]
   uint8_t* alive;
   const uint32_t* stopq;
   uint32_t* nstop;
@@ -1585,52 +1597,104 @@ struct McompactArgs {
   uint32_t* heap_top;
   uint32_t* skew_n;
   uint64_t cap0, cap1;
+  uint32_t R, tstride, n_staged;
 };
+
+// Exclusive scan, in one block, of a table of `rows` rows x `len` entries (row stride
+// `stride`) flattened row-major; each thread owns one contiguous range of the flattened
+// index (all of its loads in flight before the block scan).  Writes the prefixes to `out`
+// (same layout) and row r's first prefix to rbase[r] (LDS, rows + 1 entries).  Returns the total.
+__device__ __forceinline__ uint64_t block_scan_table(const uint32_t* in, uint32_t* out, uint32_t rows, uint32_t len,
+                                                     uint32_t stride, uint32_t* scratch, uint32_t* rbase) {
+  const uint32_t tid = threadIdx.x, L = rows * len, per = (L + kScanThreads - 1) / kScanThreads;
+  const uint32_t i0 = min(L, tid * per), i1 = min(L, i0 + per);
+  uint32_t sum = 0;
+  {
+    uint32_t r = len ? i0 / len : 0u, c = i0 - r * len;
+    for (uint32_t i = i0; i < i1; ++i) {
+      sum += in[(size_t)r * stride + c];
+      if (++c == len) { c = 0; ++r; }
+    }
+  }
+  uint32_t t;
+  uint32_t run = block_excl_sum<kScanThreads>(sum, scratch, &t);
+  {
+    uint32_t r = len ? i0 / len : 0u, c = i0 - r * len;
+    for (uint32_t i = i0; i < i1; ++i) {
+      const size_t x = (size_t)r * stride + c;
+      const uint32_t v = in[x];
+      out[x] = run;
+      if (c == 0 && rbase) rbase[r] = run;
+      run += v;
+      if (++c == len) { c = 0; ++r; }
+    }
+  }
+  if (tid == 0 && rbase) rbase[rows] = t;
+  __syncthreads();
+  return t;
+}
 
 __global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactArgs a) {
   __shared__ uint32_t scratch[kScanThreads / kWave + 1];
-  __shared__ uint64_t s_run[2];
+  __shared__ uint32_t s_obase[AGX_MAX_RANKS + 1];
   begin_step(a.step, a.heap_top);
   commit_stops(a.alive, a.stopq, a.nstop);
-  const int tid = threadIdx.x;
+  if (threadIdx.x == 0) *a.skew_n = 0u;
+  const uint64_t nbl = block_scan_table(a.ch.cnt, a.off0, 1, a.ch.nb, a.ch.nb, scratch, nullptr);
+  const uint64_t ntl = block_scan_table(a.tcnt, a.off1, a.R, a.ch.nb, a.tstride, scratch, s_obase);
+  const uint32_t tid = threadIdx.x;
+  const bool over = nbl > a.cap0 || ntl > a.cap1;
   if (tid == 0) {
-    s_run[0] = s_run[1] = 0;
-    *a.skew_n = 0u;
-  }
-  __syncthreads();
-  for (int sdx = 0; sdx < 2; ++sdx) {
-    uint32_t* off = sdx == 0 ? a.off0 : a.off1;
-    for (uint32_t base = 0; base < a.ch.nb; base += kScanThreads) {
-      const uint32_t i = base + tid;
-      uint32_t v = i < a.ch.nb ? a.ch.cnt[sdx * a.ch.nb + i] : 0u, t;
-      const uint32_t ex = block_excl_sum<kScanThreads>(v, scratch, &t);
-      if (i < a.ch.nb) off[i] = (uint32_t)(s_run[sdx] + ex);
-      __syncthreads();
-      if (tid == 0) s_run[sdx] += t;
-      __syncthreads();
-    }
-  }
-  if (tid == 0) {
-    const bool over = s_run[0] > a.cap0 || s_run[1] > a.cap1;
     if (over) atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
-    a.d_total[0] = over ? 0u : (uint32_t)s_run[0];
-    a.d_total[1] = over ? 0u : (uint32_t)s_run[1];
+    a.d_total[0] = over ? 0u : (uint32_t)nbl;
+    a.d_total[1] = over ? 0u : (uint32_t)ntl;
+    a.cvec[a.R] = over ? 0u : nbl;  // backlog kept locally
+    a.cvec[a.R + 1] = a.n_staged;
+  }
+  if (tid < a.R) a.cvec[tid] = over ? 0u : (uint64_t)(s_obase[tid + 1] - s_obase[tid]);
+}
+
+// block-wide copy of n envelopes, four per thread in flight
+__device__ __forceinline__ void copy_run(const CMsgs& s, uint32_t so, const Msgs& d, uint32_t dof, uint32_t n) {
+  constexpr uint32_t U = 4;
+  for (uint32_t i0 = 0; i0 < n; i0 += U * kThreads) {
+    uint32_t k[U], sv[U], pv[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kThreads + threadIdx.x;
+      if (i < n) {
+        k[u] = s.key[so + i];
+        sv[u] = s.src[so + i];
+        pv[u] = s.pay[so + i];
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kThreads + threadIdx.x;
+      if (i < n) {
+        d.key[dof + i] = k[u];
+        d.src[dof + i] = sv[u];
+        d.pay[dof + i] = pv[u];
+      }
+    }
   }
 }
 
 __global__ void __launch_bounds__(kThreads) k_mcompact_copy(McompactArgs a) {
-  if (a.d_total[0] == 0 && a.d_total[1] == 0) return;
-  for (uint32_t c = blockIdx.x; c < 2 * a.ch.nb; c += gridDim.x) {
+  const bool go = a.d_total[0] != 0 || a.d_total[1] != 0;
+  for (uint32_t c = blockIdx.x; c < a.ch.nb; c += gridDim.x) {
     const uint32_t n = a.ch.cnt[c];
-    if (!n) continue;
-    const CMsgs& s = a.ch.arena(c);
-    const uint32_t so = a.ch.off[c];
-    const Msgs& d = c < a.ch.nb ? a.out0 : a.out1;
-    const uint32_t dof = c < a.ch.nb ? a.off0[c] : a.off1[c - a.ch.nb];
-    for (uint32_t i = threadIdx.x; i < n; i += kThreads) {
-      d.key[dof + i] = s.key[so + i];
-      d.src[dof + i] = s.src[so + i];
-      d.pay[dof + i] = s.pay[so + i];
+    if (go && n) {  // backlog chunk c -> front of the sort input
+      copy_run(a.ch.bl, a.ch.off[c], a.out0, a.off0[c], n);
+    }
+    for (uint32_t q = 0; q < a.R; ++q) {  // bucket c's run for owner q -> s2
+      const size_t x = (size_t)q * a.tstride + c;
+      const uint32_t m = a.tcnt[x];
+      if (!m) continue;
+      const uint32_t so = a.toff[x], dof = a.off1[x];
+      if (go) copy_run(a.eg, so, a.out1, dof, m);
+      __syncthreads();  // every thread has read the count before it is cleared
+      if (threadIdx.x == 0) a.tcnt[x] = 0u;  // the apply writes non-zero entries only
     }
   }
 }
@@ -1669,6 +1733,10 @@ __global__ void __launch_bounds__(kThreads) k_gen_rmat(const uint64_t* lrow, con
   }
 }
 
+__global__ void k_set_u32(uint32_t* p, uint32_t v) {
+  if (threadIdx.x == 0) *p = v;
+}
+
 // fused mode: messages in flight after the last superstep = its backlog + tells + staged
 __global__ void __launch_bounds__(kScanThreads) k_inflight_fused(const uint32_t* blc0, const uint32_t* blc1,
                                                                  const uint32_t* emc0, const uint32_t* emc1,
@@ -1685,17 +1753,6 @@ __global__ void __launch_bounds__(kScanThreads) k_inflight_fused(const uint32_t*
   atomicAdd(&s, v);
   __syncthreads();
   if (threadIdx.x == 0) *out = s;
-}
-
-// partition helper: per-owner send counts (digit totals of the owner pass) -> u64 vector
-__global__ void k_pack_counts(const uint32_t* tot, const uint32_t* d_total, uint64_t* vec, uint32_t R,
-                              uint32_t n_staged) {
-  uint32_t i = threadIdx.x;
-  if (i < R) vec[i] = d_total[1] ? tot[i] : 0u;
-  if (i == 0) {
-    vec[R] = d_total[0];  // backlog kept locally
-    vec[R + 1] = n_staged;
-  }
 }
 
 }  // namespace agx
