@@ -12,6 +12,8 @@ import pathlib
 import threading
 
 LIB_PATH = pathlib.Path(__file__).resolve().parent / "lib" / "libakka_gpu.so"
+if os.environ.get("AKKA_AMD_LIB"):  # A/B diagnostics: an alternative in-tree build
+    LIB_PATH = pathlib.Path(os.environ["AKKA_AMD_LIB"]).resolve()
 
 _lib = None
 _lock = threading.Lock()

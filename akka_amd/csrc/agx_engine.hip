@@ -150,6 +150,7 @@ struct agx_engine {
   bool fused = false;
   DevMsgs bl2, eg0, eg1;
   uint32_t *d_tcnt[2] = {nullptr, nullptr}, *d_toff[2] = {nullptr, nullptr};
+  uint32_t *d_blpre = nullptr, *d_ninbox = nullptr;  // multi-pass: backlog prefix, inbox total
   uint32_t *d_blo[2] = {nullptr, nullptr}, *d_blc[2] = {nullptr, nullptr}, *d_emc[2] = {nullptr, nullptr};
   uint32_t *d_stg_off = nullptr, *d_stg_cnt = nullptr, *d_ovf = nullptr, *d_cntb = nullptr, *d_parv = nullptr;
   uint32_t* h_cntb = nullptr;  // pinned [kLag][kGraphSteps][nb]: per-superstep inbox sizes of the replays in flight
@@ -358,7 +359,12 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     ca.alive = e->d_alive;
     ca.stopq = e->d_stopq;
     ca.nstop = e->d_nstop;
-    ca.step = e->pw ? e->d_step : nullptr;
+    ca.step = e->d_step;  // superstep counter: CRDT heap parity and the backlog arena parity
+    ca.blpre = e->d_blpre;
+    ca.bl_stot = e->d_blpre + e->nb;
+    ca.bl_sbase = e->d_blpre + e->nb + kMaxBlSlices;
+    ca.d_ninbox = e->d_ninbox;
+    ca.bypass = 1;
     ca.heap_top = e->d_heap_top;
     ca.skew_n = e->d_skew_n;
     ca.cap = e->cap;
@@ -370,7 +376,8 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     ca.bits = e->plan.bits[0];
     {
       Scope s(e, K_CROWSCAN);
-      hipLaunchKernelGGL(k_chunk_rowscan, dim3(1u << ca.bits), dim3(kThreads), 0, e->stream, ca);
+      hipLaunchKernelGGL(k_chunk_rowscan, dim3((1u << ca.bits) + (e->nb + kBlSlice - 1) / kBlSlice), dim3(kThreads), 0,
+                         e->stream, ca);
     }
     {
       Scope s(e, K_CDOWN);
@@ -446,6 +453,15 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     g.cap = e->acap;
     g.tstride = e->tstride;
     g.region = e->region;
+  }
+  if (!e->fused && e->R == 1) {  // multi-pass: the backlog stays in place (parity arenas bl / bl2)
+    ba.pstep = e->d_step;
+    ba.cap = e->cap;
+    ba.blpre = e->d_blpre;
+    ba.bl_sbase = e->d_blpre + e->nb + kMaxBlSlices;
+    ba.d_ninbox = e->d_ninbox;
+    ba.g.bl[0] = e->bl.m();
+    ba.g.bl[1] = e->bl2.m();
   }
   if (e->R > 1) {  // tells leave grouped by owner rank (phase 1 packs them for the exchange)
     ba.nx_shift = kOwnerShift;
@@ -829,8 +845,8 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
       rep_steps[slot] = cnt;
       hipMemcpyAsync(e->h_cntb + slot * ring_row, e->d_cntb, (size_t)cnt * e->nb * 4, hipMemcpyDeviceToHost,
                      e->stream);
-    } else {  // inbox total of the replay's last superstep
-      hipMemcpyAsync(&e->h_pin[slot], e->d_n, 4, hipMemcpyDeviceToHost, e->stream);
+    } else {  // inbox total (sorted + backlog) of the replay's last superstep
+      hipMemcpyAsync(&e->h_pin[slot], e->d_ninbox, 4, hipMemcpyDeviceToHost, e->stream);
     }
     hipEventRecord(ev[slot], e->stream);
   }
@@ -1029,6 +1045,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   // first-pass histogram columns: ~2048 units per arena at most (G buckets per unit)
   e->G = (e->nb + 2047) / 2048;
   if (const char* s = getenv("AGX_UNIT_G")) e->G = (uint32_t)std::max(1, atoi(s));  // test knob
+  e->G = std::min<uint32_t>(e->G, kMaxUnitChunks);
   e->ng = (e->nb + e->G - 1) / e->G;
   e->nunits = 2 * e->ng + kStagedChunks;
   e->cstride = (e->nunits + 3) & ~3u;
@@ -1097,6 +1114,12 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(hipMemset(e->d_tcnt[0], 0, tsz * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(dalloc(&e->d_moff0, e->nb));
     CREATE_TRY(dalloc(&e->d_moff1, tsz));
+  }
+  if (!e->fused && e->R == 1) {  // multi-pass: backlog arenas by superstep parity
+    CREATE_TRY(alloc_msgs(e->bl2, e->acap));
+    CREATE_TRY(dalloc(&e->d_blpre, e->nb + 2 * kMaxBlSlices));  // [nb] prefixes, [64] slice totals, [64] bases
+    CREATE_TRY(dalloc(&e->d_ninbox, 1));
+    CREATE_TRY(hipMemset(e->d_ninbox, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   }
   if (e->fused) {
     const uint64_t tsz = (uint64_t)kRadix * e->tstride;
@@ -1182,7 +1205,7 @@ agx_status agx_destroy(agx_engine* e) {
   if (e->h_cntb) hipHostFree(e->h_cntb); hipFree(e->d_parv);
   hipFree(e->d_skew_list); hipFree(e->d_skew_n);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
-  hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_n); hipFree(e->d_total);
+  hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_blpre); hipFree(e->d_ninbox); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_sred); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);
   hipFree(e->d_heap); hipFree(e->d_heap_top); hipFree(e->d_step); hipFree(e->d_rx); hipFree(e->d_s2rows);
   if (e->h_pin) hipHostFree(e->h_pin);

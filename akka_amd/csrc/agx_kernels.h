@@ -156,9 +156,10 @@ struct SplitLds {
   uint32_t *key, *src, *pay;  // [kTile]
 };
 
-template <int NT>
-__device__ __forceinline__ void split_tile(const CMsgs& in, uint32_t base, uint32_t cnt, const Msgs& out,
-                                           uint32_t shift, uint32_t bits, const SplitLds& S) {
+// `ld(q, k, sv, pv)` loads item q < cnt of the tile.
+template <int NT, class Load>
+__device__ __forceinline__ void split_tile_ld(const Load& ld, uint32_t cnt, const Msgs& out, uint32_t shift,
+                                              uint32_t bits, const SplitLds& S) {
   constexpr int NW = NT / kWave, IPT = kTile / NT, DPT = kRadix / NT;
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t lane = lane_id();
@@ -171,13 +172,8 @@ __device__ __forceinline__ void split_tile(const CMsgs& in, uint32_t base, uint3
 #pragma unroll
   for (int r = 0; r < IPT; ++r) {
     const uint32_t q = wbase + r * kWave + lane;
-    if (q < cnt) {
-      k[r] = in.key[base + q];
-      sv[r] = in.src[base + q];
-      pv[r] = in.pay[base + q];
-    } else {
-      k[r] = 0xFFFFFFFFu;
-    }
+    if (q < cnt) ld(q, k[r], sv[r], pv[r]);
+    else k[r] = 0xFFFFFFFFu;
   }
 #pragma unroll
   for (int r = 0; r < IPT; ++r) {
@@ -248,6 +244,18 @@ __device__ __forceinline__ void split_tile(const CMsgs& in, uint32_t base, uint3
   __syncthreads();
 }
 
+template <int NT>
+__device__ __forceinline__ void split_tile(const CMsgs& in, uint32_t base, uint32_t cnt, const Msgs& out,
+                                           uint32_t shift, uint32_t bits, const SplitLds& S) {
+  split_tile_ld<NT>(
+      [&](uint32_t q, uint32_t& k, uint32_t& sv, uint32_t& pv) {
+        k = in.key[base + q];
+        sv = in.src[base + q];
+        pv = in.pay[base + q];
+      },
+      cnt, out, shift, bits, S);
+}
+
 // digit bases: s_dbase[d] = exclusive scan of tot[d] over digits; returns the total
 __device__ __forceinline__ uint32_t digit_bases(const uint32_t* tot, uint32_t nd, uint32_t* s_dbase, uint32_t* scratch) {
   const int tid = threadIdx.x;
@@ -303,6 +311,47 @@ __device__ __forceinline__ uint32_t scan_row(uint32_t* row, uint32_t len, uint32
 // each digit row into an exclusive prefix over units; the downsweep block of unit
 // u places that unit's chunks in order (canonical order preserved).
 // =========================================================================
+// Exclusive scan, in one block, of a table of `rows` rows x `len` entries (row stride
+// `stride`) flattened row-major; each thread owns one contiguous range of the flattened
+// index (all of its loads in flight before the block scan).  Writes the prefixes to `out`
+// (same layout) and row r's first prefix to rbase[r] (LDS, rows + 1 entries).  Returns the total.
+template <int NT>
+__device__ __forceinline__ uint64_t block_scan_table(const uint32_t* in, uint32_t* out, uint32_t rows, uint32_t len,
+                                                     uint32_t stride, uint32_t* scratch, uint32_t* rbase,
+                                                     uint32_t* total = nullptr) {
+  const uint32_t tid = threadIdx.x, L = rows * len, per = (L + NT - 1) / NT;
+  const uint32_t i0 = min(L, tid * per), i1 = min(L, i0 + per);
+  uint32_t sum = 0;
+  {
+    uint32_t r = len ? i0 / len : 0u, c = i0 - r * len;
+    for (uint32_t i = i0; i < i1; ++i) {
+      sum += in[(size_t)r * stride + c];
+      if (++c == len) { c = 0; ++r; }
+    }
+  }
+  uint32_t t;
+  uint32_t run = block_excl_sum<NT>(sum, scratch, &t);
+  {
+    uint32_t r = len ? i0 / len : 0u, c = i0 - r * len;
+    for (uint32_t i = i0; i < i1; ++i) {
+      const size_t x = (size_t)r * stride + c;
+      const uint32_t v = in[x];
+      out[x] = run;
+      if (c == 0 && rbase) rbase[r] = run;
+      run += v;
+      if (++c == len) { c = 0; ++r; }
+    }
+  }
+  if (tid == 0 && rbase) rbase[rows] = t;
+  if (tid == 0 && total) *total = t;
+  __syncthreads();
+  return t;
+}
+
+constexpr uint32_t kMaxUnitChunks = kThreads;  // chunks per histogram unit (G) — one per thread
+constexpr uint32_t kBlSlice = kThreads * 8;     // backlog-prefix slice (buckets per rowscan block)
+constexpr uint32_t kMaxBlSlices = kWave;        // nb <= 2^17 (n_local < 2^28): one wave sums the slices
+
 struct ChunkSortArgs {
   Chunks ch;
   Msgs out;
@@ -317,8 +366,13 @@ struct ChunkSortArgs {
   uint32_t* step;      // CRDT heap parity (null when no CRDT kind is registered)
   uint32_t* heap_top;
   uint32_t* skew_n;    // skew list of the coming apply: reset here
+  uint32_t* blpre;     // bypass: [nb] slice-local exclusive scan of the backlog chunk counts (rowscan blocks >= nd)
+  uint32_t* bl_stot;   // bypass: [slices] backlog total per slice of kBlSlice buckets
+  uint32_t* bl_sbase;  // bypass: out: [slices] exclusive scan of bl_stot (downsweep block 0)
+  uint32_t* d_ninbox;  // bypass: out: messages in this superstep's inboxes (sorted + backlog)
   uint64_t cap;
   uint32_t stride, nunits, ng, G, shift, bits;
+  uint32_t bypass;     // backlog chunks are read in place by the apply (not sorted; units < ng skipped)
 };
 
 // one block per digit: exclusive prefix over units (in place) + digit total;
@@ -331,6 +385,24 @@ __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs a) {
     if (threadIdx.x == 0) *a.skew_n = 0u;
   }
   const uint32_t d = blockIdx.x;
+  if (d >= (1u << a.bits) && a.bypass) {  // extra blocks: backlog prefix, one slice of kBlSlice buckets each
+    const uint32_t sl = d - (1u << a.bits), i0 = sl * kBlSlice + threadIdx.x * 8;
+    uint32_t v[8], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = i0 + j < a.ch.nb ? a.ch.cnt[i0 + j] : 0u;
+      sum += v[j];
+    }
+    uint32_t t;
+    uint32_t ex = block_excl_sum<kThreads>(sum, scratch, &t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (i0 + j < a.ch.nb) a.blpre[i0 + j] = ex;  // slice-local; + bl_sbase[slice] in the apply
+      ex += v[j];
+    }
+    if (threadIdx.x == 0) a.bl_stot[sl] = t;
+    return;
+  }
   if (d >= (1u << a.bits)) return;
   const uint32_t t = scan_row(a.hist + (size_t)d * a.stride, a.nunits, scratch);
   if (threadIdx.x == 0) a.tot[d] = t;
@@ -341,11 +413,12 @@ __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
   __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
   __shared__ uint32_t scratch[kWaves + 1];
   __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
+  __shared__ uint32_t s_cpre[kMaxUnitChunks + 2], s_coff[kMaxUnitChunks];
   const SplitLds S{&whist[0][0], s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
   const int tid = threadIdx.x;
   const uint32_t nd = 1u << a.bits;
   const uint32_t total = digit_bases(a.tot, nd, s_dbase, scratch);
-  const bool over = total > a.cap;
+  const bool over = total > a.cap;  // the sorted mail must fit A (the apply checks mail + backlog)
   if (blockIdx.x == 0) {
     for (uint32_t d = tid; d < nd; d += kThreads) a.bstart[d] = s_dbase[d];
     if (tid == 0) {
@@ -353,10 +426,18 @@ __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
       *a.d_n = over ? 0u : total;
       if (over) atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
     }
+    if (a.bypass && tid < kWave) {  // backlog (read in place by the apply): slice bases, inbox total
+      const uint32_t nsl = (a.ch.nb + kBlSlice - 1) / kBlSlice;
+      const uint32_t v = (uint32_t)tid < nsl ? a.bl_stot[tid] : 0u;
+      const uint32_t inc = wave_incl_sum(v);
+      if ((uint32_t)tid < nsl) a.bl_sbase[tid] = inc - v;
+      if (tid == kWave - 1) *a.d_ninbox = over ? 0u : total + inc;
+    }
   }
   if (over) return;
 
   for (uint32_t u = blockIdx.x; u < a.nunits; u += gridDim.x) {
+    if (a.bypass && u < a.ng) continue;  // backlog units: nothing counted, nothing to move
     // chunk range of this unit
     uint32_t c0, c1;
     if (u < a.ng) {
@@ -376,14 +457,44 @@ __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
       s_base[d] = s_dbase[d] + *hp;
       *hp = 0u;
     }
+    // the unit's chunks as one stream (tiles cross chunk boundaries: small chunks — skewed
+    // or sparse supersteps — do not cost a tile each); chunk j of the unit holds stream
+    // items [s_cpre[j], s_cpre[j+1])
+    const uint32_t nc = c1 - c0;  // <= kMaxUnitChunks
+    {
+      const uint32_t j = tid;
+      const uint32_t v = j < nc ? a.ch.cnt[c0 + j] : 0u;
+      if (j < nc) s_coff[j] = a.ch.off[c0 + j];
+      uint32_t t;
+      const uint32_t ex = block_excl_sum<kThreads>(v, scratch, &t);
+      if (j <= nc) s_cpre[j] = ex;
+      if (j == 0) s_cpre[kMaxUnitChunks + 1] = t;
+    }
     __syncthreads();
-    for (uint32_t c = c0; c < c1; ++c) {
-      const uint32_t cnt = a.ch.cnt[c];
-      if (cnt == 0) continue;
-      const CMsgs& src = a.ch.arena(c);
-      const uint32_t off = a.ch.off[c];
-      for (uint32_t sub = 0; sub < cnt; sub += kTile)
-        split_tile<kThreads>(src, off + sub, min((uint32_t)kTile, cnt - sub), a.out, a.shift, a.bits, S);
+    const uint32_t ntot = s_cpre[kMaxUnitChunks + 1];
+    const CMsgs& src = a.ch.arena(c0);  // one arena per unit
+    if (ntot >= nc * (uint32_t)(kTile / 2)) {  // large chunks: tile by tile, direct addressing
+      for (uint32_t j = 0; j < nc; ++j) {
+        const uint32_t cnt = s_cpre[j + 1 <= nc - 1 ? j + 1 : kMaxUnitChunks + 1] - s_cpre[j];
+        for (uint32_t sub = 0; sub < cnt; sub += kTile)
+          split_tile<kThreads>(src, s_coff[j] + sub, min((uint32_t)kTile, cnt - sub), a.out, a.shift, a.bits, S);
+      }
+      continue;
+    }
+    for (uint32_t t0 = 0; t0 < ntot; t0 += kTile) {
+      const auto ld = [&](uint32_t q, uint32_t& k, uint32_t& sv, uint32_t& pv) {
+        const uint32_t i = t0 + q;
+        uint32_t lo = 0, hi = nc - 1;  // last chunk whose start <= i
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          if (s_cpre[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        const uint32_t x = s_coff[lo] + (i - s_cpre[lo]);
+        k = src.key[x];
+        sv = src.src[x];
+        pv = src.pay[x];
+      };
+      split_tile_ld<kThreads>(ld, min((uint32_t)kTile, ntot - t0), a.out, a.shift, a.bits, S);
     }
   }
 }
@@ -609,6 +720,11 @@ struct BucketArgs {
   uint32_t nhist_stride, nx_shift, nx_bits;
   uint32_t G, ng;          // histogram units: G buckets per column, ng units per arena
   uint32_t nb, kmax;
+  uint64_t cap;            // bypass: message capacity of the inbox index space
+  const uint32_t* pstep;   // bypass (single-rank multi-pass): superstep counter; backlog arena parity = step & 1
+  const uint32_t* blpre;   // bypass: backlog prefix (bucket b's inbox index space starts at bstart[b] +
+  const uint32_t* bl_sbase;  // blpre[b] + bl_sbase[b / kBlSlice]); chunk_off/cnt[b] locate its backlog in g.bl[par ^ 1]
+  const uint32_t* d_ninbox;  // bypass: sorted + backlog messages of this superstep
   uint32_t par;            // fused: parity of this superstep (arenas/tables written; read = par ^ 1)
   uint32_t slot;           // fused: index of this superstep within its graph replay (row of g.cntb)
   uint32_t* skew_list;     // buckets whose inbox exceeds one LDS tile (appended by the fast launch)
@@ -675,14 +791,33 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
     const int wv = tid / kWave;
     const uint32_t lane = lane_id();
     const uint64_t ltm = lanemask_lt();
-    for (int i = tid; i < kBWaves * kRadix; i += kBThreads) whist[i] = 0;
-    __syncthreads();
     uint32_t k[kBIpt], d[kBIpt], rk[kBIpt];
+    int mono = 1;  // destinations non-decreasing in sender order (local topologies): already grouped
 #pragma unroll
     for (int r = 0; r < kBIpt; ++r) {
       const uint32_t i = wv * (kBIpt * kWave) + r * kWave + lane;
       k[r] = i < emtot ? ukey[i] : 0u;
       d[r] = (k[r] >> a.nx_shift) & (nd - 1);
+      if (i < emtot && i > 0) mono &= ((ukey[i - 1] >> a.nx_shift) & (nd - 1)) <= d[r];
+    }
+    if (__syncthreads_and(mono)) {  // every tell's slot is embase + its sender-order index
+#pragma unroll
+      for (int r = 0; r < kBIpt; ++r) {
+        const uint32_t i = wv * (kBIpt * kWave) + r * kWave + lane;
+        if (i < emtot) {
+          g.eg[w].key[embase + i] = k[r];
+          g.eg[w].src[embase + i] = usrc[i];
+          g.eg[w].pay[embase + i] = upay[i];
+        }
+      }
+      if (tid == 0 && g.emc[w]) g.emc[w][b] = emtot;
+      return;
+    }
+    for (int i = tid; i < kBWaves * kRadix; i += kBThreads) whist[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r) {
+      const uint32_t i = wv * (kBIpt * kWave) + r * kWave + lane;
       rk[r] = wave_rank(i < emtot, d[r], a.nx_bits, whist + wv * kRadix, ltm);
     }
     __syncthreads();
@@ -770,7 +905,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   }
   uint32_t bltot;
   uint32_t blex = block_excl_sum<kBThreads>(nbl_t, L.scratch, &bltot);
-  const Msgs blw = kGather ? a.g.bl[w] : a.bl;  // backlog arena written by this superstep
+  constexpr bool kBypass = !kGather && !kOwner;
+  const Msgs blw = (kGather || kBypass) ? a.g.bl[w] : a.bl;  // backlog arena written by this superstep
   if (tid == 0) {
     if constexpr (kGather) {
       a.g.blo[w][b] = lo;
@@ -819,10 +955,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         blw.pay[o] = pv;
       }
     }
-    if (!kGather && !kOwner && tid == 0) {  // all queued mail is in this bucket: one bin of the next first-pass histogram
-      const uint32_t d = ((b << kBucketBits) >> a.nx_shift) & nhmask;
-      atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + b / a.G], bltot);
-    }
+    // (single rank: the backlog stays in place for the next apply — not part of the next sort)
   }
   __syncthreads();
 
@@ -1180,8 +1313,11 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   const uint32_t lane = lane_id();
   const uint64_t ltm = lanemask_lt();
   const GatherArgs& g = a.g;
-  const uint32_t wpar = kGather ? a.par : 0u, rpar = wpar ^ 1u;  // fused: write parity w, read parity w ^ 1
-  uint32_t* const skew_n = a.skew_n + wpar;
+  // (kBypass: single-rank multi-pass — the previous backlog is read in place, not sorted)
+  constexpr bool kBypass = !kGather && !kOwner;
+  // fused / bypass: write parity w, read parity w ^ 1
+  const uint32_t wpar = kGather ? a.par : kBypass ? (*a.pstep & 1u) : 0u, rpar = wpar ^ 1u;
+  uint32_t* const skew_n = a.skew_n + (kGather ? wpar : 0u);  // (non-fused: one list, reset by the sort)
   if (kGather && !kSkew && blockIdx.x == 0 && tid == 0) {
     // reset the per-parity cursors that the NEXT superstep (parity rpar) will use (the previous
     // superstep, which used them, is complete)
@@ -1190,7 +1326,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     if (g.heap_top) g.heap_top[rpar] = 0u;
   }
   if (!kGather && !kSkew && blockIdx.x == 0) {
-    if (tid == 0 && *a.d_n > 0) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
+    if (tid == 0 && *(kBypass ? a.d_ninbox : a.d_n) > 0) atomicAdd((unsigned long long*)&a.stats[ST_STEPS], 1ull);
     for (uint32_t i = tid; i < kStagedChunks; i += kBThreads) a.chunk_cnt[2 * a.nb + i] = 0;  // staged consumed
   }
 
@@ -1213,8 +1349,22 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     }
     if (!kGather) {
       if (tid == 0) {
-        s_lo = a.bstart[b];
-        s_hi = a.bstart[b + 1];
+        if constexpr (kBypass) {  // inbox = [previous backlog, in place][sorted new mail]
+          const uint32_t bs = a.bstart[b], be = a.bstart[b + 1], bp = a.blpre[b] + a.bl_sbase[b / kBlSlice];
+          const uint32_t blc = a.chunk_cnt[b], blo = a.chunk_off[b];
+          s_g[0] = blc;
+          s_g[1] = blo;
+          s_g[3] = bs;
+          s_lo = bs + bp;
+          s_hi = bs + bp + blc + (be - bs);
+          if ((uint64_t)s_hi > a.cap) {  // mail + backlog over the message capacity: report, drop
+            atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
+            s_lo = s_hi = 0u;
+          }
+        } else {
+          s_lo = a.bstart[b];
+          s_hi = a.bstart[b + 1];
+        }
         s_g[5] = s_hi - s_lo > (uint32_t)kBucket;
         if (!kSkew && s_g[5]) a.skew_list[atomicAdd(skew_n, 1u)] = b;
       }
@@ -1283,6 +1433,8 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       if (tid == 0 && s_g[2]) g.stg_cnt[b] = 0u;
     }
     const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
+    // bypass: inbox item q < xblc is backlog item q (g.bl[rpar] at xblo + q), else sorted item xbst + q - xblc
+    const uint32_t xblc = kBypass ? s_g[0] : 0u, xblo = kBypass ? s_g[1] : 0u, xbst = kBypass ? s_g[3] : lo;
     GatherView gv{};
     if (kGather) {
       gv.segp = s_pay;
@@ -1303,10 +1455,14 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         if (q < cnt) {
           if (kGather) {
             gv.load(g, rpar, q, k[r], sv[r], pv[r]);
+          } else if (kBypass && q < xblc) {
+            k[r] = g.bl[rpar].key[xblo + q];
+            sv[r] = g.bl[rpar].src[xblo + q];
+            pv[r] = g.bl[rpar].pay[xblo + q];
           } else {
-            k[r] = a.in.key[lo + q];
-            sv[r] = a.in.src[lo + q];
-            pv[r] = a.in.pay[lo + q];
+            k[r] = a.in.key[xbst + q - xblc];
+            sv[r] = a.in.src[xbst + q - xblc];
+            pv[r] = a.in.pay[xbst + q - xblc];
           }
         } else {
           k[r] = 0xFFFFFFFFu;
@@ -1402,7 +1558,11 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       // keep = alive ? min(len, C) : 0 (tail-drop: the first `keep` in canonical order are
       // admitted); messages of an actor already at `keep` are dead letters and skip the
       // ranking, so a hot actor of a bounded mailbox costs one key read per arrival.
-      auto gkey = [&](uint32_t q) -> uint32_t { return kGather ? gv.key(g, rpar, q) : a.in.key[lo + q]; };
+      auto gkey = [&](uint32_t q) -> uint32_t {
+        if (kGather) return gv.key(g, rpar, q);
+        if (kBypass && q < xblc) return g.bl[rpar].key[xblo + q];
+        return a.in.key[xbst + q - xblc];
+      };
       uint32_t* s_run = s_key;   // LDS items are unused on this path
       uint32_t* s_tmp = s_src;
       uint32_t* s_keep = s_ecnt;  // (bucket_finish re-initialises ecnt)
@@ -1477,9 +1637,12 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
             if (kGather) {
               uint32_t k2;
               gv.load(g, rpar, q, k2, sv[r], pv[r]);
+            } else if (kBypass && q < xblc) {
+              sv[r] = g.bl[rpar].src[xblo + q];
+              pv[r] = g.bl[rpar].pay[xblo + q];
             } else {
-              sv[r] = a.in.src[lo + q];
-              pv[r] = a.in.pay[lo + q];
+              sv[r] = a.in.src[xbst + q - xblc];
+              pv[r] = a.in.pay[xbst + q - xblc];
             }
           }
         }
@@ -1600,48 +1763,14 @@ struct McompactArgs {
   uint32_t R, tstride, n_staged;
 };
 
-// Exclusive scan, in one block, of a table of `rows` rows x `len` entries (row stride
-// `stride`) flattened row-major; each thread owns one contiguous range of the flattened
-// index (all of its loads in flight before the block scan).  Writes the prefixes to `out`
-// (same layout) and row r's first prefix to rbase[r] (LDS, rows + 1 entries).  Returns the total.
-__device__ __forceinline__ uint64_t block_scan_table(const uint32_t* in, uint32_t* out, uint32_t rows, uint32_t len,
-                                                     uint32_t stride, uint32_t* scratch, uint32_t* rbase) {
-  const uint32_t tid = threadIdx.x, L = rows * len, per = (L + kScanThreads - 1) / kScanThreads;
-  const uint32_t i0 = min(L, tid * per), i1 = min(L, i0 + per);
-  uint32_t sum = 0;
-  {
-    uint32_t r = len ? i0 / len : 0u, c = i0 - r * len;
-    for (uint32_t i = i0; i < i1; ++i) {
-      sum += in[(size_t)r * stride + c];
-      if (++c == len) { c = 0; ++r; }
-    }
-  }
-  uint32_t t;
-  uint32_t run = block_excl_sum<kScanThreads>(sum, scratch, &t);
-  {
-    uint32_t r = len ? i0 / len : 0u, c = i0 - r * len;
-    for (uint32_t i = i0; i < i1; ++i) {
-      const size_t x = (size_t)r * stride + c;
-      const uint32_t v = in[x];
-      out[x] = run;
-      if (c == 0 && rbase) rbase[r] = run;
-      run += v;
-      if (++c == len) { c = 0; ++r; }
-    }
-  }
-  if (tid == 0 && rbase) rbase[rows] = t;
-  __syncthreads();
-  return t;
-}
-
 __global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactArgs a) {
   __shared__ uint32_t scratch[kScanThreads / kWave + 1];
   __shared__ uint32_t s_obase[AGX_MAX_RANKS + 1];
   begin_step(a.step, a.heap_top);
   commit_stops(a.alive, a.stopq, a.nstop);
   if (threadIdx.x == 0) *a.skew_n = 0u;
-  const uint64_t nbl = block_scan_table(a.ch.cnt, a.off0, 1, a.ch.nb, a.ch.nb, scratch, nullptr);
-  const uint64_t ntl = block_scan_table(a.tcnt, a.off1, a.R, a.ch.nb, a.tstride, scratch, s_obase);
+  const uint64_t nbl = block_scan_table<kScanThreads>(a.ch.cnt, a.off0, 1, a.ch.nb, a.ch.nb, scratch, nullptr);
+  const uint64_t ntl = block_scan_table<kScanThreads>(a.tcnt, a.off1, a.R, a.ch.nb, a.tstride, scratch, s_obase);
   const uint32_t tid = threadIdx.x;
   const bool over = nbl > a.cap0 || ntl > a.cap1;
   if (tid == 0) {
