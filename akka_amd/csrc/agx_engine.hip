@@ -122,7 +122,7 @@ struct agx_engine {
   uint32_t *d_gid = nullptr, *d_route = nullptr;
   uint32_t ring_stride = 1, fan_k = 0;
   uint64_t fan_seed = 0, zipf_n = 0;
-  uint32_t *d_zcdf = nullptr, *d_zperm = nullptr;
+  uint32_t *d_zcdf = nullptr, *d_zperm = nullptr, *d_zidx = nullptr;
   uint64_t* d_row = nullptr;
   uint32_t* d_col = nullptr;
   // CRDT state gossips (agx_crdt.h): snapshot heap, 2 x cap rows of pw u32
@@ -274,6 +274,7 @@ DevParams make_params(agx_engine* e) {
   P.fan_seed = e->fan_seed;
   P.zipf_n = e->zipf_n;
   P.zipf_cdf = e->d_zcdf;
+  P.zipf_idx = e->d_zidx;
   P.zipf_perm = e->d_zperm;
   P.row_ptr = e->d_row;
   P.col = e->d_col;
@@ -476,24 +477,18 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     const dim3 g(grid_for(e->nb, e->apply_grid)), blk(kBThreads);
     const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
     const dim3 gs(grid_for(e->nb, e->apply_grid));  // skew list: as many blocks as there may be buckets
+#define AGX_APPLY2(W, M, G, O)                                                                   \
+  do {                                                                                           \
+    { Scope s(e, K_APPLY);                                                                       \
+      hipLaunchKernelGGL((k_bucket_apply<W, M, G, false, O>), g, blk, 0, e->stream, ba); }       \
+    { Scope s(e, K_SKEW);                                                                        \
+      hipLaunchKernelGGL((k_bucket_apply<W, M, G, true, O>), gs, blk, 0, e->stream, ba); }       \
+  } while (0)
 #define AGX_APPLY(W, M)                                                                          \
   do {                                                                                           \
-    if (e->fused) {                                                                              \
-      { Scope s(e, K_APPLY);                                                                     \
-        hipLaunchKernelGGL((k_bucket_apply<W, M, true, false>), g, blk, 0, e->stream, ba); }     \
-      { Scope s(e, K_SKEW);                                                                      \
-        hipLaunchKernelGGL((k_bucket_apply<W, M, true, true>), gs, blk, 0, e->stream, ba); }     \
-    } else if (e->R > 1) {                                                                       \
-      { Scope s(e, K_APPLY);                                                                     \
-        hipLaunchKernelGGL((k_bucket_apply<W, M, false, false, true>), g, blk, 0, e->stream, ba); } \
-      { Scope s(e, K_SKEW);                                                                      \
-        hipLaunchKernelGGL((k_bucket_apply<W, M, false, true, true>), gs, blk, 0, e->stream, ba); } \
-    } else {                                                                                     \
-      { Scope s(e, K_APPLY);                                                                     \
-        hipLaunchKernelGGL((k_bucket_apply<W, M, false, false>), g, blk, 0, e->stream, ba); }    \
-      { Scope s(e, K_SKEW);                                                                      \
-        hipLaunchKernelGGL((k_bucket_apply<W, M, false, true>), gs, blk, 0, e->stream, ba); }    \
-    }                                                                                            \
+    if (e->fused) AGX_APPLY2(W, M, true, false);                                                 \
+    else if (e->R > 1) AGX_APPLY2(W, M, false, true);                                            \
+    else AGX_APPLY2(W, M, false, false);                                                         \
   } while (0)
     if (e->pw)  // CRDT kinds registered: the variant with state gossips
       AGX_APPLY(true, KM_ALL);
@@ -508,6 +503,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     else
       AGX_APPLY(false, KM_ALL);
 #undef AGX_APPLY
+#undef AGX_APPLY2
   }
   if (e->fused) e->par ^= 1u;  // the next superstep writes the other parity
   HIP_TRY(hipGetLastError());
@@ -1195,7 +1191,7 @@ agx_status agx_destroy(agx_engine* e) {
   if (e->comm) ncclCommDestroy(e->comm);
   drop_graphs(e);
   hipFree(e->d_kind); hipFree(e->d_alive); hipFree(e->d_stopq); hipFree(e->d_nstop); hipFree(e->d_state); hipFree(e->d_gid); hipFree(e->d_route);
-  hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_row); hipFree(e->d_col);
+  hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_zidx); hipFree(e->d_row); hipFree(e->d_col);
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
   free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1);
   for (int q = 0; q < 2; ++q) {
@@ -1275,11 +1271,26 @@ agx_status agx_set_fanout(agx_engine* e, uint32_t k, uint64_t seed, const uint32
   for (uint64_t i = 0; i < n; ++i)
     if (perm[i] >= e->n_global) return set_err(AGX_EINVAL, "perm entry out of range");
   AGX_TRY(ensure_dev(e));
+  if (n >= (1ull << 32)) return set_err(AGX_EINVAL, "fanout table too large");
+  for (uint64_t i = 1; i < n; ++i)
+    if (cdf[i] < cdf[i - 1]) return set_err(AGX_EINVAL, "fanout cdf not monotone at %llu", (unsigned long long)i);
+  // search-range index: zidx[t] = first i with cdf[i] >= t << (32 - kZipfBits), clamped to n - 1
+  const uint64_t Z = 1ull << kZipfBits;
+  std::vector<uint32_t> zidx(Z + 1);
+  for (uint64_t t = 0, i = 0; t < Z; ++t) {
+    const uint64_t u = t << (32 - kZipfBits);
+    while (i < n && cdf[i] < u) ++i;
+    zidx[t] = (uint32_t)std::min<uint64_t>(i, n - 1);
+  }
+  zidx[Z] = (uint32_t)(n - 1);
   hipFree(e->d_zcdf);
   hipFree(e->d_zperm);
-  e->d_zcdf = e->d_zperm = nullptr;
+  hipFree(e->d_zidx);
+  e->d_zcdf = e->d_zperm = e->d_zidx = nullptr;
   AGX_TRY(dalloc(&e->d_zcdf, n));
   AGX_TRY(dalloc(&e->d_zperm, n));
+  AGX_TRY(dalloc(&e->d_zidx, Z + 1));
+  HIP_TRY(hipMemcpy(e->d_zidx, zidx.data(), (Z + 1) * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_zcdf, cdf, n * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->d_zperm, perm, n * 4, hipMemcpyHostToDevice));
   e->fan_k = k;

@@ -655,6 +655,11 @@ constexpr int kBIpt = kBucket / kBThreads;      // items per thread per sub-tile
 constexpr int kBAct = kBucket / kBThreads;      // actors per thread (4)
 static_assert(kBAct == 4 && kBIpt == 4, "bucket_apply assumes 4 actors and 4 inbox items per thread");
 constexpr int kStagedChunks = 256;              // host-staged tells are split over this many chunks
+#ifndef AGX_NO_MONO
+constexpr bool kMonoShortcut = true;
+#else
+constexpr bool kMonoShortcut = false;
+#endif
 constexpr int kPF = 4;                          // apply prefetch window (messages in global scratch)
 
 // Tell staging in LDS (single-pass path): tells overwrite consumed inbox slots of the same actor.
@@ -800,7 +805,7 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
       d[r] = (k[r] >> a.nx_shift) & (nd - 1);
       if (i < emtot && i > 0) mono &= ((ukey[i - 1] >> a.nx_shift) & (nd - 1)) <= d[r];
     }
-    if (__syncthreads_and(mono)) {  // every tell's slot is embase + its sender-order index
+    if (kMonoShortcut && __syncthreads_and(mono)) {  // every tell's slot is embase + its sender-order index
 #pragma unroll
       for (int r = 0; r < kBIpt; ++r) {
         const uint32_t i = wv * (kBIpt * kWave) + r * kWave + lane;
@@ -1289,8 +1294,10 @@ struct GatherView {
 // the fast path.
 // kOwner (multi-rank): tells leave grouped by owner rank into g.eg[0] + g.tcnt/toff[0]
 // (digit = key >> kOwnerShift) instead of the chunk arena + next-pass histogram.
+// (One launch with both paths spills ~20 VGPRs and measured 13% slower at 1M.)
 template <bool kWide, uint32_t KM, bool kGather, bool kSkew, bool kOwner = false>
 __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
+  constexpr bool kDefer = !kSkew;  // large inboxes are appended to the skew list
   // key/src/pay carved from one array: group_tells reuses key+src as a 16 KB histogram
   __shared__ __attribute__((aligned(16))) uint32_t s_ksp[3 * kBucket];
   uint32_t* const s_key = s_ksp;
@@ -1366,7 +1373,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
           s_hi = a.bstart[b + 1];
         }
         s_g[5] = s_hi - s_lo > (uint32_t)kBucket;
-        if (!kSkew && s_g[5]) a.skew_list[atomicAdd(skew_n, 1u)] = b;
+        if (kDefer && s_g[5]) a.skew_list[atomicAdd(skew_n, 1u)] = b;
       }
     } else {
       // fused: this bucket's row of the tell tables (chunk c = sender bucket c), its backlog,
@@ -1400,15 +1407,15 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         s_g[4] = ns;
         const uint32_t cnt = blc + tt + s_g[2];
         s_g[5] = cnt > (uint32_t)kBucket;
-        if (!kSkew && s_g[5]) a.skew_list[atomicAdd(skew_n, 1u)] = b;
+        if (kDefer && s_g[5]) a.skew_list[atomicAdd(skew_n, 1u)] = b;
         // inbox slot: the bucket's own region (no shared counter), else the overflow region
         uint64_t lo = (uint64_t)b * g.region;
-        if (!kSkew && s_g[5]) {
+        if (kDefer && s_g[5]) {
           // deferred to the skew launch, which allocates
         } else if (cnt > g.region) {
           lo = (uint64_t)a.nb * g.region + atomicAdd(&g.ovf[wpar], cnt);
         }
-        if (!kSkew && s_g[5]) {
+        if (kDefer && s_g[5]) {
         } else if (lo + cnt > g.cap) {  // arena overflow: report, drop this bucket's mail
           atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
           s_lo = 0;
@@ -1424,7 +1431,8 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     reinterpret_cast<uint32_t*>(s_alive)[tid] = alive4;
     __syncthreads();
     AGX_STAMP(a, 1);
-    if (!kSkew && s_g[5]) {  // large inbox: left to the skew-list launch (row kept for it)
+    const bool big = s_g[5] != 0;
+    if (kDefer && big) {  // large inbox: left to the skew-list launch (row kept for it)
       __syncthreads();       // every thread has read s_g before the next bucket rewrites it
       continue;
     }
@@ -1445,7 +1453,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       gv.sto = s_g[3];
     }
 
-    if constexpr (!kSkew) {
+    if constexpr (kDefer) {
       // ---- fast path: the whole bucket in one LDS tile
       uint32_t k[kBIpt], sv[kBIpt], pv[kBIpt], rk[kBIpt];
       const uint32_t wbase = w * (kBIpt * kWave);

@@ -310,3 +310,24 @@ def test_grid_stride_apply(built, monkeypatch, fused, case):
     w = MULTIPASS_CASES[case]()
     sg, so, a, b = run_both(w)
     assert_same(sg, so, a, b, f"grid-stride {case} fused={fused}")
+
+
+@pytest.mark.parametrize("shape", ["steps", "dup_edges", "tiny"])
+def test_zipf_index_ranges(built, shape):
+    """The device's indexed CDF search (top 20 bits of the draw pick a search range) returns
+    the plain binary search's answer: thresholds on range boundaries, long runs of equal
+    thresholds, 0 and 0xFFFFFFFF entries, tables shorter than the index."""
+    import dataclasses
+    n = 50_000
+    w = wl.zipf_fanout(n, k=3, ttl=3, root_every=7, throughput=3)
+    k, seed, _, perm = w.fanout
+    rng = np.random.default_rng(5)
+    if shape == "steps":  # every threshold on a multiple of 2^12 (a range boundary)
+        cdf = np.sort(rng.integers(0, 1 << 20, n, dtype=np.uint64) << np.uint64(12)).astype(np.uint32)
+    elif shape == "dup_edges":  # few distinct values, both extremes
+        cdf = np.sort(rng.choice(np.array([0, 1, 4095, 4096, 1 << 31, 0xFFFFFFFE, 0xFFFFFFFF], np.uint32), n))
+    else:  # 5 targets
+        cdf, perm = np.array([1 << 30, 1 << 31, 3 << 30, 0xF0000000, 0xFFFFFFFF], np.uint32), perm[:5]
+    w = dataclasses.replace(w, fanout=(k, seed, cdf, perm))
+    sg, so, a, b = run_both(w)
+    assert_same(sg, so, a, b, f"zipf index {shape}")
