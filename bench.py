@@ -158,8 +158,9 @@ def timed_workload(w, warmup: int, steps: int, prof_steps: int = 8, msg_capacity
                                    if v["launches"]}}
 
 
-def other_configs(quick: bool) -> dict:
-    """BASELINE.json configs other than the headline ring, each measured on one GPU."""
+def other_configs(quick: bool, only: str = "") -> dict:
+    """BASELINE.json configs other than the headline ring, each measured on one GPU
+    (`only`: just that one, for tools/cfg_one.py)."""
     from akka_amd import workloads as wl
     from akka_amd.engine import Kind
 
@@ -188,6 +189,8 @@ def other_configs(quick: bool) -> dict:
     }
     out = {}
     for name, (desc, make, warm, steps, mcap) in specs.items():
+        if only and name != only:
+            continue
         try:  # one config failing must not hide the others
             out[name] = dict(workload=desc, **timed_workload(make(), warm, steps, msg_capacity=mcap))
         except Exception as ex:
