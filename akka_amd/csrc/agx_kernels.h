@@ -660,7 +660,10 @@ constexpr bool kMonoShortcut = true;
 #else
 constexpr bool kMonoShortcut = false;
 #endif
-constexpr int kPF = 4;                          // apply prefetch window (messages in global scratch)
+#ifndef AGX_PF
+#define AGX_PF 4
+#endif
+constexpr int kPF = AGX_PF;                     // apply prefetch window (messages in global scratch)
 
 // Tell staging in LDS (single-pass path): tells overwrite consumed inbox slots of the same actor.
 struct EmitterLds {
