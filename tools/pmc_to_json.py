@@ -19,8 +19,8 @@ import os
 
 
 def kernel_class(full: str):
-    """'void agx::k_bucket_apply<false, 4u, true, false>(agx::BucketArgs)' -> 'bucket_apply'
-    (the skew-list instantiation, last template argument true -> 'bucket_apply_skew')."""
+    """'void agx::k_bucket_apply<false, 4u, true, false, false>(agx::BucketArgs)' -> 'bucket_apply'
+    (the skew-list instantiation, 4th template argument kSkew true -> 'bucket_apply_skew')."""
     n = full[5:] if full.startswith("void ") else full
     base = n.split("(")[0]
     targs = ""
@@ -29,7 +29,7 @@ def kernel_class(full: str):
     if not base.startswith("agx::k_"):
         return None
     k = base[len("agx::k_"):]
-    if k == "bucket_apply" and targs.rstrip(">").split(",")[-1].strip() == "true":
+    if k == "bucket_apply" and targs.rstrip(">").split(",")[3].strip() == "true":
         k = "bucket_apply_skew"
     return k
 
