@@ -79,24 +79,38 @@ __device__ __forceinline__ uint32_t orset_merge_entry(uint32_t l, uint32_t r, ui
 }
 
 // Phase B: one invoke of a CRDT replica.  `emit(dst, pay)` / `emit_wide(dst, handle)`.
-template <typename Emit>
+// CM: the CRDT kinds present (one bit = a single-kind population, whose merge is specialised:
+// the other kinds' code and registers vanish).  Merges issue all loads of a batch before its
+// stores (the row and the state may alias as far as the compiler knows, so a load-store-load
+// chain would serialise one memory round trip per element).
+template <uint32_t CM, typename Emit>
 __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHeap& H, uint32_t kind, uint32_t self,
                                                uint32_t l, uint32_t src, uint32_t pay, uint32_t& row_cursor,
                                                Emit& em) {
+  if constexpr (CM == (1u << AGX_KIND_GCOUNTER)) kind = AGX_KIND_GCOUNTER;
+  if constexpr (CM == (1u << AGX_KIND_PNCOUNTER)) kind = AGX_KIND_PNCOUNTER;
+  if constexpr (CM == (1u << AGX_KIND_ORSET)) kind = AGX_KIND_ORSET;
   const size_t nl = P.n_local;
   uint64_t* st = P.state + l;  // word w at st[w * nl]
   const uint32_t node = self % AGX_CRDT_NODES;
   if (is_wide(src)) {
     if ((pay >> 30) != kind - (uint32_t)AGX_KIND_GCOUNTER) return AGX_RES_UNHANDLED;  // another data type
     const uint32_t* row = H.row(pay & kHandleMask);
-    if (kind != AGX_KIND_ORSET) {  // slot-wise max
+    if (kind != AGX_KIND_ORSET) {  // slot-wise max, 8 words per batch
       const uint32_t nw = crdt_words(kind);
-      for (uint32_t i = 0; i < nw; i += 2) {
-        const uint4 v = *reinterpret_cast<const uint4*>(row + 2 * i);
-        const uint64_t r0 = ((uint64_t)v.y << 32) | v.x, r1 = ((uint64_t)v.w << 32) | v.z;
-        const uint64_t s0 = st[i * nl], s1 = st[(i + 1) * nl];
-        if (r0 > s0) st[i * nl] = r0;
-        if (r1 > s1) st[(i + 1) * nl] = r1;
+      for (uint32_t i0 = 0; i0 < nw; i0 += 8) {
+        uint4 v[4];
+        uint64_t s[8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(row + 2 * i0 + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s[u] = st[(i0 + u) * nl];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint64_t r0 = ((uint64_t)v[u].y << 32) | v[u].x, r1 = ((uint64_t)v[u].w << 32) | v[u].z;
+          if (r0 > s[2 * u]) st[(i0 + 2 * u) * nl] = r0;
+          if (r1 > s[2 * u + 1]) st[(i0 + 2 * u + 1) * nl] = r1;
+        }
       }
       return AGX_RES_SAME;
     }
@@ -111,18 +125,31 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       rvv[2 * k] = row[2 * (vw + k)];
       rvv[2 * k + 1] = row[2 * (vw + k) + 1];
     }
-    for (uint32_t e = 0; e < AGX_ORSET_ELEMS; ++e) {
-      const uint4 ra = *reinterpret_cast<const uint4*>(row + 8 * e);
-      const uint4 rb = *reinterpret_cast<const uint4*>(row + 8 * e + 4);
-      const uint32_t r[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+#ifndef AGX_ORSET_BATCH
+#define AGX_ORSET_BATCH 2
+#endif
+    constexpr uint32_t kE = AGX_ORSET_BATCH;  // elements per batch (8 row words + 4 state words each)
+    for (uint32_t e0 = 0; e0 < AGX_ORSET_ELEMS; e0 += kE) {
+      uint4 ra[kE], rb[kE];
+      uint64_t s[kE][4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const size_t wi = (size_t)(4 * e + k) * nl;
-        const uint64_t s = st[wi];
-        const uint32_t o0 = orset_merge_entry((uint32_t)s, r[2 * k], lvv[2 * k], rvv[2 * k]);
-        const uint32_t o1 = orset_merge_entry((uint32_t)(s >> 32), r[2 * k + 1], lvv[2 * k + 1], rvv[2 * k + 1]);
-        const uint64_t o = ((uint64_t)o1 << 32) | o0;
-        if (o != s) st[wi] = o;
+      for (uint32_t u = 0; u < kE; ++u) {
+        ra[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u));
+        rb[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u) + 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[u][k] = st[(size_t)(4 * (e0 + u) + k) * nl];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kE; ++u) {
+        const uint32_t r[8] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w, rb[u].x, rb[u].y, rb[u].z, rb[u].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint64_t sv = s[u][k];
+          const uint32_t o0 = orset_merge_entry((uint32_t)sv, r[2 * k], lvv[2 * k], rvv[2 * k]);
+          const uint32_t o1 = orset_merge_entry((uint32_t)(sv >> 32), r[2 * k + 1], lvv[2 * k + 1], rvv[2 * k + 1]);
+          const uint64_t o = ((uint64_t)o1 << 32) | o0;
+          if (o != sv) st[(size_t)(4 * (e0 + u) + k) * nl] = o;
+        }
       }
     }
 #pragma unroll
@@ -170,11 +197,16 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
         const uint32_t h = row_cursor++;
         if (h < H.rows) {  // snapshot of the current state, shared by the f gossips
           uint32_t* row = H.wrow(h);
-          const uint32_t nw = crdt_words(kind);
-          for (uint32_t i = 0; i < nw; i += 2) {
-            const uint64_t s0 = st[i * nl], s1 = st[(i + 1) * nl];
-            *reinterpret_cast<uint4*>(row + 2 * i) =
-                make_uint4((uint32_t)s0, (uint32_t)(s0 >> 32), (uint32_t)s1, (uint32_t)(s1 >> 32));
+          const uint32_t nw = crdt_words(kind);  // 8 | 16 | 260 words: batches of 4 (loads first)
+          for (uint32_t i0 = 0; i0 < nw; i0 += 4) {
+            uint64_t s[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s[u] = st[(i0 + u) * nl];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+              *reinterpret_cast<uint4*>(row + 2 * i0 + 4 * u) =
+                  make_uint4((uint32_t)s[2 * u], (uint32_t)(s[2 * u] >> 32), (uint32_t)s[2 * u + 1],
+                             (uint32_t)(s[2 * u + 1] >> 32));
           }
         }
         const uint32_t tagged = ((kind - (uint32_t)AGX_KIND_GCOUNTER) << 30) | h;

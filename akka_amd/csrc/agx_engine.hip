@@ -490,7 +490,16 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     else if (e->R > 1) AGX_APPLY2(W, M, false, true);                                            \
     else AGX_APPLY2(W, M, false, false);                                                         \
   } while (0)
-    if (e->pw)  // CRDT kinds registered: the variant with state gossips
+    constexpr uint32_t kCrdt = kb(AGX_KIND_GCOUNTER) | kb(AGX_KIND_PNCOUNTER) | kb(AGX_KIND_ORSET);
+    if (e->pw && km == kb(AGX_KIND_GCOUNTER))  // single-kind CRDT populations: specialised merges
+      AGX_APPLY(true, kb(AGX_KIND_GCOUNTER));
+    else if (e->pw && km == kb(AGX_KIND_PNCOUNTER))
+      AGX_APPLY(true, kb(AGX_KIND_PNCOUNTER));
+    else if (e->pw && km == kb(AGX_KIND_ORSET))
+      AGX_APPLY(true, kb(AGX_KIND_ORSET));
+    else if (e->pw && (km & ~kCrdt) == 0)  // CRDT kinds only: no plain-behaviour code
+      AGX_APPLY(true, kCrdt);
+    else if (e->pw)  // CRDT kinds registered: the variant with state gossips
       AGX_APPLY(true, KM_ALL);
     else if (km == kb(AGX_KIND_RING))  // behaviour-specialised variants (see apply_msg)
       AGX_APPLY(false, kb(AGX_KIND_RING));

@@ -978,7 +978,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       const uint32_t la = j * kBThreads + tid;
       const bool has = la < na && L.alive[la] && L.seg[la + 1] != L.seg[la];
       const uint32_t l = a0 + la;
-      kd[j] = has && (KM & (KM - 1)) != 0 ? P.kind[l] : 0u;  // single-kind variants never read it
+      kd[j] = has && (kWide || (KM & (KM - 1)) != 0) ? P.kind[l] : 0u;  // single-kind variants never read it
       x0[j] = has ? P.state[l] : 0ull;
       x1[j] = has && P.W > 1 ? P.state[(size_t)P.n_local + l] : 0ull;
     }
@@ -1167,7 +1167,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       ++nact;
       if (kWide && is_crdt(kd)) {
         for (uint32_t q = 0; q < nd; ++q) {
-          const uint32_t r = crdt_apply(P, H, kd, self, l, isrc(s0 + q), ipay(s0 + q), row_cursor, em);
+          const uint32_t r = crdt_apply<KM>(P, H, kd, self, l, isrc(s0 + q), ipay(s0 + q), row_cursor, em);
           ++ndel;
           if (r == AGX_RES_UNHANDLED) ++nunh;
         }
