@@ -161,6 +161,7 @@ struct agx_engine {
   uint32_t tstride = 4, region = 0;
   uint64_t acap = 0;  // arena capacity (fused: regions + overflow area)
   uint32_t apply_grid = kMaxApplyGrid;  // AGX_APPLY_GRID test knob: fewer blocks, each looping over buckets
+  uint32_t skew_grid = kMaxApplyGrid;   // AGX_SKEW_GRID diagnostic knob: blocks of the skew-list launch
   std::vector<uint32_t> hd_key, hd_src, hd_pay;  // staged tells on the device, not yet consumed (fused)
   bool stg_pending = false;
 
@@ -476,7 +477,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   {
     const dim3 g(grid_for(e->nb, e->apply_grid)), blk(kBThreads);
     const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
-    const dim3 gs(grid_for(e->nb, e->apply_grid));  // skew list: as many blocks as there may be buckets
+    const dim3 gs(grid_for(e->nb, std::min(e->apply_grid, e->skew_grid)));  // skew list (grid-stride)
 #define AGX_APPLY2(W, M, G, O)                                                                   \
   do {                                                                                           \
     { Scope s(e, K_APPLY);                                                                       \
@@ -1076,6 +1077,8 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   // arenas; an inbox larger than the region (skew) takes a slot of the overflow area that
   // follows, sized like the whole message capacity — no shared counter on the common path
   e->region = kBucket;
+  if (const char* s = getenv("AGX_SKEW_GRID"))
+    e->skew_grid = (uint32_t)std::min<int>(kMaxApplyGrid, std::max(1, atoi(s)));
   if (const char* s = getenv("AGX_APPLY_GRID"))
     e->apply_grid = (uint32_t)std::min<int>(kMaxApplyGrid, std::max(1, atoi(s)));
   e->acap = e->fused ? (uint64_t)e->nb * e->region + e->cap : e->cap;

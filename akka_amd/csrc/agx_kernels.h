@@ -970,9 +970,16 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   AGX_STAMP(a, 4);
   // ---- prefetch kind + state words 0/1 of actors with mail (striped: coalesced).  All loads
   // are issued before the LDS stores (the stores go through generic pointers).
+  // FORWARD_RR (C5) single pass: each actor's out-edge row and the destination of its next
+  // round-robin edge are fetched here for all four actors at once, instead of two dependent
+  // loads (row_ptr, then col) per message inside the serial drain (fdeg = kNoHint: no hint).
+  constexpr bool kFwd = kLds && !kWide && KM == kb(AGX_KIND_FORWARD_RR);
+  constexpr uint32_t kNoHint = 0xFFFFFFFFu;
+  uint64_t frb[kBAct];
+  uint32_t fdeg[kBAct], fdst[kBAct];
   {
     uint32_t kd[kBAct];
-    uint64_t x0[kBAct], x1[kBAct];
+    uint64_t x0[kBAct], x1[kBAct], fre[kBAct];
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
       const uint32_t la = j * kBThreads + tid;
@@ -981,6 +988,19 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       kd[j] = has && (kWide || (KM & (KM - 1)) != 0) ? P.kind[l] : 0u;  // single-kind variants never read it
       x0[j] = has ? P.state[l] : 0ull;
       x1[j] = has && P.W > 1 ? P.state[(size_t)P.n_local + l] : 0ull;
+      if constexpr (kFwd) {
+        frb[j] = has ? P.row_ptr[l] : 0ull;
+        fre[j] = has ? P.row_ptr[l + 1] : ~0ull;  // (no mail: deg out of range -> no hint)
+      }
+    }
+    if constexpr (kFwd) {
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        const uint64_t deg = fre[j] - frb[j];
+        const bool ok = deg < kNoHint && x1[j] <= 0xFFFFFFFFull;
+        fdeg[j] = ok ? (uint32_t)deg : kNoHint;
+        fdst[j] = ok && deg ? P.col[frb[j] + (uint32_t)x1[j] % (uint32_t)deg] : 0u;
+      }
     }
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
@@ -1009,9 +1029,30 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       uint64_t wv[2] = {w0s[la], w1s[la]};
       const uint32_t nd = min(len, T);
       ++nact;
+      uint64_t hb = 0;
+      uint32_t hdeg = kNoHint, hdst = 0;
+      bool fresh = true;  // no forward yet: the next edge is fdst
+      if constexpr (kFwd) {  // (j is wave-uniform)
+        hb = j == 0 ? frb[0] : j == 1 ? frb[1] : j == 2 ? frb[2] : frb[3];
+        hdeg = j == 0 ? fdeg[0] : j == 1 ? fdeg[1] : j == 2 ? fdeg[2] : fdeg[3];
+        hdst = j == 0 ? fdst[0] : j == 1 ? fdst[1] : j == 2 ? fdst[2] : fdst[3];
+      }
       for (uint32_t q = 0; q < nd; ++q) {
         const uint32_t sv = L.src[s0 + q], pv = L.pay[s0 + q];
-        const uint32_t r = apply_msg<KM>(P, L.kind[la], self, l, wv, sv, pv, em);
+        uint32_t r;
+        if (kFwd && hdeg != kNoHint && wv[1] <= 0xFFFFFFFFull) {
+          // apply_msg's FORWARD_RR with the prefetched row (same cursor arithmetic)
+          wv[0] += 1;
+          if (pv > 0 && hdeg) {
+            const uint32_t d = fresh ? hdst : P.col[hb + (uint32_t)wv[1] % hdeg];
+            fresh = false;
+            wv[1] += 1;
+            em(d, pv - 1);
+          }
+          r = AGX_RES_SAME;
+        } else {
+          r = apply_msg<KM>(P, L.kind[la], self, l, wv, sv, pv, em);
+        }
         ++ndel;
         if (r == AGX_RES_UNHANDLED) ++nunh;
         if (r == AGX_RES_STOPPED) {
