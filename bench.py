@@ -60,6 +60,21 @@ def kernel_bytes_per_msg(W: int) -> dict:
     }
 
 
+def kernel_rooflines(prof: dict, per_msg: dict, msgs_per_launch: int) -> dict:
+    """HBM roofline of every kernel class with algorithmic bytes: achieved = bytes per message x
+    messages per launch / average launch time (HIP events); `dominant` = largest total time."""
+    out = {}
+    for k, v in prof.items():
+        if not v["launches"] or not per_msg.get(k):
+            continue
+        avg_ms = v["total_ms"] / v["launches"]
+        ach = per_msg[k] * msgs_per_launch / (avg_ms * 1e-3) / 1e9
+        out[k] = {"achieved": round(ach, 1), "frac": round(ach / PEAK_HBM_GBS, 4), "avg_launch_ms": round(avg_ms, 4),
+                  "alg_bytes_per_launch": per_msg[k] * msgs_per_launch}
+    dom = max((k for k in prof if prof[k]["launches"]), key=lambda k: prof[k]["total_ms"], default=None)
+    return {"bound": "hbm", "peak": PEAK_HBM_GBS, "unit": "GB/s", "dominant": dom, "kernels": out}
+
+
 def cpu_baseline(hops: int) -> dict:
     """fjp_ref (restatement of Dispatcher/Mailbox/ForkJoinPool) on the host cores,
     bounded sample: the same 1M-actor ring with a smaller hop budget."""
@@ -256,13 +271,22 @@ def main():
         n_l = args.large_actors
         per = (n_l + world - 1) // world
         steps_l = args.large_steps
-        _, el_l, dl_l, sd_l = timed_ring(n_l, args.large_warmup + steps_l + 1, args.large_warmup, steps_l, world,
-                                         rank, local, msg_capacity=int(per * (2.5 if world > 1 else 1.25)) + 4096)
+        prof_l = 4
+        eng_l, el_l, dl_l, sd_l = timed_ring(n_l, args.large_warmup + steps_l + prof_l + 2, args.large_warmup, steps_l,
+                                             world, rank, local,
+                                             msg_capacity=int(per * (2.5 if world > 1 else 1.25)) + 4096, keep=True)
+        # per-kernel HIP-event timing at this size (eager launches on the engine stream)
+        eng_l.profile(True)
+        eng_l.profile_reset()
+        eng_l.run(prof_l)
+        pl = eng_l.profile_read()
+        eng_l.close()
         el_l, dl_l = reduce_ranks(el_l, dl_l, world)
         large = {"actors": n_l, "actors_per_gpu": per, "steps": steps_l, "warmup": args.large_warmup,
                  "supersteps_timed": int(sd_l), "value": dl_l / el_l, "unit": "msg/s",
                  "ms_per_step": el_l / steps_l * 1e3, "scaling": "strong",
-                 "superstep_frac": (12 + 12 + 16 * cfg_words + 2) * per / (el_l / steps_l) / 1e9 / PEAK_HBM_GBS}
+                 "superstep_frac": (12 + 12 + 16 * cfg_words + 2) * per / (el_l / steps_l) / 1e9 / PEAK_HBM_GBS,
+                 "roofline": kernel_rooflines(pl, kernel_bytes_per_msg(cfg_words), per)}
 
     value = delivered / elapsed
     # roofline of the dominant kernel (largest total time in the timed region)
