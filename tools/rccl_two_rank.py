@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Diagnostic: the RCCL exchange path (agx_comm_init + run_multi_rccl) with two
+ranks in two processes on the SAME device (a one-GPU box), checked bit-exactly
+against the BSP oracle in the sharded canonical order.  RCCL may refuse two
+ranks on one device; then this reports the refusal and exits 2.
+
+    python tools/rccl_two_rank.py [--n 20000] [--hops 8] [--workload ring|mixed]
+"""
+import argparse
+import os
+import pathlib
+import socket
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _make(a):
+    from akka_amd import workloads as wl
+    if a.workload == "ring":
+        return wl.token_ring(a.n, a.hops)
+    return wl.mixed(a.n, seed=3, throughput=2, capacity=6)
+
+
+def _rank_main(rank, world, port, a, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import numpy as np
+    import torch.distributed as dist
+    from akka_amd.engine import EngineConfig, GpuEngine
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = _make(a)
+        eng = GpuEngine(EngineConfig(device=0, n_ranks=world, rank=rank, **w.engine_kwargs()))
+        w.apply_to(eng)
+        uid = [GpuEngine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0])
+        st = eng.run()
+        ws, al = eng.read_state()
+        eng.close()
+        q.put((rank, "ok", st.__dict__ if hasattr(st, "__dict__") else dict(st._asdict()), ws, al))
+    except Exception as ex:  # report, do not hang the peer
+        q.put((rank, "error", repr(ex), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=20000)
+    ap.add_argument("--hops", type=int, default=8)
+    ap.add_argument("--workload", default="ring")
+    a = ap.parse_args()
+    import numpy as np
+    import torch.multiprocessing as mp
+    from akka_amd.engine import owner
+    from oracle import BspOracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, a, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+    errs = [r for r in res if r[1] != "ok"]
+    if errs:
+        print("RCCL two-rank run failed:", errs)
+        sys.exit(2)
+    w = _make(a)
+    ref = BspOracle(n_ranks=world, **w.engine_kwargs())
+    w.apply_to(ref)
+    so = ref.run()
+    wo, ao = ref.read_state()
+    wg = np.zeros_like(wo)
+    ag = np.zeros_like(ao)
+    own_of = np.array([owner(i, 1000, world) for i in range(w.n_actors)])
+    tot = {}
+    for rank, _, st, ws, al in res:
+        own = own_of == rank
+        wg[own] = ws[own]
+        ag[own] = al[own]
+        for k, v in st.items():
+            tot[k] = tot.get(k, 0) + v
+    print("gpu (sum over ranks):", {k: tot[k] for k in ("delivered", "dead_letters", "unhandled", "emitted", "staged")})
+    print("oracle:", {k: so[k] for k in ("delivered", "dead_letters", "unhandled", "emitted", "staged")})
+    keys = ("delivered", "dead_letters", "unhandled", "emitted", "staged")
+    # (per-rank counters, or counters already reduced over the ranks)
+    ok = all(tot[k] == so[k] for k in keys) or all(r[2][k] == so[k] for r in res for k in keys)
+    ok = ok and np.array_equal(wg, wo) and np.array_equal(ag, ao)
+    print("RCCL two-rank parity:", "OK" if ok else "MISMATCH")
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()
