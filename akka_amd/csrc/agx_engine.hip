@@ -177,6 +177,15 @@ struct agx_engine {
   bool graphs_enabled = true;
   hipGraphExec_t g1 = nullptr, gG = nullptr;
   hipGraphExec_t g1p[2] = {nullptr, nullptr}, gGp[2] = {nullptr, nullptr};  // fused: per starting parity
+  // fused "strict" replays: graphs without the (usually empty) skew-list launches.  A superstep that
+  // defers a skewed bucket marks d_abort; the rest of the replay is void and run_single runs the
+  // deferred skew launch, then continues with the full graphs (strict_ok cleared for this engine).
+  hipGraphExec_t gs1p[2] = {nullptr, nullptr}, gsGp[2] = {nullptr, nullptr};
+  uint32_t* d_abort = nullptr;  // [2] (BucketArgs::abort)
+  uint32_t* h_abort = nullptr;  // pinned [kLag][2]: the marks after each replay
+  bool strict_ok = true;        // AGX_NO_STRICT=1 disables
+  bool strict_cap = false;      // the superstep being launched / captured is strict
+  bool skew_only = false;       // recovery: the deferred skew launch alone
   unsigned long long* d_dbg = nullptr;  // AGX_STAMPS diagnostic build only
 
   // profiling
@@ -430,6 +439,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   if (e->fused) {
     ba.par = e->par;
     ba.slot = e->cur_slot;
+    if (e->strict_cap) ba.abort = e->d_abort;
     ba.P.step = e->d_parv + e->par;  // CRDT heap parity = superstep parity
   }
   if (e->fused) {
@@ -480,9 +490,9 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     const dim3 gs(grid_for(e->nb, std::min(e->apply_grid, e->skew_grid)));  // skew list (grid-stride)
 #define AGX_APPLY2(W, M, G, O)                                                                   \
   do {                                                                                           \
-    { Scope s(e, K_APPLY);                                                                       \
+    if (!e->skew_only) { Scope s(e, K_APPLY);                                                    \
       hipLaunchKernelGGL((k_bucket_apply<W, M, G, false, O>), g, blk, 0, e->stream, ba); }       \
-    { Scope s(e, K_SKEW);                                                                        \
+    if (!(G && e->strict_cap)) { Scope s(e, K_SKEW);                                             \
       hipLaunchKernelGGL((k_bucket_apply<W, M, G, true, O>), gs, blk, 0, e->stream, ba); }       \
   } while (0)
 #define AGX_APPLY(W, M)                                                                          \
@@ -795,21 +805,33 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     --left;
   }
   const bool use_graph = !e->prof && e->graphs_enabled;
-  auto graph1 = [&]() -> hipGraphExec_t& { return e->fused ? e->g1p[e->par] : e->g1; };
-  auto graphG = [&]() -> hipGraphExec_t& { return e->fused ? e->gGp[e->par] : e->gG; };
+  bool strict = e->fused && use_graph && e->strict_ok;  // replays without skew launches (see d_abort)
+  auto graph1 = [&]() -> hipGraphExec_t& {
+    return e->fused ? (strict ? e->gs1p[e->par] : e->g1p[e->par]) : e->g1;
+  };
+  auto graphG = [&]() -> hipGraphExec_t& {
+    return e->fused ? (strict ? e->gsGp[e->par] : e->gGp[e->par]) : e->gG;
+  };
   auto ensure_graphs = [&]() -> agx_status {
     if (!use_graph || graph1()) return AGX_OK;
     const uint32_t p0 = e->par;  // capturing advances the host parity: restore it
+    e->strict_cap = strict;
     agx_status s2 = capture_steps(e, 1, &graph1());
     e->par = p0;
     if (s2 == AGX_OK) s2 = capture_steps(e, agx_engine::kGraphSteps, &graphG());
     e->par = p0;
+    e->strict_cap = false;
     return s2;
   };
   // fused: per-superstep inbox sizes of each replay (pinned ring); the host counts the supersteps
   // with mail and stops at the first replay whose last superstep had none (quiescent)
   uint32_t rep_steps[kLag] = {0, 0, 0, 0};
+  uint32_t rep_start[kLag] = {0, 0, 0, 0}, rep_par[kLag] = {0, 0, 0, 0};  // supersteps launched before it; parity
+  bool rep_strict[kLag] = {false, false, false, false}, rep_void[kLag] = {false, false, false, false};
   const size_t ring_row = (size_t)agx_engine::kGraphSteps * e->nb;
+  const uint32_t left0 = left;
+  uint32_t launched_steps = 0;
+  bool recovered = false;
   auto fused_poll = [&](uint32_t slot) -> bool {
     const uint32_t* h = e->h_cntb + slot * ring_row;
     bool last_empty = rep_steps[slot] > 0;
@@ -822,18 +844,68 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     rep_steps[slot] = 0;
     return last_empty;
   };
+  // A strict replay whose superstep k deferred a skewed bucket: supersteps after k (and every
+  // replay launched after it) were no-ops.  Run k's skew launch, count k + 1 supersteps for this
+  // replay, void the later ones, continue with the full graphs.
+  auto recover = [&](uint32_t slot, uint32_t k) -> agx_status {
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->par = rep_par[slot] ^ (k & 1u);
+    e->cur_slot = k;
+    e->skew_only = true;
+    agx_status s2 = launch_apply(e, e->A);  // (advances e->par past superstep k)
+    e->skew_only = false;
+    e->cur_slot = 0;
+    AGX_TRY(s2);
+    HIP_TRY(hipMemcpyAsync(e->h_cntb + slot * ring_row + (size_t)k * e->nb, e->d_cntb + (size_t)k * e->nb,
+                           (size_t)e->nb * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemsetAsync(e->d_abort, 0, 8, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    rep_steps[slot] = k + 1u;
+    for (uint32_t q = 0; q < kLag; ++q)
+      if (q != slot && rep_steps[q]) rep_void[q] = true;
+    left = left0 - (rep_start[slot] + k + 1u);
+    strict = false;
+    e->strict_ok = false;
+    recovered = true;
+    return AGX_OK;
+  };
+  auto poll = [&](uint32_t slot) -> bool {  // true: quiescent
+    if (rep_void[slot]) {
+      rep_void[slot] = false;
+      rep_steps[slot] = 0;
+      return false;
+    }
+    if (rep_strict[slot] && rep_steps[slot]) {
+      const uint32_t* ha = e->h_abort + 2 * slot;
+      const uint32_t ab = ha[0] ? ha[0] : ha[1];
+      if (ab) {
+        const agx_status s2 = recover(slot, ab - 1u);
+        if (s2 != AGX_OK) {
+          st = s2;
+          return true;
+        }
+      }
+    }
+    return fused_poll(slot);
+  };
   uint32_t launched = 0;
+  bool quiet = false;
   for (uint32_t it = 0; st == AGX_OK && left > 0; ++it) {
     const uint32_t slot = it % kLag;
     if (it >= kLag) {
       hipEventSynchronize(ev[slot]);
       if (e->fused) {
-        if (fused_poll(slot)) break;
+        if (poll(slot)) {
+          quiet = true;
+          break;
+        }
+        if (left == 0) break;  // (a recovery recounted the supersteps run)
       } else if (e->h_pin[slot] == 0) {
         break;  // that replay ended on a superstep with no mail: quiescent
       }
     }
     uint32_t cnt;
+    const uint32_t par0 = e->par;
     if (use_graph) {
       st = ensure_graphs();
       if (st != AGX_OK) break;
@@ -849,17 +921,28 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     ++launched;
     if (e->fused) {  // per-superstep inbox sizes of this replay
       rep_steps[slot] = cnt;
+      rep_start[slot] = launched_steps;
+      rep_par[slot] = par0;
+      rep_strict[slot] = strict;
+      rep_void[slot] = false;
       hipMemcpyAsync(e->h_cntb + slot * ring_row, e->d_cntb, (size_t)cnt * e->nb * 4, hipMemcpyDeviceToHost,
                      e->stream);
+      if (strict) hipMemcpyAsync(e->h_abort + 2 * slot, e->d_abort, 8, hipMemcpyDeviceToHost, e->stream);
     } else {  // inbox total (sorted + backlog) of the replay's last superstep
       hipMemcpyAsync(&e->h_pin[slot], e->d_ninbox, 4, hipMemcpyDeviceToHost, e->stream);
     }
+    launched_steps += cnt;
     hipEventRecord(ev[slot], e->stream);
   }
   hipStreamSynchronize(e->stream);
-  if (e->fused)  // replays not polled yet, in launch order
-    for (uint32_t k = launched > kLag ? launched - kLag : 0; k < launched; ++k) fused_poll(k % kLag);
+  if (e->fused && !quiet)  // replays not polled yet, in launch order
+    for (uint32_t k = launched > kLag ? launched - kLag : 0; k < launched && st == AGX_OK; ++k)
+      if (poll(k % kLag)) {
+        quiet = true;
+        break;
+      }
   for (auto& x : ev) hipEventDestroy(x);
+  if (st == AGX_OK && recovered && !quiet && left > 0) return run_single(e, left);  // full graphs now
   return st;
 }
 
@@ -932,7 +1015,9 @@ void drop_graphs(agx_engine* e) {
   for (int q = 0; q < 2; ++q) {
     if (e->g1p[q]) hipGraphExecDestroy(e->g1p[q]);
     if (e->gGp[q]) hipGraphExecDestroy(e->gGp[q]);
-    e->g1p[q] = e->gGp[q] = nullptr;
+    if (e->gs1p[q]) hipGraphExecDestroy(e->gs1p[q]);
+    if (e->gsGp[q]) hipGraphExecDestroy(e->gsGp[q]);
+    e->g1p[q] = e->gGp[q] = e->gs1p[q] = e->gsGp[q] = nullptr;
   }
 }
 
@@ -1077,6 +1162,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   // arenas; an inbox larger than the region (skew) takes a slot of the overflow area that
   // follows, sized like the whole message capacity — no shared counter on the common path
   e->region = kBucket;
+  if (getenv("AGX_NO_STRICT")) e->strict_ok = false;
   if (const char* s = getenv("AGX_SKEW_GRID"))
     e->skew_grid = (uint32_t)std::min<int>(kMaxApplyGrid, std::max(1, atoi(s)));
   if (const char* s = getenv("AGX_APPLY_GRID"))
@@ -1155,6 +1241,10 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(hipMemcpy(e->d_parv, parv, 8, hipMemcpyHostToDevice) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "upload"));
     CREATE_TRY(hipMemset(e->d_stg_cnt, 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(hipMemset(e->d_ovf, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    CREATE_TRY(dalloc(&e->d_abort, 2));
+    CREATE_TRY(hipMemset(e->d_abort, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    CREATE_TRY(hipHostMalloc((void**)&e->h_abort, 4 * 2 * 4, hipHostMallocDefault) == hipSuccess
+                   ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
   }
   CREATE_TRY(dalloc(&e->d_skew_list, e->nb));
   CREATE_TRY(dalloc(&e->d_skew_n, 2));
@@ -1211,6 +1301,8 @@ agx_status agx_destroy(agx_engine* e) {
   }
   hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_cntb);
   if (e->h_cntb) hipHostFree(e->h_cntb); hipFree(e->d_parv);
+  hipFree(e->d_abort);
+  if (e->h_abort) hipHostFree(e->h_abort);
   hipFree(e->d_skew_list); hipFree(e->d_skew_n);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_blpre); hipFree(e->d_ninbox); hipFree(e->d_n); hipFree(e->d_total);

@@ -740,6 +740,10 @@ struct BucketArgs {
   uint64_t* stats;
   unsigned long long* bstats;  // [gridDim][kBStats] per-block counters (summed by k_stats_reduce)
   unsigned long long* dbg;  // diagnostic build only (AGX_STAMPS): per-block phase timestamps
+  // fused graphs without skew launches ("strict" replays, null otherwise): [parity] -> 1 + the replay
+  // slot of a superstep that deferred a skewed bucket; every later superstep is a no-op that
+  // passes the mark on, and the host runs the deferred skew launch and resumes (run_single)
+  uint32_t* abort;
 };
 
 #define AGX_STAMP(a, idx)                                                                         \
@@ -1387,6 +1391,13 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   // fused / bypass: write parity w, read parity w ^ 1
   const uint32_t wpar = kGather ? a.par : kBypass ? (*a.pstep & 1u) : 0u, rpar = wpar ^ 1u;
   uint32_t* const skew_n = a.skew_n + (kGather ? wpar : 0u);  // (non-fused: one list, reset by the sort)
+  if (kGather && !kSkew && a.abort) {
+    const uint32_t ab = a.abort[rpar];  // an earlier superstep of this replay deferred a bucket
+    if (ab) {
+      if (tid == 0) a.abort[wpar] = ab;  // (pass it on: the next superstep reads this parity)
+      return;
+    }
+  }
   if (kGather && !kSkew && blockIdx.x == 0 && tid == 0) {
     // reset the per-parity cursors that the NEXT superstep (parity rpar) will use (the previous
     // superstep, which used them, is complete)
@@ -1469,7 +1480,10 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         s_g[4] = ns;
         const uint32_t cnt = blc + tt + s_g[2];
         s_g[5] = cnt > (uint32_t)kBucket;
-        if (kDefer && s_g[5]) a.skew_list[atomicAdd(skew_n, 1u)] = b;
+        if (kDefer && s_g[5]) {
+          a.skew_list[atomicAdd(skew_n, 1u)] = b;
+          if (a.abort) a.abort[wpar] = a.slot + 1u;  // strict replay: the rest of it is void
+        }
         // inbox slot: the bucket's own region (no shared counter), else the overflow region
         uint64_t lo = (uint64_t)b * g.region;
         if (kDefer && s_g[5]) {

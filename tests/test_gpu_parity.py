@@ -82,6 +82,32 @@ def test_partial_run_and_resume(built):
     eng.close()
 
 
+@pytest.mark.parametrize("budgets", [(1000,), (3, 4, 1000)])
+@pytest.mark.parametrize("strict", [True, False])
+def test_strict_replay_recovery(built, monkeypatch, strict, budgets):
+    """Fused graphs without skew launches ("strict" replays): Zipf fan-out (k = 4) multiplies the
+    mail each hop until a hot bucket's inbox passes one LDS tile a few supersteps in -- in the
+    middle of an 8-superstep replay (one long run) or while single-superstep replays are in flight
+    (short budgets).  The rest of that replay is void, the deferred skew launch runs, the run goes
+    on with the full graphs; every budget must match the oracle (and the full-graph mode)."""
+    from oracle import BspOracle
+    if not strict:
+        monkeypatch.setenv("AGX_NO_STRICT", "1")
+    w = wl.zipf_fanout(20_000, k=4, ttl=6, root_every=256, throughput=1000)
+    eng = GpuEngine(EngineConfig(msg_capacity=1 << 20, **w.engine_kwargs()))  # (234 K in flight at the peak)
+    w.apply_to(eng)
+    ref = BspOracle(**w.engine_kwargs())
+    w.apply_to(ref)
+    for budget in budgets:
+        sg = eng.run(budget)
+        so = ref.run(budget)
+        for k in COUNT_KEYS:
+            assert getattr(sg, k) == so[k], (budget, k, getattr(sg, k), so[k])
+        assert np.array_equal(eng.read_state()[0], ref.read_state()[0]), budget
+    assert sg.in_flight == 0
+    eng.close()
+
+
 def test_ping_pong(built):
     w = wl.ping_pong(pairs=200, messages_per_pair=300, throughput=50)
     sg, so, a, b = run_both(w)
