@@ -1026,7 +1026,13 @@ agx_status enable_crdt(agx_engine* e, uint32_t kind) {
   const uint32_t words = kind == AGX_KIND_GCOUNTER ? AGX_GCOUNTER_WORDS
                          : kind == AGX_KIND_PNCOUNTER ? AGX_PNCOUNTER_WORDS : AGX_ORSET_WORDS;
   if (e->W < words) return set_err(AGX_EINVAL, "behaviour kind %u needs n_words >= %u", kind, words);
-  const uint32_t pw = 2 * words;
+#ifndef AGX_ROW_ALIGN
+#define AGX_ROW_ALIGN 32
+#endif
+  // row pitch in u32: rows wider than one 128-B line start on a line boundary (ORSet: 2080 B
+  // rows padded to 2176 B), so a merge's batched row loads never split a line between rows
+  const uint32_t pw = 2 * words > AGX_ROW_ALIGN ? (2 * words + AGX_ROW_ALIGN - 1) / AGX_ROW_ALIGN * AGX_ROW_ALIGN
+                                                : 2 * words;
   if (pw <= e->pw) return AGX_OK;
   if (e->started) return set_err(AGX_ESTATE, "register CRDT kinds before the first agx_run");
   const uint64_t rows = (uint64_t)e->nb * kBucket + e->cap;
