@@ -195,12 +195,12 @@ __device__ __forceinline__ uint32_t apply_msg(const DevParams& P, uint32_t kind,
       if constexpr ((KM & kb(AGX_KIND_FANOUT)) != 0) {
         w[0] += 1;
         w[1] += pay;
-        const uint32_t ttl = pay >> 28, h = pay & 0x0FFFFFFFu;
+        const uint32_t ttl = pay >> 24, h = pay & 0x00FFFFFFu;  // ttl 8 bits, hash 24 bits
         if (ttl > 0)
           for (uint32_t j = 0; j < P.fan_k; ++j) {
             uint64_t r = fanout_rand(P.fan_seed, self, h, j);
             uint32_t d = P.zipf_perm[zipf_index(P.zipf_cdf, P.zipf_idx, r)];
-            emit(d, ((ttl - 1) << 28) | ((uint32_t)r & 0x0FFFFFFFu));
+            emit(d, ((ttl - 1) << 24) | ((uint32_t)r & 0x00FFFFFFu));
           }
       }
       return AGX_RES_SAME;

@@ -91,6 +91,11 @@ const char* kClassNames[K_NCLASS] = {"chunk_rowscan", "chunk_downsweep", "sort_u
                                      "sort_downsweep", "bucket_apply", "exchange", "mcompact", "bucket_apply_skew",
                                      "fused_tick", "bucket_bounds"};
 
+constexpr uint32_t kGraphSizes[5] = {1, 2, 4, 8, 16};  // superstep replays (agx_engine::gx)
+constexpr uint32_t kStatBlk = 16;                    // d_stats block (see agx_engine::d_stats)
+constexpr uint32_t kStatSred = ST_N, kStatInfl = ST_N + kBStats;
+static_assert(kStatInfl < kStatBlk, "stats block layout");
+
 struct SortPlan {  // LSD passes over key bits [kBucketBits, key_bits)
   uint32_t npass = 1;
   uint32_t shift[4] = {0}, bits[4] = {0};
@@ -142,7 +147,10 @@ struct agx_engine {
   uint32_t* d_hist_d = nullptr;  // [kRadix][dstride] dense-pass histograms per super-tile
   uint32_t *d_tot = nullptr, *d_bstart = nullptr, *d_n = nullptr, *d_total = nullptr, *d_moff0 = nullptr, *d_moff1 = nullptr;
   unsigned long long *d_bstats = nullptr, *d_sred = nullptr;  // per-block apply counters, their sum
+  // d_stats = one block of kStatBlk u64: [0, ST_N) counters, [ST_N, +kBStats) = d_sred (sum of the
+  // per-block apply counters), [kStatInfl] = d_inflight -- read back with ONE copy + ONE sync
   uint64_t *d_stats = nullptr, *d_cvec = nullptr, *d_cmat = nullptr, *d_inflight = nullptr;
+  uint64_t* h_stat = nullptr;    // pinned copy of the d_stats block
   uint32_t* h_pin = nullptr;     // pinned ring of per-step totals
   uint64_t* h_pin64 = nullptr;   // pinned scratch (count matrix, stats)
 
@@ -173,17 +181,22 @@ struct agx_engine {
   ncclComm_t comm = nullptr;
   bool started = false;
   // superstep graphs (single rank)
-  static constexpr uint32_t kGraphSteps = 8;
+  static constexpr uint32_t kGraphSteps = 16;  // largest replay (kGraphSizes = 1, 2, 4, 8, 16)
   bool graphs_enabled = true;
-  hipGraphExec_t g1 = nullptr, gG = nullptr;
-  hipGraphExec_t g1p[2] = {nullptr, nullptr}, gGp[2] = {nullptr, nullptr};  // fused: per starting parity
+  // gx[strict][parity][size]: replays of kGraphSizes[size] supersteps; fused graphs exist per
+  // starting parity (the parity is a kernel argument), multi-pass ones use gx[0][0][*].  A budget
+  // of K supersteps replays its binary decomposition (20 = 16 + 4), never a run of singles.
+  static constexpr uint32_t kNSizes = 5;
+  hipGraphExec_t gx[2][2][kNSizes] = {};
   // fused "strict" replays: graphs without the (usually empty) skew-list launches.  A superstep that
   // defers a skewed bucket marks d_abort; the rest of the replay is void and run_single runs the
   // deferred skew launch, then continues with the full graphs (strict_ok cleared for this engine).
-  hipGraphExec_t gs1p[2] = {nullptr, nullptr}, gsGp[2] = {nullptr, nullptr};
   uint32_t* d_abort = nullptr;  // [2] (BucketArgs::abort)
   uint32_t* h_abort = nullptr;  // pinned [kLag][2]: the marks after each replay
   bool strict_ok = true;        // AGX_NO_STRICT=1 disables
+  bool strict_env = true;       // (the AGX_NO_STRICT knob; strict_ok is re-armed after clean replays)
+  uint32_t clean_steps = 0;     // fused supersteps since the last skewed bucket (full graphs)
+  hipEvent_t lag_ev[4] = {};    // run_single's replay events (created once)
   bool strict_cap = false;      // the superstep being launched / captured is strict
   bool skew_only = false;       // recovery: the deferred skew launch alone
   unsigned long long* d_dbg = nullptr;  // AGX_STAMPS diagnostic build only
@@ -705,42 +718,11 @@ agx_status sync_mirrors(agx_engine* e) {
   return AGX_OK;
 }
 
-agx_status check_error(agx_engine* e) {
-  uint64_t err = 0;
-  HIP_TRY(hipMemcpy(&err, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost));
-  if (err & kErrCapacity)
-    return set_err(AGX_ECAPACITY, "in-flight messages exceeded engine capacity (msg_capacity=%llu)",
-                   (unsigned long long)e->cap);
-  return AGX_OK;
-}
-
-agx_status fill_stats(agx_engine* e, agx_stats* out, uint64_t inflight) {
-  uint64_t s[ST_N], bs[kBStats];
+// One read-back of every counter: the apply's per-block counters are summed and the messages in
+// flight (backlog + tells of the last apply + staged) counted on the device, into the d_stats
+// block, which comes back with ONE copy and ONE stream sync.
+agx_status read_counters(agx_engine* e, uint64_t* s) {
   hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_bstats, kMaxApplyGrid, e->d_sred);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipMemcpy(s, e->d_stats, sizeof s, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(bs, e->d_sred, sizeof bs, hipMemcpyDeviceToHost));
-  s[ST_DELIVERED] = bs[0];
-  s[ST_DEAD] += bs[1];
-  s[ST_UNHANDLED] = bs[2];
-  s[ST_EMITTED] = bs[3];
-  s[ST_ACTIVE] = bs[4];
-  agx_stats st{};
-  st.delivered = s[ST_DELIVERED];
-  st.dead_letters = s[ST_DEAD] + e->staged_dead;
-  st.unhandled = s[ST_UNHANDLED];
-  st.emitted = s[ST_EMITTED];
-  st.staged = e->staged_total;
-  st.supersteps = s[ST_STEPS] + e->host_steps;
-  st.in_flight = inflight;
-  // SURVEY.md §8(d): B = E_in + f_out*E_out + 2*S*(A/M); kind+alive bytes read per activation
-  st.bytes_alg = 12ull * st.delivered + 12ull * (st.emitted) + (16ull * e->W + 2ull) * s[ST_ACTIVE];
-  if (out) *out = st;
-  return AGX_OK;
-}
-
-agx_status chunk_inflight(agx_engine* e, uint64_t* out) {
   if (e->fused)
     hipLaunchKernelGGL(k_inflight_fused, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_blc[0], e->d_blc[1],
                        e->d_emc[0], e->d_emc[1], e->d_stg_cnt, e->par ^ 1u, e->nb, (unsigned long long*)e->d_inflight);
@@ -748,9 +730,32 @@ agx_status chunk_inflight(agx_engine* e, uint64_t* out) {
     hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_chunk_cnt, e->nchunks,
                        (unsigned long long*)e->d_inflight);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_inflight, 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->h_stat, e->d_stats, kStatBlk * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  *out = e->h_pin64[0];
+  memcpy(s, e->h_stat, kStatBlk * 8);
+  return AGX_OK;
+}
+
+// counters -> agx_stats; check: report a capacity overflow recorded by the kernels
+agx_status collect_stats(agx_engine* e, agx_stats* out, bool check) {
+  uint64_t s[kStatBlk];
+  AGX_TRY(read_counters(e, s));
+  if (check && (s[ST_ERROR] & kErrCapacity))
+    return set_err(AGX_ECAPACITY, "in-flight messages exceeded engine capacity (msg_capacity=%llu)",
+                   (unsigned long long)e->cap);
+  const uint64_t* bs = s + kStatSred;
+  agx_stats st{};
+  st.delivered = bs[0];
+  st.dead_letters = s[ST_DEAD] + bs[1] + e->staged_dead;
+  st.unhandled = bs[2];
+  st.emitted = bs[3];
+  st.staged = e->staged_total;
+  st.supersteps = s[ST_STEPS] + e->host_steps;
+  // backlog + tells produced by the last apply, plus host tells not yet consumed
+  st.in_flight = s[kStatInfl] + e->n_staged_dev + e->hs_key.size();
+  // SURVEY.md §8(d): B = E_in + f_out*E_out + 2*S*(A/M); kind+alive bytes read per activation
+  st.bytes_alg = 12ull * st.delivered + 12ull * st.emitted + (16ull * e->W + 2ull) * bs[4];
+  if (out) *out = st;
   return AGX_OK;
 }
 
@@ -789,8 +794,9 @@ agx_status capture_steps(agx_engine* e, uint32_t steps, hipGraphExec_t* out) {
 
 agx_status run_single(agx_engine* e, uint32_t max_steps) {
   constexpr uint32_t kLag = 4;  // replays in flight before the host polls quiescence
-  std::vector<hipEvent_t> ev(kLag);
-  for (auto& x : ev) HIP_TRY(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+  for (auto& x : e->lag_ev)
+    if (!x) HIP_TRY(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+  hipEvent_t* ev = e->lag_ev;
   agx_status st = AGX_OK;
   uint32_t left = max_steps;
   // staged host tells enter through an eager step (the graphs assume none)
@@ -806,19 +812,24 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
   }
   const bool use_graph = !e->prof && e->graphs_enabled;
   bool strict = e->fused && use_graph && e->strict_ok;  // replays without skew launches (see d_abort)
-  auto graph1 = [&]() -> hipGraphExec_t& {
-    return e->fused ? (strict ? e->gs1p[e->par] : e->g1p[e->par]) : e->g1;
+  auto size_idx = [](uint32_t l) -> uint32_t { return l >= 16 ? 4u : l >= 8 ? 3u : l >= 4 ? 2u : l >= 2 ? 1u : 0u; };
+  auto graph = [&](uint32_t si) -> hipGraphExec_t& {
+    return e->fused ? e->gx[strict][e->par][si] : e->gx[0][0][si];
   };
-  auto graphG = [&]() -> hipGraphExec_t& {
-    return e->fused ? (strict ? e->gsGp[e->par] : e->gGp[e->par]) : e->gG;
-  };
+  // every replay size (and, fused, both starting parities) is captured at first use, so no
+  // capture ever lands in the middle of a later budget
   auto ensure_graphs = [&]() -> agx_status {
-    if (!use_graph || graph1()) return AGX_OK;
+    if (!use_graph) return AGX_OK;
     const uint32_t p0 = e->par;  // capturing advances the host parity: restore it
     e->strict_cap = strict;
-    agx_status s2 = capture_steps(e, 1, &graph1());
-    e->par = p0;
-    if (s2 == AGX_OK) s2 = capture_steps(e, agx_engine::kGraphSteps, &graphG());
+    agx_status s2 = AGX_OK;
+    for (uint32_t p = 0; p < (e->fused ? 2u : 1u) && s2 == AGX_OK; ++p)
+      for (uint32_t si = 0; si < agx_engine::kNSizes && s2 == AGX_OK; ++si) {
+        hipGraphExec_t& g = e->fused ? e->gx[strict][p][si] : e->gx[0][0][si];
+        if (g) continue;
+        e->par = p;
+        s2 = capture_steps(e, kGraphSizes[si], &g);
+      }
     e->par = p0;
     e->strict_cap = false;
     return s2;
@@ -837,8 +848,14 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     bool last_empty = rep_steps[slot] > 0;
     for (uint32_t i = 0; i < rep_steps[slot]; ++i) {
       uint64_t t = 0;
-      for (uint32_t b = 0; b < e->nb; ++b) t += h[(size_t)i * e->nb + b];
+      bool skew = false;  // a bucket's inbox over one LDS tile (it took the skew launch)
+      for (uint32_t b = 0; b < e->nb; ++b) {
+        const uint32_t v = h[(size_t)i * e->nb + b];
+        t += v;
+        skew |= v > (uint32_t)kBucket;
+      }
       if (t) ++e->host_steps;
+      e->clean_steps = skew ? 0u : e->clean_steps + 1u;
       last_empty = t == 0;
     }
     rep_steps[slot] = 0;
@@ -900,6 +917,12 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
           break;
         }
         if (left == 0) break;  // (a recovery recounted the supersteps run)
+        // two full replays without a skewed bucket: back to the strict graphs (a workload whose
+        // skew was transient -- a Zipf burst -- regains the cheaper replays)
+        if (!strict && use_graph && e->strict_env && e->clean_steps >= 2 * agx_engine::kGraphSteps) {
+          strict = true;
+          e->strict_ok = true;
+        }
       } else if (e->h_pin[slot] == 0) {
         break;  // that replay ended on a superstep with no mail: quiescent
       }
@@ -909,8 +932,9 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     if (use_graph) {
       st = ensure_graphs();
       if (st != AGX_OK) break;
-      cnt = left >= agx_engine::kGraphSteps ? agx_engine::kGraphSteps : 1;
-      hipError_t ge = hipGraphLaunch(cnt == 1 ? graph1() : graphG(), e->stream);
+      const uint32_t si = size_idx(left);
+      cnt = kGraphSizes[si];
+      hipError_t ge = hipGraphLaunch(graph(si), e->stream);
       if (ge != hipSuccess) st = set_err(AGX_EDEVICE, "hipGraphLaunch: %s", hipGetErrorString(ge));
       if (e->fused && (cnt & 1u)) e->par ^= 1u;  // the replayed supersteps advanced the parity
     } else {
@@ -941,7 +965,6 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
         quiet = true;
         break;
       }
-  for (auto& x : ev) hipEventDestroy(x);
   if (st == AGX_OK && recovered && !quiet && left > 0) return run_single(e, left);  // full graphs now
   return st;
 }
@@ -1009,16 +1032,12 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
 }
 
 void drop_graphs(agx_engine* e) {
-  if (e->g1) hipGraphExecDestroy(e->g1);
-  if (e->gG) hipGraphExecDestroy(e->gG);
-  e->g1 = e->gG = nullptr;
-  for (int q = 0; q < 2; ++q) {
-    if (e->g1p[q]) hipGraphExecDestroy(e->g1p[q]);
-    if (e->gGp[q]) hipGraphExecDestroy(e->gGp[q]);
-    if (e->gs1p[q]) hipGraphExecDestroy(e->gs1p[q]);
-    if (e->gsGp[q]) hipGraphExecDestroy(e->gsGp[q]);
-    e->g1p[q] = e->gGp[q] = e->gs1p[q] = e->gsGp[q] = nullptr;
-  }
+  for (auto& a : e->gx)
+    for (auto& b : a)
+      for (auto& g : b) {
+        if (g) hipGraphExecDestroy(g);
+        g = nullptr;
+      }
 }
 
 // First CRDT kind (or a wider one): size the snapshot heap for `kind`'s rows.
@@ -1168,7 +1187,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   // arenas; an inbox larger than the region (skew) takes a slot of the overflow area that
   // follows, sized like the whole message capacity — no shared counter on the common path
   e->region = kBucket;
-  if (getenv("AGX_NO_STRICT")) e->strict_ok = false;
+  if (getenv("AGX_NO_STRICT")) e->strict_ok = e->strict_env = false;
   if (const char* s = getenv("AGX_SKEW_GRID"))
     e->skew_grid = (uint32_t)std::min<int>(kMaxApplyGrid, std::max(1, atoi(s)));
   if (const char* s = getenv("AGX_APPLY_GRID"))
@@ -1267,20 +1286,21 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(dalloc(&e->d_tot, kRadix));
   CREATE_TRY(dalloc(&e->d_n, 4));
   CREATE_TRY(dalloc(&e->d_total, 4));
-  CREATE_TRY(dalloc(&e->d_stats, ST_N));
+  CREATE_TRY(dalloc(&e->d_stats, kStatBlk));
+  e->d_sred = (unsigned long long*)(e->d_stats + kStatSred);
+  e->d_inflight = e->d_stats + kStatInfl;
   CREATE_TRY(dalloc(&e->d_bstats, (uint64_t)kMaxApplyGrid * kBStats));
-  CREATE_TRY(dalloc(&e->d_sred, kBStats));
   CREATE_TRY(hipMemset(e->d_bstats, 0, (uint64_t)kMaxApplyGrid * kBStats * 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_heap_top, 2));
   CREATE_TRY(dalloc(&e->d_step, 1));
   CREATE_TRY(hipMemset(e->d_heap_top, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(hipMemset(e->d_step, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-  CREATE_TRY(dalloc(&e->d_inflight, 1));
   CREATE_TRY(dalloc(&e->d_cvec, AGX_MAX_RANKS + 2));
   CREATE_TRY(dalloc(&e->d_cmat, (uint64_t)AGX_MAX_RANKS * (AGX_MAX_RANKS + 2)));
   CREATE_TRY(hipMemset(e->d_n, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(hipMemset(e->d_total, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-  CREATE_TRY(hipMemset(e->d_stats, 0, ST_N * 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipMemset(e->d_stats, 0, kStatBlk * 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(hipHostMalloc((void**)&e->h_stat, kStatBlk * 8, hipHostMallocDefault) == hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
   CREATE_TRY(hipHostMalloc((void**)&e->h_pin, 64 * 4, hipHostMallocDefault) == hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
   CREATE_TRY(hipHostMalloc((void**)&e->h_pin64, (AGX_MAX_RANKS * (AGX_MAX_RANKS + 2) + 8) * 8, hipHostMallocDefault) == hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
   // empty graph rows so FORWARD_RR on an engine without a graph is well defined
@@ -1312,7 +1332,10 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_skew_list); hipFree(e->d_skew_n);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_blpre); hipFree(e->d_ninbox); hipFree(e->d_n); hipFree(e->d_total);
-  hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_sred); hipFree(e->d_inflight); hipFree(e->d_cvec); hipFree(e->d_cmat);
+  hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_cvec); hipFree(e->d_cmat);
+  if (e->h_stat) hipHostFree(e->h_stat);
+  for (auto ev : e->lag_ev)
+    if (ev) hipEventDestroy(ev);
   hipFree(e->d_heap); hipFree(e->d_heap_top); hipFree(e->d_step); hipFree(e->d_rx); hipFree(e->d_s2rows);
   if (e->h_pin) hipHostFree(e->h_pin);
   if (e->h_pin64) hipHostFree(e->h_pin64);
@@ -1531,18 +1554,15 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
     fprintf(stderr, "\n");
     HIP_TRY(hipMemset(e->d_dbg, 0, h.size() * 8));
   }
-  AGX_TRY(check_error(e));
-  return agx_get_stats(e, out);
+  // out == NULL: no counter read-back (one stream round trip less); agx_get_stats reads them
+  // later and reports a capacity overflow recorded meanwhile
+  return out ? collect_stats(e, out, true) : AGX_OK;
 }
 
 agx_status agx_get_stats(agx_engine* e, agx_stats* out) {
   if (!e) return set_err(AGX_EINVAL, "null engine");
   AGX_TRY(ensure_dev(e));
-  uint64_t infl = 0;
-  // backlog + tells produced by the last apply (chunks), plus host tells not yet consumed
-  AGX_TRY(chunk_inflight(e, &infl));
-  infl += e->n_staged_dev + e->hs_key.size();
-  return fill_stats(e, out, infl);
+  return collect_stats(e, out, true);
 }
 
 agx_status agx_read_state(agx_engine* e, uint64_t first_id, uint64_t count, uint64_t* words, uint8_t* alive) {
@@ -1637,9 +1657,8 @@ agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_steps, agx_
   agx_stats tot{};
   for (uint32_t i = 0; i < n; ++i) {
     prof_collect(engs[i]);
-    AGX_TRY(check_error(engs[i]));
     agx_stats st{};
-    AGX_TRY(agx_get_stats(engs[i], &st));
+    AGX_TRY(collect_stats(engs[i], &st, true));
     tot.delivered += st.delivered;
     tot.dead_letters += st.dead_letters;
     tot.unhandled += st.unhandled;

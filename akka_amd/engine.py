@@ -183,7 +183,11 @@ class GpuEngine:
         check(self.lib.agx_stage_tells(self._h, _ptr(dst, ctypes.c_uint32), srcp, _ptr(pay, ctypes.c_uint32),
                                        dst.size))
 
-    def run(self, max_supersteps: int = 1 << 30) -> Stats:
+    def run(self, max_supersteps: int = 1 << 30, stats: bool = True) -> Stats | None:
+        """agx_run.  stats=False skips the counter read-back (read them with stats())."""
+        if not stats:
+            check(self.lib.agx_run(self._h, min(int(max_supersteps), 0xFFFFFFFF), None))
+            return None
         st = AgxStats()
         check(self.lib.agx_run(self._h, min(int(max_supersteps), 0xFFFFFFFF), ctypes.byref(st)))
         return Stats.from_c(st)

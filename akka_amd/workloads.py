@@ -107,8 +107,8 @@ def zipf_fanout(n: int = 10_000_000, k: int = 4, ttl: int = 3, root_every: int =
     behaviour: count++, sum += payload, if ttl > 0 emit k tells to Zipf targets."""
     cdf, perm = zipf_tables(n, s, seed)
     roots = np.arange(0, n, root_every, dtype=np.uint32)
-    h = (splitmix64_np(roots.astype(np.uint64) ^ np.uint64(seed * 3)) & np.uint64(0x0FFFFFFF)).astype(np.uint32)
-    pay = (np.uint32(ttl) << np.uint32(28)) | h
+    h = (splitmix64_np(roots.astype(np.uint64) ^ np.uint64(seed * 3)) & np.uint64(0x00FFFFFF)).astype(np.uint32)
+    pay = (np.uint32(ttl) << np.uint32(24)) | h
     src = np.full(roots.size, NO_SENDER, np.uint32)
     return Workload("zipf_fanout", n, 2, k, throughput, capacity, [(0, n, Kind.FANOUT, None)],
                     fanout=(k, seed, cdf, perm), tells=(roots, src, pay.astype(np.uint32)))
@@ -292,10 +292,10 @@ def mixed(n: int = 4096, seed: int = 1, throughput: int = 3, capacity: int = 0, 
     src = rng.integers(0, n, m).astype(np.uint32)
     src[rng.random(m) < 0.1] = NO_SENDER
     pay = rng.integers(0, 12, m).astype(np.uint32)
-    # fan-out payloads carry ttl in the top 4 bits
+    # fan-out payloads carry ttl in the top 8 bits
     fan_first, fan_count = ranges[2][0], ranges[2][1]
     is_fan = (dst >= fan_first) & (dst < fan_first + fan_count)
-    pay[is_fan] = (rng.integers(0, 3, int(is_fan.sum())).astype(np.uint32) << 28) | rng.integers(
-        0, 1 << 28, int(is_fan.sum())).astype(np.uint32)
+    pay[is_fan] = (rng.integers(0, 3, int(is_fan.sum())).astype(np.uint32) << 24) | rng.integers(
+        0, 1 << 24, int(is_fan.sum())).astype(np.uint32)
     return Workload("mixed", n, 2, 2, throughput, capacity, ranges, ring_stride=7, fanout=(2, seed, cdf, perm),
                     graph=(row, col), tells=(dst, src, pay))

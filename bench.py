@@ -127,11 +127,12 @@ def timed_ring(n_total: int, hops: int, warmup: int, steps: int, world: int, ran
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    s1 = eng.run(steps)
+    eng.run(steps, stats=False)  # (the counters are read back after the timed region)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
+    s1 = eng.stats()
     if not keep:
         eng.close()
         eng = None
@@ -154,9 +155,10 @@ def timed_workload(w, warmup: int, steps: int, prof_steps: int = 8, msg_capacity
     s0 = eng.run(warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    s1 = eng.run(steps)
+    eng.run(steps, stats=False)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    s1 = eng.stats()
     eng.profile(True)
     eng.profile_reset()
     eng.run(prof_steps)

@@ -65,7 +65,7 @@ enum agx_behavior_kind {
   AGX_KIND_NONE = 0,       /* unregistered: every message is a dead letter            */
   AGX_KIND_COUNTER = 1,    /* w0 += 1; w1 += payload                                  */
   AGX_KIND_RING = 2,       /* w0 += 1; payload>0 -> tell((self+stride)%N, payload-1)  */
-  AGX_KIND_FANOUT = 3,     /* w0 += 1; w1 += payload; ttl>0 -> k Zipf tells           */
+  AGX_KIND_FANOUT = 3,     /* w0 += 1; w1 += payload; ttl=pay>>24 >0 -> k Zipf tells  */
   AGX_KIND_FORWARD_RR = 4, /* w0 += 1; payload>0 -> tell(next out-edge RR, payload-1) */
   AGX_KIND_STOP_AFTER = 5, /* w0 += 1; w0 >= w1 -> Behaviors.stopped                  */
   AGX_KIND_PINGPONG = 6,   /* BenchmarkActors.PingPong: reply to sender, stop at 0    */
@@ -186,7 +186,9 @@ agx_status agx_set_graph_rmat(agx_engine* eng, const uint64_t* row_ptr, uint32_t
 agx_status agx_stage_tells(agx_engine* eng, const uint32_t* dst, const uint32_t* src,
                            const uint32_t* payload, size_t n);
 /* Run up to max_supersteps supersteps or until quiescent; stats are cumulative
- * over the engine's lifetime.                                                 */
+ * over the engine's lifetime.  out may be NULL: the counters are then not read
+ * back (agx_get_stats does it later, and reports AGX_ECAPACITY if an overflow
+ * was recorded meanwhile).                                                    */
 agx_status agx_run(agx_engine* eng, uint32_t max_supersteps, agx_stats* out);
 agx_status agx_get_stats(agx_engine* eng, agx_stats* out);
 

@@ -129,12 +129,12 @@ static inline uint32_t ref_apply(const ref_params* P, uint32_t kind, uint32_t a,
     case AGX_KIND_FANOUT: {
       w[0] += 1;
       if (P->W > 1) w[1] += payload;
-      uint32_t ttl = payload >> 28, h = payload & 0x0FFFFFFFu;
+      uint32_t ttl = payload >> 24, h = payload & 0x00FFFFFFu; /* ttl 8 bits, hash 24 bits */
       if (ttl > 0)
         for (uint32_t j = 0; j < P->fan_k; ++j) {
           uint64_t r = ref_fanout_rand(P->fan_seed, a, h, j);
           uint32_t d = P->zipf_perm[ref_zipf_index(P->zipf_cdf, P->zipf_n, r)];
-          emit(ctx, d, a, ((ttl - 1) << 28) | ((uint32_t)r & 0x0FFFFFFFu), 0, 0);
+          emit(ctx, d, a, ((ttl - 1) << 24) | ((uint32_t)r & 0x00FFFFFFu), 0, 0);
         }
       return AGX_RES_SAME;
     }

@@ -8,6 +8,7 @@ mirrors akka_amd.engine.GpuEngine so tests can drive both with one workload.
 from __future__ import annotations
 
 import ctypes
+import os
 import pathlib
 import subprocess
 import threading
@@ -52,7 +53,7 @@ def _load_bsp():
     global _bsp
     if _bsp is None:
         build()
-        lib = ctypes.CDLL(str(BUILD / "libbsp_ref.so"))
+        lib = ctypes.CDLL(str(BUILD / os.environ.get("AGX_BSP_LIB", "libbsp_ref.so")))
         vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
         P32, P64, P8 = ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint8)
         sig = {
@@ -91,7 +92,7 @@ def _load_fjp():
     global _fjp
     if _fjp is None:
         build()
-        lib = ctypes.CDLL(str(BUILD / "libfjp_ref.so"))
+        lib = ctypes.CDLL(str(BUILD / os.environ.get("AGX_FJP_LIB", "libfjp_ref.so")))
         vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
         P32, P64, P8 = ctypes.POINTER(u32), ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint8)
         sig = {
@@ -99,6 +100,7 @@ def _load_fjp():
             "fjp_destroy": (None, [vp]),
             "fjp_register_range": (ctypes.c_int, [vp, u64, u64, u32, P64, u64]),
             "fjp_set_ring": (None, [vp, u32]),
+            "fjp_set_gossip": (None, [vp, u32, u64]),
             "fjp_set_fanout": (None, [vp, u32, u64, P32, P32, u64]),
             "fjp_set_graph": (None, [vp, P64, P32]),
             "fjp_stage": (None, [vp, P32, P32, P32, u64]),
@@ -207,6 +209,9 @@ class FjpOracle(_Base):
 
     def set_ring(self, stride):
         self.lib.fjp_set_ring(self.h, stride)
+
+    def set_gossip(self, fanout, seed):
+        self.lib.fjp_set_gossip(self.h, fanout, seed)
 
     def set_fanout(self, k, seed, cdf, perm):
         cdf, perm = _u32(cdf), _u32(perm)

@@ -1,0 +1,186 @@
+"""GPU parity at the parameters the benchmark reports (bench.py `configs`), and the
+reference's golden known-answer tests run through the HIP engine itself.
+
+Each benched configuration is run here at its own throughput / capacity / behaviour /
+graph generator, at a population large enough to take the same kernel path as the
+bench (multi-pass grouping above 2^20 actors, the skew launch, R = 8 sharding), and
+compared bit-exactly with the BSP oracle.  Golden fixtures: tests/golden/*.json
+(transcribed from the reference's specs by tests/golden/make_golden.py).
+"""
+import json
+import pathlib
+
+import numpy as np
+import pytest
+
+from akka_amd import workloads as wl
+from akka_amd.engine import EngineConfig, GpuEngine, Kind, owner
+
+pytestmark = pytest.mark.gpu
+
+GOLD = pathlib.Path(__file__).resolve().parent / "golden"
+COUNT_KEYS = ("delivered", "dead_letters", "unhandled", "emitted", "staged", "supersteps", "in_flight")
+
+
+def _load(name):
+    return json.loads((GOLD / name).read_text())
+
+
+def _run_both(w, max_steps=1 << 30, **cfg):
+    from oracle import BspOracle
+    kw = w.engine_kwargs()
+    kw.update(cfg)
+    mcap = kw.pop("msg_capacity", 0)
+    eng = GpuEngine(EngineConfig(msg_capacity=mcap, **kw))
+    w.apply_to(eng)
+    sg = eng.run(max_steps)
+    wg, ag = eng.read_state()
+    eng.close()
+    ref = BspOracle(**kw)
+    w.apply_to(ref)
+    so = ref.run(max_steps)
+    wo, ao = ref.read_state()
+    ref.close()
+    return sg, so, (wg, ag), (wo, ao)
+
+
+def _assert_same(sg, so, a, b, name):
+    for k in COUNT_KEYS:
+        assert getattr(sg, k) == so[k], f"{name}: {k} gpu={getattr(sg, k)} oracle={so[k]}"
+    assert np.array_equal(a[1], b[1]), f"{name}: alive differs"
+    diff = np.nonzero((a[0] != b[0]).any(axis=1))[0]
+    assert diff.size == 0, f"{name}: state differs at {diff[:10]}"
+
+
+# ------------------------------------------------------------------ golden KATs through the engine
+def test_mailbox_kats_on_gpu(built):
+    """MailboxConfigSpec (akka-actor-tests/.../dispatch/MailboxConfigSpec.scala:47-66,84-116):
+    capacity C => exactly the (C+1)th.. enqueues are dead letters, FIFO survivors."""
+    for case in _load("mailbox_kat.json")["cases"]:
+        eng = GpuEngine(EngineConfig(n_actors=1, throughput=case["throughput"], capacity=case["capacity"], n_words=2))
+        eng.register_range(0, 1, Kind.COUNTER)
+        eng.tell(np.zeros(len(case["payloads"]), np.uint32), case["payloads"])
+        st = eng.run()
+        w, _ = eng.read_state()
+        eng.close()
+        assert st.delivered == case["delivered"], case["name"]
+        assert st.dead_letters == case["dead_letters"], case["name"]
+        assert int(w[0, 1]) == case["sum"], case["name"]
+        if "supersteps" in case:
+            assert st.supersteps == case["supersteps"], case["name"]
+
+
+def test_pingpong_kats_on_gpu(built):
+    """BenchmarkActors.PingPong invocation counts (pingpong_kat.json)."""
+    for c in _load("pingpong_kat.json")["cases"]:
+        w = wl.ping_pong(c["pairs"], c["messages_per_pair"], c["throughput"], c["in_flight"])
+        eng = GpuEngine(EngineConfig(**w.engine_kwargs()))
+        w.apply_to(eng)
+        st = eng.run()
+        eng.close()
+        assert st.delivered == c["delivered"] and st.dead_letters == c["dead_letters"], c
+
+
+def test_ring_kats_on_gpu(built):
+    for c in _load("ring_kat.json")["cases"]:
+        w = wl.token_ring(c["n"], c["hops"])
+        eng = GpuEngine(EngineConfig(**w.engine_kwargs()))
+        w.apply_to(eng)
+        st = eng.run()
+        words, alive = eng.read_state()
+        eng.close()
+        assert st.delivered == c["delivered"] and st.supersteps == c["supersteps"], c
+        assert (words[:, 0] == c["count"]).all() and alive.all(), c
+
+
+@pytest.mark.parametrize("C", [0, 3])
+def test_throughput_zero_behaves_as_one(built, C):
+    """throughput = 0 drains one message per mailbox run: the code clamps to max(throughput, 1)
+    (akka-actor/src/main/scala/akka/dispatch/Mailbox.scala:261), not "drain until empty"."""
+    w = wl.mixed(3000, seed=17 + C, throughput=0, capacity=C)
+    sg, so, a, b = _run_both(w)
+    _assert_same(sg, so, a, b, f"T=0 C={C}")
+    w1 = wl.mixed(3000, seed=17 + C, throughput=1, capacity=C)
+    s1, _, a1, _ = _run_both(w1)
+    assert (sg.delivered, sg.dead_letters, sg.supersteps) == (s1.delivered, s1.dead_letters, s1.supersteps)
+    assert np.array_equal(a[0], a1[0])
+
+
+# ------------------------------------------------------------------ C5 as benched
+def test_c5_power_law_bounded_as_benched(built):
+    """bench C5: FORWARD_RR over the device-generated R-MAT power-law graph, BoundedMailbox(64),
+    throughput 5, one message per actor with ttl 15 -- at 2.2M actors (> 2^20: the multi-pass
+    grouping + in-place backlog path of the 100M bench) and the bench's 2 + 10 superstep window,
+    then to quiescence."""
+    w = wl.power_law_forward(2_200_000, ttl=15, capacity=64, throughput=5, device_graph=True)
+    sg, so, a, b = _run_both(w, max_steps=12)
+    _assert_same(sg, so, a, b, "C5 12 supersteps")
+    assert sg.dead_letters > 0 and sg.in_flight > 0
+    sg, so, a, b = _run_both(w)
+    _assert_same(sg, so, a, b, "C5 to quiescence")
+
+
+@pytest.mark.parametrize("ranks", [8])
+def test_c5_power_law_sharded_loopback(built, ranks):
+    """C5 hash-sharded over 8 ranks (ShardRegion extractShardId ownership, loopback exchange)."""
+    from oracle import BspOracle
+    w = wl.power_law_forward(300_000, ttl=10, capacity=64, throughput=5, device_graph=True)
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.engine_kwargs())) for r in range(ranks)]
+    for e in engs:
+        w.apply_to(e)
+    sg = GpuEngine.group_run(engs)
+    ref = BspOracle(n_ranks=ranks, **w.engine_kwargs())
+    w.apply_to(ref)
+    so = ref.run()
+    for k in ("delivered", "dead_letters", "unhandled", "emitted", "staged", "in_flight"):
+        assert getattr(sg, k) == so[k], (k, getattr(sg, k), so[k])
+    wo, ao = ref.read_state()
+    own_of = np.array([owner(i, 1000, ranks) for i in range(w.n_actors)])
+    wg = np.zeros_like(wo)
+    ag = np.zeros_like(ao)
+    for e in engs:
+        x, y = e.read_state()
+        own = own_of == e.cfg.rank
+        wg[own] = x[own]
+        ag[own] = y[own]
+        e.close()
+    assert np.array_equal(wg, wo) and np.array_equal(ag, ao)
+    assert sg.dead_letters > 0
+
+
+# ------------------------------------------------------------------ C4 ORSet on the skew path
+def test_c4_orset_100k_skew_path(built):
+    """bench C4 ORSet: 3 messages per replica per superstep (tick + 2 gossips) exceed one
+    2048-message bucket tile, so every bucket takes the skew launch -- at 100k replicas."""
+    w = wl.crdt_gossip(100_000, Kind.ORSET, rounds=5)
+    sg, so, a, b = _run_both(w)
+    _assert_same(sg, so, a, b, "C4 ORSet 100k")
+    assert sg.in_flight == 0 and sg.unhandled == 0
+
+
+def test_c4_gcounter_as_benched_window(built):
+    """bench C4 GCounter shape (fanout 2, throughput 5) at 200k replicas, partial window."""
+    w = wl.crdt_gossip(200_000, Kind.GCOUNTER, rounds=40)
+    sg, so, a, b = _run_both(w, max_steps=28)
+    _assert_same(sg, so, a, b, "C4 GCounter 28 supersteps")
+
+
+# ------------------------------------------------------------------ C3 as benched
+@pytest.mark.parametrize("variant", ["tree", "steady"])
+def test_c3_zipf_as_benched(built, variant):
+    """bench C3: Zipf(1.1) FANOUT, 1/64 roots, unbounded, throughput 5;
+    'tree' = k 4, ttl 3; 'steady' = k 1, ttl 64 -- 2M actors, the bench's supersteps window."""
+    if variant == "tree":
+        w = wl.zipf_fanout(2_000_000, k=4, ttl=3, root_every=64, throughput=5)
+    else:
+        w = wl.zipf_fanout(2_000_000, k=1, ttl=64, root_every=64, throughput=5)
+    sg, so, a, b = _run_both(w, max_steps=24)
+    _assert_same(sg, so, a, b, f"C3 {variant}")
+
+
+def test_c1_ping_pong_as_benched(built):
+    """bench C1 shape: 1000 pairs, 100 in flight per pair, throughput 50 (one bucket, the skew
+    path), short messages-per-pair so the oracle finishes in seconds; run to completion."""
+    w = wl.ping_pong(1000, messages_per_pair=2_000, throughput=50)
+    sg, so, a, b = _run_both(w, msg_capacity=1 << 20)
+    _assert_same(sg, so, a, b, "C1")

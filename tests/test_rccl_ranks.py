@@ -1,0 +1,29 @@
+"""The real multi-process RCCL path on one GPU: N ranks (processes) with one engine each,
+agx_comm_init + run_multi_rccl (ncclAllGather of the count vectors, grouped
+ncclSend/ncclRecv of envelopes and CRDT rows), bit-exact against the BSP oracle in the
+sharded canonical order.  tools/rccl_two_rank.py gives every rank its own NCCL_HOSTID so
+RCCL accepts several ranks on one device (socket transport on loopback)."""
+import pathlib
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+@pytest.mark.parametrize("workload,world,n,hops", [
+    ("ring", 2, 20_000, 8),
+    ("mixed", 3, 20_000, 8),
+    ("orset", 2, 6_000, 6),
+    ("power", 4, 60_000, 8),
+    ("zipf", 2, 30_000, 3),
+])
+def test_rccl_ranks_parity(built, workload, world, n, hops):
+    cmd = [sys.executable, "-u", str(ROOT / "tools" / "rccl_two_rank.py"), "--split-hosts", "--world", str(world),
+           "--n", str(n), "--hops", str(hops), "--workload", workload]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    tail = (r.stdout[-1500:] + "\n" + r.stderr[-1500:])
+    assert r.returncode == 0, tail
+    assert "parity: OK" in r.stdout, tail

@@ -1,10 +1,14 @@
 #!/usr/bin/env python3
-"""Diagnostic: the RCCL exchange path (agx_comm_init + run_multi_rccl) with two
-ranks in two processes on the SAME device (a one-GPU box), checked bit-exactly
-against the BSP oracle in the sharded canonical order.  RCCL may refuse two
-ranks on one device; then this reports the refusal and exits 2.
+"""The RCCL exchange path (agx_comm_init + run_multi_rccl) with `--world` ranks in
+separate processes on the SAME device (a one-GPU box), checked bit-exactly against
+the BSP oracle in the sharded canonical order.  RCCL refuses two ranks on one
+device of one host ("Duplicate GPU detected"); --split-hosts gives every rank its
+own NCCL_HOSTID, so the ranks look like separate hosts and exchange over RCCL's
+socket transport on loopback -- the same ncclSend/ncclRecv/ncclAllGather calls as
+over xGMI on a multi-GPU node.  Exit 0 = parity, 1 = mismatch, 2 = a rank failed.
 
-    python tools/rccl_two_rank.py [--n 20000] [--hops 8] [--workload ring|mixed]
+    python tools/rccl_two_rank.py --split-hosts [--world 2] [--n 20000] [--hops 8]
+                                  [--workload ring|mixed|orset|power|zipf]
 """
 import argparse
 import os
@@ -26,14 +30,27 @@ def _free_port():
 
 def _make(a):
     from akka_amd import workloads as wl
+    from akka_amd.engine import Kind
     if a.workload == "ring":
         return wl.token_ring(a.n, a.hops)
+    if a.workload == "orset":  # CRDT snapshot rows travel beside the envelopes
+        return wl.crdt_gossip(a.n, Kind.ORSET, rounds=a.hops, throughput=2)
+    if a.workload == "power":  # C5 shape: bounded(64) forwarding over the R-MAT graph
+        return wl.power_law_forward(a.n, ttl=a.hops, capacity=64, throughput=5, device_graph=True)
+    if a.workload == "zipf":
+        return wl.zipf_fanout(a.n, k=4, ttl=3, root_every=16, throughput=3)
     return wl.mixed(a.n, seed=3, throughput=2, capacity=6)
 
 
 def _rank_main(rank, world, port, a, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if a.split_hosts:
+        # RCCL refuses two ranks on one device of one host ("Duplicate GPU detected"); a distinct
+        # host id per rank makes them two "hosts" that talk over the socket transport on loopback
+        os.environ["NCCL_HOSTID"] = f"agx-rank-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     import numpy as np
     import torch.distributed as dist
     from akka_amd.engine import EngineConfig, GpuEngine
@@ -60,12 +77,14 @@ def main():
     ap.add_argument("--n", type=int, default=20000)
     ap.add_argument("--hops", type=int, default=8)
     ap.add_argument("--workload", default="ring")
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--split-hosts", action="store_true", help="one NCCL_HOSTID per rank (one-GPU box)")
     a = ap.parse_args()
     import numpy as np
     import torch.multiprocessing as mp
     from akka_amd.engine import owner
     from oracle import BspOracle
-    world = 2
+    world = a.world
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
