@@ -75,29 +75,72 @@ def kernel_rooflines(prof: dict, per_msg: dict, msgs_per_launch: int) -> dict:
     return {"bound": "hbm", "peak": PEAK_HBM_GBS, "unit": "GB/s", "dominant": dom, "kernels": out}
 
 
-def cpu_baseline(hops: int) -> dict:
-    """fjp_ref (restatement of Dispatcher/Mailbox/ForkJoinPool) on the host cores,
-    bounded sample: the same 1M-actor ring with a smaller hop budget."""
-    from akka_amd import workloads as wl
-    from oracle import BspOracle, FjpOracle
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    w = wl.token_ring(N_PER_GPU, hops, throughput=5)
+
+def _fjp_rate(w, threads: int) -> dict:
+    from oracle import FjpOracle
     f = FjpOracle(**w.engine_kwargs())
     w.apply_to(f)
-    st = f.run(cores)
-    fjp_rate = st["delivered"] / f.wall_s
+    st = f.run(threads)
+    wall = f.wall_s
     f.close()
-    b = BspOracle(**w.engine_kwargs())
-    w.apply_to(b)
+    return {"value": st["delivered"] / wall, "delivered": st["delivered"], "dead_letters": st["dead_letters"],
+            "wall_s": round(wall, 3)}
+
+
+def cpu_baseline(hops: int) -> dict:
+    """fjp_ref (oracle/fjp_ref.cpp: restatement of Dispatcher + Mailbox + a lock-free work-stealing
+    ForkJoinPool) on the host cores, on bounded samples of each workload.  The
+    headline `value` is the C2 ring sample; `configs` carries C1 (the reference's own CPU-only
+    JMH config, ForkJoinActorBenchmark.pingPong), C3, C4 and C5 samples.  bsp_ref = the
+    single-threaded deterministic oracle on the same ring."""
+    from akka_amd import workloads as wl
+    from akka_amd.engine import Kind
+    from oracle import BspOracle
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    cores = min(cores, len(os.sched_getaffinity(0)))
+    ring = wl.token_ring(N_PER_GPU, hops, throughput=5)
+    head = _fjp_rate(ring, cores)
+    b = BspOracle(**ring.engine_kwargs())
+    ring.apply_to(b)
     t0 = time.perf_counter()
     sb = b.run()
     bsp_s = time.perf_counter() - t0
     b.close()
-    return {"value": fjp_rate, "unit": "msg/s", "cores": cores, "kind": "port",
-            "sample": f"fjp_ref ForkJoin-dispatcher restatement, 1M-actor token ring, hops={hops} "
-                      f"({st['delivered']} deliveries, {f.wall_s:.2f} s, throughput=5)",
-            "bsp_ref_1thread_msg_s": sb["delivered"] / bsp_s}
+    samples = {
+        "C1_ping_pong": ("ForkJoinActorBenchmark.pingPong: 1000 pairs, throughput 50, 100 in flight per pair, "
+                         "100000 messages per pair (the JMH run uses 2,000,000)",
+                         lambda: wl.ping_pong(1000, messages_per_pair=100_000, throughput=50)),
+        "C3_zipf_tree": ("1M actors, Zipf(1.1) FANOUT k=4 ttl=3, 1/64 roots, throughput 5, to quiescence",
+                         lambda: wl.zipf_fanout(1_000_000, k=4, ttl=3, root_every=64, throughput=5)),
+        "C4_gcounter_gossip": ("200k GCounter replicas, 8 rounds of full-state gossip to 2 peers",
+                               lambda: wl.crdt_gossip(200_000, Kind.GCOUNTER, rounds=8)),
+        "C4_orset_gossip": ("50k ORSet replicas, 4 rounds of full-state gossip to 2 peers",
+                            lambda: wl.crdt_gossip(50_000, Kind.ORSET, rounds=4)),
+        "C5_power_law_bounded": ("1M actors, power-law R-MAT graph, FORWARD_RR ttl 15, BoundedMailbox(64)",
+                                 lambda: wl.power_law_forward(1_000_000, ttl=15, capacity=64, throughput=5)),
+    }
+    configs = {}
+    for name, (desc, make) in samples.items():
+        try:
+            configs[name] = dict(sample=desc, unit="msg/s", **_fjp_rate(make(), cores))
+        except Exception as ex:  # one sample failing must not hide the others
+            configs[name] = {"sample": desc, "error": repr(ex)}
+    return {"value": head["value"], "unit": "msg/s", "cores": cores, "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"fjp_ref ForkJoin-dispatcher restatement (lock-free work-stealing pool, {cores} threads), "
+                      f"1M-actor token ring, hops={hops} ({head['delivered']} deliveries, {head['wall_s']} s, "
+                      f"throughput=5)",
+            "bsp_ref_1thread_msg_s": sb["delivered"] / bsp_s, "configs": configs}
 
 
 def timed_ring(n_total: int, hops: int, warmup: int, steps: int, world: int, rank: int, local: int,
