@@ -35,7 +35,7 @@ class AgxCfg(ctypes.Structure):
         ("n_ranks", ctypes.c_uint32),
         ("rank", ctypes.c_uint32),
         ("num_shards", ctypes.c_uint32),
-        ("reserved0", ctypes.c_uint32),
+        ("bucket_actors", ctypes.c_uint32),
         ("msg_capacity", ctypes.c_uint64),
     ]
 

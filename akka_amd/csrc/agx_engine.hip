@@ -96,7 +96,7 @@ constexpr uint32_t kStatBlk = 16;                    // d_stats block (see agx_e
 constexpr uint32_t kStatSred = ST_N, kStatInfl = ST_N + kBStats;
 static_assert(kStatInfl < kStatBlk, "stats block layout");
 
-struct SortPlan {  // LSD passes over key bits [kBucketBits, key_bits)
+struct SortPlan {  // LSD passes over key bits [bb, key_bits)
   uint32_t npass = 1;
   uint32_t shift[4] = {0}, bits[4] = {0};
 };
@@ -109,6 +109,7 @@ struct agx_engine {
   uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0;
   uint32_t max_supers = 1, dstride = 4, dsuper = kSuper;  // dense passes: super-tiles, table row stride, tile size
   uint32_t T = 1, C = 0, W = 1, kmax = 1, R = 1, rank = 0, num_shards = 1000, key_bits = 1;
+  uint32_t bb = kBucketBits;  // bucket bits (agx_cfg.bucket_actors)
 
   // sharding tables (R > 1)
   std::vector<uint32_t> h_gid, h_route;
@@ -132,7 +133,7 @@ struct agx_engine {
   uint32_t* d_col = nullptr;
   // CRDT state gossips (agx_crdt.h): snapshot heap, 2 x cap rows of pw u32
   uint32_t pw = 0, gossip_f = 0;
-  uint64_t heap_rows = 0;  // per parity: one kBucket-row region per bucket, then an overflow area of `cap` rows
+  uint64_t heap_rows = 0;  // per parity: one region of 2^bb rows per bucket, then an overflow area of `cap` rows
   uint64_t gossip_seed = 0;
   uint32_t *d_heap = nullptr, *d_heap_top = nullptr, *d_step = nullptr;
   uint32_t *d_rx = nullptr, *d_s2rows = nullptr;  // multi-rank: received rows / rows packed for sending
@@ -419,7 +420,7 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
   if (e->plan.npass > 1) {  // digits of the last pass are not buckets: find the bucket starts
     Scope s(e, K_BOUNDS);
     hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((e->nb + kThreads) / kThreads, 4096)), dim3(kThreads), 0,
-                       e->stream, src->key, e->d_n, e->nb, e->d_bstart);
+                       e->stream, src->key, e->d_n, e->nb, e->bb, e->d_bstart);
     HIP_TRY(hipGetLastError());
   }
   *result = src;
@@ -446,6 +447,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.nx_shift = e->plan.shift[0];
   ba.nx_bits = e->plan.bits[0];
   ba.nb = e->nb;
+  ba.bb = e->bb;
   ba.kmax = e->kmax;
   ba.stats = e->d_stats;
   ba.bstats = e->d_bstats;
@@ -581,11 +583,11 @@ agx_status prepare_run(agx_engine* e) {
     }
     // stable counting sort by destination bucket: each bucket's staged tells are one run
     std::vector<uint32_t> off(e->nb + 1, 0), cnt(e->nb, 0);
-    for (uint64_t i = 0; i < n; ++i) cnt[e->hs_key[i] >> kBucketBits]++;
+    for (uint64_t i = 0; i < n; ++i) cnt[e->hs_key[i] >> e->bb]++;
     for (uint32_t b = 0; b < e->nb; ++b) off[b + 1] = off[b] + cnt[b];
     std::vector<uint32_t> k(n), sv(n), pv(n), pos(off.begin(), off.end() - 1);
     for (uint64_t i = 0; i < n; ++i) {
-      const uint32_t o = pos[e->hs_key[i] >> kBucketBits]++;
+      const uint32_t o = pos[e->hs_key[i] >> e->bb]++;
       k[o] = e->hs_key[i];
       sv[o] = e->hs_src[i];
       pv[o] = e->hs_pay[i];
@@ -1060,7 +1062,7 @@ agx_status enable_crdt(agx_engine* e, uint32_t kind) {
                                                 : 2 * words;
   if (pw <= e->pw) return AGX_OK;
   if (e->started) return set_err(AGX_ESTATE, "register CRDT kinds before the first agx_run");
-  const uint64_t rows = (uint64_t)e->nb * kBucket + e->cap;
+  const uint64_t rows = ((uint64_t)e->nb << e->bb) + e->cap;
   if (rows + e->cap >= (1ull << 30)) return set_err(AGX_EINVAL, "CRDT kinds need msg_capacity < 2^29 - n_actors");
   hipFree(e->d_heap);
   hipFree(e->d_rx);
@@ -1085,6 +1087,10 @@ agx_status validate_cfg(const agx_cfg* c) {
   if (c->n_words == 0 || c->n_words > AGX_MAX_WORDS) return set_err(AGX_EINVAL, "n_words must be 1..%u", AGX_MAX_WORDS);
   uint32_t R = c->n_ranks ? c->n_ranks : 1;
   if (R > AGX_MAX_RANKS || c->rank >= R) return set_err(AGX_EINVAL, "bad rank %u / n_ranks %u", c->rank, R);
+  if (c->num_shards > (uint32_t)INT32_MAX) return set_err(AGX_EINVAL, "num_shards must be < 2^31 (maxNumberOfShards is an Int)");
+  const uint32_t ba = c->bucket_actors;
+  if (ba && (ba & (ba - 1) || ba < (1u << kMinBucketBits) || ba > (uint32_t)kBucket))
+    return set_err(AGX_EINVAL, "bucket_actors must be 0 or a power of two in [%d, %d]", 1 << kMinBucketBits, kBucket);
   return AGX_OK;
 }
 
@@ -1125,6 +1131,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->R = cfg->n_ranks ? cfg->n_ranks : 1;
   e->rank = cfg->rank;
   e->num_shards = cfg->num_shards ? cfg->num_shards : 1000;
+  e->bb = cfg->bucket_actors ? ceil_log2(cfg->bucket_actors) : (uint32_t)kBucketBits;
   e->graphs_enabled = getenv("AGX_NO_GRAPH") == nullptr && getenv("AGX_STAMPS") == nullptr;
   agx_status st = ensure_dev(e);
   if (st) { delete e; return st; }
@@ -1161,8 +1168,8 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   }
   e->max_supers = (uint32_t)((std::max(e->cap, e->cap_emit) + e->dsuper - 1) / e->dsuper + 1);
   e->dstride = (e->max_supers + 3) & ~3u;
-  // buckets of 2^kBucketBits actors; LSD passes over key bits [kBucketBits, key_bits), <= kRadixBits each
-  e->nb = (uint32_t)((nl + kBucket - 1) / kBucket);
+  // buckets of 2^bb actors; LSD passes over key bits [bb, key_bits), <= kRadixBits each
+  e->nb = (uint32_t)((nl + (1ull << e->bb) - 1) >> e->bb);
   e->nchunks = 2 * e->nb + kStagedChunks;
   // first-pass histogram columns: ~2048 units per arena at most (G buckets per unit)
   e->G = (e->nb + 2047) / 2048;
@@ -1172,7 +1179,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->nunits = 2 * e->ng + kStagedChunks;
   e->cstride = (e->nunits + 3) & ~3u;
   {
-    const uint32_t lo = kBucketBits, hi = std::max<uint32_t>(e->key_bits, kBucketBits + 1);
+    const uint32_t lo = e->bb, hi = std::max<uint32_t>(e->key_bits, e->bb + 1);
     // AGX_RADIX_BITS (test knob): narrower digits, so that small populations take the multi-pass path
     uint32_t rb = kRadixBits;
     if (const char* s = getenv("AGX_RADIX_BITS")) rb = std::min<uint32_t>(kRadixBits, std::max(1, atoi(s)));

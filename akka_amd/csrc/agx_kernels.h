@@ -2,7 +2,8 @@
 //
 // One BSP superstep replaces one round of Mailbox.run/processMailbox over every
 // scheduled mailbox (akka-actor/src/main/scala/akka/dispatch/Mailbox.scala:227-277).
-// Actors are grouped in buckets of 2^kBucketBits consecutive local ids.
+// Actors are grouped in buckets of 2^bb consecutive local ids (bb <= kBucketBits, chosen per
+// engine: agx_cfg.bucket_actors); one bucket's inbox up to one LDS tile takes the fast path.
 //
 //   k_bucket_apply     per bucket: stable in-bucket counting sort of its mail by
 //                      actor (LDS wave multisplit), segmented drain with the
@@ -31,9 +32,9 @@ constexpr int kWaves = kThreads / kWave;
 constexpr int kIpt = 8;
 constexpr int kTile = kThreads * kIpt;  // 2048 envelopes per sort tile
 
-constexpr int kBucketBits = 11;
-constexpr int kBucket = 1 << kBucketBits;  // actors per bucket
-constexpr int kActPerThread = kBucket / kThreads;
+constexpr int kBucketBits = 11;            // widest bucket (the LDS per-actor arrays' size)
+constexpr int kBucket = 1 << kBucketBits;  // max actors per bucket = messages per apply tile
+constexpr int kMinBucketBits = 5;
 
 constexpr int kRadixBits = 9;  // max digit width of one pass
 constexpr int kRadix = 1 << kRadixBits;
@@ -717,7 +718,7 @@ struct GatherArgs {
 struct BucketArgs {
   DevParams P;
   GatherArgs g;
-  CMsgs in;                // mail sorted by bucket (local key >> kBucketBits)
+  CMsgs in;                // mail sorted by bucket (local key >> bb)
   const uint32_t* d_n;
   const uint32_t* bstart;  // bucket starts [nb + 1]
   Msgs scr;                // general path: bucket-local sorted copy (index space of `in`)
@@ -728,6 +729,7 @@ struct BucketArgs {
   uint32_t nhist_stride, nx_shift, nx_bits;
   uint32_t G, ng;          // histogram units: G buckets per column, ng units per arena
   uint32_t nb, kmax;
+  uint32_t bb;             // bucket bits: bucket b = local actors [b << bb, (b + 1) << bb), bb <= kBucketBits
   uint64_t cap;            // bypass: message capacity of the inbox index space
   const uint32_t* pstep;   // bypass (single-rank multi-pass): superstep counter; backlog arena parity = step & 1
   const uint32_t* blpre;   // bypass: backlog prefix (bucket b's inbox index space starts at bstart[b] +
@@ -887,12 +889,12 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   CrdtHeap H{};
   if (kWide) H = crdt_heap(P);
   // Snapshot rows of bucket b (one lane allocates for its wave / block): the bucket's own heap
-  // region [b*kBucket, (b+1)*kBucket) through an LDS cursor, then the overflow area after all
-  // regions through the shared cursor — no contended atomic for the common case.
+  // region [b << bb, (b+1) << bb) (one row per actor) through an LDS cursor, then the overflow
+  // area after all regions through the shared cursor — no contended atomic for the common case.
   auto alloc_rows = [&](uint32_t n) -> uint32_t {
     const uint32_t r = atomicAdd(L.rowtop, n);
-    if (r + n <= (uint32_t)kBucket) return b * (uint32_t)kBucket + r;
-    return a.nb * (uint32_t)kBucket + atomicAdd(H.top, n);
+    if (r + n <= (1u << a.bb)) return (b << a.bb) + r;
+    return (a.nb << a.bb) + atomicAdd(H.top, n);
   };
 
   AGX_STAMP(a, 3);
@@ -937,7 +939,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     __syncthreads();
     for (uint32_t q = tid; q < cnt; q += kBThreads) {  // queued messages, in actor order
       const uint32_t key = ikey(q);
-      const uint32_t la = key & (kBucket - 1);
+      const uint32_t la = key & ((1u << a.bb) - 1u);
       const uint32_t p = q - L.seg[la];
       const uint32_t len = L.seg[la + 1] - L.seg[la];
       const uint32_t keep = (C == 0 || len < C) ? len : C;
@@ -1385,6 +1387,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t lane = lane_id();
   const uint64_t ltm = lanemask_lt();
+  const uint32_t amask = (1u << a.bb) - 1u;  // actor index within the bucket
   const GatherArgs& g = a.g;
   // (kBypass: single-rank multi-pass — the previous backlog is read in place, not sorted)
   constexpr bool kBypass = !kGather && !kOwner;
@@ -1414,13 +1417,13 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   for (uint32_t it = blockIdx.x; it < nwork; it += gridDim.x) {
     const uint32_t b = kSkew ? a.skew_list[it] : it;
     AGX_STAMP(a, 0);
-    const uint32_t a0 = b << kBucketBits;
-    const uint32_t na = min((uint32_t)kBucket, P.n_local - a0);
+    const uint32_t a0 = b << a.bb;
+    const uint32_t na = min(1u << a.bb, P.n_local - a0);
     if (tid < 5) s_stat[tid] = 0;
     if (tid == 0) s_rowtop = 0;
     for (uint32_t d = tid; d < kRadix; d += kBThreads) s_nh[d] = 0;
     uint32_t* my_tc = nullptr;  // (fused) this thread's table entry, zeroed once the bucket is processed
-    uint32_t alive4 = 0;        // alive flags of actors 4*tid..4*tid+3, loaded first (a0 is a multiple of kBucket)
+    uint32_t alive4 = 0;        // alive flags of actors 4*tid..4*tid+3, loaded first (a0 is a multiple of 32)
     {
       const uint32_t la0 = tid * 4;
       if (la0 + 4 <= na) alive4 = *reinterpret_cast<const uint32_t*>(P.alive + a0 + la0);
@@ -1570,7 +1573,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
 #pragma unroll
       for (int r = 0; r < kBIpt; ++r) {
         const uint32_t q = wbase + r * kWave + lane;
-        if (q < cnt && q > 0) ok &= (s_key[q - 1] & (kBucket - 1)) <= (k[r] & (kBucket - 1));
+        if (q < cnt && q > 0) ok &= (s_key[q - 1] & amask) <= (k[r] & amask);
       }
       const bool presorted = __syncthreads_and(ok) != 0;
       uint32_t tl[kBAct];
@@ -1578,7 +1581,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
 #pragma unroll
         for (int r = 0; r < kBIpt; ++r) {
           const uint32_t q = wbase + r * kWave + lane;
-          if (q < cnt) atomicAdd(&s_seg[k[r] & (kBucket - 1)], 1u);
+          if (q < cnt) atomicAdd(&s_seg[k[r] & amask], 1u);
         }
         __syncthreads();
 #pragma unroll
@@ -1589,7 +1592,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
 #pragma unroll
         for (int r = 0; r < kBIpt; ++r) {
           const uint32_t q = wbase + r * kWave + lane;
-          rk[r] = wave_rank(q < cnt, k[r] & (kBucket - 1), kBucketBits, whist + w * kBucket, ltm);
+          rk[r] = wave_rank(q < cnt, k[r] & amask, a.bb, whist + w * kBucket, ltm);
         }
         __syncthreads();
         // per actor: wave prefixes in place, segment length
@@ -1625,7 +1628,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         for (int r = 0; r < kBIpt; ++r) {
           const uint32_t q = wbase + r * kWave + lane;
           if (q < cnt) {
-            const uint32_t la = k[r] & (kBucket - 1);
+            const uint32_t la = k[r] & amask;
             const uint32_t pos = s_seg[la] + whist[w * kBucket + la] + rk[r];
             s_key[pos] = k[r];
             s_src[pos] = sv[r];
@@ -1659,7 +1662,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         for (int j = 0; j < 4; ++j) kk[j] = q0 + j * kBThreads + tid < cnt ? gkey(q0 + j * kBThreads + tid) : 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (q0 + j * kBThreads + tid < cnt) atomicAdd(&s_seg[kk[j] & (kBucket - 1)], 1u);
+          if (q0 + j * kBThreads + tid < cnt) atomicAdd(&s_seg[kk[j] & amask], 1u);
       }
       __syncthreads();
       uint32_t ndead0 = 0;
@@ -1701,7 +1704,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         for (int r = 0; r < kBIpt; ++r) {
           k[r] = kn[r];
           const uint32_t q = wbase + r * kWave + lane;
-          const uint32_t la = k[r] & (kBucket - 1);
+          const uint32_t la = k[r] & amask;
           live[r] = q < cnt && s_run[la] < s_keep[la];  // actor not yet full: rank it
           any |= live[r];
         }
@@ -1731,7 +1734,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
           }
         }
 #pragma unroll
-        for (int r = 0; r < kBIpt; ++r) rk[r] = wave_rank(live[r], k[r] & (kBucket - 1), kBucketBits, whist + w * kBucket, ltm);
+        for (int r = 0; r < kBIpt; ++r) rk[r] = wave_rank(live[r], k[r] & amask, a.bb, whist + w * kBucket, ltm);
         __syncthreads();
         for (uint32_t la = tid; la < kBucket; la += kBThreads) {
           uint32_t run = 0;
@@ -1747,7 +1750,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
 #pragma unroll
         for (int r = 0; r < kBIpt; ++r) {
           if (!live[r]) continue;
-          const uint32_t la = k[r] & (kBucket - 1);
+          const uint32_t la = k[r] & amask;
           const uint32_t rank = s_run[la] + whist[w * kBucket + la] + rk[r];  // among this actor's arrivals
           if (rank < s_keep[la]) {
             const uint32_t pos = lo + s_seg[la] + rank;
@@ -1771,13 +1774,13 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
 // (one thread per bucket, binary search over the sorted keys; the top levels of every
 // search hit the same cached lines).
 __global__ void __launch_bounds__(kThreads) k_bucket_bounds(const uint32_t* key, const uint32_t* d_n, uint32_t nb,
-                                                            uint32_t* bstart) {
+                                                            uint32_t bb, uint32_t* bstart) {
   const uint32_t n = *d_n;
   for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x <= nb; x += gridDim.x * kThreads) {
     uint32_t lo = 0, hi = n;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (((key[mid] & kLocalMask) >> kBucketBits) < x) lo = mid + 1; else hi = mid;
+      if (((key[mid] & kLocalMask) >> bb) < x) lo = mid + 1; else hi = mid;
     }
     bstart[x] = lo;
   }

@@ -63,6 +63,7 @@ class EngineConfig:
     num_shards: int = 1000
     device: int = 0
     msg_capacity: int = 0
+    bucket_actors: int = 0       # actors per apply bucket (0 = 2048; power of two in [32, 2048])
 
     def to_c(self) -> AgxCfg:
         c = AgxCfg()
@@ -78,6 +79,7 @@ class EngineConfig:
         c.rank = int(self.rank)
         c.num_shards = int(self.num_shards)
         c.msg_capacity = int(self.msg_capacity)
+        c.bucket_actors = int(self.bucket_actors)
         return c
 
 

@@ -40,10 +40,16 @@ class Workload:
     fanout: tuple | None = None  # (k, seed, cdf, perm)
     graph: tuple | None = None   # (row_ptr, col)
     tells: tuple | None = None   # (dst, src, payload)
+    bucket_actors: int = 0       # GPU engine hint (agx_cfg.bucket_actors): deep mailboxes want small buckets
 
     def engine_kwargs(self) -> dict:
+        """Semantic parameters (shared by the GPU engine and the CPU oracles)."""
         return dict(n_actors=self.n_actors, throughput=self.throughput, capacity=self.capacity,
                     n_words=self.n_words, max_emit=self.max_emit)
+
+    def gpu_kwargs(self) -> dict:
+        """engine_kwargs + the GPU engine's layout hints (EngineConfig)."""
+        return dict(self.engine_kwargs(), bucket_actors=self.bucket_actors)
 
     def apply_to(self, target, stage_tells: bool = True) -> None:
         for first, count, kind, init in self.ranges:
@@ -152,8 +158,10 @@ def crdt_gossip(n: int = 1_000_000, kind: int = Kind.GCOUNTER, rounds: int = 32,
     dst = np.concatenate([odst, tdst])
     pay = np.concatenate([ops, tick])
     src = np.full(dst.size, NO_SENDER, np.uint32)
+    # a replica receives its tick + `fanout` gossips per superstep: buckets of 512 replicas keep
+    # the ~3 x 512 messages in one 2048-message apply tile (the fast path)
     return Workload(f"crdt_gossip_{kind}", n, CRDT_WORDS[kind], fanout + 1, throughput, capacity,
-                    [(0, n, kind, None)], gossip=(fanout, seed), tells=(dst, src, pay))
+                    [(0, n, kind, None)], gossip=(fanout, seed), tells=(dst, src, pay), bucket_actors=512)
 
 
 def crdt_mixed(n: int = 4096, rounds: int = 4, seed: int = 3, throughput: int = 3, capacity: int = 0) -> Workload:
@@ -263,7 +271,10 @@ def ping_pong(pairs: int = 1000, messages_per_pair: int = 2_000_000, throughput:
     dst = np.repeat(ping, in_flight)
     src = dst + np.uint32(1)
     pay = np.zeros(dst.size, np.uint32)
-    return Workload("ping_pong", n, 2, 1, throughput, 0, [(0, n, Kind.PINGPONG, init)], tells=(dst, src, pay))
+    # in_flight tells per pair: ~in_flight/2 queued per actor -> buckets of 2048/in_flight actors fit one tile
+    ba = max(32, min(2048, 1 << max(0, (2048 // max(in_flight, 1)).bit_length() - 1)))
+    return Workload("ping_pong", n, 2, 1, throughput, 0, [(0, n, Kind.PINGPONG, init)], tells=(dst, src, pay),
+                    bucket_actors=ba)
 
 
 # ------------------------------------------------------------------ small mixed workload for parity tests

@@ -154,7 +154,7 @@ def timed_ring(n_total: int, hops: int, warmup: int, steps: int, world: int, ran
     from akka_amd.engine import EngineConfig, GpuEngine
 
     w = wl.token_ring(n_total, hops)
-    cfg = EngineConfig(device=local, n_ranks=world, rank=rank, **w.engine_kwargs())
+    cfg = EngineConfig(device=local, n_ranks=world, rank=rank, **w.gpu_kwargs())
     cfg.msg_capacity = msg_capacity
     eng = GpuEngine(cfg)
     w.apply_to(eng)
@@ -190,7 +190,7 @@ def timed_workload(w, warmup: int, steps: int, prof_steps: int = 8, msg_capacity
     from akka_amd.engine import EngineConfig, GpuEngine
 
     t0 = time.perf_counter()
-    cfg = EngineConfig(**w.engine_kwargs())
+    cfg = EngineConfig(**w.gpu_kwargs())
     cfg.msg_capacity = msg_capacity
     eng = GpuEngine(cfg)
     w.apply_to(eng)

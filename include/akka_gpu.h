@@ -132,7 +132,10 @@ typedef struct agx_cfg {
   uint32_t n_ranks;       /* GPUs the population is hash-sharded over (1 = single GPU) */
   uint32_t rank;          /* this engine's rank                                        */
   uint32_t num_shards;    /* ShardRegion number-of-shards (1000 in typed sharding)     */
-  uint32_t reserved0;
+  uint32_t bucket_actors;  /* actors per apply bucket: 0 = 2048, else a power of two in [32, 2048].
+                             One workgroup drains a bucket; a bucket whose inbox exceeds 2048
+                             messages takes the skew path -- populations with deep mailboxes
+                             (ping-pong pairs, CRDT replicas with gossips) want small buckets */
   uint64_t msg_capacity;  /* max messages in flight on this rank (0 = 4 x local actors)*/
 } agx_cfg;
 

@@ -26,12 +26,13 @@ def _load(name):
     return json.loads((GOLD / name).read_text())
 
 
-def _run_both(w, max_steps=1 << 30, **cfg):
+def _run_both(w, max_steps=1 << 30, bucket_actors=None, **cfg):
     from oracle import BspOracle
     kw = w.engine_kwargs()
     kw.update(cfg)
     mcap = kw.pop("msg_capacity", 0)
-    eng = GpuEngine(EngineConfig(msg_capacity=mcap, **kw))
+    ba = w.bucket_actors if bucket_actors is None else bucket_actors
+    eng = GpuEngine(EngineConfig(msg_capacity=mcap, bucket_actors=ba, **kw))
     w.apply_to(eng)
     sg = eng.run(max_steps)
     wg, ag = eng.read_state()
@@ -74,7 +75,7 @@ def test_pingpong_kats_on_gpu(built):
     """BenchmarkActors.PingPong invocation counts (pingpong_kat.json)."""
     for c in _load("pingpong_kat.json")["cases"]:
         w = wl.ping_pong(c["pairs"], c["messages_per_pair"], c["throughput"], c["in_flight"])
-        eng = GpuEngine(EngineConfig(**w.engine_kwargs()))
+        eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
         w.apply_to(eng)
         st = eng.run()
         eng.close()
@@ -84,7 +85,7 @@ def test_pingpong_kats_on_gpu(built):
 def test_ring_kats_on_gpu(built):
     for c in _load("ring_kat.json")["cases"]:
         w = wl.token_ring(c["n"], c["hops"])
-        eng = GpuEngine(EngineConfig(**w.engine_kwargs()))
+        eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
         w.apply_to(eng)
         st = eng.run()
         words, alive = eng.read_state()
@@ -125,7 +126,7 @@ def test_c5_power_law_sharded_loopback(built, ranks):
     """C5 hash-sharded over 8 ranks (ShardRegion extractShardId ownership, loopback exchange)."""
     from oracle import BspOracle
     w = wl.power_law_forward(300_000, ttl=10, capacity=64, throughput=5, device_graph=True)
-    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.engine_kwargs())) for r in range(ranks)]
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.gpu_kwargs())) for r in range(ranks)]
     for e in engs:
         w.apply_to(e)
     sg = GpuEngine.group_run(engs)
@@ -149,12 +150,14 @@ def test_c5_power_law_sharded_loopback(built, ranks):
 
 
 # ------------------------------------------------------------------ C4 ORSet on the skew path
-def test_c4_orset_100k_skew_path(built):
-    """bench C4 ORSet: 3 messages per replica per superstep (tick + 2 gossips) exceed one
-    2048-message bucket tile, so every bucket takes the skew launch -- at 100k replicas."""
+@pytest.mark.parametrize("ba", [512, 2048])
+def test_c4_orset_100k(built, ba):
+    """bench C4 ORSet at 100k replicas: 3 messages per replica per superstep (tick + 2 gossips).
+    With the workload's 512-replica buckets they fit the fast path's 2048-message tile; with
+    2048-replica buckets every bucket takes the skew launch."""
     w = wl.crdt_gossip(100_000, Kind.ORSET, rounds=5)
-    sg, so, a, b = _run_both(w)
-    _assert_same(sg, so, a, b, "C4 ORSet 100k")
+    sg, so, a, b = _run_both(w, bucket_actors=ba)
+    _assert_same(sg, so, a, b, f"C4 ORSet 100k bucket {ba}")
     assert sg.in_flight == 0 and sg.unhandled == 0
 
 
@@ -179,8 +182,11 @@ def test_c3_zipf_as_benched(built, variant):
 
 
 def test_c1_ping_pong_as_benched(built):
-    """bench C1 shape: 1000 pairs, 100 in flight per pair, throughput 50 (one bucket, the skew
-    path), short messages-per-pair so the oracle finishes in seconds; run to completion."""
+    """bench C1 shape: 1000 pairs, 100 in flight per pair, throughput 50, short messages-per-pair
+    so the oracle finishes in seconds; run to completion -- with the workload's 32-actor buckets
+    (fast path) and with one 2048-actor bucket (the skew path)."""
     w = wl.ping_pong(1000, messages_per_pair=2_000, throughput=50)
     sg, so, a, b = _run_both(w, msg_capacity=1 << 20)
+    _assert_same(sg, so, a, b, "C1")
+    sg, so, a, b = _run_both(w, msg_capacity=1 << 20, bucket_actors=2048)
     _assert_same(sg, so, a, b, "C1")

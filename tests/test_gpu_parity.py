@@ -15,11 +15,12 @@ pytestmark = pytest.mark.gpu
 COUNT_KEYS = ("delivered", "dead_letters", "unhandled", "emitted", "staged", "supersteps", "in_flight")
 
 
-def run_both(w, max_steps=1 << 30, **cfg):
+def run_both(w, max_steps=1 << 30, bucket_actors=None, **cfg):
     from oracle import BspOracle
     kw = w.engine_kwargs()
     kw.update(cfg)
-    eng = GpuEngine(EngineConfig(**kw))
+    ba = w.bucket_actors if bucket_actors is None else bucket_actors
+    eng = GpuEngine(EngineConfig(bucket_actors=ba, **kw))
     w.apply_to(eng)
     sg = eng.run(max_steps)
     ref = BspOracle(**kw)
@@ -60,7 +61,7 @@ def test_partial_run_and_resume(built):
     """agx_run with a superstep budget, then resume: same as one long run."""
     from oracle import BspOracle
     w = wl.mixed(2000, seed=9, throughput=2, capacity=5)
-    eng = GpuEngine(EngineConfig(**w.engine_kwargs()))
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
     w.apply_to(eng)
     ref = BspOracle(**w.engine_kwargs())
     w.apply_to(ref)
@@ -94,7 +95,7 @@ def test_strict_replay_recovery(built, monkeypatch, strict, budgets):
     if not strict:
         monkeypatch.setenv("AGX_NO_STRICT", "1")
     w = wl.zipf_fanout(20_000, k=4, ttl=6, root_every=256, throughput=1000)
-    eng = GpuEngine(EngineConfig(msg_capacity=1 << 20, **w.engine_kwargs()))  # (234 K in flight at the peak)
+    eng = GpuEngine(EngineConfig(msg_capacity=1 << 20, **w.gpu_kwargs()))  # (234 K in flight at the peak)
     w.apply_to(eng)
     ref = BspOracle(**w.engine_kwargs())
     w.apply_to(ref)
@@ -146,7 +147,7 @@ def test_loopback_sharded(built, ranks):
     bit-exact vs the oracle in the sharded canonical order."""
     from oracle import BspOracle
     w = wl.mixed(3000, seed=ranks, throughput=2, capacity=6)
-    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.engine_kwargs())) for r in range(ranks)]
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.gpu_kwargs())) for r in range(ranks)]
     for e in engs:
         w.apply_to(e)
     sg = GpuEngine.group_run(engs)
@@ -173,7 +174,7 @@ def test_ring_1m_properties(built):
     """Full C2 size (1M actors): size-independent properties."""
     n, hops = 1_000_000, 16
     w = wl.token_ring(n, hops)
-    eng = GpuEngine(EngineConfig(**w.engine_kwargs()))
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
     w.apply_to(eng)
     st = eng.run()
     words, alive = eng.read_state()
@@ -207,7 +208,7 @@ def test_crdt_gcounter_1m_converges(built):
     """C4 size (1M replicas): every replica converges to the join of the 8 writers."""
     n, rounds = 1_000_000, 40
     w = wl.crdt_gossip(n, Kind.GCOUNTER, rounds=rounds)
-    eng = GpuEngine(EngineConfig(**w.engine_kwargs()))
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
     w.apply_to(eng)
     st = eng.run()
     words, _ = eng.read_state()
@@ -228,7 +229,7 @@ def test_crdt_loopback_sharded(built, ranks, workload):
         w = wl.crdt_gossip(2000, Kind.ORSET, rounds=8, throughput=2, capacity=0)
     else:
         w = wl.crdt_mixed(3000, rounds=4, throughput=2, capacity=5)
-    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.engine_kwargs())) for r in range(ranks)]
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.gpu_kwargs())) for r in range(ranks)]
     for e in engs:
         w.apply_to(e)
     sg = GpuEngine.group_run(engs)
@@ -279,7 +280,7 @@ def test_multipass_loopback_sharded(built, monkeypatch):
     monkeypatch.setenv("AGX_RADIX_BITS", "2")
     ranks = 3
     w = wl.mixed(30_000, seed=11, throughput=2, capacity=6)
-    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.engine_kwargs())) for r in range(ranks)]
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.gpu_kwargs())) for r in range(ranks)]
     for e in engs:
         w.apply_to(e)
     sg = GpuEngine.group_run(engs)
@@ -357,3 +358,40 @@ def test_zipf_index_ranges(built, shape):
     w = dataclasses.replace(w, fanout=(k, seed, cdf, perm))
     sg, so, a, b = run_both(w)
     assert_same(sg, so, a, b, f"zipf index {shape}")
+
+
+# ------------------------------------------------------------------ bucket width (agx_cfg.bucket_actors)
+BUCKET_CASES = {
+    "mixed": lambda: wl.mixed(6000, seed=21, throughput=3, capacity=5),
+    "ping_pong": lambda: wl.ping_pong(300, messages_per_pair=600, throughput=50),
+    "zipf": lambda: wl.zipf_fanout(30_000, k=4, ttl=3, root_every=16, throughput=7),
+    "power_law": lambda: wl.power_law_forward(30_000, ttl=6, capacity=8, throughput=5),
+    "orset": lambda: wl.crdt_gossip(6000, Kind.ORSET, rounds=5),
+    "crdt_mixed": lambda: wl.crdt_mixed(6000, rounds=4, throughput=2, capacity=5),
+}
+
+
+@pytest.mark.parametrize("ba", [32, 128, 512, 2048])
+@pytest.mark.parametrize("case", sorted(BUCKET_CASES))
+def test_bucket_width(built, case, ba):
+    """Any bucket width gives the oracle's result (buckets only group actors for the apply)."""
+    w = BUCKET_CASES[case]()
+    sg, so, a, b = run_both(w, bucket_actors=ba)
+    assert_same(sg, so, a, b, f"bucket {ba} {case}")
+
+
+@pytest.mark.parametrize("ba", [32, 512])
+@pytest.mark.parametrize("case", ["mixed", "zipf", "orset"])
+def test_bucket_width_multipass(built, monkeypatch, case, ba):
+    """Small buckets on the multi-pass grouping path (narrow radix digits)."""
+    monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    w = BUCKET_CASES[case]()
+    sg, so, a, b = run_both(w, bucket_actors=ba)
+    assert_same(sg, so, a, b, f"multipass bucket {ba} {case}")
+
+
+def test_bucket_width_rejects_bad_values(built):
+    from akka_amd._lib import AgxError
+    for ba in (3, 16, 48, 4096):
+        with pytest.raises(AgxError):
+            GpuEngine(EngineConfig(n_actors=100, bucket_actors=ba))

@@ -21,7 +21,7 @@ elif a.workload in ("c4g", "c4o"):
                        rounds=40)
 else:
     w = wl.ping_pong(1000, messages_per_pair=2_000_000, throughput=50)
-cfg = EngineConfig(**w.engine_kwargs())
+cfg = EngineConfig(**w.gpu_kwargs())
 if a.workload == "c1":
     cfg.msg_capacity = 1 << 20
 eng = GpuEngine(cfg)

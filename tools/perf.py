@@ -32,7 +32,7 @@ def main():
         w = wl.power_law_forward(a.n, ttl=hops, capacity=64, throughput=5)
     else:
         raise SystemExit("unknown workload")
-    eng = GpuEngine(EngineConfig(**w.engine_kwargs()))
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
     t0 = time.perf_counter()
     w.apply_to(eng)
     eng.run(16)

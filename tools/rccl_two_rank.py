@@ -57,7 +57,7 @@ def _rank_main(rank, world, port, a, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         w = _make(a)
-        eng = GpuEngine(EngineConfig(device=0, n_ranks=world, rank=rank, **w.engine_kwargs()))
+        eng = GpuEngine(EngineConfig(device=0, n_ranks=world, rank=rank, **w.gpu_kwargs()))
         w.apply_to(eng)
         uid = [GpuEngine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
