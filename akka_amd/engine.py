@@ -34,6 +34,10 @@ class Kind:
 CRDT_NODES = 8
 ORSET_ELEMS = 64
 CRDT_WORDS = {Kind.GCOUNTER: 8, Kind.PNCOUNTER: 16, Kind.ORSET: 260}
+# delta-CRDT mode (agx_set_delta_crdt): data + envelope/selector area + delta log (include/akka_gpu.h)
+DELTA_ENV_WORDS, DELTA_LOG = 12, 64
+CRDT_DELTA_WORDS = {k: w + DELTA_ENV_WORDS + DELTA_LOG * (6 if k == Kind.ORSET else 2) for k, w in CRDT_WORDS.items()}
+DELTA_WRITE = 0x800000
 WIDE_BIT = 0x80000000
 
 
@@ -45,6 +49,7 @@ class Op:
     REMOVE = 4
     CLEAR = 5
     GOSSIP = 6
+    DELTA_TICK = 7
 
     @staticmethod
     def make(op: int, arg: int = 0) -> int:
@@ -157,6 +162,10 @@ class GpuEngine:
 
     def set_gossip(self, fanout: int, seed: int) -> None:
         check(self.lib.agx_set_gossip(self._h, fanout, seed))
+
+    def set_delta_crdt(self, max_delta_size: int) -> None:
+        """Replicator delta-crdt.enabled / max-delta-size (0 = off)."""
+        check(self.lib.agx_set_delta_crdt(self._h, max_delta_size))
 
     def set_fanout(self, k: int, seed: int, cdf, perm) -> None:
         cdf = _u32(cdf)

@@ -12,7 +12,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .engine import CRDT_NODES, CRDT_WORDS, Kind, NO_SENDER, Op
+from .engine import CRDT_DELTA_WORDS, CRDT_NODES, CRDT_WORDS, DELTA_WRITE, Kind, NO_SENDER, Op
 
 SEED = 0x5EED
 M64 = (1 << 64) - 1
@@ -37,6 +37,7 @@ class Workload:
     ranges: list = field(default_factory=list)  # (first, count, kind, init_state or None)
     ring_stride: int | None = None
     gossip: tuple | None = None  # (fanout, seed)
+    delta_crdt: int = 0          # Replicator max-delta-size (0 = full-state gossip only)
     fanout: tuple | None = None  # (k, seed, cdf, perm)
     graph: tuple | None = None   # (row_ptr, col)
     tells: tuple | None = None   # (dst, src, payload)
@@ -58,6 +59,8 @@ class Workload:
             target.set_ring(self.ring_stride)
         if self.gossip is not None:
             target.set_gossip(*self.gossip)
+        if self.delta_crdt:
+            target.set_delta_crdt(self.delta_crdt)
         if self.fanout is not None:
             target.set_fanout(*self.fanout)
         if self.graph is not None:
@@ -162,6 +165,33 @@ def crdt_gossip(n: int = 1_000_000, kind: int = Kind.GCOUNTER, rounds: int = 32,
     # the ~3 x 512 messages in one 2048-message apply tile (the fast path)
     return Workload(f"crdt_gossip_{kind}", n, CRDT_WORDS[kind], fanout + 1, throughput, capacity,
                     [(0, n, kind, None)], gossip=(fanout, seed), tells=(dst, src, pay), bucket_actors=512)
+
+
+def crdt_delta(n: int = 1_000_000, kind: int = Kind.ORSET, rounds: int = 32, write: bool = True,
+               ops_per_replica: int = 0, gossip_rounds: int = 0, fanout: int = 1, max_delta_size: int = 50,
+               throughput: int = 5, seed: int = SEED, capacity: int = 0, bucket_actors: int = 512) -> Workload:
+    """C4 with delta-CRDT replication (Replicator delta-crdt.enabled, DD/Replicator.scala:1646-1695,
+    1953-2027; DD/DeltaPropagationSelector.scala): keys of 8 replicas (id = 8 * key + node).  Each
+    replica first applies `ops_per_replica` host updates, then runs `rounds` DeltaPropagationTicks
+    (`write`: each tick also tells the replica one seeded Update, a writer client) and, if
+    `gossip_rounds`, that many full-state GossipTicks to `fanout` random replicas of its key."""
+    ids = np.arange(n, dtype=np.uint32)
+    dsts, pays = [], []
+    if ops_per_replica:
+        dsts.append(np.repeat(ids, ops_per_replica))
+        pays.append(crdt_ops(n, kind, ops_per_replica, seed).reshape(-1))
+    if rounds:
+        dsts.append(ids)
+        pays.append(np.full(n, Op.make(Op.DELTA_TICK, (rounds - 1) | (DELTA_WRITE if write else 0)), np.uint32))
+    if gossip_rounds:
+        dsts.append(ids)
+        pays.append(np.full(n, Op.make(Op.GOSSIP, gossip_rounds - 1), np.uint32))
+    dst = np.concatenate(dsts)
+    pay = np.concatenate(pays)
+    src = np.full(dst.size, NO_SENDER, np.uint32)
+    return Workload(f"crdt_delta_{kind}", n, CRDT_DELTA_WORDS[kind], max(4, fanout + 1), throughput, capacity,
+                    [(0, n, kind, None)], gossip=(fanout, seed), delta_crdt=max_delta_size, tells=(dst, src, pay),
+                    bucket_actors=bucket_actors)
 
 
 def crdt_mixed(n: int = 4096, rounds: int = 4, seed: int = 3, throughput: int = 3, capacity: int = 0) -> Workload:

@@ -82,7 +82,7 @@ enum agx_behavior_kind {
 #define AGX_RES_STOPPED 1u
 #define AGX_RES_UNHANDLED 2u
 
-#define AGX_MAX_WORDS 260u
+#define AGX_MAX_WORDS 656u /* = AGX_ORSET_DELTA_WORDS (the widest layout) */
 #define AGX_MAX_RANKS 16u
 
 /* --- CRDT behaviours ---------------------------------------------------------
@@ -119,7 +119,49 @@ enum agx_behavior_kind {
 #define AGX_OP_REMOVE 4u
 #define AGX_OP_CLEAR 5u
 #define AGX_OP_GOSSIP 6u
+#define AGX_OP_DELTA_TICK 7u
 #define AGX_OP(op, arg) (((uint32_t)(op) << 24) | ((uint32_t)(arg) & 0xFFFFFFu))
+
+/* --- delta-CRDT replication (agx_set_delta_crdt; Replicator delta-crdt.enabled) --------
+ * Replicas form keys of AGX_CRDT_NODES consecutive ids (key = id / 8, node = id % 8): the
+ * 8 replicas of a key are the key's DataEnvelopes on 8 Replicator nodes, and gossip (full
+ * state and deltas) only flows between them.  Each replica's state words are the data
+ * words followed by the envelope/selector area and a delta log (u32 view, D = data words):
+ *   u32[2D + 0..7]    DataEnvelope.deltaVersions (seqNr last applied per node; DD/Replicator.scala:910-917)
+ *   u32[2D + 8]       DeltaPropagationSelector.deltaCounter  (DD/DeltaPropagationSelector.scala:44-57)
+ *   u32[2D + 9]       deltaNodeRoundRobinCounter
+ *   u32[2D + 10..17]  deltaSentToNode per node (0 = nothing sent)
+ *   u32[2D + 24 + AGX_DELTA_LOG_U32(kind) * (seq % AGX_DELTA_LOG) ...]  deltaEntries ring:
+ *       counters: {seq, type (0 = NoDeltaPlaceholder, 1 = increments delta, 2 = decrements delta), value lo, hi}
+ *       ORSet:    {seq, type (1 AddDeltaOp, 2 RemoveDeltaOp, 3 FullStateDeltaOp) | elem << 8, version, 0, vvector[8]}
+ * Ops on a delta replica:
+ *   AGX_OP_DELTA_TICK  arg = k | AGX_DELTA_WRITE?   DeltaPropagationTick (DD/Replicator.scala:1953-1963):
+ *       (AGX_DELTA_WRITE: first tell itself one seeded local update -- a writer client), then for
+ *       each node of this tick's round-robin slice with deltas after deltaSentToNode, merge them
+ *       into one delta group (DeltaOp.merge, max-delta-size) and tell that replica a
+ *       DeltaPropagation(fromSeqNr, toSeqNr); if k > 0, DELTA_TICK(k-1) to itself.
+ *   a DeltaPropagation is applied with causal delivery for ORSet (skip if already handled or a
+ *   seqNr is missing, DD/Replicator.scala:1965-2027) and ORSet.mergeDelta (DD/ORSet.scala:455-501);
+ *   counters merge it (no causal delivery needed).  A group that is a NoDeltaPlaceholder
+ *   (too large, or a no-op update in range) is still told, empty, and ignored by the receiver.  */
+#define AGX_DELTA_WRITE 0x800000u
+#define AGX_DELTA_LOG 64u            /* ring entries per replica (seqNrs not yet sent to every node) */
+#define AGX_DELTA_ENV_WORDS 12u      /* u64 words of the envelope / selector area */
+#define AGX_DELTA_MAX_SIZE 50u       /* Replicator max-delta-size (reference.conf delta-crdt) */
+#define AGX_DELTA_LOG_U32(orset) ((orset) ? 12u : 4u)
+/* CRDT message rows (u32).  Full state: the data words, then (delta mode) deltaVersions[8].
+ * DeltaPropagation (payload carries AGX_DELTA_ROW_BIT):
+ *   [0] ops in the group (bit 31: NoDeltaPlaceholder) [1] from node [2] fromSeqNr [3] toSeqNr
+ *   [4..11] the sender's deltaVersions, then the body --
+ *   counters: [12] 1 = increments slot present | 2 = decrements slot present, [13..14] / [15..16] values;
+ *   ORSet, per op: [type | n << 8] then AddDeltaOp: vvector(from), n x (element, version);
+ *     RemoveDeltaOp: element, deltaDot version, vvector[8];  FullStateDeltaOp: vvector[8].
+ * A group has < max-delta-size (<= 50) ops over <= AGX_DELTA_LOG seqNrs: <= 574 u32.        */
+#define AGX_DELTA_ROW_BIT 0x20000000u
+#define AGX_ORSET_DELTA_ROW_U32 576u
+#define AGX_GCOUNTER_DELTA_WORDS (AGX_GCOUNTER_WORDS + AGX_DELTA_ENV_WORDS + AGX_DELTA_LOG * 2u)
+#define AGX_PNCOUNTER_DELTA_WORDS (AGX_PNCOUNTER_WORDS + AGX_DELTA_ENV_WORDS + AGX_DELTA_LOG * 2u)
+#define AGX_ORSET_DELTA_WORDS (AGX_ORSET_WORDS + AGX_DELTA_ENV_WORDS + AGX_DELTA_LOG * 6u)
 
 typedef struct agx_cfg {
   uint32_t abi_version;   /* must be AGX_ABI_VERSION                                   */
@@ -174,6 +216,12 @@ agx_status agx_set_fanout(agx_engine* eng, uint32_t k, uint64_t seed, const uint
  * drawn uniformly from the other actors with the counter RNG (seed, self,
  * countdown, j) — Replicator.selectRandomNode (DD/Replicator.scala:2063-2064). */
 agx_status agx_set_gossip(agx_engine* eng, uint32_t fanout, uint64_t seed);
+/* Delta-CRDT replication (Replicator `delta-crdt.enabled = on`, `max-delta-size`,
+ * akka-distributed-data/src/main/resources/reference.conf:65-72): 0 = off (full-state
+ * gossip among all replicas of one key), 1..AGX_DELTA_MAX_SIZE = on, with keys of 8 replicas
+ * (see "delta-CRDT replication" above).  Call before the first agx_run; CRDT actors then need
+ * n_words >= the *_DELTA_WORDS of their kind.                                               */
+agx_status agx_set_delta_crdt(agx_engine* eng, uint32_t max_delta_size);
 /* Out-edge lists in CSR over GLOBAL ids: row_ptr[n_actors+1], col[row_ptr[n]].  */
 agx_status agx_set_graph(agx_engine* eng, const uint64_t* row_ptr, const uint32_t* col);
 /* The same CSR with the destinations generated on the device (workload setup for

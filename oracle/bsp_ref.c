@@ -230,6 +230,24 @@ void bsp_set_gossip(bsp_sim* s, uint32_t fanout, uint64_t seed) {
   s->P.gossip_seed = seed;
 }
 
+/* delta-crdt.enabled / max-delta-size (include/akka_gpu.h agx_set_delta_crdt) */
+int bsp_set_delta_crdt(bsp_sim* s, uint32_t max_delta_size) {
+  if (max_delta_size > AGX_DELTA_MAX_SIZE) return 1;
+  s->P.delta_max = max_delta_size;
+  uint32_t rw = 0;
+  for (uint64_t a = 0; a < s->n; ++a) {
+    const uint32_t k = s->kind[a];
+    const uint32_t need = k == AGX_KIND_GCOUNTER ? AGX_GCOUNTER_DELTA_WORDS
+                          : k == AGX_KIND_PNCOUNTER ? AGX_PNCOUNTER_DELTA_WORDS
+                          : k == AGX_KIND_ORSET ? AGX_ORSET_DELTA_WORDS : 0u;
+    if (max_delta_size && need > s->W) return 1;
+    const uint32_t r = ref_row_words(k, max_delta_size);
+    if (r > rw) rw = r;
+  }
+  if (ev_set_rw(&s->backlog, rw) || ev_set_rw(&s->emitted, rw) || ev_set_rw(&s->staged, rw)) return 1;
+  return 0;
+}
+
 int bsp_set_fanout(bsp_sim* s, uint32_t k, uint64_t seed, const uint32_t* cdf, const uint32_t* perm, uint64_t n) {
   s->P.fan_k = k;
   s->P.fan_seed = seed;
@@ -336,11 +354,11 @@ static int bsp_step(bsp_sim* s) {
 }
 
 int bsp_run(bsp_sim* s, uint32_t max_steps, agx_stats* out) {
-  for (uint32_t i = 0; i < max_steps; ++i)
+  for (uint32_t i = 0; i < max_steps && !s->P.error; ++i)
     if (!bsp_step(s)) break;
   s->st.in_flight = s->backlog.n + s->emitted.n + s->staged.n;
   if (out) *out = s->st;
-  return 0;
+  return s->P.error ? AGX_ECAPACITY : 0;
 }
 
 void bsp_read_state(bsp_sim* s, uint64_t first, uint64_t count, uint64_t* words, uint8_t* alive) {
@@ -381,3 +399,12 @@ void bsp_pncounter_merge(uint64_t* out_p, uint64_t* out_n, const uint64_t* ap, c
   bsp_gcounter_merge(out_p, ap, bp, r);
   bsp_gcounter_merge(out_n, an, bn, r);
 }
+
+/* ORSet deltas and VersionVector (crdt_ref.h), for the ORSetSpec delta / VersionVectorSpec KATs. */
+uint32_t bsp_orset_delta_bytes(void) { return (uint32_t)sizeof(orset_delta); }
+void bsp_orset_add_d(uint64_t* w, orset_delta* d, uint32_t node, uint32_t e, uint32_t ver) { orset_add_d(w, d, node, e, ver); }
+void bsp_orset_remove_d(uint64_t* w, orset_delta* d, uint32_t node, uint32_t e) { orset_remove_d(w, d, node, e); }
+void bsp_orset_clear_d(uint64_t* w, orset_delta* d) { orset_clear_d(w, d); }
+int bsp_orset_delta_merge(orset_delta* d1, const orset_delta* d2) { return orset_delta_merge(d1, d2); }
+void bsp_orset_merge_delta(uint64_t* w, const orset_delta* d) { orset_merge_delta(w, d); }
+uint32_t bsp_vv_compare(const uint32_t* a, const uint32_t* b) { return vv_compare(a, b); }

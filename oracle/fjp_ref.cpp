@@ -406,6 +406,18 @@ void fjp_set_gossip(void* h, uint32_t fanout, uint64_t seed) {
   s->P.gossip_seed = seed;
 }
 
+// delta-crdt.enabled / max-delta-size (see bsp_set_delta_crdt)
+int fjp_set_delta_crdt(void* h, uint32_t max_delta_size) {
+  Sim* s = (Sim*)h;
+  if (max_delta_size > AGX_DELTA_MAX_SIZE) return 1;
+  s->P.delta_max = max_delta_size;
+  for (uint64_t a = 0; a < s->P.n; ++a) {
+    const uint32_t r = ref_row_words(s->actors[a].kind, max_delta_size);
+    if (r > s->rw) s->rw = r;
+  }
+  return 0;
+}
+
 void fjp_set_fanout(void* h, uint32_t k, uint64_t seed, const uint32_t* cdf, const uint32_t* perm, uint64_t n) {
   Sim* s = (Sim*)h;
   s->zipf_cdf.assign(cdf, cdf + n);

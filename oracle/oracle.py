@@ -21,7 +21,7 @@ _lock = threading.Lock()
 _bsp = None
 _fjp = None
 
-W_MAX = 260
+W_MAX = 656
 NO_SENDER = 0xFFFFFFFF
 
 
@@ -62,11 +62,19 @@ def _load_bsp():
             "bsp_register_range": (ctypes.c_int, [vp, u64, u64, u32, P64, u64]),
             "bsp_set_ring": (None, [vp, u32]),
             "bsp_set_gossip": (None, [vp, u32, u64]),
+            "bsp_set_delta_crdt": (ctypes.c_int, [vp, u32]),
             "bsp_orset_merge": (None, [P64, P64]),
             "bsp_orset_add": (None, [P64, u32, u32]),
             "bsp_orset_remove": (None, [P64, u32]),
             "bsp_orset_subtract_dots": (None, [P32, P32, P32]),
             "bsp_crdt_peer": (u32, [u64, u32, u32, u32, u64]),
+            "bsp_orset_delta_bytes": (u32, []),
+            "bsp_orset_add_d": (None, [P64, vp, u32, u32, u32]),
+            "bsp_orset_remove_d": (None, [P64, vp, u32, u32]),
+            "bsp_orset_clear_d": (None, [P64, vp]),
+            "bsp_orset_delta_merge": (ctypes.c_int, [vp, vp]),
+            "bsp_orset_merge_delta": (None, [P64, vp]),
+            "bsp_vv_compare": (u32, [P32, P32]),
             "bsp_set_fanout": (ctypes.c_int, [vp, u32, u64, P32, P32, u64]),
             "bsp_set_graph": (ctypes.c_int, [vp, P64, P32]),
             "bsp_stage": (ctypes.c_int, [vp, P32, P32, P32, u64]),
@@ -101,6 +109,7 @@ def _load_fjp():
             "fjp_register_range": (ctypes.c_int, [vp, u64, u64, u32, P64, u64]),
             "fjp_set_ring": (None, [vp, u32]),
             "fjp_set_gossip": (None, [vp, u32, u64]),
+            "fjp_set_delta_crdt": (ctypes.c_int, [vp, u32]),
             "fjp_set_fanout": (None, [vp, u32, u64, P32, P32, u64]),
             "fjp_set_graph": (None, [vp, P64, P32]),
             "fjp_stage": (None, [vp, P32, P32, P32, u64]),
@@ -154,6 +163,10 @@ class BspOracle(_Base):
     def set_gossip(self, fanout, seed):
         self.lib.bsp_set_gossip(self.h, fanout, seed)
 
+    def set_delta_crdt(self, max_delta_size):
+        if self.lib.bsp_set_delta_crdt(self.h, max_delta_size):
+            raise ValueError("bsp_set_delta_crdt failed")
+
     def set_fanout(self, k, seed, cdf, perm):
         cdf, perm = _u32(cdf), _u32(perm)
         self.lib.bsp_set_fanout(self.h, k, seed, _p(cdf, ctypes.c_uint32), _p(perm, ctypes.c_uint32), cdf.size)
@@ -172,7 +185,9 @@ class BspOracle(_Base):
 
     def run(self, max_supersteps=1 << 30):
         st = Stats()
-        self.lib.bsp_run(self.h, min(int(max_supersteps), 0xFFFFFFFF), ctypes.byref(st))
+        rc = self.lib.bsp_run(self.h, min(int(max_supersteps), 0xFFFFFFFF), ctypes.byref(st))
+        if rc:
+            raise OverflowError(f"bsp_run: status {rc} (delta log overflow)")
         return st.as_dict()
 
     def read_state(self, first=0, count=None):
@@ -348,3 +363,83 @@ class orset:
 
 def crdt_peer(seed: int, self_id: int, round_: int, j: int, n: int) -> int:
     return int(_load_bsp().bsp_crdt_peer(seed, self_id, round_, j, n))
+
+
+class OrsetDop(ctypes.Structure):
+    """crdt_ref.h orset_dop: one AtomicDeltaOp (DD/ORSet.scala:43-96)."""
+    _fields_ = [("type", ctypes.c_uint32), ("n", ctypes.c_uint32), ("elem", ctypes.c_uint32 * 64),
+                ("dot", (ctypes.c_uint32 * 8) * 64), ("vv", ctypes.c_uint32 * 8)]
+
+
+class OrsetDelta(ctypes.Structure):
+    """crdt_ref.h orset_delta: None (nops 0), an AtomicDeltaOp or a DeltaGroup (DD/ORSet.scala:99-120)."""
+    _fields_ = [("group", ctypes.c_uint32), ("nops", ctypes.c_uint32), ("ops", OrsetDop * 64)]
+    TYPES = {1: "add", 2: "remove", 3: "full"}
+
+
+class orset_delta:
+    """ORSet values with their delta (ORSet.add/remove/clear/mergeDelta/DeltaOp.merge restated in
+    crdt_ref.h) -- for the ORSetSpec delta KATs.  A value is (state words, OrsetDelta)."""
+
+    @staticmethod
+    def _lib():
+        lib = _load_bsp()
+        assert lib.bsp_orset_delta_bytes() == ctypes.sizeof(OrsetDelta)
+        return lib
+
+    @staticmethod
+    def empty():
+        return orset.empty(), OrsetDelta()
+
+    @staticmethod
+    def _copy(v):
+        w, d = v
+        d2 = OrsetDelta()
+        ctypes.memmove(ctypes.byref(d2), ctypes.byref(d), ctypes.sizeof(OrsetDelta))
+        return np.array(w, copy=True), d2
+
+    @staticmethod
+    def add(v, node, e, ver):
+        w, d = orset_delta._copy(v)
+        orset_delta._lib().bsp_orset_add_d(_p(w, ctypes.c_uint64), ctypes.byref(d), node, e, ver)
+        return w, d
+
+    @staticmethod
+    def remove(v, node, e):
+        w, d = orset_delta._copy(v)
+        orset_delta._lib().bsp_orset_remove_d(_p(w, ctypes.c_uint64), ctypes.byref(d), node, e)
+        return w, d
+
+    @staticmethod
+    def clear(v):
+        w, d = orset_delta._copy(v)
+        orset_delta._lib().bsp_orset_clear_d(_p(w, ctypes.c_uint64), ctypes.byref(d))
+        return w, d
+
+    @staticmethod
+    def reset(v):
+        return np.array(v[0], copy=True), OrsetDelta()
+
+    @staticmethod
+    def merge(a, b):
+        return orset.merge(a[0], b[0]), OrsetDelta()
+
+    @staticmethod
+    def merge_delta(v, d):
+        w = np.array(v[0], copy=True)
+        orset_delta._lib().bsp_orset_merge_delta(_p(w, ctypes.c_uint64), ctypes.byref(d))
+        return w, OrsetDelta()
+
+    @staticmethod
+    def delta_merge(d1, d2):
+        out = OrsetDelta()
+        ctypes.memmove(ctypes.byref(out), ctypes.byref(d1), ctypes.sizeof(OrsetDelta))
+        if orset_delta._lib().bsp_orset_delta_merge(ctypes.byref(out), ctypes.byref(d2)):
+            raise OverflowError("delta group too long")
+        return out
+
+
+def vv_compare(a, b) -> str:
+    """VersionVector.compareTo on the fixed layout: '==' | '<' | '>' | '<>'."""
+    a, b = _u32(a), _u32(b)
+    return ("==", "<", ">", "<>")[_load_bsp().bsp_vv_compare(_p(a, ctypes.c_uint32), _p(b, ctypes.c_uint32))]

@@ -175,6 +175,196 @@ def orset_kats():
     }
 
 
+def versionvector_kats():
+    """VersionVectorSpec programs (node1..node4 -> 0..3).  `inc` draws the new version from one
+    global counter, as VersionVector.increment does from Timestamp.counter (VersionVector.scala:277-281).
+    ops: ["new", v] | ["copy", v, x] | ["inc", v, x, node] (v = x + node) | ["merge", v, x, y];
+    checks: ["size", v, n] | ["contains", v, node, bool] | ["cmp", x, y, "<"|">"|"<>"|"==", bool]
+    | ["gt_at", x, y, node] (x.versionAt(node) > y.versionAt(node)) | ["eq_at", x, y, node]."""
+    chain1 = [["new", "a1"], ["inc", "a2", "a1", 0], ["inc", "a3", "a2", 1], ["inc", "a4", "a3", 0]]
+    chain2 = [["new", "b1"], ["inc", "b2", "b1", 0], ["inc", "b3", "b2", 1], ["inc", "b4", "b3", 0]]
+    five = [["new", "a1"], ["inc", "a2", "a1", 0], ["inc", "a3", "a2", 1], ["inc", "a4", "a3", 1],
+            ["inc", "a5", "a4", 2]]
+    merged = lambda n: [["size", "m1", n], ["size", "m2", n]] + [["contains", m, k, True] for m in ("m1", "m2")
+                                                                  for k in range(n)] + \
+        [["cmp", "b3", "m1", "<", True], ["cmp", "a5", "m1", "<", True], ["cmp", "b3", "m2", "<", True],
+         ["cmp", "a5", "m2", "<", True], ["cmp", "m1", "m2", "==", True]]
+    return {
+        "source": "akka-distributed-data/src/test/scala/akka/cluster/ddata/VersionVectorSpec.scala",
+        "cases": [
+            {"name": "have zero versions when created (:32-35)", "ops": [["new", "v"]], "checks": [["size", "v", 0]]},
+            {"name": "not happen before itself (:37-42)", "ops": [["new", "v1"], ["new", "v2"]],
+             "checks": [["cmp", "v1", "v2", "<>", False]]},
+            {"name": "increment correctly (:44-54)",
+             "ops": [["new", "v1"], ["inc", "v2", "v1", 0], ["inc", "v3", "v2", 0], ["inc", "v4", "v3", 1]],
+             "checks": [["gt_at", "v2", "v1", 0], ["gt_at", "v3", "v2", 0], ["eq_at", "v4", "v3", 0],
+                        ["gt_at", "v4", "v3", 1]]},
+            {"name": "misc comparison test 1 (:56-68)", "ops": chain1 + chain2,
+             "checks": [["cmp", "a4", "b4", "<>", False]]},
+            {"name": "misc comparison test 2 (:70-83)", "ops": chain1 + chain2 + [["inc", "b5", "b4", 2]],
+             "checks": [["cmp", "a4", "b5", "<", True]]},
+            {"name": "misc comparison test 3 (:85-93)",
+             "ops": [["new", "a1"], ["inc", "a2", "a1", 0], ["new", "b1"], ["inc", "b2", "b1", 1]],
+             "checks": [["cmp", "a2", "b2", "<>", True]]},
+            {"name": "misc comparison test 4 (:95-107)",
+             "ops": [["new", "a1"], ["inc", "a2", "a1", 0], ["inc", "a3", "a2", 1], ["inc", "a4", "a3", 0],
+                     ["new", "b1"], ["inc", "b2", "b1", 0], ["inc", "b3", "b2", 0], ["inc", "b4", "b3", 2]],
+             "checks": [["cmp", "a4", "b4", "<>", True]]},
+            {"name": "misc comparison test 5 (:109-122)",
+             "ops": [["new", "a1"], ["inc", "a2", "a1", 1], ["inc", "a3", "a2", 1], ["new", "b1"],
+                     ["inc", "b2", "b1", 0], ["inc", "b3", "b2", 1], ["inc", "b4", "b3", 1], ["inc", "b5", "b4", 2]],
+             "checks": [["cmp", "a3", "b5", "<", True], ["cmp", "b5", "a3", ">", True]]},
+            {"name": "misc comparison test 6 (:124-135)",
+             "ops": [["new", "a1"], ["inc", "a2", "a1", 0], ["inc", "a3", "a2", 1], ["new", "b1"],
+                     ["inc", "b2", "b1", 0], ["inc", "b3", "b2", 0]],
+             "checks": [["cmp", "a3", "b3", "<>", True], ["cmp", "b3", "a3", "<>", True]]},
+            {"name": "misc comparison test 7 (:137-150)",
+             "ops": five + [["copy", "b1", "a4"], ["inc", "b2", "b1", 1], ["inc", "b3", "b2", 1]],
+             "checks": [["cmp", "a5", "b3", "<>", True], ["cmp", "b3", "a5", "<>", True]]},
+            {"name": "misc comparison test 8 (:152-164)",
+             "ops": [["new", "a1"], ["inc", "a2", "a1", 0], ["inc", "a3", "a2", 2], ["inc", "b1", "a3", 1],
+                     ["inc", "a4", "a3", 2]],
+             "checks": [["cmp", "a4", "b1", "<>", True], ["cmp", "b1", "a4", "<>", True]]},
+            {"name": "correctly merge two version vectors (:166-197)",
+             "ops": five + [["copy", "b1", "a4"], ["inc", "b2", "b1", 1], ["inc", "b3", "b2", 1],
+                            ["merge", "m1", "b3", "a5"], ["merge", "m2", "a5", "b3"]],
+             "checks": merged(3)},
+            {"name": "correctly merge two disjoint version vectors (:199-232)",
+             "ops": five + [["new", "b1"], ["inc", "b2", "b1", 3], ["inc", "b3", "b2", 3],
+                            ["merge", "m1", "b3", "a5"], ["merge", "m2", "a5", "b3"]],
+             "checks": merged(4)},
+            {"name": "pass blank version vector incrementing (:234-249)",
+             "ops": [["new", "v1"], ["new", "v2"], ["inc", "vv1", "v1", 0], ["inc", "vv2", "v2", 1]],
+             "checks": [["cmp", "vv1", "v1", ">", True], ["cmp", "vv2", "v2", ">", True],
+                        ["cmp", "vv1", "v2", ">", True], ["cmp", "vv2", "v1", ">", True],
+                        ["cmp", "vv2", "vv1", ">", False], ["cmp", "vv1", "vv2", ">", False]]},
+            {"name": "pass merging behavior (:251-264)",
+             "ops": [["new", "a"], ["new", "b"], ["inc", "a1", "a", 0], ["inc", "b1", "b", 1], ["inc", "a2", "a1", 0],
+                     ["merge", "c", "a2", "b1"], ["inc", "c1", "c", 2]],
+             "checks": [["cmp", "c1", "a2", ">", True], ["cmp", "c1", "b1", ">", True]]},
+        ],
+    }
+
+
+def orset_delta_kats():
+    """ORSetSpec "ORSet deltas" programs (:230-487) and "not pollute the vvector of result during
+    mergeRemoveDelta" (:588-600).  node1..node3 -> 0..2, nodeA/nodeB -> 0/1; elements numbered by
+    first appearance; versions from one global counter (Timestamp.counter).
+    ops: ["empty", x] | ["add", x, y, node, e] (x = y.add(node, e)) | ["remove", x, y, node, e]
+    | ["clear", x, y] | ["reset", x, y] (resetDelta) | ["merge", x, y, z] | ["merge_delta", x, y, d]
+    | ["delta", d, x] (x.delta.get) | ["dmerge", d, d1, d2] (d1.merge(d2));
+    checks: ["elements", x, [..]] | ["absent", x, e] | ["equal", x, y] | ["vv_has", x, node, bool]
+    | ["add_op", d, [..]] (asAddDeltaOp(d).underlying.elements) | ["group", d, size, last_type]
+    | ["last_add", d, [..]] (the last op of a DeltaGroup is an AddDeltaOp with these elements)."""
+    return {
+        "source": "akka-distributed-data/src/test/scala/akka/cluster/ddata/ORSetSpec.scala",
+        "cases": [
+            {"name": "work for additions (:242-271)",
+             "ops": [["empty", "s1"], ["add", "s2", "s1", 0, "a"], ["delta", "d2", "s2"],
+                     ["merge_delta", "t1", "s1", "d2"],
+                     ["reset", "r2", "s2"], ["add", "s3a", "r2", 0, "b"], ["add", "s3", "s3a", 0, "c"],
+                     ["delta", "d3", "s3"], ["merge_delta", "t2", "s2", "d3"],
+                     ["reset", "r3", "s3"], ["add", "s4", "r3", 1, "d"], ["delta", "d4", "s4"],
+                     ["merge_delta", "t3", "s3", "d4"],
+                     ["add", "s5", "r3", 0, "e"], ["merge", "s6", "s5", "s4"], ["merge_delta", "t4", "s5", "d4"],
+                     ["add", "s7", "r3", 0, "d"], ["merge", "s8", "s7", "s4"], ["merge_delta", "t5", "s7", "d4"],
+                     ["delta", "d7", "s7"], ["merge_delta", "t6", "s4", "d7"]],
+             "checks": [["add_op", "d2", ["a"]], ["equal", "t1", "s2"], ["add_op", "d3", ["b", "c"]],
+                        ["equal", "t2", "s3"], ["add_op", "d4", ["d"]], ["equal", "t3", "s4"], ["equal", "t4", "s6"],
+                        ["equal", "t5", "s8"], ["equal", "t6", "s8"]]},
+            {"name": "handle another concurrent add scenario (:273-285)",
+             "ops": [["empty", "s1"], ["add", "s2", "s1", 0, "a"], ["add", "s3", "s2", 0, "b"],
+                     ["add", "s4", "s2", 1, "c"], ["merge", "s5", "s4", "s3"], ["delta", "d3", "s3"],
+                     ["merge_delta", "s6", "s4", "d3"]],
+             "checks": [["elements", "s5", ["a", "b", "c"]], ["elements", "s6", ["a", "b", "c"]]]},
+            {"name": "merge deltas into delta groups (:287-313)",
+             "ops": [["empty", "s1"], ["add", "s2", "s1", 0, "a"], ["delta", "d2", "s2"], ["reset", "r2", "s2"],
+                     ["add", "s3", "r2", 0, "b"], ["delta", "d3", "s3"], ["dmerge", "d4", "d2", "d3"],
+                     ["merge_delta", "t1", "s1", "d4"], ["merge_delta", "t2", "s2", "d4"],
+                     ["reset", "r3", "s3"], ["remove", "s5", "r3", 0, "b"], ["delta", "d5", "s5"],
+                     ["dmerge", "d6", "d4", "d5"], ["merge_delta", "t3", "s3", "d6"],
+                     ["reset", "r5", "s5"], ["add", "s7", "r5", 0, "c"], ["reset", "r7", "s7"],
+                     ["add", "s8", "r7", 0, "d"], ["delta", "d7", "s7"], ["delta", "d8", "s8"],
+                     ["dmerge", "d9a", "d6", "d7"], ["dmerge", "d9", "d9a", "d8"],
+                     ["merge_delta", "t4", "s5", "d9"], ["merge_delta", "t5a", "s5", "d7"],
+                     ["merge_delta", "t5", "t5a", "d8"]],
+             "checks": [["add_op", "d4", ["a", "b"]], ["equal", "t1", "s3"], ["equal", "t2", "s3"],
+                        ["group", "d6", 2, "remove"], ["equal", "t3", "s5"], ["last_add", "d9", ["c", "d"]],
+                        ["group", "d9", 3, "add"], ["equal", "t4", "s8"], ["equal", "t5", "s8"]]},
+            {"name": "work for removals (:315-334)",
+             "ops": [["empty", "s1"], ["add", "x1", "s1", 0, "a"], ["add", "x2", "x1", 0, "b"], ["reset", "s2", "x2"],
+                     ["remove", "s3", "s2", 0, "b"], ["merge", "t1", "s2", "s3"], ["delta", "d3", "s3"],
+                     ["merge_delta", "t2", "s2", "d3"],
+                     ["add", "x4", "s2", 1, "c"], ["reset", "s4", "x4"], ["merge", "s5", "s4", "s3"],
+                     ["merge_delta", "t3", "s4", "d3"],
+                     ["add", "s6", "s5", 1, "b"], ["merge_delta", "t4", "s6", "d3"]],
+             "checks": [["equal", "t1", "s3"], ["equal", "t2", "s3"], ["elements", "t2", ["a"]],
+                        ["elements", "s5", ["a", "c"]], ["equal", "t3", "s5"], ["equal", "t4", "s6"],
+                        ["elements", "t4", ["a", "b", "c"]]]},
+            {"name": "work for clear (:336-358)",
+             "ops": [["empty", "s1"], ["add", "x1", "s1", 0, "a"], ["add", "s2", "x1", 0, "b"], ["reset", "r2", "s2"],
+                     ["clear", "s3", "r2"], ["reset", "r3", "s3"], ["add", "s4", "r3", 0, "c"],
+                     ["merge", "t1", "s2", "s3"], ["delta", "d3", "s3"], ["merge_delta", "t2", "s2", "d3"],
+                     ["delta", "d4", "s4"], ["merge_delta", "t3", "s2", "d3"], ["merge_delta", "s5", "t3", "d4"],
+                     ["add", "s6", "r2", 1, "d"], ["merge", "s7", "s6", "s3"], ["merge_delta", "t4", "s6", "d3"],
+                     ["add", "s8", "s7", 1, "b"], ["merge_delta", "t5", "s8", "d3"]],
+             "checks": [["equal", "t1", "s3"], ["equal", "t2", "s3"], ["elements", "s5", ["c"]], ["equal", "s5", "s4"],
+                        ["elements", "s7", ["d"]], ["equal", "t4", "s7"], ["equal", "t5", "s8"],
+                        ["elements", "t5", ["b", "d"]]]},
+            {"name": "handle a mixed add/remove scenario (:360-377)",
+             "ops": [["empty", "s1"], ["reset", "r1", "s1"], ["remove", "s2", "r1", 0, "e"], ["reset", "r2", "s2"],
+                     ["add", "s3", "r2", 0, "b"], ["reset", "r3", "s3"], ["add", "s4", "r3", 0, "a"],
+                     ["reset", "r4", "s4"], ["remove", "s5", "r4", 0, "b"], ["delta", "d3", "s3"],
+                     ["delta", "d4", "s4"], ["delta", "d5", "s5"], ["dmerge", "g1a", "d3", "d4"],
+                     ["dmerge", "g1", "g1a", "d5"], ["merge_delta", "s7", "s2", "g1"],
+                     ["add", "s8", "r2", 1, "z"], ["merge_delta", "s9", "s8", "g1"]],
+             "checks": [["elements", "s7", ["a"]], ["elements", "s9", ["a", "z"]]]},
+            {"name": "handle a mixed add/remove scenario 2 (:379-399)",
+             "ops": [["empty", "s1"], ["reset", "r1", "s1"], ["add", "s2", "r1", 0, "a"], ["reset", "r2", "s2"],
+                     ["add", "s3", "r2", 0, "b"], ["reset", "r3", "s3"], ["add", "s4", "r3", 1, "a"],
+                     ["reset", "r4", "s4"], ["remove", "s5", "r4", 0, "a"], ["delta", "d2", "s2"],
+                     ["delta", "d3", "s3"], ["dmerge", "delta1", "d2", "d3"], ["delta", "delta2", "s4"],
+                     ["empty", "t1"], ["merge_delta", "t2a", "t1", "delta1"], ["merge_delta", "t2", "t2a", "delta2"],
+                     ["reset", "rt2", "t2"], ["add", "t3", "rt2", 2, "z"], ["delta", "d5", "s5"],
+                     ["merge_delta", "t4", "t3", "d5"]],
+             "checks": [["elements", "s5", ["b"]], ["elements", "t2", ["a", "b"]], ["elements", "t4", ["b", "z"]]]},
+            {"name": "handle a mixed add/remove scenario 3 (:401-421)",
+             "ops": [["empty", "s1"], ["reset", "r1", "s1"], ["add", "s2", "r1", 0, "a"], ["reset", "r2", "s2"],
+                     ["add", "s3", "r2", 0, "b"], ["reset", "r3", "s3"], ["add", "s4", "r3", 1, "a"],
+                     ["reset", "r4", "s4"], ["remove", "s5", "r4", 0, "a"], ["delta", "d2", "s2"],
+                     ["delta", "d3", "s3"], ["dmerge", "delta1", "d2", "d3"], ["empty", "t1"],
+                     ["merge_delta", "t2", "t1", "delta1"], ["reset", "rt2", "t2"], ["add", "t3", "rt2", 2, "a"],
+                     ["delta", "d5", "s5"], ["merge_delta", "t4", "t3", "d5"]],
+             "checks": [["elements", "s5", ["b"]], ["elements", "t2", ["a", "b"]], ["elements", "t4", ["b", "a"]]]},
+            {"name": "not have anomalies for ORSet in complex but realistic scenario (:423-455)",
+             "ops": [["empty", "e0"], ["add", "x1", "e0", 0, "q"], ["remove", "n11", "x1", 0, "q"], ["delta", "dl11", "n11"],
+                     ["reset", "r11", "n11"], ["add", "x2", "r11", 0, "z"], ["remove", "n12", "x2", 0, "z"],
+                     ["delta", "dl12", "n12"], ["merge_delta", "x3", "e0", "dl11"], ["reset", "x3r", "x3"],
+                     ["add", "n21", "x3r", 1, "x"], ["delta", "dl21", "n21"], ["reset", "r21", "n21"],
+                     ["add", "x4", "r21", 1, "a"], ["remove", "n22", "x4", 1, "a"], ["delta", "dl22", "n22"],
+                     ["merge_delta", "y1", "e0", "dl11"], ["merge_delta", "y2", "y1", "dl21"],
+                     ["merge_delta", "n31", "y2", "dl12"], ["merge", "m1", "n31", "n22"],
+                     ["merge_delta", "m2", "n31", "dl22"]],
+             "checks": [["absent", "m1", "a"], ["elements", "m2", ["x"]]]},
+            {"name": "require causal delivery of deltas (:457-486)",
+             "ops": [["empty", "e"], ["add", "s0", "e", 0, "a"], ["reset", "r0", "s0"], ["add", "s11", "r0", 0, "b"],
+                     ["reset", "r11", "s11"], ["add", "s12", "r11", 0, "c"], ["add", "s21", "r0", 1, "d"],
+                     ["delta", "d21", "s21"], ["delta", "d12", "s12"], ["delta", "d11", "s11"],
+                     ["merge_delta", "x1", "s0", "d21"], ["merge_delta", "s31", "x1", "d12"],
+                     ["merge_delta", "y1", "s0", "d11"], ["merge_delta", "y2", "y1", "d12"],
+                     ["merge_delta", "s41", "y2", "d21"], ["merge", "s32", "s31", "s41"]],
+             "checks": [["elements", "s31", ["a", "c", "d"]], ["elements", "s41", ["a", "b", "c", "d"]],
+                        ["elements", "s32", ["a", "c", "d"]]]},
+            {"name": "not pollute the vvector of result during mergeRemoveDelta (:588-600)",
+             "ops": [["empty", "e"], ["add", "a", "e", 0, "a"], ["add", "x1", "a", 1, "b"], ["remove", "x2", "x1", 1, "b"],
+                     ["reset", "x3", "x2"], ["remove", "a1", "x3", 0, "a"], ["delta", "da", "a"],
+                     ["delta", "da1", "a1"], ["merge_delta", "y1", "e", "da"], ["merge_delta", "a2", "y1", "da1"]],
+             "checks": [["vv_has", "a", 0, True], ["vv_has", "a", 1, False], ["vv_has", "a1", 0, True],
+                        ["vv_has", "a1", 1, True], ["elements", "a2", []], ["vv_has", "a2", 1, False]]},
+        ],
+    }
+
+
 def mailbox_kats():
     """Queue semantics as engine runs on one receiver (COUNTER behaviour:
     w0 = messages invoked, w1 = sum of payloads)."""
@@ -226,6 +416,8 @@ def main():
         "gcounter_kat.json": gcounter_kats(),
         "pncounter_kat.json": pncounter_kats(),
         "orset_kat.json": orset_kats(),
+        "orset_delta_kat.json": orset_delta_kats(),
+        "versionvector_kat.json": versionvector_kats(),
         "mailbox_kat.json": mailbox_kats(),
         "pingpong_kat.json": pingpong_kats(),
         "ring_kat.json": ring_kats(),

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from akka_amd import workloads as wl
-from akka_amd.engine import Kind
+from akka_amd.engine import Kind, Op
 from oracle import BspOracle, FjpOracle, crdt, java_hash, shard_id
 
 GOLD = pathlib.Path(__file__).resolve().parent / "golden"
@@ -260,3 +260,162 @@ def test_crdt_gossip_converges_to_writers_merge(kind):
                 op, arg = int(p) >> 24, int(p) & 0xFFFFFF
                 exp[k if op == 1 else 8 + k] += arg
     assert all(np.array_equal(r, exp) for r in ws)
+
+
+def test_versionvector_kats():
+    """VersionVectorSpec (merge / compare / increment) on the fixed 8-node layout; versions come
+    from one global counter like Timestamp.counter (VersionVector.scala:277-281)."""
+    from oracle.oracle import vv_compare
+    for c in load("versionvector_kat.json")["cases"]:
+        vs, clock = {}, [0]
+        for op in c["ops"]:
+            if op[0] == "new":
+                vs[op[1]] = np.zeros(8, np.uint32)
+            elif op[0] == "copy":
+                vs[op[1]] = vs[op[2]].copy()
+            elif op[0] == "inc":
+                clock[0] += 1
+                v = vs[op[2]].copy()
+                v[op[3]] = clock[0]
+                vs[op[1]] = v
+            elif op[0] == "merge":
+                vs[op[1]] = np.maximum(vs[op[2]], vs[op[3]])
+        for chk in c["checks"]:
+            k = chk[0]
+            if k == "size":
+                assert int(np.count_nonzero(vs[chk[1]])) == chk[2], (c["name"], chk)
+            elif k == "contains":
+                assert bool(vs[chk[1]][chk[2]]) == chk[3], (c["name"], chk)
+            elif k == "cmp":
+                assert (vv_compare(vs[chk[1]], vs[chk[2]]) == chk[3]) == chk[4], (c["name"], chk)
+            elif k == "gt_at":
+                assert vs[chk[1]][chk[3]] > vs[chk[2]][chk[3]], (c["name"], chk)
+            elif k == "eq_at":
+                assert vs[chk[1]][chk[3]] == vs[chk[2]][chk[3]], (c["name"], chk)
+
+
+def test_orset_delta_kats():
+    """ORSetSpec "ORSet deltas" (AddDeltaOp / RemoveDeltaOp / FullStateDeltaOp / DeltaGroup,
+    mergeDelta, mergeRemoveDelta) through the oracle's restatement (crdt_ref.h)."""
+    from oracle.oracle import OrsetDelta, orset, orset_delta
+    for c in load("orset_delta_kat.json")["cases"]:
+        vals, deltas, idx, clock = {}, {}, {}, [0]
+        el = lambda name: idx.setdefault(name, len(idx))
+        for op in c["ops"]:
+            k = op[0]
+            if k == "empty":
+                vals[op[1]] = orset_delta.empty()
+            elif k == "add":
+                clock[0] += 1
+                vals[op[1]] = orset_delta.add(vals[op[2]], op[3], el(op[4]), clock[0])
+            elif k == "remove":
+                vals[op[1]] = orset_delta.remove(vals[op[2]], op[3], el(op[4]))
+            elif k == "clear":
+                vals[op[1]] = orset_delta.clear(vals[op[2]])
+            elif k == "reset":
+                vals[op[1]] = orset_delta.reset(vals[op[2]])
+            elif k == "merge":
+                vals[op[1]] = orset_delta.merge(vals[op[2]], vals[op[3]])
+            elif k == "merge_delta":
+                vals[op[1]] = orset_delta.merge_delta(vals[op[2]], deltas[op[3]])
+            elif k == "delta":
+                d = vals[op[2]][1]
+                assert d.nops > 0, (c["name"], op, "delta.get on None")
+                deltas[op[1]] = d
+            elif k == "dmerge":
+                deltas[op[1]] = orset_delta.delta_merge(deltas[op[2]], deltas[op[3]])
+            else:
+                raise AssertionError(op)
+        inv = lambda: {v: k for k, v in idx.items()}
+        for chk in c["checks"]:
+            k = chk[0]
+            if k == "elements":
+                assert {inv()[e] for e in orset.elements(vals[chk[1]][0])} == set(chk[2]), (c["name"], chk)
+            elif k == "absent":
+                assert el(chk[2]) not in orset.elements(vals[chk[1]][0]), (c["name"], chk)
+            elif k == "equal":  # ORSet.equals: elementsMap and vvector, not the delta
+                assert np.array_equal(vals[chk[1]][0], vals[chk[2]][0]), (c["name"], chk)
+            elif k == "vv_has":
+                assert bool(orset.vvector(vals[chk[1]][0]).get(chk[2], 0)) == chk[3], (c["name"], chk)
+            elif k in ("add_op", "last_add"):
+                d = deltas[chk[1]]
+                op = d.ops[d.nops - 1]
+                assert (k == "last_add") == bool(d.group) and OrsetDelta.TYPES[op.type] == "add", (c["name"], chk)
+                assert {inv()[op.elem[i]] for i in range(op.n)} == set(chk[2]), (c["name"], chk)
+            elif k == "group":
+                d = deltas[chk[1]]
+                assert d.group and d.nops == chk[2], (c["name"], chk)
+                assert OrsetDelta.TYPES[d.ops[d.nops - 1].type] == chk[3], (c["name"], chk)
+
+
+@pytest.mark.parametrize("kind", [Kind.GCOUNTER, Kind.PNCOUNTER, Kind.ORSET])
+def test_delta_crdt_converges(kind):
+    """Delta-CRDT replication on the oracle (DeltaPropagationSelector + receiveDeltaPropagation):
+    counters converge from deltas alone to the slot-wise sums of each node's updates; ORSet
+    replicas converge once full-state gossip runs beside the deltas (a RemoveDeltaOp only removes
+    an element whose dots it covers, DD/ORSet.scala:471-501, so deltas alone can leave dots that
+    the full-state merge drops -- as in the reference)."""
+    n, opr = 8 * 40, 6
+    gossip = 40 if kind == Kind.ORSET else 0
+    w = wl.crdt_delta(n, kind, rounds=24, write=False, ops_per_replica=opr, gossip_rounds=gossip)
+    o = BspOracle(**w.engine_kwargs())
+    w.apply_to(o)
+    st = o.run()
+    assert st["in_flight"] == 0 and st["unhandled"] == 0 and st["dead_letters"] == 0
+    ws, _ = o.read_state()
+    D = wl.CRDT_WORDS[kind]
+    data = ws[:, :D].reshape(-1, 8, D)
+    assert all(np.array_equal(g[0], g[i]) for g in data for i in range(8))
+    env = ws[:, D:D + 12].view(np.uint32)
+    assert (env[:, 8] == opr).all()  # deltaCounter: one seqNr per update
+    if kind != Kind.ORSET:
+        ops = wl.crdt_ops(n, kind, opr)
+        exp = np.zeros((n, D), np.uint64)
+        for a in range(n):
+            for p in ops[a]:
+                op, arg = int(p) >> 24, int(p) & 0xFFFFFF
+                exp[a & ~7, (8 if op == Op.DECREMENT else 0) + a % 8] += arg
+        assert np.array_equal(data[:, 0], exp[::8])
+    else:  # causal delivery: every replica applied every other node's deltas in order
+        for a in range(n):
+            dv = env[a, :8].copy()
+            dv[a % 8] = opr
+            assert (dv == opr).all()
+
+
+def test_delta_crdt_placeholders_and_log_capacity():
+    """max-delta-size: a group of >= M ops is a NoDeltaPlaceholder (never applied; deltaSentToNode
+    still advances, DD/DeltaPropagationSelector.scala:112-131), so without full-state gossip the
+    receivers keep nothing; a counter update by 0 records a NoDeltaPlaceholder
+    (DD/Replicator.scala:1648-1652).  More than AGX_DELTA_LOG unsent seqNrs overflow the log."""
+    n = 16
+    w = wl.crdt_delta(n, Kind.ORSET, rounds=4, write=False, ops_per_replica=6, max_delta_size=2)
+    o = BspOracle(**w.engine_kwargs())
+    w.apply_to(o)
+    o.run()
+    ws, _ = o.read_state()
+    env = ws[:, 260:272].view(np.uint32)
+    adds_only = (wl.crdt_ops(n, Kind.ORSET, 6) >> 24 == Op.ADD).all(axis=1)  # one AddDeltaOp: deltaSize 1
+    assert adds_only.any() and not adds_only.all()
+    for a in range(n):
+        for b in range(8):
+            if b != a % 8:
+                assert env[a, b] == (6 if adds_only[(a & ~7) + b] else 0), (a, b)
+    assert (env[:, 8] == 6).all()
+    # a zero increment in the range turns the whole counter group into a placeholder
+    w = wl.crdt_delta(n, Kind.GCOUNTER, rounds=4, write=False)
+    o = BspOracle(**w.engine_kwargs())
+    w.apply_to(o, stage_tells=False)
+    ids = np.arange(n, dtype=np.uint32)
+    o.tell(np.concatenate([ids, ids, ids]),
+           np.concatenate([np.full(n, Op.make(Op.INCREMENT, 5), np.uint32), np.full(n, Op.make(Op.INCREMENT, 0), np.uint32),
+                           np.full(n, Op.make(Op.DELTA_TICK, 3), np.uint32)]))
+    o.run()
+    ws, _ = o.read_state()
+    assert all(ws[a, b] == (5 if b == a % 8 else 0) for a in range(n) for b in range(8))
+    # log overflow: 70 updates with no propagation
+    w = wl.crdt_delta(n, Kind.ORSET, rounds=0, write=False, ops_per_replica=70)
+    o = BspOracle(**w.engine_kwargs())
+    w.apply_to(o)
+    with pytest.raises(OverflowError):
+        o.run()
