@@ -80,6 +80,9 @@ SIGNATURES = {
                                             ctypes.c_void_p, ctypes.c_size_t]),
     "agx_set_ring": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32]),
     "agx_set_gossip": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64]),
+    "agx_set_delta_crdt": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32]),
+    "agx_set_behaviors": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "agx_set_fanout": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, c_u32p, c_u32p,
                                         ctypes.c_uint64]),
     "agx_set_graph": (ctypes.c_int32, [ctypes.c_void_p, c_u64p, c_u32p]),

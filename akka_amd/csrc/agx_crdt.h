@@ -9,6 +9,11 @@
 //                                   (:164-229), mergeDisjointKeys (:236-259),
 //                                   subtractDots (:127-160), VersionVector.merge
 //   GossipTick -> gossipTo          DD/Replicator.scala:1316,2029-2064
+//   delta-CRDT replication (agx_set_delta_crdt):
+//     receiveUpdate delta bookkeeping DD/Replicator.scala:1646-1695
+//     DeltaPropagationSelector        DD/DeltaPropagationSelector.scala:44-155
+//     receiveDeltaPropagation         DD/Replicator.scala:1965-2027 (causal delivery for ORSet)
+//     ORSet.mergeDelta / mergeRemoveDelta / DeltaOp.merge  DD/ORSet.scala:43-120,455-501
 //
 // State lives in the actor SoA (word-major u64, coalesced across the lanes of
 // a wave that drain consecutive actors).  A state gossip carries a handle to
@@ -21,8 +26,9 @@
 
 namespace agx {
 
-// state gossip payload = (data type << 30) | handle; handles index heap rows, then rx rows
-constexpr uint32_t kHandleMask = 0x3FFFFFFFu;
+// state gossip payload = (data type << 30) | (DeltaPropagation << 29) | handle; handles index
+// heap rows, then rx rows
+constexpr uint32_t kHandleMask = AGX_DELTA_ROW_BIT - 1u;
 
 __device__ __forceinline__ bool is_wide(uint32_t src) { return (src & AGX_WIDE_BIT) && src != AGX_NO_SENDER; }
 __device__ __forceinline__ bool is_crdt(uint32_t kind) {
@@ -64,19 +70,352 @@ __device__ __forceinline__ uint32_t crdt_peer(uint64_t seed, uint32_t self, uint
   return d >= self ? d + 1u : d;
 }
 
-// Phase A: tells and snapshot rows one message will produce (no state access).
-__device__ __forceinline__ uint32_t crdt_count(const DevParams& P, uint32_t src, uint32_t pay, uint32_t* rows) {
-  if (is_wide(src) || (pay >> 24) != AGX_OP_GOSSIP) return 0;
-  const uint32_t f = P.n_global > 1 ? P.gossip_f : 0u;
-  *rows += f ? 1u : 0u;
-  return f + ((pay & 0xFFFFFFu) > 0 ? 1u : 0u);
-}
-
 __device__ __forceinline__ uint32_t orset_merge_entry(uint32_t l, uint32_t r, uint32_t lvv, uint32_t rvv) {
   if (l == r) return l;
   const uint32_t lk = l > rvv ? l : 0u, rk = r > lvv ? r : 0u;
   return lk > rk ? lk : rk;
 }
+
+// Delta-CRDT mode: the replicas of a key are [self & ~7, +m), m = min(8, n - (self & ~7)); the
+// full-state gossip peer is uniform over the other m - 1 (Replicator.selectRandomNode).
+__device__ __forceinline__ uint32_t key_size(uint32_t self, uint32_t n) {
+  const uint32_t m = n - (self & ~(AGX_CRDT_NODES - 1u));
+  return m < AGX_CRDT_NODES ? m : AGX_CRDT_NODES;
+}
+__device__ __forceinline__ uint32_t crdt_key_peer(uint64_t seed, uint32_t self, uint32_t round, uint32_t j, uint32_t n) {
+  const uint32_t m = key_size(self, n), node = self % AGX_CRDT_NODES;
+  const uint32_t d = (uint32_t)(fanout_rand(seed, self, round | 0x08000000u, j) % (uint64_t)(m - 1u));
+  return self - node + (d >= node ? d + 1u : d);
+}
+
+// u32 view of one actor's word-major state (u32 i = half i & 1 of word i >> 1)
+struct St32 {
+  uint64_t* st;
+  size_t nl;
+  __device__ __forceinline__ uint32_t ld(uint32_t i) const {
+    const uint64_t v = st[(size_t)(i >> 1) * nl];
+    return (i & 1u) ? (uint32_t)(v >> 32) : (uint32_t)v;
+  }
+  __device__ __forceinline__ void put(uint32_t i, uint32_t x) const {
+    reinterpret_cast<uint32_t*>(st + (size_t)(i >> 1) * nl)[i & 1u] = x;
+  }
+};
+
+// Envelope / selector area and delta log (include/akka_gpu.h "delta-CRDT replication"), u32 indices
+__device__ __forceinline__ uint32_t dl_env(uint32_t kind) { return 2u * crdt_words(kind); }
+__device__ __forceinline__ uint32_t dl_entry(uint32_t kind, uint32_t seq) {
+  return dl_env(kind) + 2u * AGX_DELTA_ENV_WORDS + AGX_DELTA_LOG_U32(kind == AGX_KIND_ORSET) * (seq % AGX_DELTA_LOG);
+}
+// DeltaPropagationSelector.nodesSliceSize over the na = m - 1 other nodes (gossipIntervalDivisor 5)
+__device__ __forceinline__ uint32_t dl_slice_size(uint32_t na) {
+  uint32_t s = na / 5u + 1u;
+  s = s < 2u ? 2u : s;
+  const uint32_t cap = na < 10u ? na : 10u;
+  return s < cap ? s : cap;
+}
+// i-th node of this tick's round-robin slice (Replicator.allNodes sorted, self excluded)
+__device__ __forceinline__ uint32_t dl_slice_node(uint32_t node, uint32_t na, uint32_t s, uint32_t rr, uint32_t i) {
+  const uint32_t k = na <= s ? i : (rr % na + i) % na;
+  return k >= node ? k + 1u : k;
+}
+
+// Phase A of a delta replica's drain: the selector state the ticks of this drain will see.
+struct DeltaSim {
+  bool on;
+  uint32_t ctr, rr;
+  uint32_t sent[AGX_CRDT_NODES];
+};
+
+// Does this op record a delta (a valid local update of this kind)?
+__device__ __forceinline__ bool dl_records(uint32_t kind, uint32_t op, uint32_t arg) {
+  if (op == AGX_OP_INCREMENT) return kind != AGX_KIND_ORSET;
+  if (op == AGX_OP_DECREMENT) return kind == AGX_KIND_PNCOUNTER;
+  if (op == AGX_OP_ADD || op == AGX_OP_REMOVE) return kind == AGX_KIND_ORSET && arg < AGX_ORSET_ELEMS;
+  if (op == AGX_OP_CLEAR) return kind == AGX_KIND_ORSET;
+  return false;
+}
+
+// Phase A: tells and snapshot rows one message will produce.  Delta replicas simulate the
+// selector (deltaCounter, deltaSentToNode, round robin) over the drain, so a DeltaPropagationTick
+// counts exactly the propagations phase B will tell.
+__device__ __forceinline__ uint32_t crdt_count(const DevParams& P, uint32_t kind, uint32_t self, uint32_t l,
+                                               uint32_t src, uint32_t pay, uint32_t* rows, DeltaSim& ds) {
+  if (is_wide(src)) return 0;
+  const uint32_t op = pay >> 24, arg = pay & 0xFFFFFFu;
+  const bool dm = P.delta_max != 0;
+  if (dm && (op == AGX_OP_DELTA_TICK || dl_records(kind, op, arg)) && !ds.on) {
+    const St32 s{P.state + l, P.n_local};
+    const uint32_t e0 = dl_env(kind);
+    ds.on = true;
+    ds.ctr = s.ld(e0 + 8);
+    ds.rr = s.ld(e0 + 9);
+#pragma unroll
+    for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) ds.sent[n] = s.ld(e0 + 10 + n);
+  }
+  if (op == AGX_OP_GOSSIP) {
+    const uint32_t f = P.n_global > 1 && (!dm || key_size(self, P.n_global) > 1) ? P.gossip_f : 0u;
+    *rows += f ? 1u : 0u;
+    return f + (arg > 0 ? 1u : 0u);
+  }
+  if (!dm) return 0;
+  if (dl_records(kind, op, arg)) {
+    ++ds.ctr;
+    return 0;
+  }
+  if (op != AGX_OP_DELTA_TICK) return 0;
+  uint32_t t = (arg & AGX_DELTA_WRITE) ? 1u : 0u;
+  const uint32_t node = self % AGX_CRDT_NODES, na = key_size(self, P.n_global) - 1u;
+  if (na) {
+    const uint32_t sz = dl_slice_size(na);
+    const uint32_t s = na <= sz ? na : sz;
+    for (uint32_t i = 0; i < s; ++i) {
+      const uint32_t x = dl_slice_node(node, na, sz, ds.rr, i);
+      uint32_t sx = 0;
+#pragma unroll
+      for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) sx = n == x ? ds.sent[n] : sx;
+      if (ds.ctr > sx) {
+        ++t;
+        ++*rows;
+#pragma unroll
+        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) ds.sent[n] = n == x ? ds.ctr : ds.sent[n];
+      }
+    }
+    ds.rr += sz;
+  }
+  return t + ((arg & 0xFFFFu) > 0 ? 1u : 0u);
+}
+
+// A local update with delta-crdt on: the next seqNr's log entry (DeltaPropagationSelector.update).
+// The ring slot it overwrites must have been sent to every other node of the key, else the
+// engine reports AGX_ECAPACITY.
+__device__ __forceinline__ uint32_t dl_record(const DevParams& P, const St32& s, uint32_t kind, uint32_t self) {
+  const uint32_t e0 = dl_env(kind);
+  const uint32_t q = s.ld(e0 + 8) + 1u;
+  s.put(e0 + 8, q);
+  if (q > AGX_DELTA_LOG) {
+    const uint32_t m = key_size(self, P.n_global), node = self % AGX_CRDT_NODES;
+    bool lost = false;
+    for (uint32_t n = 0; n < m; ++n) lost |= n != node && s.ld(e0 + 10 + n) < q - AGX_DELTA_LOG;
+    if (lost) atomicOr(P.err, 1ull);  // kErrCapacity
+  }
+  const uint32_t x = dl_entry(kind, q);
+  s.put(x, q);
+  return x;
+}
+
+// DeltaPropagation row of seqNrs (j, ctr]: collectPropagations' merged group (DeltaOp.merge: runs of
+// AddDeltaOps coalesce) or a NoDeltaPlaceholder (max-delta-size reached / a no-delta update).
+__device__ __forceinline__ void dl_group_row(const DevParams& P, const St32& s, uint32_t kind, uint32_t node, uint32_t j,
+                                             uint32_t* row) {
+  const uint32_t e0 = dl_env(kind), ctr = s.ld(e0 + 8);
+  row[1] = node;
+  row[2] = j + 1u;
+  row[3] = ctr;
+#pragma unroll
+  for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) row[4 + n] = s.ld(e0 + n);
+  bool ph = false;
+  if (kind != AGX_KIND_ORSET) {  // GCounter / PNCounter: slot max over the range
+    uint64_t v0 = 0, v1 = 0;
+    uint32_t has = 0;
+    for (uint32_t q = j + 1; q <= ctr; ++q) {
+      const uint32_t x = dl_entry(kind, q), t = s.ld(x + 1);
+      if (t == 0) {
+        ph = true;
+        break;
+      }
+      const uint64_t v = ((uint64_t)s.ld(x + 3) << 32) | s.ld(x + 2);
+      has |= t;
+      if (t == 1u) v0 = v > v0 ? v : v0;
+      else v1 = v > v1 ? v : v1;
+    }
+    row[12] = has;
+    row[13] = (uint32_t)v0;
+    row[14] = (uint32_t)(v0 >> 32);
+    row[15] = (uint32_t)v1;
+    row[16] = (uint32_t)(v1 >> 32);
+  } else {
+    uint32_t o = 12, nops = 0, hdr = 0, cnt = 0, vmax = 0;
+    bool last_add = false;
+    for (uint32_t q = j + 1; q <= ctr; ++q) {
+      const uint32_t x = dl_entry(kind, q), te = s.ld(x + 1), t = te & 0xFFu, ver = s.ld(x + 2);
+      if (t == 1u && last_add) {  // AddDeltaOp.merge(AddDeltaOp): one more (element, version)
+        if (nops >= P.delta_max) {  // (max-delta-size 1: even one coalesced AddDeltaOp is too large)
+          ph = true;
+          break;
+        }
+        row[o++] = te >> 8;
+        row[o++] = ver;
+        ++cnt;
+        vmax = ver;
+        continue;
+      }
+      if (last_add) row[hdr] = 1u | (cnt << 8), row[hdr + 1] = vmax;  // close the add run
+      if (q > j + 1 && nops + 1u >= P.delta_max) {  // deltaSize >= maxDeltaSize
+        ph = true;
+        break;
+      }
+      ++nops;
+      last_add = t == 1u;
+      if (last_add) {
+        hdr = o;
+        o += 2;
+        row[o++] = te >> 8;
+        row[o++] = ver;
+        cnt = 1;
+        vmax = ver;
+      } else {
+        row[o++] = t | ((t == 2u ? 1u : 0u) << 8);
+        if (t == 2u) {
+          row[o++] = te >> 8;
+          row[o++] = ver;
+        }
+#pragma unroll
+        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) row[o++] = s.ld(x + 4 + n);
+      }
+    }
+    if (!ph && last_add) row[hdr] = 1u | (cnt << 8), row[hdr + 1] = vmax;
+    row[0] = nops;
+  }
+  if (ph) row[0] = 0x80000000u;
+}
+
+// ORSet: apply one received DeltaPropagation group (mergeDelta, DD/ORSet.scala:455-501)
+__device__ __forceinline__ void orset_merge_delta_row(const St32& s, const uint32_t* row, uint32_t from) {
+  constexpr uint32_t vb = AGX_ORSET_ELEMS * AGX_CRDT_NODES;  // u32 index of the vvector
+  uint32_t lvv[AGX_CRDT_NODES];
+#pragma unroll
+  for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) lvv[n] = s.ld(vb + n);
+  const uint32_t nops = row[0];
+  uint32_t o = 12;
+  for (uint32_t i = 0; i < nops; ++i) {
+    const uint32_t h = row[o], t = h & 0xFFu, cnt = h >> 8;
+    if (t == 1u) {  // dryMerge(addDeltaOp = true): the run's elements only, the last pair of an element wins
+      const uint32_t vf = row[o + 1];
+      const uint32_t p0 = o + 2;
+      uint64_t seen = 0;
+      for (uint32_t k = cnt; k-- > 0;) {
+        const uint32_t e = row[p0 + 2 * k], ver = row[p0 + 2 * k + 1];
+        if ((seen >> e) & 1ull) continue;
+        seen |= 1ull << e;
+        uint32_t d[AGX_CRDT_NODES];
+        bool here = false;
+#pragma unroll
+        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
+          d[n] = s.ld(e * AGX_CRDT_NODES + n);
+          here |= d[n] != 0u;
+        }
+#pragma unroll
+        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
+          const uint32_t r = n == from ? ver : 0u, rvv = n == from ? vf : 0u;
+          const uint32_t x = here ? orset_merge_entry(d[n], r, lvv[n], rvv) : (r > lvv[n] ? r : 0u);
+          if (x != d[n]) s.put(e * AGX_CRDT_NODES + n, x);
+        }
+      }
+#pragma unroll
+      for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n)
+        if (n == from && vf > lvv[n]) {
+          lvv[n] = vf;
+          s.put(vb + n, vf);
+        }
+      o = p0 + 2 * cnt;
+    } else if (t == 2u) {  // mergeRemoveDelta
+      const uint32_t e = row[o + 1], ver = row[o + 2];
+      const uint32_t* rvv = row + o + 3;
+      uint32_t d[AGX_CRDT_NODES];
+      bool here = false, del = true;
+#pragma unroll
+      for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
+        d[n] = s.ld(e * AGX_CRDT_NODES + n);
+        here |= d[n] != 0u;
+        del &= d[n] <= rvv[n];  // covered on every node (an unknown node has rvv 0)
+      }
+      if (here && del)
+#pragma unroll
+        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n)
+          if (d[n]) s.put(e * AGX_CRDT_NODES + n, 0u);
+#pragma unroll
+      for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n)
+        if (n == from && ver > lvv[n]) {
+          lvv[n] = ver;
+          s.put(vb + n, ver);
+        }
+      o += 11;
+    } else {  // FullStateDeltaOp: dryMerge(addDeltaOp = false) with an empty elementsMap
+      const uint32_t* rvv = row + o + 1;
+      for (uint32_t e = 0; e < AGX_ORSET_ELEMS; ++e)
+#pragma unroll
+        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
+          const uint32_t x = s.ld(e * AGX_CRDT_NODES + n);
+          if (x && x <= rvv[n]) s.put(e * AGX_CRDT_NODES + n, 0u);
+        }
+#pragma unroll
+      for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n)
+        if (rvv[n] > lvv[n]) {
+          lvv[n] = rvv[n];
+          s.put(vb + n, rvv[n]);
+        }
+      o += 9;
+    }
+  }
+}
+
+// a received DeltaPropagation (receiveDeltaPropagation + DataEnvelope.merge)
+__device__ __forceinline__ void dl_receive(const St32& s, uint32_t kind, const uint32_t* row) {
+  if (row[0] & 0x80000000u) return;  // NoDeltaPlaceholder: not part of the propagation
+  const uint32_t e0 = dl_env(kind), from = row[1];
+  if (kind != AGX_KIND_ORSET) {  // not RequiresCausalDeliveryOfDeltas: merge the sender's envelope
+    for (uint32_t b = 0; b < 2; ++b)
+      if (row[12] & (1u << b)) {
+        uint64_t* slot = s.st + (size_t)(b * AGX_CRDT_NODES + from) * s.nl;
+        const uint64_t x = ((uint64_t)row[14 + 2 * b] << 32) | row[13 + 2 * b];
+        if (x > *slot) *slot = x;
+      }
+#pragma unroll
+    for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
+      const uint32_t c = s.ld(e0 + n);
+      if (row[4 + n] > c) s.put(e0 + n, row[4 + n]);
+    }
+    return;
+  }
+  const uint32_t cur = s.ld(e0 + from);
+  if (cur >= row[3] || row[2] > cur + 1u) return;  // already handled / a seqNr is missing
+  orset_merge_delta_row(s, row, from);
+  s.put(e0 + from, row[3]);  // deltaVersions.merge(VersionVector(fromNode, toSeqNr))
+}
+
+// DeltaPropagationTick (DD/Replicator.scala:1953-1963); returns the row cursor advance
+template <typename Emit>
+__device__ __forceinline__ void dl_tick(const DevParams& P, const CrdtHeap& H, uint32_t kind, uint32_t self,
+                                        const St32& s, uint32_t arg, uint32_t& row_cursor, Emit& em) {
+  const uint32_t k = arg & 0xFFFFu;
+  if (arg & AGX_DELTA_WRITE) {  // a writer client: one seeded Update told to the replica
+    const uint64_t r = fanout_rand(P.gossip_seed, self, k | 0x04000000u, 0);
+    const uint32_t amount = 1u + (uint32_t)((r >> 32) & 3u);
+    uint32_t op;
+    if (kind == AGX_KIND_GCOUNTER) op = AGX_OP(AGX_OP_INCREMENT, amount);
+    else if (kind == AGX_KIND_PNCOUNTER) op = AGX_OP(((r >> 34) & 1u) ? AGX_OP_DECREMENT : AGX_OP_INCREMENT, amount);
+    else op = AGX_OP(((r >> 40) & 3u) ? AGX_OP_ADD : AGX_OP_REMOVE, (uint32_t)(r >> 48) % AGX_ORSET_ELEMS);
+    em(self, op);
+  }
+  const uint32_t node = self % AGX_CRDT_NODES, na = key_size(self, P.n_global) - 1u;
+  if (na) {
+    const uint32_t e0 = dl_env(kind), rr = s.ld(e0 + 9), ctr = s.ld(e0 + 8);
+    const uint32_t sz = dl_slice_size(na), cnt = na <= sz ? na : sz;
+    const uint32_t tag = ((kind - (uint32_t)AGX_KIND_GCOUNTER) << 30) | AGX_DELTA_ROW_BIT;
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint32_t x = dl_slice_node(node, na, sz, rr, i);
+      const uint32_t j = s.ld(e0 + 10 + x);
+      if (ctr <= j) continue;  // deltaEntriesAfter(j) is empty
+      const uint32_t h = row_cursor++;
+      if (h < H.rows) dl_group_row(P, s, kind, node, j, H.wrow(h));
+      s.put(e0 + 10 + x, ctr);  // deltaSentToNode(node) = last seqNr (also for a placeholder)
+      em.wide(self - node + x, tag | h);
+    }
+    s.put(e0 + 9, rr + sz);  // deltaNodeRoundRobinCounter += sliceSize
+  }
+  if (k > 0) em(self, AGX_OP(AGX_OP_DELTA_TICK, (k - 1u) | (arg & AGX_DELTA_WRITE)));
+}
+
 
 // Phase B: one invoke of a CRDT replica.  `emit(dst, pay)` / `emit_wide(dst, handle)`.
 // CM: the CRDT kinds present (one bit = a single-kind population, whose merge is specialised:
@@ -93,9 +432,24 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
   const size_t nl = P.n_local;
   uint64_t* st = P.state + l;  // word w at st[w * nl]
   const uint32_t node = self % AGX_CRDT_NODES;
+  const bool dm = P.delta_max != 0;
+  const St32 s32{st, nl};
   if (is_wide(src)) {
     if ((pay >> 30) != kind - (uint32_t)AGX_KIND_GCOUNTER) return AGX_RES_UNHANDLED;  // another data type
     const uint32_t* row = H.row(pay & kHandleMask);
+    if (pay & AGX_DELTA_ROW_BIT) {  // a DeltaPropagation
+      if (!dm) return AGX_RES_UNHANDLED;
+      dl_receive(s32, kind, row);
+      return AGX_RES_SAME;
+    }
+    if (dm) {  // DataEnvelope.merge: the deltaVersions after the data words
+      const uint32_t e0 = dl_env(kind);
+#pragma unroll
+      for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
+        const uint32_t c = s32.ld(e0 + n), r = row[e0 + n];
+        if (r > c) s32.put(e0 + n, r);
+      }
+    }
     if (kind != AGX_KIND_ORSET) {  // slot-wise max, 8 words per batch
       const uint32_t nw = crdt_words(kind);
       for (uint32_t i0 = 0; i0 < nw; i0 += 8) {
@@ -162,17 +516,34 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
   const uint32_t op = pay >> 24, arg = pay & 0xFFFFFFu;
   switch (op) {
     case AGX_OP_INCREMENT:
-      if (kind == AGX_KIND_ORSET) return AGX_RES_UNHANDLED;
-      st[node * nl] += arg;
+    case AGX_OP_DECREMENT: {
+      if (kind == AGX_KIND_ORSET || (op == AGX_OP_DECREMENT && kind != AGX_KIND_PNCOUNTER)) return AGX_RES_UNHANDLED;
+      const uint32_t w = (op == AGX_OP_DECREMENT ? AGX_CRDT_NODES : 0u) + node;
+      const uint64_t v = st[w * nl] + arg;
+      st[w * nl] = v;
+      if (dm) {  // delta = the counter of the new slot value; an update by 0 has none (placeholder)
+        const uint32_t x = dl_record(P, s32, kind, self);
+        s32.put(x + 1, arg ? (op == AGX_OP_DECREMENT ? 2u : 1u) : 0u);
+        s32.put(x + 2, (uint32_t)v);
+        s32.put(x + 3, (uint32_t)(v >> 32));
+      }
       return AGX_RES_SAME;
-    case AGX_OP_DECREMENT:
-      if (kind != AGX_KIND_PNCOUNTER) return AGX_RES_UNHANDLED;
-      st[(AGX_CRDT_NODES + node) * nl] += arg;
-      return AGX_RES_SAME;
+    }
     case AGX_OP_ADD:
     case AGX_OP_REMOVE:
     case AGX_OP_CLEAR: {
       if (kind != AGX_KIND_ORSET || (op != AGX_OP_CLEAR && arg >= AGX_ORSET_ELEMS)) return AGX_RES_UNHANDLED;
+      if (dm) {  // AddDeltaOp (element, dot) / RemoveDeltaOp (element, deltaDot, vvector) / FullStateDeltaOp
+        constexpr uint32_t vb = AGX_ORSET_ELEMS * AGX_CRDT_NODES;
+        const uint32_t x = dl_record(P, s32, kind, self);
+        const uint32_t vn = s32.ld(vb + node);
+        s32.put(x + 1, (op == AGX_OP_ADD ? 1u : op == AGX_OP_REMOVE ? 2u : 3u) | (op == AGX_OP_CLEAR ? 0u : arg << 8));
+        s32.put(x + 2, op == AGX_OP_ADD ? vn + 1u : op == AGX_OP_REMOVE ? vn : 0u);
+        s32.put(x + 3, 0u);
+        if (op != AGX_OP_ADD)
+#pragma unroll
+          for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) s32.put(x + 4 + n, s32.ld(vb + n));
+      }
       if (op == AGX_OP_CLEAR) {
         for (uint32_t w = 0; w < AGX_ORSET_ELEMS * AGX_CRDT_NODES / 2; ++w) st[w * nl] = 0;
         return AGX_RES_SAME;
@@ -191,13 +562,17 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       for (int k = 0; k < 4; ++k) st[(size_t)(4 * arg + k) * nl] = dots[k];
       return AGX_RES_SAME;
     }
+    case AGX_OP_DELTA_TICK:
+      if (!dm) return AGX_RES_UNHANDLED;
+      dl_tick(P, H, kind, self, s32, arg, row_cursor, em);
+      return AGX_RES_SAME;
     case AGX_OP_GOSSIP: {
-      const uint32_t f = P.n_global > 1 ? P.gossip_f : 0u;
+      const uint32_t f = P.n_global > 1 && (!dm || key_size(self, P.n_global) > 1) ? P.gossip_f : 0u;
       if (f) {
         const uint32_t h = row_cursor++;
-        if (h < H.rows) {  // snapshot of the current state, shared by the f gossips
+        if (h < H.rows) {  // snapshot of the current state (+ deltaVersions), shared by the f gossips
           uint32_t* row = H.wrow(h);
-          const uint32_t nw = crdt_words(kind);  // 8 | 16 | 260 words: batches of 4 (loads first)
+          const uint32_t nw = crdt_words(kind) + (dm ? AGX_CRDT_NODES / 2u : 0u);  // batches of 4 (loads first)
           for (uint32_t i0 = 0; i0 < nw; i0 += 4) {
             uint64_t s[4];
 #pragma unroll
@@ -210,7 +585,9 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
           }
         }
         const uint32_t tagged = ((kind - (uint32_t)AGX_KIND_GCOUNTER) << 30) | h;
-        for (uint32_t j = 0; j < f; ++j) em.wide(crdt_peer(P.gossip_seed, self, arg, j, P.n_global), tagged);
+        for (uint32_t j = 0; j < f; ++j)
+          em.wide(dm ? crdt_key_peer(P.gossip_seed, self, arg, j, P.n_global) : crdt_peer(P.gossip_seed, self, arg, j, P.n_global),
+                  tagged);
       }
       if (arg > 0) em(self, AGX_OP(AGX_OP_GOSSIP, arg - 1u));
       return AGX_RES_SAME;

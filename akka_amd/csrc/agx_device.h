@@ -39,6 +39,13 @@ struct DevParams {
   const uint32_t* step;     // superstep counter (bumped by the first kernel of a step)
   uint32_t heap_rows, pw, gossip_f;
   uint64_t gossip_seed;
+  uint32_t delta_max;             // delta-CRDT mode (Replicator max-delta-size), 0 = off
+  unsigned long long* err;        // stats[ST_ERROR]: capacity errors raised inside a behaviour
+  // compiled behaviours (agx_set_behaviors): case / action tables, behaviour b = cases [bfirst[b], bfirst[b+1])
+  const agx_case* bcase;
+  const agx_act* bact;
+  const uint32_t* bfirst;
+  uint32_t n_beh;
 };
 
 // ------------------------------------------------------------------ RNG
@@ -164,17 +171,94 @@ __device__ __forceinline__ int block_excl_max(int v, int* scratch) {
 // KM is the set of behaviour kinds compiled in (bit k = kind k).  The engine
 // launches the narrowest specialisation that covers every registered kind, so a
 // population of one behaviour runs a small, branch-free apply kernel.
-constexpr uint32_t kb(uint32_t k) { return 1u << k; }
+constexpr uint32_t kb(uint32_t k) { return 1u << (k < AGX_KIND_COMPILED ? k : AGX_KIND_COMPILED); }
 constexpr uint32_t KM_ALL = kb(AGX_KIND_COUNTER) | kb(AGX_KIND_RING) | kb(AGX_KIND_FANOUT) | kb(AGX_KIND_FORWARD_RR) |
                             kb(AGX_KIND_STOP_AFTER) | kb(AGX_KIND_PINGPONG) | kb(AGX_KIND_EVEN);
 
+// ---- compiled behaviours (include/akka_gpu.h "compiled behaviours"; akka_amd/typed.py lowers them)
+__device__ __forceinline__ uint64_t cb_operand(uint32_t src, uint32_t word, int64_t k, uint32_t pay, const uint64_t* w,
+                                               uint32_t sender, uint32_t self) {
+  uint64_t b = 0;
+  switch (src) {
+    case AGX_V_PAYLOAD: b = pay; break;
+    case AGX_V_TAG: b = pay >> 24; break;
+    case AGX_V_ARG: b = pay & 0xFFFFFFu; break;
+    case AGX_V_WORD: b = w[word & 1u]; break;
+    case AGX_V_SENDER: b = sender; break;
+    case AGX_V_SELF: b = self; break;
+    default: break;
+  }
+  return b + (uint64_t)k;
+}
+__device__ __forceinline__ bool cb_cmp(uint32_t op, uint64_t a, uint64_t b) {
+  switch (op) {
+    case AGX_CMP_EQ: return a == b;
+    case AGX_CMP_NE: return a != b;
+    case AGX_CMP_LT: return a < b;
+    case AGX_CMP_LE: return a <= b;
+    case AGX_CMP_GT: return a > b;
+    case AGX_CMP_GE: return a >= b;
+    default: return true;
+  }
+}
+// ReceiveBuilder.receive (TY/javadsl/ReceiveBuilder.scala:209-218): the first case whose tests hold
+template <typename Emit>
+__device__ __forceinline__ uint32_t compiled_apply(const DevParams& P, uint32_t& kind, uint32_t self, uint64_t* w,
+                                                uint32_t src, uint32_t pay, Emit& emit) {
+  const uint32_t b = kind - AGX_KIND_COMPILED;
+  if (b >= P.n_beh) return AGX_RES_UNHANDLED;
+  const uint32_t c1 = P.bfirst[b + 1];
+  for (uint32_t c = P.bfirst[b]; c < c1; ++c) {
+    const agx_case C = P.bcase[c];
+    if (!cb_cmp(C.cmp1, cb_operand(C.src1, C.word1, C.k1, pay, w, src, self),
+                cb_operand(C.src2, C.word2, C.k2, pay, w, src, self)))
+      continue;
+    if (!cb_cmp(C.cmp2, cb_operand(C.src3, C.word3, C.k3, pay, w, src, self),
+                cb_operand(C.src4, C.word4, C.k4, pay, w, src, self)))
+      continue;
+    for (uint32_t i = C.act_first; i < (uint32_t)C.act_first + C.act_count; ++i) {
+      const agx_act A = P.bact[i];
+      const uint64_t v = cb_operand(A.src, A.sword, A.k, pay, w, src, self);
+      switch (A.op) {
+        case AGX_A_SET: w[A.word & 1u] = v; break;
+        case AGX_A_ADD: w[A.word & 1u] += v; break;
+        case AGX_A_MAX: w[A.word & 1u] = v > w[A.word & 1u] ? v : w[A.word & 1u]; break;
+        case AGX_A_MIN: w[A.word & 1u] = v < w[A.word & 1u] ? v : w[A.word & 1u]; break;
+        case AGX_A_TELL: {
+          uint64_t d;
+          if (A.dsrc == AGX_V_SELF) {  // (self + dk) mod n: ring neighbours
+            int64_t x = ((int64_t)self + A.dk) % (int64_t)P.n_global;
+            d = (uint64_t)(x < 0 ? x + (int64_t)P.n_global : x);
+          } else {
+            d = cb_operand(A.dsrc, A.dword, A.dk, pay, w, src, self);
+          }
+          emit(d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d, A.or_mask ? ((uint32_t)v & 0xFFFFFFu) | A.or_mask : (uint32_t)v);
+          break;
+        }
+        default: break;
+      }
+    }
+    if (C.result == AGX_RES_BECOME) {
+      kind = AGX_KIND_COMPILED + C.next;
+      return AGX_RES_SAME;
+    }
+    return C.result;
+  }
+  return AGX_RES_UNHANDLED;
+}
+
+// `kind` is the actor's current behaviour: a compiled behaviour's become updates it (the caller
+// keeps it for the rest of the drain and stores it back).
 template <uint32_t KM, typename Emit>
-__device__ __forceinline__ uint32_t apply_msg(const DevParams& P, uint32_t kind, uint32_t self, uint32_t local,
+__device__ __forceinline__ uint32_t apply_msg(const DevParams& P, uint32_t& kind_io, uint32_t self, uint32_t local,
                                               uint64_t* w, uint32_t src, uint32_t pay, Emit&& emit) {
+  uint32_t kind = kind_io;
   if constexpr (KM == kb(AGX_KIND_RING)) kind = AGX_KIND_RING;  // single-kind specialisations: no dispatch
   if constexpr (KM == kb(AGX_KIND_FORWARD_RR)) kind = AGX_KIND_FORWARD_RR;
   if constexpr (KM == kb(AGX_KIND_FANOUT)) kind = AGX_KIND_FANOUT;
   if constexpr (KM == kb(AGX_KIND_COUNTER)) kind = AGX_KIND_COUNTER;
+  if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
+    if (kind >= AGX_KIND_COMPILED) return compiled_apply(P, kind_io, self, w, src, pay, emit);
   switch (kind) {
     case AGX_KIND_COUNTER:
       if constexpr ((KM & kb(AGX_KIND_COUNTER)) != 0) {

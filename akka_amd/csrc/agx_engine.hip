@@ -92,6 +92,7 @@ const char* kClassNames[K_NCLASS] = {"chunk_rowscan", "chunk_downsweep", "sort_u
                                      "fused_tick", "bucket_bounds"};
 
 constexpr uint32_t kGraphSizes[4] = {1, 2, 4, 8};  // superstep replays (agx_engine::gx)
+constexpr uint32_t kRowAlign = 32;  // CRDT row pitch (u32) of rows wider than one 128-B line
 constexpr uint32_t kStatBlk = 16;                    // d_stats block (see agx_engine::d_stats)
 constexpr uint32_t kStatSred = ST_N, kStatInfl = ST_N + kBStats;
 static_assert(kStatInfl < kStatBlk, "stats block layout");
@@ -133,6 +134,12 @@ struct agx_engine {
   uint32_t* d_col = nullptr;
   // CRDT state gossips (agx_crdt.h): snapshot heap, 2 x cap rows of pw u32
   uint32_t pw = 0, gossip_f = 0;
+  uint32_t delta_max = 0;  // delta-CRDT mode (agx_set_delta_crdt): Replicator max-delta-size, 0 = off
+  // compiled behaviours (agx_set_behaviors)
+  agx_case* d_bcase = nullptr;
+  agx_act* d_bact = nullptr;
+  uint32_t* d_bfirst = nullptr;
+  uint32_t n_beh = 0;
   uint64_t heap_rows = 0;  // per parity: one region of 2^bb rows per bucket, then an overflow area of `cap` rows
   uint64_t gossip_seed = 0;
   uint32_t *d_heap = nullptr, *d_heap_top = nullptr, *d_step = nullptr;
@@ -319,6 +326,12 @@ DevParams make_params(agx_engine* e) {
   P.pw = e->pw;
   P.gossip_f = e->gossip_f;
   P.gossip_seed = e->gossip_seed;
+  P.delta_max = e->delta_max;
+  P.bcase = e->d_bcase;
+  P.bact = e->d_bact;
+  P.bfirst = e->d_bfirst;
+  P.n_beh = e->n_beh;
+  P.err = reinterpret_cast<unsigned long long*>(e->d_stats + ST_ERROR);
   return P;
 }
 
@@ -537,6 +550,10 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
       AGX_APPLY(false, kb(AGX_KIND_FANOUT));
     else if (km == kb(AGX_KIND_COUNTER))
       AGX_APPLY(false, kb(AGX_KIND_COUNTER));
+    else if (km == kb(AGX_KIND_COMPILED))  // compiled behaviours only (agx_set_behaviors)
+      AGX_APPLY(false, kb(AGX_KIND_COMPILED));
+    else if (km & kb(AGX_KIND_COMPILED))
+      AGX_APPLY(false, KM_ALL | kb(AGX_KIND_COMPILED));
     else
       AGX_APPLY(false, KM_ALL);
 #undef AGX_APPLY
@@ -1048,22 +1065,24 @@ void drop_graphs(agx_engine* e) {
       }
 }
 
-// First CRDT kind (or a wider one): size the snapshot heap for `kind`'s rows.
+// First CRDT kind (or a wider one): size the snapshot heap for `kind`'s rows (full state, plus
+// deltaVersions and DeltaPropagation rows in delta-CRDT mode; include/akka_gpu.h).
 agx_status enable_crdt(agx_engine* e, uint32_t kind) {
   const uint32_t words = kind == AGX_KIND_GCOUNTER ? AGX_GCOUNTER_WORDS
                          : kind == AGX_KIND_PNCOUNTER ? AGX_PNCOUNTER_WORDS : AGX_ORSET_WORDS;
-  if (e->W < words) return set_err(AGX_EINVAL, "behaviour kind %u needs n_words >= %u", kind, words);
-#ifndef AGX_ROW_ALIGN
-#define AGX_ROW_ALIGN 32
-#endif
+  const uint32_t need = !e->delta_max ? words
+                        : kind == AGX_KIND_GCOUNTER ? AGX_GCOUNTER_DELTA_WORDS
+                        : kind == AGX_KIND_PNCOUNTER ? AGX_PNCOUNTER_DELTA_WORDS : AGX_ORSET_DELTA_WORDS;
+  if (e->W < need) return set_err(AGX_EINVAL, "behaviour kind %u needs n_words >= %u", kind, need);
+  const uint32_t ru = !e->delta_max ? 2 * words : kind == AGX_KIND_ORSET ? AGX_ORSET_DELTA_ROW_U32
+                                                                          : 2 * words + AGX_CRDT_NODES;
   // row pitch in u32: rows wider than one 128-B line start on a line boundary (ORSet: 2080 B
   // rows padded to 2176 B), so a merge's batched row loads never split a line between rows
-  const uint32_t pw = 2 * words > AGX_ROW_ALIGN ? (2 * words + AGX_ROW_ALIGN - 1) / AGX_ROW_ALIGN * AGX_ROW_ALIGN
-                                                : 2 * words;
+  const uint32_t pw = ru > kRowAlign ? (ru + kRowAlign - 1) / kRowAlign * kRowAlign : ru;
   if (pw <= e->pw) return AGX_OK;
   if (e->started) return set_err(AGX_ESTATE, "register CRDT kinds before the first agx_run");
   const uint64_t rows = ((uint64_t)e->nb << e->bb) + e->cap;
-  if (rows + e->cap >= (1ull << 30)) return set_err(AGX_EINVAL, "CRDT kinds need msg_capacity < 2^29 - n_actors");
+  if (rows + e->cap > kHandleMask) return set_err(AGX_EINVAL, "CRDT kinds need msg_capacity < 2^28 - n_actors");
   hipFree(e->d_heap);
   hipFree(e->d_rx);
   hipFree(e->d_s2rows);
@@ -1354,6 +1373,7 @@ agx_status agx_destroy(agx_engine* e) {
   for (auto ev : e->lag_ev)
     if (ev) hipEventDestroy(ev);
   hipFree(e->d_heap); hipFree(e->d_heap_top); hipFree(e->d_step); hipFree(e->d_rx); hipFree(e->d_s2rows);
+  hipFree(e->d_bcase); hipFree(e->d_bact); hipFree(e->d_bfirst);
   if (e->h_pin) hipHostFree(e->h_pin);
   if (e->h_pin64) hipHostFree(e->h_pin64);
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
@@ -1367,7 +1387,12 @@ agx_status agx_register_range(agx_engine* e, uint64_t first_id, uint64_t count, 
   if (!e) return set_err(AGX_EINVAL, "null engine");
   AGX_TRY(ensure_dev(e));
   AGX_TRY(sync_mirrors(e));  // device state is authoritative after a run
-  if (first_id + count > e->n_global || kind >= AGX_KIND_MAX) return set_err(AGX_EINVAL, "bad range or kind");
+  const bool compiled = kind >= AGX_KIND_COMPILED && kind < AGX_KIND_COMPILED + AGX_MAX_BEHAVIORS;
+  if (first_id + count > e->n_global || (kind >= AGX_KIND_MAX && !compiled)) return set_err(AGX_EINVAL, "bad range or kind");
+  const uint32_t kCrdtMask = kb(AGX_KIND_GCOUNTER) | kb(AGX_KIND_PNCOUNTER) | kb(AGX_KIND_ORSET);
+  if (count && ((compiled && (e->kinds_mask & kCrdtMask)) ||
+                (kind >= AGX_KIND_GCOUNTER && kind <= AGX_KIND_ORSET && (e->kinds_mask & kb(AGX_KIND_COMPILED)))))
+    return set_err(AGX_EINVAL, "compiled behaviours and CRDT replicas need separate engines");
   if ((kind == AGX_KIND_FORWARD_RR || kind == AGX_KIND_STOP_AFTER) && e->W < 2)
     return set_err(AGX_EINVAL, "behaviour kind %u needs n_words >= 2", kind);
   if (init && stride < e->W * 8ull) return set_err(AGX_EINVAL, "state_stride smaller than n_words*8");
@@ -1404,6 +1429,63 @@ agx_status agx_set_gossip(agx_engine* e, uint32_t fanout, uint64_t seed) {
   e->gossip_f = fanout;
   e->gossip_seed = seed;
   drop_graphs(e);  // behaviour parameters are captured in the superstep graphs
+  return AGX_OK;
+}
+
+agx_status agx_set_behaviors(agx_engine* e, const agx_case* cases, uint32_t n_cases, const agx_act* acts,
+                             uint32_t n_acts, const uint32_t* first, uint32_t n_beh) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  if (e->started) return set_err(AGX_ESTATE, "set compiled behaviours before agx_run");
+  if (n_beh == 0 || n_beh > AGX_MAX_BEHAVIORS || n_cases > AGX_MAX_CASES || n_acts > AGX_MAX_ACTS || !first ||
+      (n_cases && !cases) || (n_acts && !acts))
+    return set_err(AGX_EINVAL, "compiled behaviours: bad table sizes");
+  if (first[0] != 0 || first[n_beh] != n_cases) return set_err(AGX_EINVAL, "first[] must run from 0 to n_cases");
+  for (uint32_t b = 0; b < n_beh; ++b)
+    if (first[b] > first[b + 1]) return set_err(AGX_EINVAL, "first[] must be non-decreasing");
+  auto opnd_ok = [](uint32_t src, uint32_t word) { return src <= AGX_V_SELF && word <= 1u; };
+  for (uint32_t c = 0; c < n_cases; ++c) {
+    const agx_case& C = cases[c];
+    if (!opnd_ok(C.src1, C.word1) || !opnd_ok(C.src2, C.word2) || !opnd_ok(C.src3, C.word3) ||
+        !opnd_ok(C.src4, C.word4) || C.cmp1 > AGX_CMP_GE || C.cmp2 > AGX_CMP_GE || C.result > AGX_RES_BECOME ||
+        (C.result == AGX_RES_BECOME && C.next >= n_beh) || (uint32_t)C.act_first + C.act_count > n_acts)
+      return set_err(AGX_EINVAL, "compiled behaviours: bad case %u", c);
+  }
+  for (uint32_t i = 0; i < n_acts; ++i) {
+    const agx_act& A = acts[i];
+    if (A.op < AGX_A_SET || A.op > AGX_A_TELL || A.word > 1u || !opnd_ok(A.src, A.sword) ||
+        (A.op == AGX_A_TELL && !opnd_ok(A.dsrc, A.dword)))
+      return set_err(AGX_EINVAL, "compiled behaviours: bad action %u (state words 0..1)", i);
+  }
+  AGX_TRY(ensure_dev(e));
+  hipFree(e->d_bcase);
+  hipFree(e->d_bact);
+  hipFree(e->d_bfirst);
+  e->d_bcase = nullptr;
+  e->d_bact = nullptr;
+  e->d_bfirst = nullptr;
+  AGX_TRY(dalloc(&e->d_bcase, std::max<uint32_t>(n_cases, 1)));
+  AGX_TRY(dalloc(&e->d_bact, std::max<uint32_t>(n_acts, 1)));
+  AGX_TRY(dalloc(&e->d_bfirst, n_beh + 1));
+  if (n_cases) HIP_TRY(hipMemcpy(e->d_bcase, cases, n_cases * sizeof(agx_case), hipMemcpyHostToDevice));
+  if (n_acts) HIP_TRY(hipMemcpy(e->d_bact, acts, n_acts * sizeof(agx_act), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->d_bfirst, first, (n_beh + 1) * 4ull, hipMemcpyHostToDevice));
+  e->n_beh = n_beh;
+  drop_graphs(e);  // the tables are kernel parameters captured in the superstep graphs
+  return AGX_OK;
+}
+
+agx_status agx_set_delta_crdt(agx_engine* e, uint32_t max_delta_size) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  if (max_delta_size > AGX_DELTA_MAX_SIZE)
+    return set_err(AGX_EINVAL, "max_delta_size %u > %u (DeltaPropagation rows are sized for it)", max_delta_size,
+                   AGX_DELTA_MAX_SIZE);
+  if (max_delta_size && e->kmax < 4) return set_err(AGX_EINVAL, "delta-CRDT replicas need max_emit >= 4");
+  if (max_delta_size && e->n_global >= (1ull << 30)) return set_err(AGX_EINVAL, "delta-CRDT needs n_actors < 2^30");
+  if (e->started && max_delta_size != e->delta_max) return set_err(AGX_ESTATE, "set delta-CRDT mode before agx_run");
+  e->delta_max = max_delta_size;
+  for (uint32_t k = AGX_KIND_GCOUNTER; k <= AGX_KIND_ORSET; ++k)
+    if (e->kinds_mask & kb(k)) AGX_TRY(enable_crdt(e, k));
+  drop_graphs(e);
   return AGX_OK;
 }
 

@@ -992,7 +992,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       const uint32_t la = j * kBThreads + tid;
       const bool has = la < na && L.alive[la] && L.seg[la + 1] != L.seg[la];
       const uint32_t l = a0 + la;
-      kd[j] = has && (kWide || (KM & (KM - 1)) != 0) ? P.kind[l] : 0u;  // single-kind variants never read it
+      kd[j] = has && (kWide || (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0) ? P.kind[l] : 0u;  // single-kind variants never read it
       x0[j] = has ? P.state[l] : 0ull;
       x1[j] = has && P.W > 1 ? P.state[(size_t)P.n_local + l] : 0ull;
       if constexpr (kFwd) {
@@ -1034,6 +1034,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       EmitterLds em{&P, L.key, L.src, L.pay, s0, self, 0, 0, L.nh, a.nx_shift, nhmask};
       uint64_t wv[2] = {w0s[la], w1s[la]};
       const uint32_t nd = min(len, T);
+      uint32_t kcur = L.kind[la];  // (a compiled behaviour's become changes it)
       ++nact;
       uint64_t hb = 0;
       uint32_t hdeg = kNoHint, hdst = 0;
@@ -1057,7 +1058,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           }
           r = AGX_RES_SAME;
         } else {
-          r = apply_msg<KM>(P, L.kind[la], self, l, wv, sv, pv, em);
+          r = apply_msg<KM>(P, kcur, self, l, wv, sv, pv, em);
         }
         ++ndel;
         if (r == AGX_RES_UNHANDLED) ++nunh;
@@ -1070,6 +1071,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       }
       P.state[l] = wv[0];
       if (P.W > 1) P.state[(size_t)P.n_local + l] = wv[1];
+      if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
+        if (kcur != L.kind[la]) P.kind[l] = (uint8_t)kcur;
       nall += em.n_all;
       ndead += em.n_all - em.n_valid;
       ecl[j] = em.n_valid;
@@ -1154,9 +1157,12 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       Emitter<false> em{&P, {}, 0, self, 0, 0, L.nh, a.nx_shift, nhmask};
       uint64_t wv[2] = {w0s[la], w1s[la]};  // behaviours read/write state words 0-1 only
       const uint32_t nd = min(len, T);
-      const uint32_t kd = L.kind[la];
+      uint32_t kd = L.kind[la];
       if (kWide && is_crdt(kd)) {
-        for (uint32_t q = 0; q < nd; ++q) em.count(crdt_count(P, isrc(s0 + q), ipay(s0 + q), &nrows_t));
+        DeltaSim ds;
+        ds.on = false;
+        for (uint32_t q = 0; q < nd; ++q)
+          em.count(crdt_count(P, kd, self, l, isrc(s0 + q), ipay(s0 + q), &nrows_t, ds));
       } else if constexpr (!kLds) {  // messages in global scratch: loads issued kPF at a time
         bool stop = false;
         for (uint32_t q0 = 0; q0 < nd && !stop; q0 += kPF) {
@@ -1228,7 +1234,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       Emitter<true> em{&P, a.em, embase + L.ecnt[la], self, 0, 0, L.nh, a.nx_shift, nhmask};
       uint64_t wv[2] = {w0s[la], w1s[la]};  // behaviours read/write state words 0-1 only
       const uint32_t nd = min(len, T);
-      const uint32_t kd = L.kind[la];
+      uint32_t kd = L.kind[la];
       ++nact;
       if (kWide && is_crdt(kd)) {
         for (uint32_t q = 0; q < nd; ++q) {
@@ -1267,6 +1273,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         }
         P.state[l] = wv[0];
         if (P.W > 1) P.state[(size_t)P.n_local + l] = wv[1];
+        if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
+          if (kd != L.kind[la]) P.kind[l] = (uint8_t)kd;
       }
       nall += em.n_all;
       ndead += em.n_all - em.n_valid;

@@ -163,6 +163,12 @@ class GpuEngine:
     def set_gossip(self, fanout: int, seed: int) -> None:
         check(self.lib.agx_set_gossip(self._h, fanout, seed))
 
+    def set_behaviors(self, tables) -> None:
+        """Compiled behaviours (akka_amd.typed.compile_behaviors -> agx_set_behaviors)."""
+        check(self.lib.agx_set_behaviors(self._h, ctypes.addressof(tables.cases), len(tables.cases),
+                                         ctypes.addressof(tables.acts), len(tables.acts),
+                                         _ptr(tables.first, ctypes.c_uint32), tables.n_behaviors))
+
     def set_delta_crdt(self, max_delta_size: int) -> None:
         """Replicator delta-crdt.enabled / max-delta-size (0 = off)."""
         check(self.lib.agx_set_delta_crdt(self._h, max_delta_size))

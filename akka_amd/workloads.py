@@ -38,6 +38,7 @@ class Workload:
     ring_stride: int | None = None
     gossip: tuple | None = None  # (fanout, seed)
     delta_crdt: int = 0          # Replicator max-delta-size (0 = full-state gossip only)
+    behaviors: object = None     # compiled behaviour tables (akka_amd.typed.Tables)
     fanout: tuple | None = None  # (k, seed, cdf, perm)
     graph: tuple | None = None   # (row_ptr, col)
     tells: tuple | None = None   # (dst, src, payload)
@@ -61,6 +62,8 @@ class Workload:
             target.set_gossip(*self.gossip)
         if self.delta_crdt:
             target.set_delta_crdt(self.delta_crdt)
+        if self.behaviors is not None:
+            target.set_behaviors(self.behaviors)
         if self.fanout is not None:
             target.set_fanout(*self.fanout)
         if self.graph is not None:
@@ -340,3 +343,52 @@ def mixed(n: int = 4096, seed: int = 1, throughput: int = 3, capacity: int = 0, 
         0, 1 << 24, int(is_fan.sum())).astype(np.uint32)
     return Workload("mixed", n, 2, 2, throughput, capacity, ranges, ring_stride=7, fanout=(2, seed, cdf, perm),
                     graph=(row, col), tells=(dst, src, pay))
+
+
+def compiled(n: int = 4096, seed: int = 1, throughput: int = 3, capacity: int = 0, tells_per_actor: int = 3,
+             builtin: bool = False) -> Workload:
+    """Typed behaviours lowered by akka_amd.typed (compiled behaviour tables): the DSL versions of
+    counter / ring / stop-after / ping-pong and a pair of behaviours that become each other, side
+    by side (and beside the built-in kinds with `builtin`), random tells between them."""
+    from . import typed
+    rng = np.random.default_rng(seed)
+    lib = typed.library(ring_stride=7)
+    sw = typed.switch()
+    tables = typed.compile_behaviors([lib["counter"], lib["ring"], lib["stop_after"], lib["ping_pong"], sw])
+    kinds = [tables.kind_of(lib[k]) for k in ("counter", "ring", "stop_after", "ping_pong")] + [tables.kind_of(sw)]
+    if builtin:
+        kinds += [Kind.COUNTER, Kind.RING, Kind.PINGPONG, Kind.STOP_AFTER]
+    per = n // len(kinds)
+    ranges = []
+    for i, kd in enumerate(kinds):
+        first = i * per
+        count = per if i < len(kinds) - 1 else n - first
+        init = None
+        if kd in (tables.kind_of(lib["stop_after"]), Kind.STOP_AFTER):
+            init = np.zeros((count, 2), np.uint64)
+            init[:, 1] = rng.integers(1, 6, count)
+        elif kd in (tables.kind_of(lib["ping_pong"]), Kind.PINGPONG):
+            init = np.zeros((count, 2), np.uint64)
+            init[:, 0] = rng.integers(0, 5, count)
+        ranges.append((first, count, kd, init))
+    m = n * tells_per_actor
+    dst = rng.integers(0, n + 8, m).astype(np.uint32)  # a few unknown refs -> dead letters
+    src = rng.integers(0, n, m).astype(np.uint32)
+    src[rng.random(m) < 0.1] = NO_SENDER
+    pay = rng.integers(0, 12, m).astype(np.uint32)
+    sw_first, sw_count = ranges[4][0], ranges[4][1]
+    is_sw = (dst >= sw_first) & (dst < sw_first + sw_count)
+    k = int(is_sw.sum())
+    pay[is_sw] = (rng.integers(1, 4, k).astype(np.uint32) << 24) | rng.integers(0, 6, k).astype(np.uint32)
+    return Workload("compiled", n, 2, 1, throughput, capacity, ranges, ring_stride=7, tells=(dst, src, pay),
+                    behaviors=tables)
+
+
+def compiled_ring(n: int = 1_000_000, hops: int = 256, throughput: int = 5) -> Workload:
+    """C2's token ring with the ring behaviour written in the typed DSL (akka_amd.typed.library)."""
+    from . import typed
+    ring = typed.library(ring_stride=1)["ring"]
+    tables = typed.compile_behaviors([ring])
+    w = token_ring(n, hops, throughput)
+    w.name, w.ranges, w.behaviors = "compiled_ring", [(0, n, tables.kind_of(ring), None)], tables
+    return w

@@ -127,6 +127,9 @@ def cpu_baseline(hops: int) -> dict:
                                lambda: wl.crdt_gossip(200_000, Kind.GCOUNTER, rounds=8)),
         "C4_orset_gossip": ("50k ORSet replicas, 4 rounds of full-state gossip to 2 peers",
                             lambda: wl.crdt_gossip(50_000, Kind.ORSET, rounds=4)),
+        "C4_orset_delta_gossip": ("200k delta-CRDT ORSet replicas (keys of 8), 8 DeltaPropagationTicks with a "
+                                  "writer update each",
+                                  lambda: wl.crdt_delta(200_000, Kind.ORSET, rounds=8, write=True)),
         "C5_power_law_bounded": ("1M actors, power-law R-MAT graph, FORWARD_RR ttl 15, BoundedMailbox(64)",
                                  lambda: wl.power_law_forward(1_000_000, ttl=15, capacity=64, throughput=5)),
     }
@@ -242,6 +245,15 @@ def other_configs(quick: bool, only: str = "") -> dict:
             "1M Replicator-style ORSet replicas (64-element universe, 8 nodes, dots + version vector), full-state "
             "gossip to 2 random peers per tick, ORSet.merge",
             lambda: wl.crdt_gossip(1_000_000, Kind.ORSET, rounds=20), 2, 12, 0),
+        "C4_orset_delta_gossip": (
+            "1M Replicator-style ORSet replicas with delta-CRDT replication (keys of 8 replicas = 8 nodes): each "
+            "DeltaPropagationTick tells the replica one writer Update (add/remove) and propagates the merged delta "
+            "groups to a round-robin slice of 2 nodes (DeltaPropagationSelector, causal delivery, ORSet.mergeDelta)",
+            lambda: wl.crdt_delta(1_000_000, Kind.ORSET, rounds=40, write=True), 4, 24, 0),
+        "C4_gcounter_delta_gossip": (
+            "1M Replicator-style GCounter replicas with delta-CRDT replication (keys of 8): each "
+            "DeltaPropagationTick tells one writer increment and propagates the counter deltas to 2 nodes",
+            lambda: wl.crdt_delta(1_000_000, Kind.GCOUNTER, rounds=40, write=True), 4, 24, 0),
         "C1_ping_pong": (
             "akka-bench-jmh ForkJoinActorBenchmark.pingPong shape: 1000 PingPong pairs, 100 in flight per pair, "
             "throughput 50",

@@ -81,6 +81,51 @@ enum agx_behavior_kind {
 #define AGX_RES_SAME 0u
 #define AGX_RES_STOPPED 1u
 #define AGX_RES_UNHANDLED 2u
+#define AGX_RES_BECOME 3u /* compiled behaviours: the next behaviour is agx_case.next */
+
+/* --- compiled behaviours ------------------------------------------------------
+ * A typed Behaviors.receiveMessage / javadsl ReceiveBuilder subset lowered to tables
+ * (akka_amd/typed.py is the lowering; TY/scaladsl/Behaviors.scala:101-121,
+ * TY/javadsl/ReceiveBuilder.scala:48-98,209-218).  An actor of kind AGX_KIND_COMPILED + b
+ * runs behaviour b: cases [first[b], first[b+1]) are tried in order and the first whose
+ * message tests and state guard hold runs its actions, then returns its result --
+ * Behaviors.same, stopped, unhandled, or a become to behaviour `next` (stored in the
+ * actor's kind byte).  No matching case = Behaviors.unhandled (ReceiveBuilder.receive).
+ * Compiled behaviours keep their state in words 0 and 1 (two u64 fields).
+ * Operands: value = base(src, word) + k, base = 0 (AGX_V_CONST), the payload, its tag
+ * (payload >> 24), its argument (payload & 0xFFFFFF), state word `word`, the sender id or
+ * the actor's own id.  Comparisons are unsigned 64-bit.                              */
+#define AGX_KIND_COMPILED 16u
+#define AGX_MAX_BEHAVIORS 64u
+#define AGX_MAX_CASES 1024u
+#define AGX_MAX_ACTS 4096u
+enum agx_operand { AGX_V_CONST = 0, AGX_V_PAYLOAD = 1, AGX_V_TAG = 2, AGX_V_ARG = 3, AGX_V_WORD = 4,
+                   AGX_V_SENDER = 5, AGX_V_SELF = 6 };
+enum agx_cmp { AGX_CMP_ANY = 0, AGX_CMP_EQ = 1, AGX_CMP_NE = 2, AGX_CMP_LT = 3, AGX_CMP_LE = 4, AGX_CMP_GT = 5,
+               AGX_CMP_GE = 6 };
+enum agx_action_op {
+  AGX_A_SET = 1,  /* word[w] = operand                                          */
+  AGX_A_ADD = 2,  /* word[w] += operand (wrapping)                              */
+  AGX_A_MAX = 3,  /* word[w] = max(word[w], operand)                            */
+  AGX_A_MIN = 4,
+  AGX_A_TELL = 5  /* tell(dst operand, payload): payload = (u32)operand, or with a message tag
+                     (or_mask != 0) (operand & 0xFFFFFF) | or_mask; a dst operand based on the
+                     actor's own id is taken mod n_actors (ring neighbours); an unknown id is a
+                     dead letter */
+};
+typedef struct agx_case {
+  uint8_t src1, word1, cmp1, src2; /* test 1: operand(src1, word1, k1) cmp1 operand(src2, word2, k2) */
+  uint8_t word2, src3, word3, cmp2; /* test 2: operand(src3, word3, k3) cmp2 operand(src4, word4, k4) */
+  uint8_t src4, word4, result, next;
+  uint16_t act_first, act_count;    /* actions [act_first, act_first + act_count) */
+  int64_t k1, k2, k3, k4;
+} agx_case; /* 48 B */
+typedef struct agx_act {
+  uint8_t op, word, src, sword;     /* action; target word; operand (src, sword, k)  */
+  uint8_t dsrc, dword, pad0, pad1;  /* AGX_A_TELL destination operand (dsrc, dword, dk) */
+  uint32_t or_mask;                 /* AGX_A_TELL: payload |= or_mask (a message tag)  */
+  int64_t k, dk;
+} agx_act; /* 32 B */
 
 #define AGX_MAX_WORDS 656u /* = AGX_ORSET_DELTA_WORDS (the widest layout) */
 #define AGX_MAX_RANKS 16u
@@ -222,6 +267,11 @@ agx_status agx_set_gossip(agx_engine* eng, uint32_t fanout, uint64_t seed);
  * (see "delta-CRDT replication" above).  Call before the first agx_run; CRDT actors then need
  * n_words >= the *_DELTA_WORDS of their kind.                                               */
 agx_status agx_set_delta_crdt(agx_engine* eng, uint32_t max_delta_size);
+/* Compiled behaviours (see "compiled behaviours" above): behaviour b = cases
+ * [first[b], first[b+1]); first has n_behaviors + 1 entries.  Replaces the tables of an
+ * earlier call; call before agx_run.  Register actors with kind AGX_KIND_COMPILED + b.      */
+agx_status agx_set_behaviors(agx_engine* eng, const agx_case* cases, uint32_t n_cases, const agx_act* acts,
+                             uint32_t n_acts, const uint32_t* first, uint32_t n_behaviors);
 /* Out-edge lists in CSR over GLOBAL ids: row_ptr[n_actors+1], col[row_ptr[n]].  */
 agx_status agx_set_graph(agx_engine* eng, const uint64_t* row_ptr, const uint32_t* col);
 /* The same CSR with the destinations generated on the device (workload setup for

@@ -36,6 +36,10 @@ typedef struct {
   uint64_t gossip_seed;
   uint32_t delta_max;      /* delta-CRDT mode: Replicator max-delta-size (0 = off) */
   uint32_t error;          /* set on a delta-log overflow (engine: AGX_ECAPACITY) */
+  const agx_case* bcase;   /* compiled behaviours (agx_set_behaviors) */
+  const agx_act* bact;
+  const uint32_t* bfirst;
+  uint32_t n_beh;
 } ref_params;
 
 /* tell(dst, payload) from `self`; row != NULL = a CRDT state gossip carrying
@@ -358,8 +362,82 @@ static inline uint32_t ref_apply_crdt(ref_params* P, uint32_t kind, uint32_t a, 
   }
 }
 
-static inline uint32_t ref_apply(ref_params* P, uint32_t kind, uint32_t a, uint64_t* w, uint32_t src,
+/* ---------------------------------------------------------------------------
+ * Compiled behaviours (include/akka_gpu.h): a typed Behaviors.receiveMessage / ReceiveBuilder
+ * restated as its case table.  ReceiveBuilder.receive (TY/javadsl/ReceiveBuilder.scala:209-218)
+ * tries the handlers in order and takes the first whose class and predicate match; none ->
+ * Behaviors.unhandled.  A become replaces the actor's behaviour for its next message
+ * (TY/Behavior.scala:150 canonicalize, ActorAdapter.next TY/internal/adapter/ActorAdapter.scala:152-168). */
+static inline uint64_t ref_operand(uint32_t src, uint32_t word, int64_t k, uint32_t pay, const uint64_t* w,
+                                   uint32_t sender, uint32_t self) {
+  uint64_t b = 0;
+  if (src == AGX_V_PAYLOAD) b = pay;
+  else if (src == AGX_V_TAG) b = pay >> 24;
+  else if (src == AGX_V_ARG) b = pay & 0xFFFFFFu;
+  else if (src == AGX_V_WORD) b = w[word];
+  else if (src == AGX_V_SENDER) b = sender;
+  else if (src == AGX_V_SELF) b = self;
+  return b + (uint64_t)k;
+}
+static inline int ref_cmp(uint32_t op, uint64_t a, uint64_t b) {
+  switch (op) {
+    case AGX_CMP_EQ: return a == b;
+    case AGX_CMP_NE: return a != b;
+    case AGX_CMP_LT: return a < b;
+    case AGX_CMP_LE: return a <= b;
+    case AGX_CMP_GT: return a > b;
+    case AGX_CMP_GE: return a >= b;
+    default: return 1;
+  }
+}
+static inline uint32_t ref_apply_compiled(const ref_params* P, uint32_t* kind, uint32_t a, uint64_t* w, uint32_t src,
+                                          uint32_t pay, ref_emit_fn emit, void* ctx) {
+  const uint32_t b = *kind - AGX_KIND_COMPILED;
+  if (b >= P->n_beh) return AGX_RES_UNHANDLED;
+  for (uint32_t c = P->bfirst[b]; c < P->bfirst[b + 1]; ++c) {
+    const agx_case* C = &P->bcase[c];
+    if (!ref_cmp(C->cmp1, ref_operand(C->src1, C->word1, C->k1, pay, w, src, a),
+                 ref_operand(C->src2, C->word2, C->k2, pay, w, src, a)))
+      continue;
+    if (!ref_cmp(C->cmp2, ref_operand(C->src3, C->word3, C->k3, pay, w, src, a),
+                 ref_operand(C->src4, C->word4, C->k4, pay, w, src, a)))
+      continue;
+    for (uint32_t i = C->act_first; i < (uint32_t)C->act_first + C->act_count; ++i) {
+      const agx_act* A = &P->bact[i];
+      const uint64_t v = ref_operand(A->src, A->sword, A->k, pay, w, src, a);
+      if (A->op == AGX_A_SET) w[A->word] = v;
+      else if (A->op == AGX_A_ADD) w[A->word] += v;
+      else if (A->op == AGX_A_MAX) { if (v > w[A->word]) w[A->word] = v; }
+      else if (A->op == AGX_A_MIN) { if (v < w[A->word]) w[A->word] = v; }
+      else if (A->op == AGX_A_TELL) {
+        uint64_t d;
+        if (A->dsrc == AGX_V_SELF) {
+          int64_t x = ((int64_t)a + A->dk) % (int64_t)P->n;
+          d = (uint64_t)(x < 0 ? x + (int64_t)P->n : x);
+        } else {
+          d = ref_operand(A->dsrc, A->dword, A->dk, pay, w, src, a);
+        }
+        emit(ctx, d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d, a,
+             A->or_mask ? ((uint32_t)v & 0xFFFFFFu) | A->or_mask : (uint32_t)v, (const uint64_t*)0, 0u);
+      }
+    }
+    if (C->result == AGX_RES_BECOME) {
+      *kind = AGX_KIND_COMPILED + C->next;
+      return AGX_RES_SAME;
+    }
+    return C->result;
+  }
+  return AGX_RES_UNHANDLED;
+}
+
+/* `kind` in/out: a compiled behaviour's become changes it for the actor's next message. */
+static inline uint32_t ref_apply(ref_params* P, uint32_t* kind_io, uint32_t a, uint64_t* w, uint32_t src,
                                  uint32_t payload, const uint64_t* row, ref_emit_fn emit, void* ctx) {
+  const uint32_t kind = *kind_io;
+  if (kind >= AGX_KIND_COMPILED) {
+    if (ref_is_wide(src)) return AGX_RES_UNHANDLED;
+    return ref_apply_compiled(P, kind_io, a, w, src, payload, emit, ctx);
+  }
   if (kind >= AGX_KIND_GCOUNTER && kind <= AGX_KIND_ORSET)
     return ref_apply_crdt(P, kind, a, w, src, payload, row, emit, ctx);
   if (ref_is_wide(src)) return AGX_RES_UNHANDLED; /* a state gossip is not in this behaviour's protocol */

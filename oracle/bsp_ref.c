@@ -151,6 +151,9 @@ typedef struct bsp_sim {
   uint32_t* zipf_perm;
   uint64_t* row_ptr;
   uint32_t* col;
+  agx_case* bcase;
+  agx_act* bact;
+  uint32_t* bfirst;
   /* mail */
   envvec backlog, emitted, staged;
   agx_stats st;
@@ -200,6 +203,7 @@ void bsp_destroy(bsp_sim* s) {
   if (!s) return;
   free(s->kind); free(s->alive); free(s->state); free(s->order);
   free(s->zipf_cdf); free(s->zipf_perm); free(s->row_ptr); free(s->col);
+  free(s->bcase); free(s->bact); free(s->bfirst);
   free(s->backlog.v); free(s->emitted.v); free(s->staged.v);
   free(s->backlog.rows); free(s->emitted.rows); free(s->staged.rows);
   free(s);
@@ -207,7 +211,8 @@ void bsp_destroy(bsp_sim* s) {
 
 int bsp_register_range(bsp_sim* s, uint64_t first, uint64_t count, uint32_t kind, const uint64_t* init,
                        uint64_t stride_words) {
-  if (first + count > s->n || kind >= AGX_KIND_MAX) return 1;
+  const int compiled = kind >= AGX_KIND_COMPILED && kind < AGX_KIND_COMPILED + AGX_MAX_BEHAVIORS;
+  if (first + count > s->n || (kind >= AGX_KIND_MAX && !compiled)) return 1;
   if ((kind == AGX_KIND_FORWARD_RR || kind == AGX_KIND_STOP_AFTER) && s->W < 2) return 1;
   uint32_t rw = ref_crdt_words(kind);
   if (rw) {
@@ -228,6 +233,24 @@ void bsp_set_ring(bsp_sim* s, uint32_t stride) { s->P.ring_stride = stride; }
 void bsp_set_gossip(bsp_sim* s, uint32_t fanout, uint64_t seed) {
   s->P.gossip_f = fanout;
   s->P.gossip_seed = seed;
+}
+
+/* compiled behaviour tables (include/akka_gpu.h agx_set_behaviors; copied) */
+int bsp_set_behaviors(bsp_sim* s, const agx_case* cases, uint32_t n_cases, const agx_act* acts, uint32_t n_acts,
+                      const uint32_t* first, uint32_t n_beh) {
+  free(s->bcase); free(s->bact); free(s->bfirst);
+  s->bcase = (agx_case*)malloc((n_cases ? n_cases : 1) * sizeof(agx_case));
+  s->bact = (agx_act*)malloc((n_acts ? n_acts : 1) * sizeof(agx_act));
+  s->bfirst = (uint32_t*)malloc((n_beh + 1) * 4);
+  if (!s->bcase || !s->bact || !s->bfirst) return 2;
+  memcpy(s->bcase, cases, n_cases * sizeof(agx_case));
+  memcpy(s->bact, acts, n_acts * sizeof(agx_act));
+  memcpy(s->bfirst, first, (n_beh + 1) * 4);
+  s->P.bcase = s->bcase;
+  s->P.bact = s->bact;
+  s->P.bfirst = s->bfirst;
+  s->P.n_beh = n_beh;
+  return 0;
 }
 
 /* delta-crdt.enabled / max-delta-size (include/akka_gpu.h agx_set_delta_crdt) */
@@ -329,9 +352,11 @@ static int bsp_step(bsp_sim* s) {
     if (!L) continue;
     if (!s->alive[a]) { s->st.dead_letters += L; continue; }
     uint64_t nd = L < s->T ? L : s->T;
+    uint32_t kcur = s->kind[a];
     for (uint64_t p = 0; p < nd; ++p) {
-      uint32_t r = ref_apply(&s->P, s->kind[a], a, &s->state[(uint64_t)a * s->W], in[b + p].src, in[b + p].payload,
+      uint32_t r = ref_apply(&s->P, &kcur, a, &s->state[(uint64_t)a * s->W], in[b + p].src, in[b + p].payload,
                              rw ? inrows + (b + p) * rw : (const uint64_t*)0, emit_cb, s);
+      s->kind[a] = (uint8_t)kcur;
       s->st.delivered++;
       if (r == AGX_RES_UNHANDLED) s->st.unhandled++;
       if (r == AGX_RES_STOPPED) {

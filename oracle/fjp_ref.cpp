@@ -164,6 +164,9 @@ struct Sim {
   std::vector<uint64_t> state;  // actor-major
   std::vector<uint32_t> zipf_cdf, zipf_perm, col;
   std::vector<uint64_t> row_ptr;
+  std::vector<agx_case> bcase;  // compiled behaviours
+  std::vector<agx_act> bact;
+  std::vector<uint32_t> bfirst;
   Pool pool;
   std::vector<uint32_t> st_dst, st_src, st_pay;  // staged tells
   agx_stats st{};
@@ -261,7 +264,7 @@ void run_mailbox(Sim* s, uint32_t a, Worker* w) {
     if (ac.status.load(std::memory_order_acquire) & kClosed) {
       w->dead++;  // cleanUp -> deadLetters
     } else {
-      uint32_t r = ref_apply(&s->P, ac.kind, a, &s->state[(uint64_t)a * s->W], src, pay, row, emit_cb, &ctx);
+      uint32_t r = ref_apply(&s->P, &ac.kind, a, &s->state[(uint64_t)a * s->W], src, pay, row, emit_cb, &ctx);
       w->delivered++;
       if (r == AGX_RES_UNHANDLED) w->unhandled++;
       if (r == AGX_RES_STOPPED) ac.status.fetch_or(kClosed, std::memory_order_acq_rel);
@@ -383,7 +386,8 @@ void fjp_destroy(void* h) {
 int fjp_register_range(void* h, uint64_t first, uint64_t count, uint32_t kind, const uint64_t* init,
                        uint64_t stride_words) {
   Sim* s = (Sim*)h;
-  if (first + count > s->n || kind >= AGX_KIND_MAX) return 1;
+  const bool compiled = kind >= AGX_KIND_COMPILED && kind < AGX_KIND_COMPILED + AGX_MAX_BEHAVIORS;
+  if (first + count > s->n || (kind >= AGX_KIND_MAX && !compiled)) return 1;
   const uint32_t rw = ref_crdt_words(kind);
   if (rw) {
     if (s->W < rw) return 1;
@@ -404,6 +408,20 @@ void fjp_set_gossip(void* h, uint32_t fanout, uint64_t seed) {
   Sim* s = (Sim*)h;
   s->P.gossip_f = fanout;
   s->P.gossip_seed = seed;
+}
+
+// compiled behaviour tables (see bsp_set_behaviors)
+int fjp_set_behaviors(void* h, const agx_case* cases, uint32_t n_cases, const agx_act* acts, uint32_t n_acts,
+                      const uint32_t* first, uint32_t n_beh) {
+  Sim* s = (Sim*)h;
+  s->bcase.assign(cases, cases + n_cases);
+  s->bact.assign(acts, acts + n_acts);
+  s->bfirst.assign(first, first + n_beh + 1);
+  s->P.bcase = s->bcase.data();
+  s->P.bact = s->bact.data();
+  s->P.bfirst = s->bfirst.data();
+  s->P.n_beh = n_beh;
+  return 0;
 }
 
 // delta-crdt.enabled / max-delta-size (see bsp_set_delta_crdt)

@@ -63,6 +63,7 @@ def _load_bsp():
             "bsp_set_ring": (None, [vp, u32]),
             "bsp_set_gossip": (None, [vp, u32, u64]),
             "bsp_set_delta_crdt": (ctypes.c_int, [vp, u32]),
+            "bsp_set_behaviors": (ctypes.c_int, [vp, vp, u32, vp, u32, P32, u32]),
             "bsp_orset_merge": (None, [P64, P64]),
             "bsp_orset_add": (None, [P64, u32, u32]),
             "bsp_orset_remove": (None, [P64, u32]),
@@ -110,6 +111,7 @@ def _load_fjp():
             "fjp_set_ring": (None, [vp, u32]),
             "fjp_set_gossip": (None, [vp, u32, u64]),
             "fjp_set_delta_crdt": (ctypes.c_int, [vp, u32]),
+            "fjp_set_behaviors": (ctypes.c_int, [vp, vp, u32, vp, u32, P32, u32]),
             "fjp_set_fanout": (None, [vp, u32, u64, P32, P32, u64]),
             "fjp_set_graph": (None, [vp, P64, P32]),
             "fjp_stage": (None, [vp, P32, P32, P32, u64]),
@@ -162,6 +164,13 @@ class BspOracle(_Base):
 
     def set_gossip(self, fanout, seed):
         self.lib.bsp_set_gossip(self.h, fanout, seed)
+
+    def set_behaviors(self, t):
+        first = _u32(t.first)
+        self._keep.append(t) if hasattr(self, "_keep") else None
+        if self.lib.bsp_set_behaviors(self.h, ctypes.addressof(t.cases), len(t.cases), ctypes.addressof(t.acts),
+                                       len(t.acts), _p(first, ctypes.c_uint32), t.n_behaviors):
+            raise ValueError("bsp_set_behaviors failed")
 
     def set_delta_crdt(self, max_delta_size):
         if self.lib.bsp_set_delta_crdt(self.h, max_delta_size):
@@ -227,6 +236,17 @@ class FjpOracle(_Base):
 
     def set_gossip(self, fanout, seed):
         self.lib.fjp_set_gossip(self.h, fanout, seed)
+
+    def set_behaviors(self, t):
+        first = _u32(t.first)
+        self._keep.append(t) if hasattr(self, "_keep") else None
+        if self.lib.fjp_set_behaviors(self.h, ctypes.addressof(t.cases), len(t.cases), ctypes.addressof(t.acts),
+                                       len(t.acts), _p(first, ctypes.c_uint32), t.n_behaviors):
+            raise ValueError("fjp_set_behaviors failed")
+
+    def set_delta_crdt(self, max_delta_size):
+        if self.lib.fjp_set_delta_crdt(self.h, max_delta_size):
+            raise ValueError("fjp_set_delta_crdt failed")
 
     def set_fanout(self, k, seed, cdf, perm):
         cdf, perm = _u32(cdf), _u32(perm)
