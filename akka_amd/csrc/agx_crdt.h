@@ -208,6 +208,7 @@ __device__ __forceinline__ uint32_t dl_record(const DevParams& P, const St32& s,
 __device__ __forceinline__ void dl_group_row(const DevParams& P, const St32& s, uint32_t kind, uint32_t node, uint32_t j,
                                              uint32_t* row) {
   const uint32_t e0 = dl_env(kind), ctr = s.ld(e0 + 8);
+  row[0] = 0;  // (rows are recycled: every field the receiver reads is written)
   row[1] = node;
   row[2] = j + 1u;
   row[3] = ctr;

@@ -1151,6 +1151,10 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->rank = cfg->rank;
   e->num_shards = cfg->num_shards ? cfg->num_shards : 1000;
   e->bb = cfg->bucket_actors ? ceil_log2(cfg->bucket_actors) : (uint32_t)kBucketBits;
+  if (const char* s = getenv("AGX_BUCKET_ACTORS")) {  // diagnostic: override the bucket width (power of two)
+    const uint32_t ba = (uint32_t)atoi(s);
+    if (ba >= (1u << kMinBucketBits) && ba <= (uint32_t)kBucket && !(ba & (ba - 1))) e->bb = ceil_log2(ba);
+  }
   e->graphs_enabled = getenv("AGX_NO_GRAPH") == nullptr && getenv("AGX_STAMPS") == nullptr;
   agx_status st = ensure_dev(e);
   if (st) { delete e; return st; }

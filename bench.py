@@ -249,11 +249,11 @@ def other_configs(quick: bool, only: str = "") -> dict:
             "1M Replicator-style ORSet replicas with delta-CRDT replication (keys of 8 replicas = 8 nodes): each "
             "DeltaPropagationTick tells the replica one writer Update (add/remove) and propagates the merged delta "
             "groups to a round-robin slice of 2 nodes (DeltaPropagationSelector, causal delivery, ORSet.mergeDelta)",
-            lambda: wl.crdt_delta(1_000_000, Kind.ORSET, rounds=40, write=True), 4, 24, 0),
+            lambda: wl.crdt_delta(1_000_000, Kind.ORSET, rounds=40, write=True), 4, 24, 8_000_000),
         "C4_gcounter_delta_gossip": (
             "1M Replicator-style GCounter replicas with delta-CRDT replication (keys of 8): each "
             "DeltaPropagationTick tells one writer increment and propagates the counter deltas to 2 nodes",
-            lambda: wl.crdt_delta(1_000_000, Kind.GCOUNTER, rounds=40, write=True), 4, 24, 0),
+            lambda: wl.crdt_delta(1_000_000, Kind.GCOUNTER, rounds=40, write=True), 4, 24, 8_000_000),
         "C1_ping_pong": (
             "akka-bench-jmh ForkJoinActorBenchmark.pingPong shape: 1000 PingPong pairs, 100 in flight per pair, "
             "throughput 50",

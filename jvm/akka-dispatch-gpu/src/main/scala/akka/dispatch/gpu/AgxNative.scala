@@ -28,6 +28,7 @@ object AgxNative {
   final val KindGCounter = 8
   final val KindPNCounter = 9
   final val KindORSet = 10
+  final val KindCompiled = 16 // + behaviour index (agx_set_behaviors)
 
   // agx_status
   final val Ok = 0
@@ -67,6 +68,26 @@ object AgxNative {
     h("agx_register_range", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, JAVA_LONG, JAVA_INT, ADDRESS, JAVA_LONG))
   val setRing: MethodHandle = h("agx_set_ring", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT))
   val setGossip: MethodHandle = h("agx_set_gossip", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_LONG))
+  val setDeltaCrdt: MethodHandle = h("agx_set_delta_crdt", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT))
+  val setBehaviors: MethodHandle = h(
+    "agx_set_behaviors",
+    FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, ADDRESS, JAVA_INT, ADDRESS, JAVA_INT))
+
+  /** struct agx_case (48 B): 12 x u8 (src1, word1, cmp1, src2, word2, src3, word3, cmp2, src4, word4,
+   *  result, next), u16 act_first, u16 act_count, 4 x i64 (k1..k4) */
+  val Case: StructLayout = MemoryLayout.structLayout(
+    MemoryLayout.sequenceLayout(12, JAVA_BYTE).withName("bytes"),
+    JAVA_SHORT.withName("act_first"),
+    JAVA_SHORT.withName("act_count"),
+    MemoryLayout.sequenceLayout(4, JAVA_LONG).withName("k"))
+
+  /** struct agx_act (32 B): u8 op, word, src, sword, dsrc, dword, pad, pad; u32 or_mask; i64 k, dk */
+  val Act: StructLayout = MemoryLayout.structLayout(
+    MemoryLayout.sequenceLayout(8, JAVA_BYTE).withName("bytes"),
+    JAVA_INT.withName("or_mask"),
+    MemoryLayout.paddingLayout(4),
+    JAVA_LONG.withName("k"),
+    JAVA_LONG.withName("dk"))
   val stageTells: MethodHandle =
     h("agx_stage_tells", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG))
   val run: MethodHandle = h("agx_run", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, ADDRESS))

@@ -106,7 +106,7 @@ def test_delta_orset_converges_100k(built):
     key's 8 replicas to one value, with every replica's deltaVersions at each writer's last seqNr."""
     n = 100_000
     w = wl.crdt_delta(n, Kind.ORSET, rounds=12, write=False, ops_per_replica=4, gossip_rounds=40)
-    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+    eng = GpuEngine(EngineConfig(msg_capacity=8 * n, **w.gpu_kwargs()))
     w.apply_to(eng)
     st = eng.run()
     assert st.in_flight == 0 and st.unhandled == 0 and st.dead_letters == 0

@@ -1,0 +1,6 @@
+#!/bin/bash
+source tools/gpu_lib.sh r02i
+step delta 600 python -u -m pytest tests/test_gpu_delta_crdt.py tests/test_gpu_typed.py -x -v --timeout 300 --timeout-method thread
+step c4d_orset 300 python -u tools/cfg_one.py C4_orset_delta_gossip
+step c4d_gc 300 python -u tools/cfg_one.py C4_gcounter_delta_gossip
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
