@@ -138,11 +138,12 @@ __device__ __forceinline__ bool dl_records(uint32_t kind, uint32_t op, uint32_t 
 // Phase A: tells and snapshot rows one message will produce.  Delta replicas simulate the
 // selector (deltaCounter, deltaSentToNode, round robin) over the drain, so a DeltaPropagationTick
 // counts exactly the propagations phase B will tell.
+template <uint32_t CM>
 __device__ __forceinline__ uint32_t crdt_count(const DevParams& P, uint32_t kind, uint32_t self, uint32_t l,
                                                uint32_t src, uint32_t pay, uint32_t* rows, DeltaSim& ds) {
   if (is_wide(src)) return 0;
   const uint32_t op = pay >> 24, arg = pay & 0xFFFFFFu;
-  const bool dm = P.delta_max != 0;
+  const bool dm = (CM & kDeltaKM) != 0 && P.delta_max != 0;
   if (dm && (op == AGX_OP_DELTA_TICK || dl_records(kind, op, arg)) && !ds.on) {
     const St32 s{P.state + l, P.n_local};
     const uint32_t e0 = dl_env(kind);
@@ -427,13 +428,13 @@ template <uint32_t CM, typename Emit>
 __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHeap& H, uint32_t kind, uint32_t self,
                                                uint32_t l, uint32_t src, uint32_t pay, uint32_t& row_cursor,
                                                Emit& em) {
-  if constexpr (CM == (1u << AGX_KIND_GCOUNTER)) kind = AGX_KIND_GCOUNTER;
-  if constexpr (CM == (1u << AGX_KIND_PNCOUNTER)) kind = AGX_KIND_PNCOUNTER;
-  if constexpr (CM == (1u << AGX_KIND_ORSET)) kind = AGX_KIND_ORSET;
+  if constexpr ((CM & ~kDeltaKM) == (1u << AGX_KIND_GCOUNTER)) kind = AGX_KIND_GCOUNTER;
+  if constexpr ((CM & ~kDeltaKM) == (1u << AGX_KIND_PNCOUNTER)) kind = AGX_KIND_PNCOUNTER;
+  if constexpr ((CM & ~kDeltaKM) == (1u << AGX_KIND_ORSET)) kind = AGX_KIND_ORSET;
   const size_t nl = P.n_local;
   uint64_t* st = P.state + l;  // word w at st[w * nl]
   const uint32_t node = self % AGX_CRDT_NODES;
-  const bool dm = P.delta_max != 0;
+  const bool dm = (CM & kDeltaKM) != 0 && P.delta_max != 0;  // (the engine launches kDeltaKM variants then)
   const St32 s32{st, nl};
   if (is_wide(src)) {
     if ((pay >> 30) != kind - (uint32_t)AGX_KIND_GCOUNTER) return AGX_RES_UNHANDLED;  // another data type

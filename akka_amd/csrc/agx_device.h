@@ -172,6 +172,9 @@ __device__ __forceinline__ int block_excl_max(int v, int* scratch) {
 // launches the narrowest specialisation that covers every registered kind, so a
 // population of one behaviour runs a small, branch-free apply kernel.
 constexpr uint32_t kb(uint32_t k) { return 1u << (k < AGX_KIND_COMPILED ? k : AGX_KIND_COMPILED); }
+// KM flag (not a kind): the variant runs delta-CRDT replication (agx_set_delta_crdt).  Variants
+// without it compile the delta code out (its registers would spill the full-state merges).
+constexpr uint32_t kDeltaKM = 1u << 31;
 constexpr uint32_t KM_ALL = kb(AGX_KIND_COUNTER) | kb(AGX_KIND_RING) | kb(AGX_KIND_FANOUT) | kb(AGX_KIND_FORWARD_RR) |
                             kb(AGX_KIND_STOP_AFTER) | kb(AGX_KIND_PINGPONG) | kb(AGX_KIND_EVEN);
 

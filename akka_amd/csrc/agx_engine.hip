@@ -532,7 +532,16 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     else AGX_APPLY2(W, M, false, false);                                                         \
   } while (0)
     constexpr uint32_t kCrdt = kb(AGX_KIND_GCOUNTER) | kb(AGX_KIND_PNCOUNTER) | kb(AGX_KIND_ORSET);
-    if (e->pw && km == kb(AGX_KIND_GCOUNTER))  // single-kind CRDT populations: specialised merges
+    if (e->pw && e->delta_max) {  // delta-CRDT replication: the variants that carry the delta code
+      if (km == kb(AGX_KIND_GCOUNTER))
+        AGX_APPLY(true, kb(AGX_KIND_GCOUNTER) | kDeltaKM);
+      else if (km == kb(AGX_KIND_PNCOUNTER))
+        AGX_APPLY(true, kb(AGX_KIND_PNCOUNTER) | kDeltaKM);
+      else if (km == kb(AGX_KIND_ORSET))
+        AGX_APPLY(true, kb(AGX_KIND_ORSET) | kDeltaKM);
+      else
+        AGX_APPLY(true, KM_ALL | kDeltaKM);
+    } else if (e->pw && km == kb(AGX_KIND_GCOUNTER))  // single-kind CRDT populations: specialised merges
       AGX_APPLY(true, kb(AGX_KIND_GCOUNTER));
     else if (e->pw && km == kb(AGX_KIND_PNCOUNTER))
       AGX_APPLY(true, kb(AGX_KIND_PNCOUNTER));
@@ -774,8 +783,16 @@ agx_status collect_stats(agx_engine* e, agx_stats* out, bool check) {
   st.supersteps = s[ST_STEPS] + e->host_steps;
   // backlog + tells produced by the last apply, plus host tells not yet consumed
   st.in_flight = s[kStatInfl] + e->n_staged_dev + e->hs_key.size();
-  // B = E_in + f_out*E_out + 2*S*(A/M); kind+alive bytes read per activation
-  st.bytes_alg = 12ull * st.delivered + 12ull * st.emitted + (16ull * e->W + 2ull) * bs[4];
+  // B = E_in + f_out*E_out + 2*S*(A/M); kind+alive bytes read per activation.
+  // S = the state words a behaviour touches: words 0-1 (plain and compiled behaviours), a CRDT's
+  // data words (a full-state merge reads and writes all of them), or with delta-CRDT replication
+  // the envelope/selector words plus one element (a delta touches a few elements; rows not counted).
+  uint64_t sw = std::min<uint64_t>(e->W, 2);
+  const uint32_t km = e->kinds_mask;
+  if (km & kb(AGX_KIND_GCOUNTER)) sw = std::max<uint64_t>(sw, AGX_GCOUNTER_WORDS);
+  if (km & kb(AGX_KIND_PNCOUNTER)) sw = std::max<uint64_t>(sw, AGX_PNCOUNTER_WORDS);
+  if (km & kb(AGX_KIND_ORSET)) sw = std::max<uint64_t>(sw, e->delta_max ? AGX_DELTA_ENV_WORDS + 4 : AGX_ORSET_WORDS);
+  st.bytes_alg = 12ull * st.delivered + 12ull * st.emitted + (16ull * std::min<uint64_t>(sw, e->W) + 2ull) * bs[4];
   if (out) *out = st;
   return AGX_OK;
 }

@@ -1162,7 +1162,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         DeltaSim ds;
         ds.on = false;
         for (uint32_t q = 0; q < nd; ++q)
-          em.count(crdt_count(P, kd, self, l, isrc(s0 + q), ipay(s0 + q), &nrows_t, ds));
+          em.count(crdt_count<KM>(P, kd, self, l, isrc(s0 + q), ipay(s0 + q), &nrows_t, ds));
       } else if constexpr (!kLds) {  // messages in global scratch: loads issued kPF at a time
         bool stop = false;
         for (uint32_t q0 = 0; q0 < nd && !stop; q0 += kPF) {
@@ -1528,6 +1528,24 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       if (tid == 0 && s_g[2]) g.stg_cnt[b] = 0u;
     }
     const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
+    if (cnt == 0) {  // no mail (most buckets of a sparse superstep at 10^7+ actors): write the empty
+                     // backlog / tell-chunk entries bucket_finish would write, skip the pipeline
+      if (tid == 0) {
+        if constexpr (kGather) {
+          g.blo[wpar][b] = lo;
+          g.blc[wpar][b] = 0u;
+        } else {
+          a.chunk_off[b] = lo;
+          a.chunk_cnt[b] = 0u;
+          a.chunk_off[a.nb + b] = (uint32_t)((uint64_t)lo * a.kmax);
+          a.chunk_cnt[a.nb + b] = 0u;
+        }
+        if constexpr (kGather || kOwner)
+          if (g.emc[wpar]) g.emc[wpar][b] = 0u;
+      }
+      __syncthreads();
+      continue;
+    }
     // bypass: inbox item q < xblc is backlog item q (g.bl[rpar] at xblo + q), else sorted item xbst + q - xblc
     const uint32_t xblc = kBypass ? s_g[0] : 0u, xblo = kBypass ? s_g[1] : 0u, xbst = kBypass ? s_g[3] : lo;
     GatherView gv{};

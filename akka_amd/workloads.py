@@ -172,7 +172,7 @@ def crdt_gossip(n: int = 1_000_000, kind: int = Kind.GCOUNTER, rounds: int = 32,
 
 def crdt_delta(n: int = 1_000_000, kind: int = Kind.ORSET, rounds: int = 32, write: bool = True,
                ops_per_replica: int = 0, gossip_rounds: int = 0, fanout: int = 1, max_delta_size: int = 50,
-               throughput: int = 5, seed: int = SEED, capacity: int = 0, bucket_actors: int = 256) -> Workload:
+               throughput: int = 5, seed: int = SEED, capacity: int = 0, bucket_actors: int = 512) -> Workload:
     """C4 with delta-CRDT replication (Replicator delta-crdt.enabled, DD/Replicator.scala:1646-1695,
     1953-2027; DD/DeltaPropagationSelector.scala): keys of 8 replicas (id = 8 * key + node).  Each
     replica first applies `ops_per_replica` host updates, then runs `rounds` DeltaPropagationTicks
