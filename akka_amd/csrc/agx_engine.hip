@@ -135,6 +135,7 @@ struct agx_engine {
   // CRDT state gossips (agx_crdt.h): snapshot heap, 2 x cap rows of pw u32
   uint32_t pw = 0, gossip_f = 0;
   uint32_t delta_max = 0;  // delta-CRDT mode (agx_set_delta_crdt): Replicator max-delta-size, 0 = off
+  bool layout_checked = false;  // RCCL: rows / tells sized alike on every rank (run_multi_rccl)
   // compiled behaviours (agx_set_behaviors)
   agx_case* d_bcase = nullptr;
   agx_act* d_bact = nullptr;
@@ -1049,6 +1050,22 @@ agx_status exchange_rccl(agx_engine* e, Plan& p) {
 agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
   const uint32_t S = e->R + 2;
   Plan p;
+  if (!e->layout_checked) {  // every rank must size rows and tells alike (same register_range / set_* calls):
+                             // the send/recv sizes of the exchange are derived from them
+    const uint64_t sig[2] = {((uint64_t)e->pw << 32) | e->delta_max, ((uint64_t)e->kmax << 32) | e->W};
+    e->h_pin64[0] = sig[0];  // (pinned: the async copy reads it after this call returns)
+    e->h_pin64[1] = sig[1];
+    HIP_TRY(hipMemcpyAsync(e->d_cvec, e->h_pin64, 16, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, 2, ncclUint64, e->comm, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_cmat, (size_t)e->R * 16, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (uint32_t r = 0; r < e->R; ++r)
+      if (e->h_pin64[2 * r] != sig[0] || e->h_pin64[2 * r + 1] != sig[1])
+        return set_err(AGX_EINVAL, "rank %u and rank %u differ in row pitch / delta mode / max_emit / n_words "
+                       "(make the same register_range and set_* calls on every rank)", e->rank, r);
+    e->layout_checked = true;
+  }
   for (uint32_t s = 0; s < max_steps; ++s) {
     AGX_TRY(phase1(e));
     {
@@ -1141,7 +1158,7 @@ const char* agx_last_error(void) { return g_err.c_str(); }
 uint32_t agx_abi_version(void) { return AGX_ABI_VERSION; }
 
 int32_t agx_shard_id(uint32_t id, uint32_t num_shards) {
-  if (num_shards == 0) return 0;
+  if (num_shards == 0 || num_shards > (uint32_t)INT32_MAX) return 0;  // (maxNumberOfShards is an Int)
   int32_t h = java_hash_decimal(id);
   int32_t a = (h == INT32_MIN) ? INT32_MIN : (h < 0 ? -h : h);  // math.abs(Int.MinValue) stays negative
   return a % (int32_t)num_shards;
@@ -1729,6 +1746,9 @@ agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_steps, agx_
   for (uint32_t i = 0; i < n; ++i) {
     if (!engs[i] || engs[i]->R != n || engs[i]->rank != i || engs[i]->n_global != engs[0]->n_global)
       return set_err(AGX_EINVAL, "group engines must be ranks 0..n-1 of one population");
+    if (engs[i]->pw != engs[0]->pw || engs[i]->delta_max != engs[0]->delta_max || engs[i]->kmax != engs[0]->kmax ||
+        engs[i]->W != engs[0]->W)
+      return set_err(AGX_EINVAL, "group engines differ in row pitch / delta mode / max_emit / n_words");
     AGX_TRY(ensure_dev(engs[i]));
     AGX_TRY(prepare_run(engs[i]));
     engs[i]->started = true;

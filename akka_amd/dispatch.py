@@ -123,7 +123,10 @@ class Mailboxes:
         if mailbox_id == "unbounded":
             mt = UnboundedMailbox()
         elif mailbox_id == "bounded":
-            mt = self.from_config(self.config.get_config("akka.actor.default-mailbox"), "akka.dispatch.BoundedMailbox")
+            # Mailboxes.scala:211 builds a BoundedMailbox from default-mailbox; the GPU mailbox
+            # tail-drops (push timeout 0), so the lookup id keeps the capacity and drops the timeout
+            dm = self.config.get_config("akka.actor.default-mailbox")
+            mt = BoundedMailbox(dm.get_int("mailbox-capacity"), 0.0)
         elif mailbox_id.startswith(BOUNDED_CAPACITY_PREFIX):
             mt = BoundedMailbox(int(mailbox_id.split(":")[1]), 0.0)  # Mailboxes.scala:212-216
         else:

@@ -119,8 +119,8 @@ def cpu_baseline(hops: int) -> dict:
     b.close()
     samples = {
         "C1_ping_pong": ("ForkJoinActorBenchmark.pingPong: 1000 pairs, throughput 50, 100 in flight per pair, "
-                         "100000 messages per pair (the JMH run uses 2,000,000)",
-                         lambda: wl.ping_pong(1000, messages_per_pair=100_000, throughput=50)),
+                         "1,000,000 messages per pair (the JMH run uses 2,000,000)",
+                         lambda: wl.ping_pong(1000, messages_per_pair=1_000_000, throughput=50)),
         "C3_zipf_tree": ("1M actors, Zipf(1.1) FANOUT k=4 ttl=3, 1/64 roots, throughput 5, to quiescence",
                          lambda: wl.zipf_fanout(1_000_000, k=4, ttl=3, root_every=64, throughput=5)),
         "C4_gcounter_gossip": ("200k GCounter replicas, 8 rounds of full-state gossip to 2 peers",
@@ -130,8 +130,8 @@ def cpu_baseline(hops: int) -> dict:
         "C4_orset_delta_gossip": ("200k delta-CRDT ORSet replicas (keys of 8), 8 DeltaPropagationTicks with a "
                                   "writer update each",
                                   lambda: wl.crdt_delta(200_000, Kind.ORSET, rounds=8, write=True)),
-        "C5_power_law_bounded": ("1M actors, power-law R-MAT graph, FORWARD_RR ttl 15, BoundedMailbox(64)",
-                                 lambda: wl.power_law_forward(1_000_000, ttl=15, capacity=64, throughput=5)),
+        "C5_power_law_bounded": ("4M actors, power-law R-MAT graph, FORWARD_RR ttl 15, BoundedMailbox(64)",
+                                 lambda: wl.power_law_forward(4_000_000, ttl=15, capacity=64, throughput=5)),
     }
     configs = {}
     for name, (desc, make) in samples.items():
@@ -235,8 +235,13 @@ def other_configs(quick: bool, only: str = "") -> dict:
             lambda: wl.power_law_forward(n5, ttl=15, capacity=64, throughput=5, device_graph=True), 2, 10, 0),
         "C3_zipf_fanout": (
             "10M actors, Zipf(1.1) destinations over a seeded permutation, FANOUT counter/sum behaviour, k=1 steady "
-            "state (every actor holds one message, ttl 15), BoundedMailbox(1000), throughput 5",
+            "state (every actor holds one message, ttl 15), BoundedMailbox(1000) (an unbounded mailbox lets the hot "
+            "actors' backlogs grow without limit at throughput 5), throughput 5",
             lambda: wl.zipf_fanout(10_000_000, k=1, ttl=15, root_every=1, capacity=1000), 2, 10, 0),
+        "C3_zipf_tree": (
+            "10M actors, Zipf(1.1) fan-out tree of SURVEY.md 8(d): 1/64 of the actors are roots, k=4 tells per "
+            "message, ttl 3, BoundedMailbox(1000), throughput 5; timed from the first superstep (the burst)",
+            lambda: wl.zipf_fanout(10_000_000, k=4, ttl=3, root_every=64, capacity=1000), 0, 8, 0),
         "C4_gcounter_gossip": (
             "1M Replicator-style GCounter replicas (8 node slots), full-state gossip to 2 random peers per tick, "
             "merge = slot-wise max (akka-distributed-data GCounter.merge)",

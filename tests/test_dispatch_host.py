@@ -86,6 +86,7 @@ def test_lookup_errors_match_reference():
 def test_mailboxes_lookup():
     m = Mailboxes(Config.parse_string(CONF))
     assert m.lookup("unbounded") == UnboundedMailbox()
+    assert m.lookup("bounded") == BoundedMailbox(1000, 0.0)  # default-mailbox capacity (Mailboxes.scala:211)
     assert m.lookup(MailboxSelector.bounded(12)) == BoundedMailbox(12, 0.0)  # bounded-capacity:N
     assert m.lookup("bounded-mailbox") == NonBlockingBoundedMailbox(16)
     assert m.lookup("akka.actor.typed.default-mailbox") == SingleConsumerOnlyUnboundedMailbox()
