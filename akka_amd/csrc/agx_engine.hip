@@ -136,6 +136,7 @@ struct agx_engine {
   uint32_t pw = 0, gossip_f = 0;
   uint32_t delta_max = 0;  // delta-CRDT mode (agx_set_delta_crdt): Replicator max-delta-size, 0 = off
   bool layout_checked = false;  // RCCL: rows / tells sized alike on every rank (run_multi_rccl)
+  uint32_t tiny_max = kTinyMax;  // multi-pass: inboxes up to this size take the wave path (AGX_TINY, 0 = off)
   // compiled behaviours (agx_set_behaviors)
   agx_case* d_bcase = nullptr;
   agx_act* d_bact = nullptr;
@@ -515,6 +516,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     ba.g.tstride = e->tstride;
   }
   ba.dbg = e->d_dbg;
+  ba.tiny_max = e->tiny_max;
   {
     const dim3 g(grid_for(e->nb, e->apply_grid)), blk(kBThreads);
     const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
@@ -1185,6 +1187,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->rank = cfg->rank;
   e->num_shards = cfg->num_shards ? cfg->num_shards : 1000;
   e->bb = cfg->bucket_actors ? ceil_log2(cfg->bucket_actors) : (uint32_t)kBucketBits;
+  if (const char* s = getenv("AGX_TINY")) e->tiny_max = std::min<uint32_t>(kTinyMax, (uint32_t)std::max(0, atoi(s)));
   if (const char* s = getenv("AGX_BUCKET_ACTORS")) {  // diagnostic: override the bucket width (power of two)
     const uint32_t ba = (uint32_t)atoi(s);
     if (ba >= (1u << kMinBucketBits) && ba <= (uint32_t)kBucket && !(ba & (ba - 1))) e->bb = ceil_log2(ba);

@@ -746,6 +746,7 @@ struct BucketArgs {
   // slot of a superstep that deferred a skewed bucket; every later superstep is a no-op that
   // passes the mark on, and the host runs the deferred skew launch and resumes (run_single)
   uint32_t* abort;
+  uint32_t tiny_max;       // bypass: inboxes of at most this many messages take the wave path (0 = off)
 };
 
 #define AGX_STAMP(a, idx)                                                                         \
@@ -1364,6 +1365,244 @@ struct GatherView {
   }
 };
 
+// =========================================================================
+// Wave-per-bucket path (single-rank multi-pass, plain and compiled behaviours): a bucket whose
+// inbox holds at most kTinyMax messages -- most buckets of a sparse superstep at 10^7+ actors
+// (C3, C5) -- is drained by one wave with no workgroup barrier, so the 8 waves of a block
+// finish 8 such buckets in the time the block path spends on one (its ~30 barriers and 4-6
+// dependent round trips are per bucket, not per message).  Same semantics as the block path:
+// stable order by actor (inbox order within an actor), tail-drop at C, drain min(len, T), the
+// rest queued in order, Behaviors.stopped / unhandled, tells in sender (= actor) order.
+constexpr uint32_t kTinyIpl = 2;                 // inbox items per lane
+constexpr uint32_t kTinyMax = kTinyIpl * kWave;  // 128
+struct TinyLds {                                 // one per wave (2.5 KB)
+  uint32_t key[kTinyMax], src[kTinyMax], pay[kTinyMax];
+  uint16_t st[kTinyMax], len[kTinyMax];
+};
+
+// Tells of the wave path: into the bucket's tell chunk, next-pass histogram column updated
+// directly (the block path stages it in LDS).
+struct TinyEmitter {
+  const DevParams* P;
+  const BucketArgs* a;
+  uint64_t pos;
+  uint32_t self, col, nhmask;
+  uint32_t n_valid, n_all;
+  __device__ __forceinline__ void operator()(uint32_t dst, uint32_t pay) {
+    ++n_all;
+    if (dst >= P->n_global) return;  // unknown ref -> deadLetters
+    ++n_valid;
+    a->em.key[pos] = dst;  // (single rank: key = local id = global id)
+    a->em.src[pos] = self;
+    a->em.pay[pos] = pay;
+    ++pos;
+    atomicAdd(&a->nhist[(size_t)((dst >> a->nx_shift) & nhmask) * a->nhist_stride + col], 1u);
+  }
+  __device__ __forceinline__ void wide(uint32_t, uint32_t) {}
+};
+
+// max_emit 1: a message's tell is staged in LDS over the actor's already consumed inbox slots
+struct TinyStageEmitter {
+  const DevParams* P;
+  TinyLds* T;
+  uint32_t slot, self;
+  uint32_t n_valid, n_all;
+  __device__ __forceinline__ void operator()(uint32_t dst, uint32_t pay) {
+    ++n_all;
+    if (dst >= P->n_global) return;  // unknown ref -> deadLetters
+    ++n_valid;
+    T->key[slot] = dst;
+    T->src[slot] = self;
+    T->pay[slot] = pay;
+    ++slot;
+  }
+  __device__ __forceinline__ void wide(uint32_t, uint32_t) {}
+};
+
+template <uint32_t KM>
+__device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uint32_t b, uint32_t lo, uint32_t cnt,
+                                            uint32_t xblc, uint32_t xblo, uint32_t xbst, uint32_t rpar,
+                                            uint32_t wpar) {
+  const DevParams& P = a.P;
+  const uint32_t lane = lane_id();
+  const uint32_t amask = (1u << a.bb) - 1u, a0 = b << a.bb;
+  const uint32_t Tt = P.T, C = P.C;
+  // ---- items, and their stable rank by (actor, inbox position) over the whole inbox
+  uint32_t k[kTinyIpl], sv[kTinyIpl], pv[kTinyIpl], la[kTinyIpl];
+#pragma unroll
+  for (uint32_t r = 0; r < kTinyIpl; ++r) {
+    const uint32_t q = r * kWave + lane;
+    la[r] = 0xFFFFFFFFu;
+    k[r] = sv[r] = pv[r] = 0u;
+    if (q < cnt) {
+      if (q < xblc) {
+        k[r] = a.g.bl[rpar].key[xblo + q];
+        sv[r] = a.g.bl[rpar].src[xblo + q];
+        pv[r] = a.g.bl[rpar].pay[xblo + q];
+      } else {
+        k[r] = a.in.key[xbst + q - xblc];
+        sv[r] = a.in.src[xbst + q - xblc];
+        pv[r] = a.in.pay[xbst + q - xblc];
+      }
+      la[r] = k[r] & amask;
+    }
+  }
+  uint32_t rank[kTinyIpl] = {}, st[kTinyIpl] = {}, len[kTinyIpl] = {};
+  for (uint32_t j = 0; j < cnt; ++j) {  // (uniform loop)
+    const uint32_t lj = __shfl((j >> 6) ? la[1] : la[0], (int)(j & 63u), kWave);
+#pragma unroll
+    for (uint32_t r = 0; r < kTinyIpl; ++r) {
+      const bool lt = lj < la[r], eq = lj == la[r];
+      st[r] += lt;
+      len[r] += eq;
+      rank[r] += lt || (eq && j < r * kWave + lane);
+    }
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kTinyIpl; ++r)
+    if (r * kWave + lane < cnt) {
+      T.key[rank[r]] = k[r];
+      T.src[rank[r]] = sv[r];
+      T.pay[rank[r]] = pv[r];
+      T.st[rank[r]] = (uint16_t)st[r];
+      T.len[rank[r]] = (uint16_t)len[r];
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // ---- per actor (the head of its run of sorted positions; lane l owns positions 2l, 2l + 1,
+  // so lane order is actor order)
+  uint32_t hl[kTinyIpl], hlen[kTinyIpl], hkeep[kTinyIpl], hkind[kTinyIpl], nd[kTinyIpl];
+  uint64_t hw0[kTinyIpl], hw1[kTinyIpl];
+  bool head[kTinyIpl], hal[kTinyIpl];
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) {
+    const uint32_t p = lane * kTinyIpl + i;
+    head[i] = p < cnt && T.st[p] == p;
+    hl[i] = head[i] ? a0 + (T.key[p] & amask) : 0u;
+    hlen[i] = head[i] ? T.len[p] : 0u;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) {  // (all loads in flight together)
+    hal[i] = head[i] && P.alive[hl[i]];
+    hkind[i] = head[i] ? P.kind[hl[i]] : 0u;
+    hw0[i] = head[i] ? P.state[hl[i]] : 0ull;
+    hw1[i] = head[i] && P.W > 1 ? P.state[(size_t)P.n_local + hl[i]] : 0ull;
+  }
+  uint32_t ndead = 0, nq = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) {
+    const uint32_t keep = !hal[i] ? 0u : (C == 0 || hlen[i] < C) ? hlen[i] : C;  // tail-drop beyond C
+    hkeep[i] = keep;
+    ndead += hlen[i] - keep;
+    nd[i] = hal[i] ? min(hlen[i], Tt) : 0u;
+    nq += keep > Tt ? keep - Tt : 0u;
+  }
+  const uint64_t embase = (uint64_t)lo * a.kmax;
+  const Msgs blw = a.g.bl[wpar];
+  const uint32_t qinc = wave_incl_sum(nq), bltot = __shfl(qinc, kWave - 1, kWave);
+  uint32_t qoff = qinc - nq;
+  uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0, emtot = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) {  // queued beyond the throughput cap, in order
+    const uint32_t p0 = lane * kTinyIpl + i;
+    for (uint32_t q = Tt; q < hkeep[i]; ++q, ++qoff) {
+      blw.key[lo + qoff] = T.key[p0 + q];
+      blw.src[lo + qoff] = T.src[p0 + q];
+      blw.pay[lo + qoff] = T.pay[p0 + q];
+    }
+  }
+  // drain + apply.  Every message emits <= 1 tell (max_emit 1): one pass, tells staged over the
+  // actor's consumed inbox slots, then compacted in actor order.  Otherwise: count the tells on
+  // copies of the state first (phase A), then apply for real.
+  auto drain = [&](uint32_t i, auto& em) {
+    const uint32_t p0 = lane * kTinyIpl + i, l = hl[i];
+    ++nact;
+    uint64_t wv[2] = {hw0[i], hw1[i]};
+    uint32_t kd = hkind[i];
+    for (uint32_t q = 0; q < nd[i]; ++q) {
+      ++ndel;
+      const uint32_t r = apply_msg<KM>(P, kd, l, l, wv, T.src[p0 + q], T.pay[p0 + q], em);
+      if (r == AGX_RES_UNHANDLED) ++nunh;
+      if (r == AGX_RES_STOPPED) {
+        P.stopq[atomicAdd(P.nstop, 1u)] = l;
+        ndead += nd[i] - q - 1;  // drained-but-unprocessed after the stop
+        break;
+      }
+    }
+    P.state[l] = wv[0];
+    if (P.W > 1) P.state[(size_t)P.n_local + l] = wv[1];
+    if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
+      if (kd != hkind[i]) P.kind[l] = (uint8_t)kd;
+    nall += em.n_all;
+    ndead += em.n_all - em.n_valid;
+  };
+  const uint32_t col = a.ng + b / a.G, nhmask = (1u << a.nx_bits) - 1u;
+  if (a.kmax == 1) {
+    uint32_t ecl[kTinyIpl], ncount = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i) {
+      ecl[i] = 0;
+      if (!nd[i]) continue;
+      TinyStageEmitter em{&P, &T, lane * kTinyIpl + i, hl[i], 0, 0};
+      drain(i, em);
+      ecl[i] = em.n_valid;
+      ncount += em.n_valid;
+    }
+    const uint32_t tinc = wave_incl_sum(ncount);
+    emtot = __shfl(tinc, kWave - 1, kWave);
+    uint32_t toff = tinc - ncount;
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i)
+      for (uint32_t e = 0; e < ecl[i]; ++e, ++toff) {
+        const uint32_t p = lane * kTinyIpl + i + e, d = T.key[p];
+        a.em.key[embase + toff] = d;
+        a.em.src[embase + toff] = T.src[p];
+        a.em.pay[embase + toff] = T.pay[p];
+        atomicAdd(&a.nhist[(size_t)((d >> a.nx_shift) & nhmask) * a.nhist_stride + col], 1u);
+      }
+  } else {
+    uint32_t ncount = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i) {
+      if (!nd[i]) continue;
+      const uint32_t p0 = lane * kTinyIpl + i;
+      Emitter<false> em{&P, {}, 0, hl[i], 0, 0, nullptr, 0, 0};
+      uint64_t wv[2] = {hw0[i], hw1[i]};
+      uint32_t kd = hkind[i];
+      for (uint32_t q = 0; q < nd[i]; ++q)
+        if (apply_msg<KM>(P, kd, hl[i], hl[i], wv, T.src[p0 + q], T.pay[p0 + q], em) == AGX_RES_STOPPED) break;
+      ncount += em.n_valid;
+    }
+    const uint32_t tinc = wave_incl_sum(ncount);
+    emtot = __shfl(tinc, kWave - 1, kWave);
+    uint32_t toff = tinc - ncount;
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i) {
+      if (!nd[i]) continue;
+      TinyEmitter em{&P, &a, embase + toff, hl[i], col, nhmask, 0, 0};
+      drain(i, em);
+      toff += em.n_valid;
+    }
+  }
+  if (lane == 0) {
+    a.chunk_off[b] = lo;
+    a.chunk_cnt[b] = bltot;
+    a.chunk_off[a.nb + b] = (uint32_t)embase;
+    a.chunk_cnt[a.nb + b] = emtot;
+  }
+  const uint32_t v0 = wave_incl_sum(ndel), v1 = wave_incl_sum(ndead), v2 = wave_incl_sum(nunh),
+                 v3 = wave_incl_sum(nall), v4 = wave_incl_sum(nact);
+  if (lane == kWave - 1) {
+    unsigned long long* bs = a.bstats + (size_t)blockIdx.x * kBStats;
+    if (v0) atomicAdd(&bs[0], (unsigned long long)v0);
+    if (v1) atomicAdd(&bs[1], (unsigned long long)v1);
+    if (v2) atomicAdd(&bs[2], (unsigned long long)v2);
+    if (v3) atomicAdd(&bs[3], (unsigned long long)v3);
+    if (v4) atomicAdd(&bs[4], (unsigned long long)v4);
+  }
+}
+
 // kSkew = false: every bucket whose inbox fits one LDS tile (<= kBucket messages); larger
 // inboxes are appended to the skew list.  kSkew = true (launched right after): the listed
 // buckets, general path — separate instantiation, so its register pressure never reaches
@@ -1421,9 +1660,49 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     for (uint32_t i = tid; i < kStagedChunks; i += kBThreads) a.chunk_cnt[2 * a.nb + i] = 0;  // staged consumed
   }
 
+  // single-rank multi-pass, plain behaviours: groups of kBWaves buckets; each wave first drains its
+  // bucket if it is tiny (wave path), then the block drains the group's other buckets
+  constexpr bool kTiny = kBypass && !kSkew && !kWide;
+  __shared__ uint32_t s_tiny[kBWaves];
+  // (a group is kBWaves consecutive iterations of the block's grid-stride sequence, so the
+  // bucket -> block assignment, and with it the load balance, is the block path's own)
   const uint32_t nwork = kSkew ? *skew_n : a.nb;
-  for (uint32_t it = blockIdx.x; it < nwork; it += gridDim.x) {
-    const uint32_t b = kSkew ? a.skew_list[it] : it;
+  const uint32_t istride = kTiny ? kBWaves * gridDim.x : gridDim.x;
+  for (uint32_t it = blockIdx.x; it < nwork; it += istride) {
+    uint32_t bfirst = kSkew ? a.skew_list[it] : it, nblk = 1, todo = 1u, bstep = 0;
+    if constexpr (kTiny) {
+      nblk = kBWaves;
+      bstep = gridDim.x;
+      const uint32_t bw = bfirst + w * bstep;
+      bool tiny = false;
+      if (bw < a.nb && a.tiny_max) {
+        uint32_t bs = 0, lo_w = 0, hi_w = 0, blc = 0, blo = 0;
+        if (lane == 0) {  // (the block path's bypass bounds, below)
+          bs = a.bstart[bw];
+          const uint32_t be = a.bstart[bw + 1], bp = a.blpre[bw] + a.bl_sbase[bw / kBlSlice];
+          blc = a.chunk_cnt[bw];
+          blo = a.chunk_off[bw];
+          lo_w = bs + bp;
+          hi_w = lo_w + blc + (be - bs);
+        }
+        bs = __shfl(bs, 0, kWave);
+        lo_w = __shfl(lo_w, 0, kWave);
+        hi_w = __shfl(hi_w, 0, kWave);
+        blc = __shfl(blc, 0, kWave);
+        blo = __shfl(blo, 0, kWave);
+        tiny = hi_w - lo_w <= a.tiny_max && (uint64_t)hi_w <= a.cap;  // (over capacity: the block path reports it)
+        if (tiny)
+          tiny_bucket<KM>(a, reinterpret_cast<TinyLds*>(U)[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
+      }
+      if (lane == 0) s_tiny[w] = tiny || bw >= a.nb;
+      __syncthreads();
+      todo = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kBWaves; ++j) todo |= s_tiny[j] ? 0u : 1u << j;
+    }
+    for (uint32_t j = 0; j < nblk; ++j) {
+    if (!((todo >> j) & 1u)) continue;
+    const uint32_t b = bfirst + j * bstep;
     AGX_STAMP(a, 0);
     const uint32_t a0 = b << a.bb;
     const uint32_t na = min(1u << a.bb, P.n_local - a0);
@@ -1793,6 +2072,8 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       __threadfence_block();
       bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, cnt2, a0, na, wpar, ndead0);
     }
+    }  // buckets of the group (one without kTiny)
+    if constexpr (kTiny) __syncthreads();  // s_tiny and the waves' LDS are rewritten by the next group
   }
 }
 
