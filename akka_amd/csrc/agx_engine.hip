@@ -176,6 +176,9 @@ struct agx_engine {
   uint64_t host_steps = 0;     // fused: supersteps with mail, counted on the host from h_cntb
   uint32_t par = 0;  // fused: parity of the next superstep (host-tracked; graphs are captured per parity)
   uint32_t *d_skew_list = nullptr, *d_skew_n = nullptr;  // buckets for the general-path launch
+  // multi-pass, plain behaviours: skewed buckets split over workgroups (k_skew_*, agx_kernels.h)
+  uint32_t *d_sk_rec = nullptr, *d_sk_act = nullptr, *d_sk_pc = nullptr, *d_sk_meta = nullptr;
+  uint32_t sk_budget = 0, sk_rows = 0;
   uint32_t tstride = 4, region = 0;
   uint64_t acap = 0;  // arena capacity (fused: regions + overflow area)
   uint32_t apply_grid = kMaxApplyGrid;  // AGX_APPLY_GRID test knob: fewer blocks, each looping over buckets
@@ -442,6 +445,17 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
   return AGX_OK;
 }
 
+// multi-pass, plain behaviours: partition the skewed buckets over workgroups before the skew
+// launch (k_skew_plan / count / scan / scatter, agx_kernels.h); grids are fixed (graph capture),
+// the kernels stride over the device-side part and bucket counts
+void skew_prepass(agx_engine* e, const BucketArgs& ba, const SkewArgs& ska) {
+  const uint32_t gp = std::min<uint32_t>(e->sk_rows, 1024), gb = grid_for(e->nb, kMaxApplyGrid);
+  hipLaunchKernelGGL(k_skew_plan, dim3(1), dim3(kScanThreads), 0, e->stream, ba, ska);
+  hipLaunchKernelGGL(k_skew_count, dim3(gp), dim3(kBThreads), 0, e->stream, ba, ska);
+  hipLaunchKernelGGL(k_skew_scan, dim3(gb), dim3(kBThreads), 0, e->stream, ba, ska);
+  hipLaunchKernelGGL(k_skew_scatter, dim3(gp), dim3(kBThreads), 0, e->stream, ba, ska);
+}
+
 agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   // the chunk histograms consumed by this step's first pass were zeroed by k_chunk_downsweep;
   // on the multi-rank path (no chunk pass) they are never read, so stale columns are harmless
@@ -517,6 +531,9 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   }
   ba.dbg = e->d_dbg;
   ba.tiny_max = e->tiny_max;
+  ba.sk_rec = e->d_sk_rec;
+  ba.sk_act = e->d_sk_act;
+  SkewArgs ska{e->d_sk_rec, e->d_sk_act, e->d_sk_pc, e->d_sk_meta, e->sk_budget, e->sk_rows};
   {
     const dim3 g(grid_for(e->nb, e->apply_grid)), blk(kBThreads);
     const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
@@ -526,6 +543,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     if (!e->skew_only) { Scope s(e, K_APPLY);                                                    \
       hipLaunchKernelGGL((k_bucket_apply<W, M, G, false, O>), g, blk, 0, e->stream, ba); }       \
     if (!(G && e->strict_cap)) { Scope s(e, K_SKEW);                                             \
+      if (!W && !G && !O) skew_prepass(e, ba, ska);                                              \
       hipLaunchKernelGGL((k_bucket_apply<W, M, G, true, O>), gs, blk, 0, e->stream, ba); }       \
   } while (0)
 #define AGX_APPLY(W, M)                                                                          \
@@ -1316,6 +1334,15 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(dalloc(&e->d_blpre, e->nb + 2 * kMaxBlSlices));  // [nb] prefixes, [64] slice totals, [64] bases
     CREATE_TRY(dalloc(&e->d_ninbox, 1));
     CREATE_TRY(hipMemset(e->d_ninbox, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    // skewed-bucket partitions: a skewed bucket holds > kBucket messages, so at most cap / kBucket
+    // of them; parts of >= kSkSpan positions, at most sk_budget + (skewed buckets) of them
+    const uint64_t nsk = std::min<uint64_t>(e->nb, e->cap / kBucket + 1);
+    e->sk_budget = (uint32_t)std::min<uint64_t>(8192, e->cap / kSkSpan + 1);
+    e->sk_rows = e->sk_budget + (uint32_t)nsk;
+    CREATE_TRY(dalloc(&e->d_sk_rec, (uint64_t)e->nb * kSkRec));
+    CREATE_TRY(dalloc(&e->d_sk_act, nsk * 3 * kBucket));
+    CREATE_TRY(dalloc(&e->d_sk_pc, (uint64_t)e->sk_rows * kBucket));
+    CREATE_TRY(dalloc(&e->d_sk_meta, 4));
   }
   if (e->fused) {
     const uint64_t tsz = (uint64_t)kRadix * e->tstride;
@@ -1407,6 +1434,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_abort);
   if (e->h_abort) hipHostFree(e->h_abort);
   hipFree(e->d_skew_list); hipFree(e->d_skew_n);
+  hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_blpre); hipFree(e->d_ninbox); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_cvec); hipFree(e->d_cmat);

@@ -747,6 +747,9 @@ struct BucketArgs {
   // passes the mark on, and the host runs the deferred skew launch and resumes (run_single)
   uint32_t* abort;
   uint32_t tiny_max;       // bypass: inboxes of at most this many messages take the wave path (0 = off)
+  // bypass, plain behaviours: skewed buckets pre-partitioned by k_skew_* (see there); [i] = skew index
+  const uint32_t* sk_rec;  // [i][kSkRec] bucket, bounds, parts, drained and queued totals
+  const uint32_t* sk_act;  // [i][3][kBucket] per actor: admitted, drained-segment start, backlog start
 };
 
 #define AGX_STAMP(a, idx)                                                                         \
@@ -874,9 +877,12 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
   if (tid == 0 && g.emc[w]) g.emc[w][b] = emtot;
 }
 
+// bl_given != ~0: the backlog of this bucket was already written (pre-partitioned skewed bucket:
+// the inbox holds only the drained messages) and holds bl_given messages.
 template <bool kLds, bool kWide, uint32_t KM, bool kGather, bool kOwner>
 __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t lo,
-                                              uint32_t cnt, uint32_t a0, uint32_t na, uint32_t w, uint32_t ndead0) {
+                                              uint32_t cnt, uint32_t a0, uint32_t na, uint32_t w, uint32_t ndead0,
+                                              uint32_t bl_given = 0xFFFFFFFFu) {
   const DevParams& P = a.P;
   const int tid = threadIdx.x;
   const uint32_t T = P.T, C = P.C;
@@ -928,7 +934,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       a.g.blc[w][b] = bltot;
     } else {
       a.chunk_off[b] = lo;
-      a.chunk_cnt[b] = bltot;
+      a.chunk_cnt[b] = bl_given != 0xFFFFFFFFu ? bl_given : bltot;
     }
   }
   if (bltot) {
@@ -980,7 +986,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   // FORWARD_RR (C5) single pass: each actor's out-edge row and the destination of its next
   // round-robin edge are fetched here for all four actors at once, instead of two dependent
   // loads (row_ptr, then col) per message inside the serial drain (fdeg = kNoHint: no hint).
-  constexpr bool kFwd = kLds && !kWide && KM == kb(AGX_KIND_FORWARD_RR);
+  constexpr bool kFwd = !kWide && KM == kb(AGX_KIND_FORWARD_RR);
   constexpr bool kUnrollActors = KM == kb(AGX_KIND_RING);  // single pass: see sp_actor below
   constexpr uint32_t kNoHint = 0xFFFFFFFFu;
   uint64_t frb[kBAct];
@@ -1021,9 +1027,13 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   }
   uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0, emtot = 0;
   const uint64_t embase = (uint64_t)lo * a.kmax;  // this bucket's slice of the tell arena
-  if (kLds && !kWide && a.kmax == 1) {
-    // ---- single pass (each message emits <= 1 tell): drain + apply; tells are staged in LDS over the
-    // actor's own, already consumed, inbox slots (tell e of an actor <= message index q that made it)
+  if (!kWide && a.kmax == 1) {
+    // ---- single pass (each message emits <= 1 tell): drain + apply; tells are staged over the
+    // actor's own, already consumed, inbox slots (tell e of an actor <= message index q that made it):
+    // in LDS (fast path) or in the bucket's scratch copy (skew launch)
+    uint32_t* const stk = kLds ? L.key : a.scr.key + lo;
+    uint32_t* const sts = kLds ? L.src : a.scr.src + lo;
+    uint32_t* const stp = kLds ? L.pay : a.scr.pay + lo;
     uint32_t ecl[kBAct];
     auto sp_actor = [&](int j) {
       const uint32_t la = j * kBThreads + tid;
@@ -1032,7 +1042,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       if (la >= na || !len || !L.alive[la]) return;
       const uint32_t l = a0 + la;
       const uint32_t self = P.R > 1 ? P.gid[l] : l;
-      EmitterLds em{&P, L.key, L.src, L.pay, s0, self, 0, 0, L.nh, a.nx_shift, nhmask};
+      EmitterLds em{&P, stk, sts, stp, s0, self, 0, 0, L.nh, a.nx_shift, nhmask};
       uint64_t wv[2] = {w0s[la], w1s[la]};
       const uint32_t nd = min(len, T);
       uint32_t kcur = L.kind[la];  // (a compiled behaviour's become changes it)
@@ -1046,7 +1056,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         hdst = j == 0 ? fdst[0] : j == 1 ? fdst[1] : j == 2 ? fdst[2] : fdst[3];
       }
       for (uint32_t q = 0; q < nd; ++q) {
-        const uint32_t sv = L.src[s0 + q], pv = L.pay[s0 + q];
+        const uint32_t sv = sts[s0 + q], pv = stp[s0 + q];
         uint32_t r;
         if (kFwd && hdeg != kNoHint && wv[1] <= 0xFFFFFFFFull) {
           // apply_msg's FORWARD_RR with the prefetched row (same cursor arithmetic)
@@ -1106,7 +1116,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     }
     __syncthreads();
     AGX_STAMP(a, 6);
-    if constexpr (kGather || kOwner) {
+    if constexpr ((kGather || kOwner) && kLds) {
       // compact the staged tells in sender order into U (free: state was written back), then
       // group them by destination straight into this superstep's tell arena
       uint32_t* ukey = reinterpret_cast<uint32_t*>(L.U);
@@ -1133,9 +1143,9 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         const uint32_t la = j * kBThreads + tid;
         const uint32_t s0 = L.seg[la], o = L.ecnt[la];
         for (uint32_t e = 0; e < ecl[j]; ++e) {
-          a.em.key[embase + o + e] = L.key[s0 + e];
-          a.em.src[embase + o + e] = L.src[s0 + e];
-          a.em.pay[embase + o + e] = L.pay[s0 + e];
+          a.em.key[embase + o + e] = stk[s0 + e];
+          a.em.src[embase + o + e] = sts[s0 + e];
+          a.em.pay[embase + o + e] = stp[s0 + e];
         }
       };
       if constexpr (kUnrollActors) {
@@ -1143,6 +1153,10 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       } else {
 #pragma unroll 1
         for (int j = 0; j < kBAct; ++j) compact(j);
+      }
+      if constexpr (kGather || kOwner) {  // (skew launch) grouped by destination from the em arena
+        __syncthreads();
+        group_tells<false>(a, L, b, w, embase, emtot, a.em);
       }
     }
   } else {
@@ -1610,6 +1624,323 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uin
 // kOwner (multi-rank): tells leave grouped by owner rank into g.eg[0] + g.tcnt/toff[0]
 // (digit = key >> kOwnerShift) instead of the chunk arena + next-pass histogram.
 // (One launch with both paths spills ~20 VGPRs and measured 13% slower at 1M.)
+// =========================================================================
+// Skewed buckets across workgroups (single-rank multi-pass, plain and compiled behaviours).
+// A bucket whose inbox exceeds one LDS tile -- R-MAT / Zipf hot buckets of C5 / C3 hold 10^4 -
+// 10^5 arrivals plus their backlog -- is cut into parts of `span` inbox positions, one
+// workgroup each, in three launches before the skew launch:
+//   k_skew_plan     bucket bounds of every skewed bucket, parts per bucket (one block)
+//   k_skew_count    per part: arrivals per actor                     -> pc[part][actor]
+//   k_skew_scan     per bucket: exclusive prefix of pc over parts (in place), length, admission
+//                   keep = alive ? min(len, C) : 0 (tail-drop, AD/Mailbox.scala:551-565), drained
+//                   = min(keep, T) (:261), queued = keep - drained, and their segment starts
+//   k_skew_scatter  per part: stable rank of each arrival among its actor's arrivals (the part's
+//                   prefix + in-part wave ranks; a part of the previous backlog, which is already
+//                   grouped by actor in actor order, takes the rank from its run start -- a
+//                   streaming copy); admitted drained messages go to the scratch copy
+//                   at lo + dseg[actor] + rank, queued ones straight to the backlog arena at
+//                   lo + blp[actor] + rank - T (the canonical order of bucket_finish's copy)
+// The skew launch then drains each bucket from the scratch copy (<= T messages per actor), so no
+// workgroup walks a hot bucket's whole inbox alone (Mailbox.run semantics unchanged).
+// =========================================================================
+constexpr uint32_t kSkRec = 12;    // b, lo, cnt, blc, blo, bst, pbase, np, ndrain, bltot, npb, -
+constexpr uint32_t kSkSpan = 4 * kBucket;  // minimum inbox positions per part
+
+struct SkewArgs {
+  uint32_t* rec;      // [nb][kSkRec]
+  uint32_t* act;      // [nb][3][kBucket]: keep, dseg, blp
+  uint32_t* pc;       // [max_parts][kBucket] arrivals per actor -> prefix over the bucket's parts
+  uint32_t* meta;     // [0] parts, [1] span
+  uint32_t budget;    // target number of parts (the span grows beyond kSkSpan to stay near it)
+  uint32_t max_parts; // rows of pc: budget + nb (a bucket adds at most one part beyond the budget)
+};
+
+__device__ __forceinline__ uint32_t sk_key(const BucketArgs& a, const uint32_t* r, uint32_t rpar, uint32_t q) {
+  return q < r[3] ? a.g.bl[rpar].key[r[4] + q] : a.in.key[r[5] + q - r[3]];
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_skew_plan(BucketArgs a, SkewArgs k) {
+  __shared__ uint32_t scratch[kScanThreads / kWave + 1];
+  __shared__ unsigned long long s_tot;
+  const uint32_t n = *a.skew_n, tid = threadIdx.x;
+  if (tid == 0) s_tot = 0;
+  __syncthreads();
+  unsigned long long part = 0;
+  for (uint32_t i = tid; i < n; i += kScanThreads) {
+    const uint32_t b = a.skew_list[i];
+    const uint32_t bs = a.bstart[b], be = a.bstart[b + 1], bp = a.blpre[b] + a.bl_sbase[b / kBlSlice];
+    const uint32_t blc = a.chunk_cnt[b], blo = a.chunk_off[b];
+    uint32_t* r = k.rec + (size_t)i * kSkRec;
+    r[0] = b;
+    r[1] = bs + bp;
+    r[2] = blc + (be - bs);
+    r[3] = blc;
+    r[4] = blo;
+    r[5] = bs;
+    part += blc + (be - bs);
+  }
+  atomicAdd(&s_tot, part);
+  __syncthreads();
+  // parts of at least kSkSpan positions, sum over buckets of ceil(cnt / span) <= budget + n
+  const unsigned long long tot = s_tot;
+  const uint32_t bud = k.budget;
+  uint32_t span = kSkSpan;
+  if (tot > (unsigned long long)span * bud)
+    span = (uint32_t)(((tot + bud - 1) / bud + kBucket - 1) / kBucket * kBucket);
+  uint32_t carry = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += kScanThreads) {
+    const uint32_t i = i0 + tid;
+    uint32_t np = 0, npb = 0;
+    if (i < n) {  // backlog parts, then parts of the new mail (a part never mixes the two)
+      const uint32_t c = k.rec[(size_t)i * kSkRec + 2], blc = k.rec[(size_t)i * kSkRec + 3];
+      npb = (blc + span - 1) / span;
+      np = npb + (c - blc + span - 1) / span;
+    }
+    uint32_t t;
+    const uint32_t ex = block_excl_sum<kScanThreads>(np, scratch, &t);
+    if (i < n) {
+      k.rec[(size_t)i * kSkRec + 6] = carry + ex;
+      k.rec[(size_t)i * kSkRec + 7] = np;
+      k.rec[(size_t)i * kSkRec + 10] = npb;
+    }
+    carry += t;
+  }
+  if (tid == 0) {
+    k.meta[0] = carry;
+    k.meta[1] = span;
+  }
+}
+
+// part t -> (skew index, first inbox position, end) (binary search over the part bases)
+__device__ __forceinline__ bool sk_part(const BucketArgs& a, const SkewArgs& k, uint32_t t, uint32_t* s_q) {
+  if (threadIdx.x == 0) {
+    uint32_t lo = 0, hi = *a.skew_n;  // last i with pbase[i] <= t
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (k.rec[(size_t)mid * kSkRec + 6] <= t) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t* r = k.rec + (size_t)lo * kSkRec;
+    const uint32_t span = k.meta[1], p = t - r[6], npb = r[10], blc = r[3];
+    s_q[0] = lo;
+    if (p < npb) {
+      s_q[1] = p * span;
+      s_q[2] = min(blc, (p + 1) * span);
+    } else {
+      s_q[1] = blc + (p - npb) * span;
+      s_q[2] = min(r[2], blc + (p - npb + 1) * span);
+    }
+  }
+  __syncthreads();
+  return true;
+}
+
+__global__ void __launch_bounds__(kBThreads) k_skew_count(BucketArgs a, SkewArgs k) {
+  __shared__ uint32_t s_c[kBucket];
+  __shared__ uint32_t s_q[3];
+  const uint32_t tid = threadIdx.x, nparts = k.meta[0], rpar = (*a.pstep & 1u) ^ 1u, amask = (1u << a.bb) - 1u;
+  if (nparts > k.max_parts) {  // (plan and buffer disagree: never launched so; report, do nothing)
+    if (blockIdx.x == 0 && tid == 0) atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
+    return;
+  }
+  for (uint32_t t = blockIdx.x; t < nparts; t += gridDim.x) {
+    for (uint32_t i = tid; i < kBucket; i += kBThreads) s_c[i] = 0;
+    sk_part(a, k, t, s_q);
+    const uint32_t* r = k.rec + (size_t)s_q[0] * kSkRec;
+    const uint32_t q0 = s_q[1], q1 = s_q[2];
+    for (uint32_t q = q0 + tid; q < q1; q += 8 * kBThreads) {  // 8 loads in flight
+      uint32_t kk[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kk[j] = q + j * kBThreads < q1 ? sk_key(a, r, rpar, q + j * kBThreads) : 0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (q + j * kBThreads < q1) lds_hist_inc(s_c, kk[j] & amask);
+    }
+    __syncthreads();
+    uint32_t* pc = k.pc + (size_t)t * kBucket;
+    for (uint32_t i = tid; i < kBucket; i += kBThreads) pc[i] = s_c[i];  // (all rows: zero past the bucket)
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, SkewArgs k) {
+  __shared__ uint32_t scratch[2 * (kBWaves + 1)];
+  const DevParams& P = a.P;
+  const uint32_t tid = threadIdx.x, n = *a.skew_n, T = P.T, C = P.C;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    uint32_t* r = k.rec + (size_t)i * kSkRec;
+    const uint32_t b = r[0], pb = r[6], np = r[7];
+    const uint32_t a0 = b << a.bb, na = min(1u << a.bb, P.n_local - a0);
+    uint32_t len[kBAct] = {0, 0, 0, 0};
+    const uint32_t la0 = tid * kBAct;
+    for (uint32_t p = 0; p < np; ++p) {  // per actor: exclusive prefix over the parts, in place
+      uint4* row = reinterpret_cast<uint4*>(k.pc + (size_t)(pb + p) * kBucket) + tid;
+      const uint4 v = *row;
+      *row = make_uint4(len[0], len[1], len[2], len[3]);
+      len[0] += v.x; len[1] += v.y; len[2] += v.z; len[3] += v.w;
+    }
+    uint32_t keep[kBAct], dr[kBAct], qd[kBAct], sd = 0, sq = 0, ndead = 0;
+#pragma unroll
+    for (int j = 0; j < kBAct; ++j) {
+      const uint32_t la = la0 + j;
+      const bool alive = la < na && P.alive[a0 + la];
+      keep[j] = alive ? ((C == 0 || len[j] < C) ? len[j] : C) : 0u;
+      ndead += len[j] - keep[j];
+      dr[j] = min(keep[j], T);
+      qd[j] = keep[j] - dr[j];
+      sd += dr[j];
+      sq += qd[j];
+    }
+    uint32_t td, tq;
+    const uint2 ex = block_excl_sum2<kBThreads>(sd, sq, scratch, &td, &tq);
+    uint32_t* act = k.act + (size_t)i * 3 * kBucket;
+    uint32_t ds[kBAct], bs[kBAct], ed = ex.x, eq = ex.y;
+#pragma unroll
+    for (int j = 0; j < kBAct; ++j) {
+      ds[j] = ed;
+      bs[j] = eq;
+      ed += dr[j];
+      eq += qd[j];
+    }
+    reinterpret_cast<uint4*>(act)[tid] = make_uint4(keep[0], keep[1], keep[2], keep[3]);
+    reinterpret_cast<uint4*>(act + kBucket)[tid] = make_uint4(ds[0], ds[1], ds[2], ds[3]);
+    reinterpret_cast<uint4*>(act + 2 * kBucket)[tid] = make_uint4(bs[0], bs[1], bs[2], bs[3]);
+    if (tid == 0) {
+      r[8] = td;
+      r[9] = tq;
+    }
+    const uint32_t wd = wave_incl_sum(ndead);  // admission drops: dead letters (block stats slot)
+    if (lane_id() == kWave - 1 && wd) atomicAdd(&a.bstats[(size_t)blockIdx.x * kBStats + 1], (unsigned long long)wd);
+  }
+}
+
+__global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a, SkewArgs k) {
+  __shared__ __attribute__((aligned(16))) uint16_t whist[kBWaves * kBucket];  // 32 KB
+  __shared__ uint32_t s_run[kBucket], s_keep[kBucket], s_ds[kBucket], s_bs[kBucket], s_tmp[kBucket];
+  uint32_t* const s_first = s_tmp;  // backlog parts: first position of each actor's run in the part
+  __shared__ uint32_t s_q[3];
+  const DevParams& P = a.P;
+  const uint32_t tid = threadIdx.x, w = tid / kWave, lane = lane_id(), nparts = k.meta[0];
+  const uint32_t wpar = *a.pstep & 1u, rpar = wpar ^ 1u, amask = (1u << a.bb) - 1u, T = P.T;
+  const uint64_t ltm = lanemask_lt();
+  const Msgs blw = a.g.bl[wpar];
+  if (nparts > k.max_parts) return;
+  for (uint32_t t = blockIdx.x; t < nparts; t += gridDim.x) {
+    sk_part(a, k, t, s_q);
+    const uint32_t i = s_q[0], q0 = s_q[1], q1 = s_q[2];
+    const uint32_t* r = k.rec + (size_t)i * kSkRec;
+    const uint32_t lo = r[1], blc = r[3], blo = r[4], bst = r[5];
+    const uint32_t* act = k.act + (size_t)i * 3 * kBucket;
+    const uint32_t* pc = k.pc + (size_t)t * kBucket;
+    for (uint32_t la = tid; la < kBucket; la += kBThreads) {
+      s_run[la] = pc[la];
+      s_keep[la] = act[la];
+      s_ds[la] = act[kBucket + la];
+      s_bs[la] = act[2 * kBucket + la];
+    }
+    __syncthreads();
+    if (q1 <= blc) {  // a part of the previous backlog: grouped by actor, every item admitted unless
+                      // its actor stopped; rank = earlier parts' count + distance to the run start
+      for (uint32_t sub = q0; sub < q1; sub += kBucket) {
+        const uint32_t wbase = sub + w * (kBIpt * kWave);
+        uint32_t kk[kBIpt];
+#pragma unroll
+        for (int u = 0; u < kBIpt; ++u) {
+          const uint32_t q = wbase + u * kWave + lane;
+          kk[u] = q < q1 ? a.g.bl[rpar].key[blo + q] : 0u;
+          const uint32_t kp = q < q1 && q > q0 ? a.g.bl[rpar].key[blo + q - 1] : ~0u;
+          if (q < q1 && (q == q0 || (kp & amask) != (kk[u] & amask))) s_first[kk[u] & amask] = q;
+        }
+        __syncthreads();  // (a run start written in a later sub-tile belongs to another actor)
+#pragma unroll
+        for (int u = 0; u < kBIpt; ++u) {
+          const uint32_t q = wbase + u * kWave + lane, la = kk[u] & amask;
+          if (q >= q1) continue;
+          const uint32_t rank = s_run[la] + (q - s_first[la]);
+          if (rank >= s_keep[la]) continue;
+          const uint32_t sv = a.g.bl[rpar].src[blo + q], pv = a.g.bl[rpar].pay[blo + q];
+          const uint32_t pos = rank < T ? lo + s_ds[la] + rank : lo + s_bs[la] + rank - T;
+          const Msgs& d = rank < T ? a.scr : blw;
+          d.key[pos] = kk[u];
+          d.src[pos] = sv;
+          d.pay[pos] = pv;
+        }
+      }
+      __syncthreads();
+      continue;
+    }
+    for (uint32_t sub = q0; sub < q1; sub += kBucket) {
+      const uint32_t wbase = sub + w * (kBIpt * kWave);
+      uint32_t kk[kBIpt], sv[kBIpt], pv[kBIpt], rk[kBIpt];
+      bool live[kBIpt];
+      int any = 0;
+#pragma unroll
+      for (int u = 0; u < kBIpt; ++u) {
+        const uint32_t q = wbase + u * kWave + lane;
+        kk[u] = q < q1 ? sk_key(a, r, rpar, q) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kBIpt; ++u) {
+        const uint32_t q = wbase + u * kWave + lane, la = kk[u] & amask;
+        live[u] = q < q1 && s_run[la] < s_keep[la];  // actor not yet full: rank it
+        any |= live[u];
+      }
+      if (!__syncthreads_or(any)) continue;  // every arrival of this sub-tile is a dead letter
+      for (uint32_t x = tid; x < kBWaves * kBucket / 2; x += kBThreads) reinterpret_cast<uint32_t*>(whist)[x] = 0;
+#pragma unroll
+      for (int u = 0; u < kBIpt; ++u) {
+        const uint32_t q = wbase + u * kWave + lane;
+        if (live[u]) {
+          if (q < blc) {
+            sv[u] = a.g.bl[rpar].src[blo + q];
+            pv[u] = a.g.bl[rpar].pay[blo + q];
+          } else {
+            sv[u] = a.in.src[bst + q - blc];
+            pv[u] = a.in.pay[bst + q - blc];
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kBIpt; ++u) rk[u] = wave_rank(live[u], kk[u] & amask, a.bb, whist + w * kBucket, ltm);
+      __syncthreads();
+      for (uint32_t la = tid; la < kBucket; la += kBThreads) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int x = 0; x < kBWaves; ++x) {
+          const uint32_t c2 = whist[x * kBucket + la];
+          whist[x * kBucket + la] = (uint16_t)run;
+          run += c2;
+        }
+        s_tmp[la] = run;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kBIpt; ++u) {
+        if (!live[u]) continue;
+        const uint32_t la = kk[u] & amask;
+        const uint32_t rank = s_run[la] + whist[w * kBucket + la] + rk[u];  // among this actor's arrivals
+        if (rank < s_keep[la]) {
+          if (rank < T) {  // drained this superstep: the skew launch's scratch copy
+            const uint32_t pos = lo + s_ds[la] + rank;
+            a.scr.key[pos] = kk[u];
+            a.scr.src[pos] = sv[u];
+            a.scr.pay[pos] = pv[u];
+          } else {         // queued beyond the throughput cap: the backlog, in canonical order
+            const uint32_t pos = lo + s_bs[la] + rank - T;
+            blw.key[pos] = kk[u];
+            blw.src[pos] = sv[u];
+            blw.pay[pos] = pv[u];
+          }
+        }
+      }
+      __syncthreads();
+      for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] += s_tmp[la];
+      __syncthreads();
+    }
+  }
+}
+
 template <bool kWide, uint32_t KM, bool kGather, bool kSkew, bool kOwner = false>
 __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   constexpr bool kDefer = !kSkew;  // large inboxes are appended to the skew list
@@ -1955,6 +2286,17 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         if (kBypass && q < xblc) return g.bl[rpar].key[xblo + q];
         return a.in.key[xbst + q - xblc];
       };
+      if constexpr (kBypass && !kWide) {
+        // pre-partitioned by k_skew_* (above): the drained messages are in the scratch copy at
+        // [lo, lo + ndrain) in actor order, the queued ones already in this superstep's backlog
+        const uint32_t* r = a.sk_rec + (size_t)it * kSkRec;
+        const uint32_t* act = a.sk_act + (size_t)it * 3 * kBucket;
+        for (uint32_t la = tid; la < kBucket; la += kBThreads) s_seg[la] = act[kBucket + la];
+        if (tid == 0) s_seg[kBucket] = r[8];
+        __syncthreads();
+        bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, r[8], a0, na, wpar, 0u, r[9]);
+        continue;
+      }
       uint32_t* s_run = s_key;   // LDS items are unused on this path
       uint32_t* s_tmp = s_src;
       uint32_t* s_keep = s_ecnt;  // (bucket_finish re-initialises ecnt)
