@@ -599,4 +599,149 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
   }
 }
 
+// ORSet-only populations with full-state gossip: one replica's whole drain run (nd messages in
+// order) applied element-batch-outer, so its 2 KB of dots are read and written once per run
+// instead of once per message (crdt_apply's per-message loop re-reads them for every merge and
+// snapshot: C4's tick + 2 gossips per replica read the state 3x).  Same results as nd calls of
+// crdt_apply<kb(ORSET)>: message q sees the state left by messages < q, per element.  The version
+// vector chain (merge: max with the row's; add: vvector(node) + 1) is recomputed in every batch
+// from the first one (the rows' vvectors are hot in the cache); messages are re-read from the
+// inbox (LDS or scratch).  Emissions and snapshot-row allocation happen once, in message order.
+// Returns the unhandled count.
+template <typename Emit, typename Src, typename Pay>
+__device__ __forceinline__ uint32_t orset_run(const DevParams& P, const CrdtHeap& H, uint32_t self, uint32_t l,
+                                              uint32_t s0, uint32_t nd, const Src& isrc, const Pay& ipay,
+                                              uint32_t& row_cursor, Emit& em) {
+  const size_t nl = P.n_local;
+  uint64_t* st = P.state + l;  // word w at st[w * nl]
+  const uint32_t node = self % AGX_CRDT_NODES;
+  constexpr uint32_t vw = AGX_ORSET_ELEMS * AGX_CRDT_NODES / 2;  // first vvector word
+  constexpr uint32_t kMerge = 1, kAdd = 2, kRemove = 3, kClear = 4, kSnap = 5;
+  const uint32_t f = P.n_global > 1 ? P.gossip_f : 0u;
+  auto code_of = [&](uint32_t sv, uint32_t pv) -> uint32_t {
+    if (is_wide(sv)) return (pv >> 30) == (uint32_t)(AGX_KIND_ORSET - AGX_KIND_GCOUNTER) && !(pv & AGX_DELTA_ROW_BIT) ? kMerge : 0u;
+    const uint32_t op = pv >> 24, arg = pv & 0xFFFFFFu;
+    if (op == AGX_OP_ADD) return arg < AGX_ORSET_ELEMS ? kAdd : 0u;
+    if (op == AGX_OP_REMOVE) return arg < AGX_ORSET_ELEMS ? kRemove : 0u;
+    if (op == AGX_OP_CLEAR) return kClear;
+    if (op == AGX_OP_GOSSIP) return kSnap;
+    return 0u;
+  };
+  // pass 1: protocol, emissions and snapshot rows, in message order
+  uint32_t nunh = 0, nmod = 0;
+  const uint32_t rc0 = row_cursor;
+  for (uint32_t q = 0; q < nd; ++q) {
+    const uint32_t sv = isrc(s0 + q), pv = ipay(s0 + q);
+    const uint32_t c = code_of(sv, pv);
+    if (c == 0) {
+      ++nunh;
+      continue;
+    }
+    if (c != kSnap) {
+      ++nmod;
+      continue;
+    }
+    const uint32_t arg = pv & 0xFFFFFFu;
+    if (f) {
+      const uint32_t tagged = ((uint32_t)(AGX_KIND_ORSET - AGX_KIND_GCOUNTER) << 30) | row_cursor++;
+      for (uint32_t j = 0; j < f; ++j) em.wide(crdt_peer(P.gossip_seed, self, arg, j, P.n_global), tagged);
+    }
+    if (arg > 0) em(self, AGX_OP(AGX_OP_GOSSIP, arg - 1u));
+  }
+  if (nmod == 0 && row_cursor == rc0) return nunh;  // no state read or write
+  uint32_t vv0[AGX_CRDT_NODES];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t x = st[(size_t)(vw + k) * nl];
+    vv0[2 * k] = (uint32_t)x;
+    vv0[2 * k + 1] = (uint32_t)(x >> 32);
+  }
+  uint32_t cur[AGX_CRDT_NODES];
+  constexpr uint32_t kE = 2;  // elements per batch: 8 state words, 2 x 32 B of each row
+  for (uint32_t e0 = 0; e0 < AGX_ORSET_ELEMS; e0 += kE) {
+    uint32_t d[kE][AGX_CRDT_NODES];  // this batch's dots (element, node)
+    uint32_t dirty = 0;              // bit 4u + k: state word k of element e0 + u changed
+#pragma unroll
+    for (uint32_t u = 0; u < kE; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t x = st[(size_t)(4 * (e0 + u) + k) * nl];
+        d[u][2 * k] = (uint32_t)x;
+        d[u][2 * k + 1] = (uint32_t)(x >> 32);
+      }
+#pragma unroll
+    for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) cur[n] = vv0[n];
+    uint32_t h = rc0;
+    const bool last = e0 + kE == AGX_ORSET_ELEMS;
+    for (uint32_t q = 0; q < nd; ++q) {
+      const uint32_t sv = isrc(s0 + q), pv = ipay(s0 + q);
+      const uint32_t c = code_of(sv, pv);
+      const uint32_t arg = pv & 0xFFFFFFu;
+      if (c == kMerge) {  // ORSet.merge: dots per (element, node) against both vvectors, then vvector max
+        const uint32_t* row = H.row(pv & kHandleMask);
+        const uint4 va = *reinterpret_cast<const uint4*>(row + 2 * vw);
+        const uint4 vb = *reinterpret_cast<const uint4*>(row + 2 * vw + 4);
+        const uint32_t rvv[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+        uint4 ra[kE], rb[kE];
+#pragma unroll
+        for (uint32_t u = 0; u < kE; ++u) {
+          ra[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u));
+          rb[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u) + 4);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kE; ++u) {
+          const uint32_t r[8] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w, rb[u].x, rb[u].y, rb[u].z, rb[u].w};
+#pragma unroll
+          for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
+            const uint32_t o = orset_merge_entry(d[u][n], r[n], cur[n], rvv[n]);
+            dirty |= (o != d[u][n] ? 1u : 0u) << (4 * u + n / 2);
+            d[u][n] = o;
+          }
+        }
+#pragma unroll
+        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) cur[n] = max(cur[n], rvv[n]);
+      } else if (c == kAdd || c == kRemove || c == kClear) {
+        uint32_t ver = 0;
+        if (c == kAdd) {  // vvector + node; birth dot (node -> new version)
+#pragma unroll
+          for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n)
+            if (n == node) ver = cur[n] = cur[n] + 1u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kE; ++u)
+          if (c == kClear || arg == e0 + u) {
+#pragma unroll
+            for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) d[u][n] = (c == kAdd && n == node) ? ver : 0u;
+            dirty |= 0xFu << (4 * u);
+          }
+      } else if (c == kSnap && f) {  // this batch of the snapshot row (and its vvector, once)
+        const uint32_t hr = h++;
+        if (hr < H.rows) {
+          uint32_t* row = H.wrow(hr);
+#pragma unroll
+          for (uint32_t u = 0; u < kE; ++u) {
+            *reinterpret_cast<uint4*>(row + 8 * (e0 + u)) = make_uint4(d[u][0], d[u][1], d[u][2], d[u][3]);
+            *reinterpret_cast<uint4*>(row + 8 * (e0 + u) + 4) = make_uint4(d[u][4], d[u][5], d[u][6], d[u][7]);
+          }
+          if (last) {
+            *reinterpret_cast<uint4*>(row + 2 * vw) = make_uint4(cur[0], cur[1], cur[2], cur[3]);
+            *reinterpret_cast<uint4*>(row + 2 * vw + 4) = make_uint4(cur[4], cur[5], cur[6], cur[7]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kE; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if ((dirty >> (4 * u + k)) & 1u) st[(size_t)(4 * (e0 + u) + k) * nl] = ((uint64_t)d[u][2 * k + 1] << 32) | d[u][2 * k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t o = ((uint64_t)cur[2 * k + 1] << 32) | cur[2 * k];
+    if (cur[2 * k] != vv0[2 * k] || cur[2 * k + 1] != vv0[2 * k + 1]) st[(size_t)(vw + k) * nl] = o;
+  }
+  return nunh;
+}
+
 }  // namespace agx

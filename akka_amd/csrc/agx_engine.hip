@@ -848,6 +848,10 @@ agx_status capture_steps(agx_engine* e, uint32_t steps, hipGraphExec_t* out) {
   hipError_t ie = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
   hipGraphDestroy(g);
   if (ie != hipSuccess) return set_err(AGX_EDEVICE, "hipGraphInstantiate: %s", hipGetErrorString(ie));
+  // upload now: a graph's first launch would otherwise pay the upload inside the budget that
+  // first replays it (the 8-superstep graphs are first used by longer runs than the warmup)
+  hipError_t ue = hipGraphUpload(*out, e->stream);
+  if (ue != hipSuccess) return set_err(AGX_EDEVICE, "hipGraphUpload: %s", hipGetErrorString(ue));
   return AGX_OK;
 }
 

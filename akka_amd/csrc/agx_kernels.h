@@ -1252,10 +1252,15 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       uint32_t kd = L.kind[la];
       ++nact;
       if (kWide && is_crdt(kd)) {
-        for (uint32_t q = 0; q < nd; ++q) {
-          const uint32_t r = crdt_apply<KM>(P, H, kd, self, l, isrc(s0 + q), ipay(s0 + q), row_cursor, em);
-          ++ndel;
-          if (r == AGX_RES_UNHANDLED) ++nunh;
+        if constexpr (KM == kb(AGX_KIND_ORSET)) {  // whole run element-batch-outer (agx_crdt.h)
+          nunh += orset_run(P, H, self, l, s0, nd, isrc, ipay, row_cursor, em);
+          ndel += nd;
+        } else {
+          for (uint32_t q = 0; q < nd; ++q) {
+            const uint32_t r = crdt_apply<KM>(P, H, kd, self, l, isrc(s0 + q), ipay(s0 + q), row_cursor, em);
+            ++ndel;
+            if (r == AGX_RES_UNHANDLED) ++nunh;
+          }
         }
       } else {
         bool stop = false;
