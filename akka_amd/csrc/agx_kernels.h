@@ -125,6 +125,20 @@ __device__ __forceinline__ uint32_t wave_rank(bool valid, uint32_t d, uint32_t b
   return old + before;
 }
 
+// a wave-uniform pointer forced into SGPRs
+template <typename T>
+__device__ __forceinline__ T* sgpr_ptr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+
+// load through a global (address space 1) pointer: global_load, not flat_load, once the
+// compiler has lost track of where a laundered pointer points
+__device__ __forceinline__ uint32_t ldg(const uint32_t* p, uint32_t i) {
+  return ((const __attribute__((address_space(1))) uint32_t*)p)[i];
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const uint32_t lane = lane_id();
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -1356,6 +1370,21 @@ struct GatherView {
     }
     return lo < nseg ? g.eg[r].key[sego[lo] + (q - segp[lo])] : g.stg.key[sto + (q - segp[nseg])];
   }
+  // where inbox item q lives: sel 0 = backlog (bl[r]), 1 = a tell segment (eg[r]), 2 = staged (stg);
+  // LDS reads only, so a caller can issue every item's global loads back to back
+  __device__ __forceinline__ uint32_t locate(uint32_t q, uint32_t& sel) const {
+    if (q < blc) {
+      sel = 0;
+      return blo + q;
+    }
+    uint32_t lo = 0, hi = nseg;  // last segment start <= q
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (segp[mid] <= q) lo = mid; else hi = mid - 1;
+    }
+    sel = lo < nseg ? 1u : 2u;
+    return lo < nseg ? sego[lo] + (q - segp[lo]) : sto + (q - segp[nseg]);
+  }
   __device__ __forceinline__ void load(const GatherArgs& g, uint32_t r, uint32_t q, uint32_t& k, uint32_t& sv,
                                        uint32_t& pv) const {
     if (q < blc) {
@@ -2177,24 +2206,62 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       // ---- fast path: the whole bucket in one LDS tile
       uint32_t k[kBIpt], sv[kBIpt], pv[kBIpt], rk[kBIpt];
       const uint32_t wbase = w * (kBIpt * kWave);
+      {  // locate every item first (LDS only), then issue all 3 x kBIpt loads back to back: selected
+         // base pointers and no branches around the loads (per-item if/else made the compiler wait
+         // for each item's loads before the next item's: 8 dependent round trips instead of 1)
+        uint32_t sel[kBIpt], idx[kBIpt];
 #pragma unroll
-      for (int r = 0; r < kBIpt; ++r) {
-        const uint32_t q = wbase + r * kWave + lane;
-        if (q < cnt) {
-          if (kGather) {
-            gv.load(g, rpar, q, k[r], sv[r], pv[r]);
-          } else if (kBypass && q < xblc) {
-            k[r] = g.bl[rpar].key[xblo + q];
-            sv[r] = g.bl[rpar].src[xblo + q];
-            pv[r] = g.bl[rpar].pay[xblo + q];
-          } else {
-            k[r] = a.in.key[xbst + q - xblc];
-            sv[r] = a.in.src[xbst + q - xblc];
-            pv[r] = a.in.pay[xbst + q - xblc];
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t q = wbase + r * kWave + lane;
+          sel[r] = 0;
+          idx[r] = 0;
+          if (q < cnt) {
+            if (kGather) {
+              idx[r] = gv.locate(q, sel[r]);
+            } else if (kBypass && q < xblc) {
+              idx[r] = xblo + q;
+            } else {
+              sel[r] = 1;
+              idx[r] = xbst + q - xblc;
+            }
           }
-        } else {
-          k[r] = 0xFFFFFFFFu;
         }
+        // base pointers in SGPRs (uniform), so a per-item select is a register move, not a load
+        // of the pointer from the kernel-argument block at a per-lane address
+        const uint32_t *Bk = nullptr, *Bs = nullptr, *Bp = nullptr, *Ek = nullptr, *Es = nullptr, *Ep = nullptr;
+        if (kGather || kBypass) {
+          Bk = sgpr_ptr(g.bl[rpar].key);
+          Bs = sgpr_ptr(g.bl[rpar].src);
+          Bp = sgpr_ptr(g.bl[rpar].pay);
+        }
+        if (kGather) {
+          Ek = sgpr_ptr(g.eg[rpar].key);
+          Es = sgpr_ptr(g.eg[rpar].src);
+          Ep = sgpr_ptr(g.eg[rpar].pay);
+        }
+#pragma unroll
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t *pk, *ps, *pp;
+          if (kGather) {
+            pk = sel[r] == 0 ? Bk : sel[r] == 1 ? Ek : g.stg.key;
+            ps = sel[r] == 0 ? Bs : sel[r] == 1 ? Es : g.stg.src;
+            pp = sel[r] == 0 ? Bp : sel[r] == 1 ? Ep : g.stg.pay;
+          } else if (kBypass) {
+            pk = sel[r] == 0 ? Bk : a.in.key;
+            ps = sel[r] == 0 ? Bs : a.in.src;
+            pp = sel[r] == 0 ? Bp : a.in.pay;
+          } else {
+            pk = a.in.key;
+            ps = a.in.src;
+            pp = a.in.pay;
+          }
+          k[r] = ldg(pk, idx[r]);
+          sv[r] = ldg(ps, idx[r]);
+          pv[r] = ldg(pp, idx[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < kBIpt; ++r)
+          if (wbase + r * kWave + lane >= cnt) k[r] = 0xFFFFFFFFu;
       }
       __syncthreads();  // (fused) the segment list in s_pay is read before the items overwrite it
       // in-order copy + sortedness check: local topologies (rings, stencils) arrive already in
