@@ -76,14 +76,17 @@ __device__ __forceinline__ uint32_t zipf_index(const uint32_t* cdf, const uint32
 // ------------------------------------------------------------------ scans
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-// inclusive wave64 sum scan
+// inclusive wave64 sum scan over the whole (fully active) wave, in DPP: row_shr 1/2/4/8 scans each
+// 16-lane row, row_bcast 15 / 31 carry the row totals into the rows above.  Six VALU ops with DPP
+// operands instead of six ds_bpermute round trips through the LDS crossbar (__shfl_up): every
+// block scan of the apply chain uses it.  (Lanes with no DPP source keep `old` = 0.)
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    uint32_t t = __shfl_up(v, d, kWave);
-    if (lane >= (uint32_t)d) v += t;
-  }
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
   return v;
 }
 __device__ __forceinline__ int wave_incl_max(int v) {
@@ -98,23 +101,25 @@ __device__ __forceinline__ int wave_incl_max(int v) {
 
 // Block exclusive sum over NT threads (NT multiple of 64, <= 1024).
 // `scratch` needs NT/64 + 1 u32.  Returns exclusive prefix; *total = block sum.
+// Two barriers: every thread sums the NT/64 wave totals itself (LDS broadcast reads) instead of
+// one thread scanning them between two barriers.
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* scratch, uint32_t* total) {
   constexpr int NW = NT / kWave;
   const int tid = threadIdx.x, w = tid / kWave, lane = tid % kWave;
-  uint32_t inc = wave_incl_sum(v);
+  const uint32_t inc = wave_incl_sum(v);
   if (lane == kWave - 1) scratch[w] = inc;
   __syncthreads();
-  if (tid == 0) {
-    uint32_t run = 0;
-    for (int i = 0; i < NW; ++i) { uint32_t t = scratch[i]; scratch[i] = run; run += t; }
-    scratch[NW] = run;
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t t = scratch[i];
+    pre += i < w ? t : 0u;
+    tot += t;
   }
-  __syncthreads();
-  uint32_t r = scratch[w] + inc - v;
-  *total = scratch[NW];
-  __syncthreads();
-  return r;
+  *total = tot;
+  __syncthreads();  // (scratch is reused by the caller's next scan)
+  return pre + inc - v;
 }
 
 // Two block exclusive sums at once (one set of barriers).  `scratch` needs 2 * (NT/64 + 1) u32.
@@ -129,18 +134,19 @@ __device__ __forceinline__ uint2 block_excl_sum2(uint32_t v0, uint32_t v1, uint3
     scratch[NW + 1 + w] = i1;
   }
   __syncthreads();
-  if (tid < 2) {
-    uint32_t* sc = scratch + tid * (NW + 1);
-    uint32_t run = 0;
-    for (int i = 0; i < NW; ++i) { uint32_t t = sc[i]; sc[i] = run; run += t; }
-    sc[NW] = run;
+  uint32_t p0 = 0, p1 = 0, s0 = 0, s1 = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t a = scratch[i], b = scratch[NW + 1 + i];
+    p0 += i < w ? a : 0u;
+    p1 += i < w ? b : 0u;
+    s0 += a;
+    s1 += b;
   }
+  *t0 = s0;
+  *t1 = s1;
   __syncthreads();
-  const uint2 r = make_uint2(scratch[w] + i0 - v0, scratch[NW + 1 + w] + i1 - v1);
-  *t0 = scratch[NW];
-  *t1 = scratch[2 * NW + 1];
-  __syncthreads();
-  return r;
+  return make_uint2(p0 + i0 - v0, p1 + i1 - v1);
 }
 
 // Block exclusive max over NT threads; identity -1.

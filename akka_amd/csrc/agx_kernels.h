@@ -1548,7 +1548,7 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uin
   }
   const uint64_t embase = (uint64_t)lo * a.kmax;
   const Msgs blw = a.g.bl[wpar];
-  const uint32_t qinc = wave_incl_sum(nq), bltot = __shfl(qinc, kWave - 1, kWave);
+  const uint32_t qinc = wave_incl_sum(nq), bltot = (uint32_t)__builtin_amdgcn_readlane((int)qinc, kWave - 1);
   uint32_t qoff = qinc - nq;
   uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0, emtot = 0;
 #pragma unroll
@@ -1598,7 +1598,7 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uin
       ncount += em.n_valid;
     }
     const uint32_t tinc = wave_incl_sum(ncount);
-    emtot = __shfl(tinc, kWave - 1, kWave);
+    emtot = (uint32_t)__builtin_amdgcn_readlane((int)tinc, kWave - 1);
     uint32_t toff = tinc - ncount;
 #pragma unroll
     for (uint32_t i = 0; i < kTinyIpl; ++i)
@@ -1623,7 +1623,7 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uin
       ncount += em.n_valid;
     }
     const uint32_t tinc = wave_incl_sum(ncount);
-    emtot = __shfl(tinc, kWave - 1, kWave);
+    emtot = (uint32_t)__builtin_amdgcn_readlane((int)tinc, kWave - 1);
     uint32_t toff = tinc - ncount;
 #pragma unroll
     for (uint32_t i = 0; i < kTinyIpl; ++i) {
@@ -2050,11 +2050,11 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
           lo_w = bs + bp;
           hi_w = lo_w + blc + (be - bs);
         }
-        bs = __shfl(bs, 0, kWave);
-        lo_w = __shfl(lo_w, 0, kWave);
-        hi_w = __shfl(hi_w, 0, kWave);
-        blc = __shfl(blc, 0, kWave);
-        blo = __shfl(blo, 0, kWave);
+        bs = (uint32_t)__builtin_amdgcn_readlane((int)bs, 0);
+        lo_w = (uint32_t)__builtin_amdgcn_readlane((int)lo_w, 0);
+        hi_w = (uint32_t)__builtin_amdgcn_readlane((int)hi_w, 0);
+        blc = (uint32_t)__builtin_amdgcn_readlane((int)blc, 0);
+        blo = (uint32_t)__builtin_amdgcn_readlane((int)blo, 0);
         tiny = hi_w - lo_w <= a.tiny_max && (uint64_t)hi_w <= a.cap;  // (over capacity: the block path reports it)
         if (tiny)
           tiny_bucket<KM>(a, reinterpret_cast<TinyLds*>(U)[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
