@@ -182,7 +182,9 @@ struct agx_engine {
   uint32_t tstride = 4, region = 0;
   uint64_t acap = 0;  // arena capacity (fused: regions + overflow area)
   uint32_t apply_grid = kMaxApplyGrid;  // AGX_APPLY_GRID test knob: fewer blocks, each looping over buckets
-  uint32_t skew_grid = kMaxApplyGrid;   // AGX_SKEW_GRID diagnostic knob: blocks of the skew-list launch
+  // blocks of the skew-list launch (grid-stride over the list; AGX_SKEW_GRID diagnostic knob): one
+  // round of workgroups (2 per CU) -- an empty list at 10^8 actors cost 18 us with 4096 blocks
+  uint32_t skew_grid = 512;
   std::vector<uint32_t> hd_key, hd_src, hd_pay;  // staged tells on the device, not yet consumed (fused)
   bool stg_pending = false;
 
@@ -1307,7 +1309,10 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
                  ? AGX_OK
                  : set_err(AGX_EDEVICE, "hipStreamCreate failed"));
   CREATE_TRY(dalloc(&e->d_kind, nl));
-  CREATE_TRY(dalloc(&e->d_alive, nl));
+  // (padded to whole buckets: the apply loads every bucket's flags as u32 words, masked past n_local)
+  const uint64_t alive_sz = ((uint64_t)e->nb << e->bb) + kBucket + 64;
+  CREATE_TRY(dalloc(&e->d_alive, alive_sz));
+  CREATE_TRY(hipMemset(e->d_alive, 0, alive_sz) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_stopq, nl));
   CREATE_TRY(dalloc(&e->d_nstop, 4));
   CREATE_TRY(hipMemset(e->d_nstop, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));

@@ -139,6 +139,14 @@ __device__ __forceinline__ uint32_t ldg(const uint32_t* p, uint32_t i) {
   return ((const __attribute__((address_space(1))) uint32_t*)p)[i];
 }
 
+// state words 0/1 (index < 2^29: n_local < 2^28) through a 32-bit byte offset from an SGPR base
+__device__ __forceinline__ uint64_t ldg64(const uint64_t* base, uint32_t i) {
+  return *(const __attribute__((address_space(1))) uint64_t*)((const __attribute__((address_space(1))) char*)base + (i << 3));
+}
+__device__ __forceinline__ void stg64(uint64_t* base, uint32_t i, uint64_t v) {
+  *(__attribute__((address_space(1))) uint64_t*)((__attribute__((address_space(1))) char*)base + (i << 3)) = v;
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const uint32_t lane = lane_id();
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -1014,8 +1022,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       const bool has = la < na && L.alive[la] && L.seg[la + 1] != L.seg[la];
       const uint32_t l = a0 + la;
       kd[j] = has && (kWide || (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0) ? P.kind[l] : 0u;  // single-kind variants never read it
-      x0[j] = has ? P.state[l] : 0ull;
-      x1[j] = has && P.W > 1 ? P.state[(size_t)P.n_local + l] : 0ull;
+      x0[j] = has ? ldg64(P.state, l) : 0ull;  // (32-bit offsets: one VGPR per address)
+      x1[j] = has && P.W > 1 ? ldg64(P.state, P.n_local + l) : 0ull;
       if constexpr (kFwd) {
         frb[j] = has ? P.row_ptr[l] : 0ull;
         fre[j] = has ? P.row_ptr[l + 1] : ~0ull;  // (no mail: deg out of range -> no hint)
@@ -1094,8 +1102,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           break;
         }
       }
-      P.state[l] = wv[0];
-      if (P.W > 1) P.state[(size_t)P.n_local + l] = wv[1];
+      stg64(P.state, l, wv[0]);
+      if (P.W > 1) stg64(P.state, P.n_local + l, wv[1]);
       if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
         if (kcur != L.kind[la]) P.kind[l] = (uint8_t)kcur;
       nall += em.n_all;
@@ -1305,8 +1313,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
             }
           }
         }
-        P.state[l] = wv[0];
-        if (P.W > 1) P.state[(size_t)P.n_local + l] = wv[1];
+        stg64(P.state, l, wv[0]);
+        if (P.W > 1) stg64(P.state, P.n_local + l, wv[1]);
         if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
           if (kd != L.kind[la]) P.kind[l] = (uint8_t)kd;
       }
@@ -2078,9 +2086,9 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
     uint32_t alive4 = 0;        // alive flags of actors 4*tid..4*tid+3, loaded first (a0 is a multiple of 32)
     {
       const uint32_t la0 = tid * 4;
-      if (la0 + 4 <= na) alive4 = *reinterpret_cast<const uint32_t*>(P.alive + a0 + la0);
-      else
-        for (uint32_t j = 0; j < 4; ++j) alive4 |= (la0 + j < na ? (uint32_t)P.alive[a0 + la0 + j] : 0u) << (8 * j);
+      // one u32 load, no branch (the flags array is padded to whole buckets); bytes past na masked
+      alive4 = *reinterpret_cast<const uint32_t*>(P.alive + a0 + la0);
+      if (la0 + 4 > na) alive4 &= la0 >= na ? 0u : 0xFFFFFFFFu >> (8 * (4 - (na - la0)));
     }
     if (!kGather) {
       if (tid == 0) {
