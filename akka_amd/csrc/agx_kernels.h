@@ -982,7 +982,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           const uint32_t lane = lane_id(), leader = (uint32_t)__builtin_ctzll(m);
           uint32_t base = 0;
           if (lane == leader) base = alloc_rows((uint32_t)__popcll(m));
-          base = __shfl(base, (int)leader, kWave);
+          base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
           if (need) {
             const uint32_t h = base + (uint32_t)__popcll(m & lanemask_lt());
             if (h < H.rows) copy_row(H.wrow(h), H.row(pv & kHandleMask), H.pw);
@@ -1485,27 +1485,23 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uin
   const uint32_t Tt = P.T, C = P.C;
   // ---- items, and their stable rank by (actor, inbox position) over the whole inbox
   uint32_t k[kTinyIpl], sv[kTinyIpl], pv[kTinyIpl], la[kTinyIpl];
+  {  // all loads back to back (selected SGPR bases, no branch around the loads)
+    const uint32_t *Bk = sgpr_ptr(a.g.bl[rpar].key), *Bs = sgpr_ptr(a.g.bl[rpar].src), *Bp = sgpr_ptr(a.g.bl[rpar].pay);
 #pragma unroll
-  for (uint32_t r = 0; r < kTinyIpl; ++r) {
-    const uint32_t q = r * kWave + lane;
-    la[r] = 0xFFFFFFFFu;
-    k[r] = sv[r] = pv[r] = 0u;
-    if (q < cnt) {
-      if (q < xblc) {
-        k[r] = a.g.bl[rpar].key[xblo + q];
-        sv[r] = a.g.bl[rpar].src[xblo + q];
-        pv[r] = a.g.bl[rpar].pay[xblo + q];
-      } else {
-        k[r] = a.in.key[xbst + q - xblc];
-        sv[r] = a.in.src[xbst + q - xblc];
-        pv[r] = a.in.pay[xbst + q - xblc];
-      }
-      la[r] = k[r] & amask;
+    for (uint32_t r = 0; r < kTinyIpl; ++r) {
+      const uint32_t q = r * kWave + lane;
+      const bool bl = q < xblc, ok = q < cnt;
+      const uint32_t i = !ok ? 0u : bl ? xblo + q : xbst + q - xblc;
+      k[r] = ldg(bl || !ok ? Bk : a.in.key, i);
+      sv[r] = ldg(bl || !ok ? Bs : a.in.src, i);
+      pv[r] = ldg(bl || !ok ? Bp : a.in.pay, i);
     }
+#pragma unroll
+    for (uint32_t r = 0; r < kTinyIpl; ++r) la[r] = r * kWave + lane < cnt ? k[r] & amask : 0xFFFFFFFFu;
   }
   uint32_t rank[kTinyIpl] = {}, st[kTinyIpl] = {}, len[kTinyIpl] = {};
-  for (uint32_t j = 0; j < cnt; ++j) {  // (uniform loop)
-    const uint32_t lj = __shfl((j >> 6) ? la[1] : la[0], (int)(j & 63u), kWave);
+  for (uint32_t j = 0; j < cnt; ++j) {  // (uniform loop; v_readlane with a scalar lane, no LDS crossbar)
+    const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)((j >> 6) ? la[1] : la[0]), (int)(j & 63u));
 #pragma unroll
     for (uint32_t r = 0; r < kTinyIpl; ++r) {
       const bool lt = lj < la[r], eq = lj == la[r];
@@ -1542,8 +1538,8 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uin
   for (uint32_t i = 0; i < kTinyIpl; ++i) {  // (all loads in flight together)
     hal[i] = head[i] && P.alive[hl[i]];
     hkind[i] = head[i] ? P.kind[hl[i]] : 0u;
-    hw0[i] = head[i] ? P.state[hl[i]] : 0ull;
-    hw1[i] = head[i] && P.W > 1 ? P.state[(size_t)P.n_local + hl[i]] : 0ull;
+    hw0[i] = head[i] ? ldg64(P.state, hl[i]) : 0ull;
+    hw1[i] = head[i] && P.W > 1 ? ldg64(P.state, P.n_local + hl[i]) : 0ull;
   }
   uint32_t ndead = 0, nq = 0;
 #pragma unroll
