@@ -60,7 +60,7 @@ ABI_VERSION = 1
 
 # status codes (akka_gpu.h)
 STATUS = {0: "AGX_OK", 1: "AGX_EINVAL", 2: "AGX_ENOMEM", 3: "AGX_EDEVICE", 4: "AGX_ECOMM",
-          5: "AGX_ECAPACITY", 6: "AGX_ESTATE"}
+          5: "AGX_ECAPACITY", 6: "AGX_ESTATE", 7: "AGX_ERANGE"}
 
 
 class AgxError(RuntimeError):

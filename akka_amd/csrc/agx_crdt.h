@@ -522,6 +522,7 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       if (kind == AGX_KIND_ORSET || (op == AGX_OP_DECREMENT && kind != AGX_KIND_PNCOUNTER)) return AGX_RES_UNHANDLED;
       const uint32_t w = (op == AGX_OP_DECREMENT ? AGX_CRDT_NODES : 0u) + node;
       const uint64_t v = st[w * nl] + arg;
+      if (v < arg) atomicOr(P.err, 2ull);  // kErrRange: the reference's BigInt slot would not wrap
       st[w * nl] = v;
       if (dm) {  // delta = the counter of the new slot value; an update by 0 has none (placeholder)
         const uint32_t x = dl_record(P, s32, kind, self);

@@ -793,6 +793,8 @@ agx_status read_counters(agx_engine* e, uint64_t* s) {
 agx_status collect_stats(agx_engine* e, agx_stats* out, bool check) {
   uint64_t s[kStatBlk];
   AGX_TRY(read_counters(e, s));
+  if (check && (s[ST_ERROR] & kErrRange))
+    return set_err(AGX_ERANGE, "a GCounter/PNCounter slot exceeded 2^64 - 1 (u64 slots; the reference uses BigInt)");
   if (check && (s[ST_ERROR] & kErrCapacity))
     return set_err(AGX_ECAPACITY, "in-flight messages exceeded engine capacity (msg_capacity=%llu)",
                    (unsigned long long)e->cap);

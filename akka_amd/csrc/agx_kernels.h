@@ -44,6 +44,7 @@ constexpr int kScanThreads = 1024;
 // stats slots (u64) on device
 enum { ST_DELIVERED = 0, ST_DEAD = 1, ST_UNHANDLED = 2, ST_EMITTED = 3, ST_STEPS = 4, ST_ERROR = 5, ST_ACTIVE = 6, ST_N = 8 };
 constexpr uint64_t kErrCapacity = 1;
+constexpr uint64_t kErrRange = 2;  // a counter slot wrapped past 2^64 - 1 (AGX_ERANGE)
 // per-block counters of k_bucket_apply: delivered, dead, unhandled, emitted, active
 constexpr int kBStats = 5;
 constexpr uint32_t kMaxApplyGrid = 4096;

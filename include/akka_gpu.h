@@ -53,6 +53,8 @@ typedef int32_t agx_status;
 #define AGX_ECOMM 4     /* RCCL error                                       */
 #define AGX_ECAPACITY 5 /* in-flight messages exceed the engine's capacity  */
 #define AGX_ESTATE 6    /* call not valid in the engine's current state     */
+#define AGX_ERANGE 7    /* a GCounter / PNCounter slot passed 2^64 - 1: the reference's BigInt
+                           (DD/GCounter.scala:53) has no bound, the u64 slot wrapped */
 
 /* "no sender" (Actor.noSender / deadLetters as sender, AbstractDispatcher.scala:29-37) */
 #define AGX_NO_SENDER 0xFFFFFFFFu

@@ -116,3 +116,18 @@ def test_delta_orset_converges_100k(built):
     assert (data == data[:, :1]).all()
     env = ws[:, 260:272].view(np.uint32)
     assert (env[:, 8] == 4).all()
+
+
+@pytest.mark.parametrize("kind", [Kind.GCOUNTER, Kind.PNCOUNTER])
+def test_counter_slot_wrap_is_loud(built, kind):
+    """A counter slot past 2^64 - 1: the reference's BigInt (DD/GCounter.scala:53) never wraps, the
+    u64 slot would -- the engine reports AGX_ERANGE instead of a silently wrapped counter."""
+    n, W = 16, 8 if kind == Kind.GCOUNTER else 16
+    eng = GpuEngine(EngineConfig(n_actors=n, n_words=W, max_emit=1))
+    init = np.zeros((n, W), np.uint64)
+    init[3, 3] = np.uint64(0xFFFFFFFFFFFFFFF0)  # actor 3 = node 3: its own increment slot
+    eng.register_range(0, n, kind, init)
+    eng.tell([3], [Op.make(Op.INCREMENT, 32)])
+    with pytest.raises(Exception, match="AGX_ERANGE"):
+        eng.run()
+    eng.close()
