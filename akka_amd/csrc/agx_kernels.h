@@ -1017,19 +1017,56 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   {
     uint32_t kd[kBAct];
     uint64_t x0[kBAct], x1[kBAct], fre[kBAct];
+    constexpr bool kKindNeeded = kWide || (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0;
+    if constexpr (!kGather) {  // (multi-pass: the branchy form measured 6 % faster at 10^8 actors)
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        const uint32_t la = j * kBThreads + tid;
+        const bool has = la < na && L.alive[la] && L.seg[la + 1] != L.seg[la];
+        const uint32_t l = a0 + la;
+        kd[j] = has && kKindNeeded ? P.kind[l] : 0u;  // single-kind variants never read it
+        x0[j] = has ? ldg64(P.state, l) : 0ull;  // (32-bit offsets: one VGPR per address)
+        x1[j] = has && P.W > 1 ? ldg64(P.state, P.n_local + l) : 0ull;
+        if constexpr (kFwd) {
+          frb[j] = has ? P.row_ptr[l] : 0ull;
+          fre[j] = has ? P.row_ptr[l + 1] : ~0ull;  // (no mail: deg out of range -> no hint)
+        }
+      }
+    } else {
+    uint32_t hasm = 0, li[kBAct];  // actors with mail; their local ids (0 for the others)
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
       const uint32_t la = j * kBThreads + tid;
       const bool has = la < na && L.alive[la] && L.seg[la + 1] != L.seg[la];
-      const uint32_t l = a0 + la;
-      kd[j] = has && (kWide || (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0) ? P.kind[l] : 0u;  // single-kind variants never read it
-      x0[j] = has ? ldg64(P.state, l) : 0ull;  // (32-bit offsets: one VGPR per address)
-      x1[j] = has && P.W > 1 ? ldg64(P.state, P.n_local + l) : 0ull;
+      hasm |= has ? 1u << j : 0u;
+      li[j] = has ? a0 + la : 0u;
+    }
+    // fused: every load issued unconditionally, back to back (actors without mail read actor 0's
+    // words: one cached line, no traffic), then masked -- no branch around a load, no wait between
+    // them (fused RING spills 11 -> 2 VGPRs; 1M apply -3.6 %, same-box A/B)
+    const uint32_t w1off = P.W > 1 ? P.n_local : 0u;
+#pragma unroll
+    for (int j = 0; j < kBAct; ++j) {
+      kd[j] = kKindNeeded ? P.kind[li[j]] : 0u;  // single-kind variants never read it
+      x0[j] = ldg64(P.state, li[j]);  // (32-bit offsets: one VGPR per address)
+      x1[j] = ldg64(P.state, w1off + li[j]);
       if constexpr (kFwd) {
-        frb[j] = has ? P.row_ptr[l] : 0ull;
-        fre[j] = has ? P.row_ptr[l + 1] : ~0ull;  // (no mail: deg out of range -> no hint)
+        frb[j] = P.row_ptr[li[j]];
+        fre[j] = P.row_ptr[li[j] + 1];
       }
     }
+#pragma unroll
+    for (int j = 0; j < kBAct; ++j) {
+      const bool has = (hasm >> j) & 1u;
+      kd[j] = has ? kd[j] : 0u;
+      x0[j] = has ? x0[j] : 0ull;
+      x1[j] = has && P.W > 1 ? x1[j] : 0ull;
+      if constexpr (kFwd) {
+        frb[j] = has ? frb[j] : 0ull;
+        fre[j] = has ? fre[j] : ~0ull;  // (no mail: deg out of range -> no hint)
+      }
+    }
+    }  // fused
     if constexpr (kFwd) {
 #pragma unroll
       for (int j = 0; j < kBAct; ++j) {
