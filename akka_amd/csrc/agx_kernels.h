@@ -900,12 +900,25 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
   if (tid == 0 && g.emc[w]) g.emc[w][b] = emtot;
 }
 
+// the block's counters -> its own slot of the per-block stats (summed by k_stats_reduce)
+__device__ __forceinline__ void flush_stats(const BucketArgs& a, const uint32_t (&acc)[kBStats]) {
+  uint32_t v[kBStats];
+#pragma unroll
+  for (int i = 0; i < kBStats; ++i) v[i] = wave_incl_sum(acc[i]);
+  if (lane_id() == kWave - 1) {
+    unsigned long long* bs = a.bstats + (size_t)blockIdx.x * kBStats;
+#pragma unroll
+    for (int i = 0; i < kBStats; ++i)
+      if (v[i]) atomicAdd(&bs[i], (unsigned long long)v[i]);
+  }
+}
+
 // bl_given != ~0: the backlog of this bucket was already written (pre-partitioned skewed bucket:
 // the inbox holds only the drained messages) and holds bl_given messages.
 template <bool kLds, bool kWide, uint32_t KM, bool kGather, bool kOwner>
 __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t lo,
                                               uint32_t cnt, uint32_t a0, uint32_t na, uint32_t w, uint32_t ndead0,
-                                              uint32_t bl_given = 0xFFFFFFFFu) {
+                                              uint32_t (&acc)[kBStats], uint32_t bl_given = 0xFFFFFFFFu) {
   const DevParams& P = a.P;
   const int tid = threadIdx.x;
   const uint32_t T = P.T, C = P.C;
@@ -1374,21 +1387,32 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   if (!kGather && !kOwner)
     for (uint32_t d = tid; d < (1u << a.nx_bits); d += kBThreads)
       if (L.nh[d]) atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + a.ng + b / a.G], L.nh[d]);
-  // block stats -> global
-  const uint32_t lane = lane_id();
-  uint32_t v0 = wave_incl_sum(ndel), v1 = wave_incl_sum(ndead), v2 = wave_incl_sum(nunh), v3 = wave_incl_sum(nall),
-           v4 = wave_incl_sum(nact);
-  if (lane == kWave - 1) {
-    atomicAdd(&L.stat[0], (unsigned long long)v0);
-    atomicAdd(&L.stat[1], (unsigned long long)v1);
-    atomicAdd(&L.stat[2], (unsigned long long)v2);
-    atomicAdd(&L.stat[3], (unsigned long long)v3);
-    atomicAdd(&L.stat[4], (unsigned long long)v4);
+  // block stats: per-thread sums over the block's buckets, flushed once at the end of the kernel
+  // (flush_stats): no reduction, LDS atomics or barrier per bucket
+  if constexpr (kOwner || (kGather && !kLds)) {
+    // multi-rank and fused skew variants: per bucket through LDS (a flush at the end of the kernel
+    // made these variants spill: 3 -> 14 VGPRs for the multi-rank RING apply)
+    const uint32_t lane = lane_id();
+    const uint32_t v0 = wave_incl_sum(ndel), v1 = wave_incl_sum(ndead), v2 = wave_incl_sum(nunh),
+                   v3 = wave_incl_sum(nall), v4 = wave_incl_sum(nact);
+    if (lane == kWave - 1) {
+      atomicAdd(&L.stat[0], (unsigned long long)v0);
+      atomicAdd(&L.stat[1], (unsigned long long)v1);
+      atomicAdd(&L.stat[2], (unsigned long long)v2);
+      atomicAdd(&L.stat[3], (unsigned long long)v3);
+      atomicAdd(&L.stat[4], (unsigned long long)v4);
+    }
+    __syncthreads();
+    if (tid < kBStats && L.stat[tid])  // this block's own slot (no contention; no load round trip)
+      atomicAdd(&a.bstats[(size_t)blockIdx.x * kBStats + tid], L.stat[tid]);
+  } else {
+    acc[0] += ndel;
+    acc[1] += ndead;
+    acc[2] += nunh;
+    acc[3] += nall;
+    acc[4] += nact;
   }
-  __syncthreads();
-  if (tid < kBStats && L.stat[tid])  // this block's own slot (no contention; no load round trip)
-    atomicAdd(&a.bstats[(size_t)blockIdx.x * kBStats + tid], L.stat[tid]);
-  __syncthreads();
+  __syncthreads();  // (L.nh and the other per-bucket LDS arrays are reset by the next bucket)
   AGX_STAMP(a, 8);
   if (a.dbg && tid == 0) {  // diagnostic: slowest bucket of this block (cycles, bucket, inbox size)
     const unsigned long long dur = a.dbg[blockIdx.x * 16 + 8] - a.dbg[blockIdx.x * 16 + 0];
@@ -2073,6 +2097,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   __shared__ uint32_t s_tiny[kBWaves];
   // (a group is kBWaves consecutive iterations of the block's grid-stride sequence, so the
   // bucket -> block assignment, and with it the load balance, is the block path's own)
+  uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};  // this thread's counters over the block's buckets
   const uint32_t nwork = kSkew ? *skew_n : a.nb;
   const uint32_t istride = kTiny ? kBWaves * gridDim.x : gridDim.x;
   for (uint32_t it = blockIdx.x; it < nwork; it += istride) {
@@ -2388,7 +2413,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         __syncthreads();
       }
       AGX_STAMP(a, 2);
-      bucket_finish<true, kWide, KM, kGather, kOwner>(a, L, b, lo, cnt, a0, na, wpar, 0u);
+      bucket_finish<true, kWide, KM, kGather, kOwner>(a, L, b, lo, cnt, a0, na, wpar, 0u, acc);
     } else {
       // ---- general path (skewed bucket, > kBucket messages): admission first, then a stable
       // counting sort of the ADMITTED messages only into the global scratch copy.  Per actor
@@ -2408,7 +2433,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
         for (uint32_t la = tid; la < kBucket; la += kBThreads) s_seg[la] = act[kBucket + la];
         if (tid == 0) s_seg[kBucket] = r[8];
         __syncthreads();
-        bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, r[8], a0, na, wpar, 0u, r[9]);
+        bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, r[8], a0, na, wpar, 0u, acc, r[9]);
         continue;
       }
       uint32_t* s_run = s_key;   // LDS items are unused on this path
@@ -2526,11 +2551,12 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
       }
       // the scratch copy holds the admitted messages in actor order; dead letters counted here
       __threadfence_block();
-      bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, cnt2, a0, na, wpar, ndead0);
+      bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, cnt2, a0, na, wpar, ndead0, acc);
     }
     }  // buckets of the group (one without kTiny)
     if constexpr (kTiny) __syncthreads();  // s_tiny and the waves' LDS are rewritten by the next group
   }
+  if (!kOwner && !(kGather && kSkew) && blockIdx.x < nwork) flush_stats(a, acc);  // (block-uniform)
 }
 
 // Bucket starts after a multi-pass sort: bstart[x] = first index with bucket >= x
