@@ -208,7 +208,13 @@ struct agx_engine {
   // defers a skewed bucket marks d_abort; the rest of the replay is void and run_single runs the
   // deferred skew launch, then continues with the full graphs (strict_ok cleared for this engine).
   uint32_t* d_abort = nullptr;  // [2] (BucketArgs::abort)
-  uint32_t* h_abort = nullptr;  // pinned [kLag][2]: the marks after each replay
+  uint32_t* h_abort = nullptr;  // pinned [kLag][2]: the marks after each replay (eager path)
+  // fused graphs end with k_replay_out, which writes the replay's inbox-size rows and abort marks
+  // straight into the pinned host ring (device-mapped) at ring slot (replay counter % kLag): no
+  // D2H copy between replays (those cost ~26 us per replay boundary, rocprofv3 kernel trace)
+  uint32_t* d_ring = nullptr;   // device pointer of h_cntb
+  uint32_t* d_rctr = nullptr;   // device replay counter (k_replay_out)
+  uint64_t replay_ctr = 0;      // host mirror: fused graph replays launched
   bool strict_ok = true;        // AGX_NO_STRICT=1 disables
   bool strict_env = true;       // (the AGX_NO_STRICT knob; strict_ok is re-armed after clean replays)
   uint32_t clean_steps = 0;     // fused supersteps since the last skewed bucket (full graphs)
@@ -843,6 +849,10 @@ agx_status capture_steps(agx_engine* e, uint32_t steps, hipGraphExec_t* out) {
     st = launch_step_single(e);
   }
   e->cur_slot = 0;
+  if (st == AGX_OK && e->fused)  // the replay's rows and abort marks -> host ring slot (no D2H copy)
+    hipLaunchKernelGGL(k_replay_out, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_cntb, steps * e->nb,
+                       e->strict_cap ? e->d_abort : nullptr, e->d_ring, e->d_rctr,
+                       agx_engine::kGraphSteps * e->nb + 2);
   hipError_t ce = hipStreamEndCapture(e->stream, &g);
   if (st) {
     if (g) hipGraphDestroy(g);
@@ -910,12 +920,13 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
   uint32_t rep_steps[kLag] = {0, 0, 0, 0};
   uint32_t rep_start[kLag] = {0, 0, 0, 0}, rep_par[kLag] = {0, 0, 0, 0};  // supersteps launched before it; parity
   bool rep_strict[kLag] = {false, false, false, false}, rep_void[kLag] = {false, false, false, false};
-  const size_t ring_row = (size_t)agx_engine::kGraphSteps * e->nb;
+  const size_t ring_row = (size_t)agx_engine::kGraphSteps * e->nb + 2;  // rows, then the 2 abort marks
+  uint32_t rep_ring[kLag] = {0, 0, 0, 0};  // host ring slot of each replay in flight
   const uint32_t left0 = left;
   uint32_t launched_steps = 0;
   bool recovered = false;
   auto fused_poll = [&](uint32_t slot) -> bool {
-    const uint32_t* h = e->h_cntb + slot * ring_row;
+    const uint32_t* h = e->h_cntb + rep_ring[slot] * ring_row;
     bool last_empty = rep_steps[slot] > 0;
     for (uint32_t i = 0; i < rep_steps[slot]; ++i) {
       uint64_t t = 0;
@@ -944,7 +955,7 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     e->skew_only = false;
     e->cur_slot = 0;
     AGX_TRY(s2);
-    HIP_TRY(hipMemcpyAsync(e->h_cntb + slot * ring_row + (size_t)k * e->nb, e->d_cntb + (size_t)k * e->nb,
+    HIP_TRY(hipMemcpyAsync(e->h_cntb + rep_ring[slot] * ring_row + (size_t)k * e->nb, e->d_cntb + (size_t)k * e->nb,
                            (size_t)e->nb * 4, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipMemsetAsync(e->d_abort, 0, 8, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -964,7 +975,7 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
       return false;
     }
     if (rep_strict[slot] && rep_steps[slot]) {
-      const uint32_t* ha = e->h_abort + 2 * slot;
+      const uint32_t* ha = e->h_cntb + rep_ring[slot] * ring_row + agx_engine::kGraphSteps * e->nb;
       const uint32_t ab = ha[0] ? ha[0] : ha[1];
       if (ab) {
         const agx_status s2 = recover(slot, ab - 1u);
@@ -1020,9 +1031,14 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
       rep_par[slot] = par0;
       rep_strict[slot] = strict;
       rep_void[slot] = false;
-      hipMemcpyAsync(e->h_cntb + slot * ring_row, e->d_cntb, (size_t)cnt * e->nb * 4, hipMemcpyDeviceToHost,
-                     e->stream);
-      if (strict) hipMemcpyAsync(e->h_abort + 2 * slot, e->d_abort, 8, hipMemcpyDeviceToHost, e->stream);
+      if (use_graph) {  // written by the graph's k_replay_out into ring slot (replay counter % kLag)
+        rep_ring[slot] = (uint32_t)(e->replay_ctr++ % kLag);
+      } else {          // eager superstep: copied (the ring slots are all free between run_single calls)
+        rep_ring[slot] = slot;
+        uint32_t* hr = e->h_cntb + slot * ring_row;
+        hipMemcpyAsync(hr, e->d_cntb, (size_t)cnt * e->nb * 4, hipMemcpyDeviceToHost, e->stream);
+        hr[agx_engine::kGraphSteps * e->nb] = hr[agx_engine::kGraphSteps * e->nb + 1] = 0u;
+      }
     } else {  // inbox total (sorted + backlog) of the replay's last superstep
       hipMemcpyAsync(&e->h_pin[slot], e->d_ninbox, 4, hipMemcpyDeviceToHost, e->stream);
     }
@@ -1374,13 +1390,17 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(dalloc(&e->d_stg_cnt, e->nb));
     CREATE_TRY(dalloc(&e->d_ovf, 2));
     CREATE_TRY(dalloc(&e->d_cntb, (uint64_t)agx_engine::kGraphSteps * e->nb));
-    CREATE_TRY(hipHostMalloc((void**)&e->h_cntb, 4ull * agx_engine::kGraphSteps * e->nb * 4, hipHostMallocDefault) ==
+    CREATE_TRY(hipHostMalloc((void**)&e->h_cntb, 4ull * (agx_engine::kGraphSteps * e->nb + 2) * 4, hipHostMallocDefault) ==
                        hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
     CREATE_TRY(dalloc(&e->d_parv, 2));
     const uint32_t parv[2] = {0u, 1u};
     CREATE_TRY(hipMemcpy(e->d_parv, parv, 8, hipMemcpyHostToDevice) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "upload"));
     CREATE_TRY(hipMemset(e->d_stg_cnt, 0, e->nb * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(hipMemset(e->d_ovf, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    CREATE_TRY(hipHostGetDevicePointer((void**)&e->d_ring, e->h_cntb, 0) == hipSuccess ? AGX_OK
+                   : set_err(AGX_EDEVICE, "hipHostGetDevicePointer"));
+    CREATE_TRY(dalloc(&e->d_rctr, 1));
+    CREATE_TRY(hipMemset(e->d_rctr, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(dalloc(&e->d_abort, 2));
     CREATE_TRY(hipMemset(e->d_abort, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(hipHostMalloc((void**)&e->h_abort, 4 * 2 * 4, hipHostMallocDefault) == hipSuccess
@@ -1442,7 +1462,7 @@ agx_status agx_destroy(agx_engine* e) {
   }
   hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_cntb);
   if (e->h_cntb) hipHostFree(e->h_cntb); hipFree(e->d_parv);
-  hipFree(e->d_abort);
+  hipFree(e->d_abort); hipFree(e->d_rctr);
   if (e->h_abort) hipHostFree(e->h_abort);
   hipFree(e->d_skew_list); hipFree(e->d_skew_n);
   hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);

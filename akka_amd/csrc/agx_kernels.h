@@ -2738,6 +2738,19 @@ __global__ void __launch_bounds__(kThreads) k_gen_rmat(const uint64_t* lrow, con
   }
 }
 
+// End of a fused superstep graph: the replay's per-superstep inbox sizes (and strict abort marks)
+// into ring slot (*ctr % 4) of the device-mapped pinned host ring -- one block, so the counter it
+// reads and bumps is never raced.  The host knows the slot of every replay (same counter).
+__global__ void __launch_bounds__(kScanThreads) k_replay_out(const uint32_t* cntb, uint32_t n, const uint32_t* abort,
+                                                            uint32_t* ring, uint32_t* ctr, uint32_t stride) {
+  const uint32_t c = *ctr;
+  uint32_t* dst = ring + (size_t)(c % 4u) * stride;
+  for (uint32_t i = threadIdx.x; i < n; i += kScanThreads) dst[i] = cntb[i];
+  if (threadIdx.x < 2) dst[stride - 2 + threadIdx.x] = abort ? abort[threadIdx.x] : 0u;
+  __syncthreads();
+  if (threadIdx.x == 0) *ctr = c + 1u;
+}
+
 __global__ void k_set_u32(uint32_t* p, uint32_t v) {
   if (threadIdx.x == 0) *p = v;
 }
