@@ -91,7 +91,7 @@ const char* kClassNames[K_NCLASS] = {"chunk_rowscan", "chunk_downsweep", "sort_u
                                      "sort_downsweep", "bucket_apply", "exchange", "mcompact", "bucket_apply_skew",
                                      "fused_tick", "bucket_bounds"};
 
-constexpr uint32_t kGraphSizes[4] = {1, 2, 4, 8};  // superstep replays (agx_engine::gx)
+constexpr uint32_t kGraphSizes[5] = {1, 2, 4, 8, 16};  // superstep replays (agx_engine::gx)
 constexpr uint32_t kRowAlign = 32;  // CRDT row pitch (u32) of rows wider than one 128-B line
 constexpr uint32_t kStatBlk = 16;                    // d_stats block (see agx_engine::d_stats)
 constexpr uint32_t kStatSred = ST_N, kStatInfl = ST_N + kBStats;
@@ -196,13 +196,14 @@ struct agx_engine {
   ncclComm_t comm = nullptr;
   bool started = false;
   // superstep graphs (single rank)
-  static constexpr uint32_t kGraphSteps = 8;  // largest replay (kGraphSizes = 1, 2, 4, 8); measured: 16-superstep
-                                             // replays with 4 in flight stall the stream (67 vs 24.7 us/superstep)
+  static constexpr uint32_t kGraphSteps = 16;  // largest replay (kGraphSizes = 1, 2, 4, 8, 16); a replay boundary costs
+                                              // ~18 us (graph launch + k_replay_out); with D2H copies per replay,
+                                              // 16-superstep replays had measured slower (67 vs 24.7 us/superstep)
   bool graphs_enabled = true;
   // gx[strict][parity][size]: replays of kGraphSizes[size] supersteps; fused graphs exist per
   // starting parity (the parity is a kernel argument), multi-pass ones use gx[0][0][*].  A budget
   // of K supersteps replays its binary decomposition (20 = 8 + 8 + 4), never a run of singles.
-  static constexpr uint32_t kNSizes = 4;
+  static constexpr uint32_t kNSizes = 5;
   hipGraphExec_t gx[2][2][kNSizes] = {};
   // fused "strict" replays: graphs without the (usually empty) skew-list launches.  A superstep that
   // defers a skewed bucket marks d_abort; the rest of the replay is void and run_single runs the
@@ -218,7 +219,7 @@ struct agx_engine {
   bool strict_ok = true;        // AGX_NO_STRICT=1 disables
   bool strict_env = true;       // (the AGX_NO_STRICT knob; strict_ok is re-armed after clean replays)
   uint32_t clean_steps = 0;     // fused supersteps since the last skewed bucket (full graphs)
-  uint32_t max_replay_si = 3;   // largest replay used: kGraphSizes[max_replay_si] (AGX_MAX_REPLAY knob)
+  uint32_t max_replay_si = 4;   // largest replay used: kGraphSizes[max_replay_si] (AGX_MAX_REPLAY knob)
   hipEvent_t lag_ev[4] = {};    // run_single's replay events (created once)
   bool strict_cap = false;      // the superstep being launched / captured is strict
   bool skew_only = false;       // recovery: the deferred skew launch alone
@@ -891,7 +892,7 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
   bool strict = e->fused && use_graph && e->strict_ok;  // replays without skew launches (see d_abort)
   const uint32_t max_si = e->max_replay_si;
   auto size_idx = [&](uint32_t l) -> uint32_t {
-    uint32_t si = l >= 8 ? 3u : l >= 4 ? 2u : l >= 2 ? 1u : 0u;
+    uint32_t si = l >= 16 ? 4u : l >= 8 ? 3u : l >= 4 ? 2u : l >= 2 ? 1u : 0u;
     return si < max_si ? si : max_si;
   };
   auto graph = [&](uint32_t si) -> hipGraphExec_t& {
@@ -1305,7 +1306,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   if (getenv("AGX_NO_STRICT")) e->strict_ok = e->strict_env = false;
   if (const char* s = getenv("AGX_MAX_REPLAY")) {  // diagnostic: cap the replay length (1, 2, 4, 8)
     const uint32_t m = (uint32_t)std::max(1, atoi(s));
-    e->max_replay_si = m >= 8 ? 3u : m >= 4 ? 2u : m >= 2 ? 1u : 0u;
+    e->max_replay_si = m >= 16 ? 4u : m >= 8 ? 3u : m >= 4 ? 2u : m >= 2 ? 1u : 0u;
   }
   if (const char* s = getenv("AGX_SKEW_GRID"))
     e->skew_grid = (uint32_t)std::min<int>(kMaxApplyGrid, std::max(1, atoi(s)));
