@@ -1443,6 +1443,10 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->h_row.assign(e->n_local + 1, 0);
   CREATE_TRY(dalloc(&e->d_row, e->n_local + 1));
   CREATE_TRY(hipMemset(e->d_row, 0, (e->n_local + 1) * 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  // the hipMemsets above run on the null stream, which a non-blocking engine stream does not wait
+  // for: without this, the first upload (prepare_run, on e->stream) could land before a memset of
+  // the same buffer (seen: alive flags zeroed after their upload -> every tell a dead letter)
+  CREATE_TRY(hipDeviceSynchronize() == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "hipDeviceSynchronize"));
 #undef CREATE_TRY
   *out = e;
   return AGX_OK;
