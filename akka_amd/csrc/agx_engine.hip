@@ -146,6 +146,7 @@ struct agx_engine {
   uint64_t gossip_seed = 0;
   uint32_t *d_heap = nullptr, *d_heap_top = nullptr, *d_step = nullptr;
   uint32_t *d_rx = nullptr, *d_s2rows = nullptr;  // multi-rank: received rows / rows packed for sending
+  uint32_t *d_s2p = nullptr, *d_rcvp = nullptr;    // multi-rank: tells as (key, src, payload) triples, sent / received
 
   DevMsgs A, B, scr, bl, em, stg, s2;
   uint64_t stg_cap = 0;
@@ -1069,26 +1070,31 @@ agx_status fix_rx(agx_engine* e, const Plan& p) {
 }
 
 agx_status exchange_rccl(agx_engine* e, Plan& p) {
+  // one contiguous (key, src, payload) run per peer: R sends instead of 3R (k_pack_aos / k_unpack_aos)
+  hipLaunchKernelGGL(k_pack_aos, dim3(grid_for(e->cap_emit / kThreads + 1, 2048)), dim3(kThreads), 0, e->stream,
+                     e->s2.c(), e->d_total, e->d_s2p);
+  HIP_TRY(hipGetLastError());
   NCCL_TRY(ncclGroupStart());
   for (uint32_t q = 0; q < e->R; ++q) {
     if (p.send_cnt[q]) {
       const uint64_t o = p.send_off[q], n = p.send_cnt[q];
-      NCCL_TRY(ncclSend(e->s2.key + o, n, ncclUint32, (int)q, e->comm, e->stream));
-      NCCL_TRY(ncclSend(e->s2.src + o, n, ncclUint32, (int)q, e->comm, e->stream));
-      NCCL_TRY(ncclSend(e->s2.pay + o, n, ncclUint32, (int)q, e->comm, e->stream));
+      NCCL_TRY(ncclSend(e->d_s2p + 3 * o, 3 * n, ncclUint32, (int)q, e->comm, e->stream));
       if (e->pw && q != e->rank)
         NCCL_TRY(ncclSend(e->d_s2rows + o * e->pw, n * e->pw, ncclUint32, (int)q, e->comm, e->stream));
     }
     if (p.recv_cnt[q]) {
       const uint64_t o = p.recv_off[q], n = p.recv_cnt[q];
-      NCCL_TRY(ncclRecv(e->A.key + o, n, ncclUint32, (int)q, e->comm, e->stream));
-      NCCL_TRY(ncclRecv(e->A.src + o, n, ncclUint32, (int)q, e->comm, e->stream));
-      NCCL_TRY(ncclRecv(e->A.pay + o, n, ncclUint32, (int)q, e->comm, e->stream));
+      NCCL_TRY(ncclRecv(e->d_rcvp + 3 * (o - p.n_bl), 3 * n, ncclUint32, (int)q, e->comm, e->stream));
       if (e->pw && q != e->rank)
         NCCL_TRY(ncclRecv(e->d_rx + o * e->pw, n * e->pw, ncclUint32, (int)q, e->comm, e->stream));
     }
   }
   NCCL_TRY(ncclGroupEnd());
+  if (p.n_recv) {  // received runs in sender-rank order after the local backlog (the sharded canonical order)
+    hipLaunchKernelGGL(k_unpack_aos, dim3(grid_for(p.n_recv / kThreads + 1, 2048)), dim3(kThreads), 0, e->stream,
+                       e->d_rcvp, (uint32_t)p.n_recv, e->A.m(), (uint32_t)p.n_bl);
+    HIP_TRY(hipGetLastError());
+  }
   return AGX_OK;
 }
 
@@ -1351,6 +1357,8 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     const uint64_t tsz = (uint64_t)e->R * e->tstride;
     CREATE_TRY(alloc_msgs(e->eg0, e->cap_emit));
     CREATE_TRY(alloc_msgs(e->s2, e->cap_emit));
+    CREATE_TRY(dalloc(&e->d_s2p, 3 * e->cap_emit));
+    CREATE_TRY(dalloc(&e->d_rcvp, 3 * e->cap));
     CREATE_TRY(dalloc(&e->d_tcnt[0], tsz));
     CREATE_TRY(dalloc(&e->d_toff[0], tsz));
     CREATE_TRY(hipMemset(e->d_tcnt[0], 0, tsz * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
@@ -1462,6 +1470,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_zidx); hipFree(e->d_row); hipFree(e->d_col);
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
   free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1);
+  hipFree(e->d_s2p); hipFree(e->d_rcvp);
   for (int q = 0; q < 2; ++q) {
     hipFree(e->d_tcnt[q]); hipFree(e->d_toff[q]); hipFree(e->d_blo[q]); hipFree(e->d_blc[q]); hipFree(e->d_emc[q]);
   }

@@ -2751,6 +2751,26 @@ __global__ void __launch_bounds__(kScanThreads) k_replay_out(const uint32_t* cnt
   if (threadIdx.x == 0) *ctr = c + 1u;
 }
 
+// Multi-rank exchange: the owner-major tells (SoA) interleaved as (key, src, payload) triples, so
+// each peer's run is ONE contiguous ncclSend instead of three; and back to SoA after the receive.
+__global__ void __launch_bounds__(kThreads) k_pack_aos(CMsgs s, const uint32_t* d_total, uint32_t* out) {
+  const uint32_t n = d_total[1];
+  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+    const uint32_t k = s.key[i], sv = s.src[i], pv = s.pay[i];
+    out[3 * (size_t)i] = k;
+    out[3 * (size_t)i + 1] = sv;
+    out[3 * (size_t)i + 2] = pv;
+  }
+}
+__global__ void __launch_bounds__(kThreads) k_unpack_aos(const uint32_t* in, uint32_t n, Msgs d, uint32_t dof) {
+  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+    const uint32_t k = in[3 * (size_t)i], sv = in[3 * (size_t)i + 1], pv = in[3 * (size_t)i + 2];
+    d.key[dof + i] = k;
+    d.src[dof + i] = sv;
+    d.pay[dof + i] = pv;
+  }
+}
+
 __global__ void k_set_u32(uint32_t* p, uint32_t v) {
   if (threadIdx.x == 0) *p = v;
 }
