@@ -1,0 +1,81 @@
+// agx_apply.hip — k_bucket_apply instantiations of one variant group (agx_variants.h).
+// Built once per group with -DAGX_VGROUP=g; the unit with AGX_VGROUP_DISPATCH also holds the
+// dispatcher agx_launch_apply() that routes a variant id to its group.
+#include <hip/hip_runtime.h>
+
+#include "agx_variants.h"
+
+#ifndef AGX_VGROUP
+#error "build agx_apply.hip with -DAGX_VGROUP=<group>"
+#endif
+
+#define AGX_CAT2(a, b) a##b
+#define AGX_CAT(a, b) AGX_CAT2(a, b)
+#define AGX_GROUP_FN AGX_CAT(agx_launch_apply_g, AGX_VGROUP)
+
+namespace agx {
+
+hipError_t agx_launch_apply_g0(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_apply_g1(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_apply_g2(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_apply_g3(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_apply_g4(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_apply_g5(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_apply_g6(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_apply_g7(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+static_assert(kVGroups == 8, "one declaration per group");
+
+namespace {
+
+template <uint32_t V>
+hipError_t launch_v(uint32_t mode, bool skew, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  constexpr bool W = kVariants[V].wide;
+  constexpr uint32_t M = kVariants[V].km;
+  const dim3 blk(kBThreads);
+  switch (mode * 2 + (skew ? 1u : 0u)) {
+    case M_FUSED * 2: hipLaunchKernelGGL((k_bucket_apply<W, M, true, false, false>), g, blk, 0, s, ba); break;
+    case M_FUSED * 2 + 1: hipLaunchKernelGGL((k_bucket_apply<W, M, true, true, false>), g, blk, 0, s, ba); break;
+    case M_OWNER * 2: hipLaunchKernelGGL((k_bucket_apply<W, M, false, false, true>), g, blk, 0, s, ba); break;
+    case M_OWNER * 2 + 1: hipLaunchKernelGGL((k_bucket_apply<W, M, false, true, true>), g, blk, 0, s, ba); break;
+    case M_BYPASS * 2: hipLaunchKernelGGL((k_bucket_apply<W, M, false, false, false>), g, blk, 0, s, ba); break;
+    case M_BYPASS * 2 + 1: hipLaunchKernelGGL((k_bucket_apply<W, M, false, true, false>), g, blk, 0, s, ba); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// the variants of this group, V in [0, V_N)
+template <uint32_t V>
+hipError_t group_dispatch(uint32_t vid, uint32_t mode, bool skew, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  if constexpr (V >= V_N) {
+    return hipErrorInvalidValue;
+  } else {
+    if constexpr (kVariantGroup[V] == AGX_VGROUP)
+      if (vid == V) return launch_v<V>(mode, skew, g, s, ba);
+    return group_dispatch<V + 1>(vid, mode, skew, g, s, ba);
+  }
+}
+
+}  // namespace
+
+hipError_t AGX_GROUP_FN(uint32_t vid, uint32_t mode, bool skew, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  return group_dispatch<0>(vid, mode, skew, g, s, ba);
+}
+
+#if AGX_VGROUP == 0
+hipError_t agx_launch_apply(uint32_t vid, uint32_t mode, bool skew, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  if (vid >= V_N) return hipErrorInvalidValue;
+  switch (kVariantGroup[vid]) {
+    case 0: return agx_launch_apply_g0(vid, mode, skew, g, s, ba);
+    case 1: return agx_launch_apply_g1(vid, mode, skew, g, s, ba);
+    case 2: return agx_launch_apply_g2(vid, mode, skew, g, s, ba);
+    case 3: return agx_launch_apply_g3(vid, mode, skew, g, s, ba);
+    case 4: return agx_launch_apply_g4(vid, mode, skew, g, s, ba);
+    case 5: return agx_launch_apply_g5(vid, mode, skew, g, s, ba);
+    case 6: return agx_launch_apply_g6(vid, mode, skew, g, s, ba);
+    default: return agx_launch_apply_g7(vid, mode, skew, g, s, ba);
+  }
+}
+#endif
+
+}  // namespace agx

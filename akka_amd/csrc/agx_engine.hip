@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "agx_kernels.h"
+#include "agx_variants.h"
 
 using namespace agx;
 
@@ -466,6 +467,31 @@ void skew_prepass(agx_engine* e, const BucketArgs& ba, const SkewArgs& ska) {
   hipLaunchKernelGGL(k_skew_scatter, dim3(gp), dim3(kBThreads), 0, e->stream, ba, ska);
 }
 
+// the k_bucket_apply variant for the registered behaviour kinds (agx_variants.h)
+uint32_t apply_variant(const agx_engine* e) {
+  const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
+  if (e->pw && e->delta_max) {  // delta-CRDT replication: the variants that carry the delta code
+    if (km == kb(AGX_KIND_GCOUNTER)) return V_GC_DELTA;
+    if (km == kb(AGX_KIND_PNCOUNTER)) return V_PN_DELTA;
+    if (km == kb(AGX_KIND_ORSET)) return V_OR_DELTA;
+    return V_ALL_DELTA;
+  }
+  if (e->pw) {  // CRDT kinds registered: single-kind populations get specialised merges
+    if (km == kb(AGX_KIND_GCOUNTER)) return V_GC;
+    if (km == kb(AGX_KIND_PNCOUNTER)) return V_PN;
+    if (km == kb(AGX_KIND_ORSET)) return V_OR;
+    if ((km & ~kCrdtKM) == 0) return V_CRDT;  // CRDT kinds only: no plain-behaviour code
+    return V_ALL_WIDE;
+  }
+  if (km == kb(AGX_KIND_RING)) return V_RING;  // behaviour-specialised variants (see apply_msg)
+  if (km == kb(AGX_KIND_FORWARD_RR)) return V_FWD;
+  if (km == kb(AGX_KIND_FANOUT)) return V_FANOUT;
+  if (km == kb(AGX_KIND_COUNTER)) return V_COUNTER;
+  if (km == kb(AGX_KIND_COMPILED)) return V_COMPILED;  // compiled behaviours only (agx_set_behaviors)
+  if (km & kb(AGX_KIND_COMPILED)) return V_ALL_COMPILED;
+  return V_ALL;
+}
+
 agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   // the chunk histograms consumed by this step's first pass were zeroed by k_chunk_downsweep;
   // on the multi-rank path (no chunk pass) they are never read, so stale columns are harmless
@@ -545,59 +571,19 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.sk_act = e->d_sk_act;
   SkewArgs ska{e->d_sk_rec, e->d_sk_act, e->d_sk_pc, e->d_sk_meta, e->sk_budget, e->sk_rows};
   {
-    const dim3 g(grid_for(e->nb, e->apply_grid)), blk(kBThreads);
-    const uint32_t km = e->kinds_mask & ~kb(AGX_KIND_NONE);
+    const uint32_t vid = apply_variant(e);
+    const uint32_t mode = e->fused ? M_FUSED : e->R > 1 ? M_OWNER : M_BYPASS;
+    const dim3 g(grid_for(e->nb, e->apply_grid));
     const dim3 gs(grid_for(e->nb, std::min(e->apply_grid, e->skew_grid)));  // skew list (grid-stride)
-#define AGX_APPLY2(W, M, G, O)                                                                   \
-  do {                                                                                           \
-    if (!e->skew_only) { Scope s(e, K_APPLY);                                                    \
-      hipLaunchKernelGGL((k_bucket_apply<W, M, G, false, O>), g, blk, 0, e->stream, ba); }       \
-    if (!(G && e->strict_cap)) { Scope s(e, K_SKEW);                                             \
-      if (!W && !G && !O) skew_prepass(e, ba, ska);                                              \
-      hipLaunchKernelGGL((k_bucket_apply<W, M, G, true, O>), gs, blk, 0, e->stream, ba); }       \
-  } while (0)
-#define AGX_APPLY(W, M)                                                                          \
-  do {                                                                                           \
-    if (e->fused) AGX_APPLY2(W, M, true, false);                                                 \
-    else if (e->R > 1) AGX_APPLY2(W, M, false, true);                                            \
-    else AGX_APPLY2(W, M, false, false);                                                         \
-  } while (0)
-    constexpr uint32_t kCrdt = kb(AGX_KIND_GCOUNTER) | kb(AGX_KIND_PNCOUNTER) | kb(AGX_KIND_ORSET);
-    if (e->pw && e->delta_max) {  // delta-CRDT replication: the variants that carry the delta code
-      if (km == kb(AGX_KIND_GCOUNTER))
-        AGX_APPLY(true, kb(AGX_KIND_GCOUNTER) | kDeltaKM);
-      else if (km == kb(AGX_KIND_PNCOUNTER))
-        AGX_APPLY(true, kb(AGX_KIND_PNCOUNTER) | kDeltaKM);
-      else if (km == kb(AGX_KIND_ORSET))
-        AGX_APPLY(true, kb(AGX_KIND_ORSET) | kDeltaKM);
-      else
-        AGX_APPLY(true, KM_ALL | kDeltaKM);
-    } else if (e->pw && km == kb(AGX_KIND_GCOUNTER))  // single-kind CRDT populations: specialised merges
-      AGX_APPLY(true, kb(AGX_KIND_GCOUNTER));
-    else if (e->pw && km == kb(AGX_KIND_PNCOUNTER))
-      AGX_APPLY(true, kb(AGX_KIND_PNCOUNTER));
-    else if (e->pw && km == kb(AGX_KIND_ORSET))
-      AGX_APPLY(true, kb(AGX_KIND_ORSET));
-    else if (e->pw && (km & ~kCrdt) == 0)  // CRDT kinds only: no plain-behaviour code
-      AGX_APPLY(true, kCrdt);
-    else if (e->pw)  // CRDT kinds registered: the variant with state gossips
-      AGX_APPLY(true, KM_ALL);
-    else if (km == kb(AGX_KIND_RING))  // behaviour-specialised variants (see apply_msg)
-      AGX_APPLY(false, kb(AGX_KIND_RING));
-    else if (km == kb(AGX_KIND_FORWARD_RR))
-      AGX_APPLY(false, kb(AGX_KIND_FORWARD_RR));
-    else if (km == kb(AGX_KIND_FANOUT))
-      AGX_APPLY(false, kb(AGX_KIND_FANOUT));
-    else if (km == kb(AGX_KIND_COUNTER))
-      AGX_APPLY(false, kb(AGX_KIND_COUNTER));
-    else if (km == kb(AGX_KIND_COMPILED))  // compiled behaviours only (agx_set_behaviors)
-      AGX_APPLY(false, kb(AGX_KIND_COMPILED));
-    else if (km & kb(AGX_KIND_COMPILED))
-      AGX_APPLY(false, KM_ALL | kb(AGX_KIND_COMPILED));
-    else
-      AGX_APPLY(false, KM_ALL);
-#undef AGX_APPLY
-#undef AGX_APPLY2
+    if (!e->skew_only) {
+      Scope s(e, K_APPLY);
+      HIP_TRY(agx_launch_apply(vid, mode, false, g, e->stream, ba));
+    }
+    if (!(mode == M_FUSED && e->strict_cap)) {
+      Scope s(e, K_SKEW);
+      if (!kVariants[vid].wide && mode == M_BYPASS) skew_prepass(e, ba, ska);
+      HIP_TRY(agx_launch_apply(vid, mode, true, gs, e->stream, ba));
+    }
   }
   if (e->fused) e->par ^= 1u;  // the next superstep writes the other parity
   HIP_TRY(hipGetLastError());
@@ -797,15 +783,25 @@ agx_status read_counters(agx_engine* e, uint64_t* s) {
   return AGX_OK;
 }
 
-// counters -> agx_stats; check: report a capacity overflow recorded by the kernels
+// The kernels' sticky error word -> status.  The bits are never cleared: after a capacity
+// overflow mail was dropped, after a counter wrap a slot is wrong, so every later result of the
+// engine is suspect -- each later agx_run / agx_get_stats reports the same error (agx_get_stats
+// still fills its counters); destroy the engine and start over.
+agx_status error_status(const agx_engine* e, uint64_t err) {
+  if (err & kErrRange)
+    return set_err(AGX_ERANGE, "a GCounter/PNCounter slot exceeded 2^64 - 1 (u64 slots; the reference uses BigInt)");
+  if (err & kErrCapacity)
+    return set_err(AGX_ECAPACITY, "in-flight messages exceeded engine capacity (msg_capacity=%llu)",
+                   (unsigned long long)e->cap);
+  return AGX_OK;
+}
+
+// counters -> agx_stats (filled even when an error is reported); check: report an error
+// recorded by the kernels
 agx_status collect_stats(agx_engine* e, agx_stats* out, bool check) {
   uint64_t s[kStatBlk];
   AGX_TRY(read_counters(e, s));
-  if (check && (s[ST_ERROR] & kErrRange))
-    return set_err(AGX_ERANGE, "a GCounter/PNCounter slot exceeded 2^64 - 1 (u64 slots; the reference uses BigInt)");
-  if (check && (s[ST_ERROR] & kErrCapacity))
-    return set_err(AGX_ECAPACITY, "in-flight messages exceeded engine capacity (msg_capacity=%llu)",
-                   (unsigned long long)e->cap);
+  const agx_status est = check ? error_status(e, s[ST_ERROR]) : AGX_OK;
   const uint64_t* bs = s + kStatSred;
   agx_stats st{};
   st.delivered = bs[0];
@@ -827,7 +823,7 @@ agx_status collect_stats(agx_engine* e, agx_stats* out, bool check) {
   if (km & kb(AGX_KIND_ORSET)) sw = std::max<uint64_t>(sw, e->delta_max ? AGX_DELTA_ENV_WORDS + 4 : AGX_ORSET_WORDS);
   st.bytes_alg = 12ull * st.delivered + 12ull * st.emitted + (16ull * std::min<uint64_t>(sw, e->W) + 2ull) * bs[4];
   if (out) *out = st;
-  return AGX_OK;
+  return est;
 }
 
 // one superstep on one rank: [chunks] -> group by bucket -> in-bucket sort + drain + apply -> [chunks]
@@ -1019,7 +1015,10 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
       const uint32_t si = size_idx(left);
       cnt = kGraphSizes[si];
       hipError_t ge = hipGraphLaunch(graph(si), e->stream);
-      if (ge != hipSuccess) st = set_err(AGX_EDEVICE, "hipGraphLaunch: %s", hipGetErrorString(ge));
+      if (ge != hipSuccess) {  // nothing ran: no parity, ring slot or replay-counter change
+        st = set_err(AGX_EDEVICE, "hipGraphLaunch: %s", hipGetErrorString(ge));
+        break;
+      }
       if (e->fused && (cnt & 1u)) e->par ^= 1u;  // the replayed supersteps advanced the parity
     } else {
       cnt = 1;
@@ -1047,6 +1046,8 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     launched_steps += cnt;
     hipEventRecord(ev[slot], e->stream);
   }
+  // the kernels' error word rides on the final sync (agx_run checks it even when out == NULL)
+  hipMemcpyAsync(e->h_stat + ST_ERROR, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost, e->stream);
   hipStreamSynchronize(e->stream);
   if (e->fused && !quiet)  // replays not polled yet, in launch order
     for (uint32_t k = launched > kLag ? launched - kLag : 0; k < launched && st == AGX_OK; ++k)
@@ -1137,6 +1138,7 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
     AGX_TRY(fix_rx(e, p));
     AGX_TRY(phase2(e, p.n_bl + p.n_recv + p.n_staged, p.n_bl + p.n_recv));
   }
+  HIP_TRY(hipMemcpyAsync(e->h_stat + ST_ERROR, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return AGX_OK;
 }
@@ -1371,10 +1373,12 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(dalloc(&e->d_ninbox, 1));
     CREATE_TRY(hipMemset(e->d_ninbox, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     // skewed-bucket partitions: a skewed bucket holds > kBucket messages, so at most cap / kBucket
-    // of them; parts of >= kSkSpan positions, at most sk_budget + (skewed buckets) of them
+    // of them; parts of >= kSkSpan positions.  k_skew_plan rounds a bucket's backlog parts and its
+    // new-mail parts up separately, so each skewed bucket adds up to TWO parts beyond the budget:
+    // at most sk_budget + 2 x (skewed buckets) rows of pc
     const uint64_t nsk = std::min<uint64_t>(e->nb, e->cap / kBucket + 1);
     e->sk_budget = (uint32_t)std::min<uint64_t>(8192, e->cap / kSkSpan + 1);
-    e->sk_rows = e->sk_budget + (uint32_t)nsk;
+    e->sk_rows = e->sk_budget + 2 * (uint32_t)nsk;
     CREATE_TRY(dalloc(&e->d_sk_rec, (uint64_t)e->nb * kSkRec));
     CREATE_TRY(dalloc(&e->d_sk_act, nsk * 3 * kBucket));
     CREATE_TRY(dalloc(&e->d_sk_pc, (uint64_t)e->sk_rows * kBucket));
@@ -1569,6 +1573,17 @@ agx_status agx_set_behaviors(agx_engine* e, const agx_case* cases, uint32_t n_ca
     if (A.op < AGX_A_SET || A.op > AGX_A_TELL || A.word > 1u || !opnd_ok(A.src, A.sword) ||
         (A.op == AGX_A_TELL && !opnd_ok(A.dsrc, A.dword)))
       return set_err(AGX_EINVAL, "compiled behaviours: bad action %u (state words 0..1)", i);
+  }
+  // the apply kernels reserve kmax tell slots per message (single pass: the tell overwrites the
+  // message's own consumed LDS slot; otherwise a bucket's tells live in [lo*kmax, (lo+cnt)*kmax)):
+  // a case that tells more often would overwrite unprocessed mail or the next bucket's tells
+  for (uint32_t c = 0; c < n_cases; ++c) {
+    uint32_t tells = 0;
+    for (uint32_t i = cases[c].act_first; i < (uint32_t)cases[c].act_first + cases[c].act_count; ++i)
+      tells += acts[i].op == AGX_A_TELL;
+    if (tells > e->kmax)
+      return set_err(AGX_EINVAL, "compiled behaviours: case %u tells %u times per message, max_emit is %u", c, tells,
+                     e->kmax);
   }
   AGX_TRY(ensure_dev(e));
   hipFree(e->d_bcase);
@@ -1767,9 +1782,9 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
     fprintf(stderr, "\n");
     HIP_TRY(hipMemset(e->d_dbg, 0, h.size() * 8));
   }
-  // out == NULL: no counter read-back (one stream round trip less); agx_get_stats reads them
-  // later and reports a capacity overflow recorded meanwhile
-  return out ? collect_stats(e, out, true) : AGX_OK;
+  // out == NULL: no counter read-back (one stream round trip less; agx_get_stats reads them
+  // later), but the error word came back with the run's final sync
+  return out ? collect_stats(e, out, true) : error_status(e, e->h_stat[ST_ERROR]);
 }
 
 agx_status agx_get_stats(agx_engine* e, agx_stats* out) {

@@ -81,7 +81,7 @@ __device__ __forceinline__ void commit_stops(uint8_t* alive, const uint32_t* sto
   __syncthreads();
   if (threadIdx.x == 0) *nstop = 0;
 }
-__global__ void __launch_bounds__(kScanThreads) k_commit_stops(uint8_t* alive, const uint32_t* stopq, uint32_t* nstop) {
+static __global__ void __launch_bounds__(kScanThreads) k_commit_stops(uint8_t* alive, const uint32_t* stopq, uint32_t* nstop) {
   commit_stops(alive, stopq, nstop);
 }
 
@@ -401,7 +401,7 @@ struct ChunkSortArgs {
 
 // one block per digit: exclusive prefix over units (in place) + digit total;
 // block 0 also commits the previous step's stops.
-__global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs a) {
+static __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs a) {
   __shared__ uint32_t scratch[kWaves + 1];
   if (blockIdx.x == 0) {
     begin_step(a.step, a.heap_top);
@@ -432,7 +432,7 @@ __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs a) {
   if (threadIdx.x == 0) a.tot[d] = t;
 }
 
-__global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
+static __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
   __shared__ uint32_t whist[kWaves][kRadix];
   __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
   __shared__ uint32_t scratch[kWaves + 1];
@@ -563,7 +563,7 @@ __device__ __forceinline__ void count4(uint32_t* h, const uint4& v, uint32_t shi
   }
 }
 
-__global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
+static __global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
   __shared__ uint32_t h[kWaves][kRadix];
   const uint32_t n = *a.d_n, nt = div_up(n, a.super);
   const int tid = threadIdx.x, w = tid / kWave;
@@ -597,7 +597,7 @@ __global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(kThreads) k_sort_rowscan(SortArgs a) {
+static __global__ void __launch_bounds__(kThreads) k_sort_rowscan(SortArgs a) {
   __shared__ uint32_t scratch[kWaves + 1];
   const uint32_t d = blockIdx.x;
   if (d >= (1u << a.bits)) return;
@@ -605,7 +605,7 @@ __global__ void __launch_bounds__(kThreads) k_sort_rowscan(SortArgs a) {
   if (threadIdx.x == 0) a.tot[d] = t;
 }
 
-__global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) {
+static __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) {
   __shared__ uint32_t whist[kWaves][kRadix];
   __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
   __shared__ uint32_t scratch[kWaves + 1];
@@ -1752,14 +1752,15 @@ struct SkewArgs {
   uint32_t* pc;       // [max_parts][kBucket] arrivals per actor -> prefix over the bucket's parts
   uint32_t* meta;     // [0] parts, [1] span
   uint32_t budget;    // target number of parts (the span grows beyond kSkSpan to stay near it)
-  uint32_t max_parts; // rows of pc: budget + nb (a bucket adds at most one part beyond the budget)
+  uint32_t max_parts; // rows of pc: budget + 2 x (skewed buckets) (a bucket's backlog and new-mail parts are
+                      // rounded up separately: at most two parts beyond the budget each)
 };
 
 __device__ __forceinline__ uint32_t sk_key(const BucketArgs& a, const uint32_t* r, uint32_t rpar, uint32_t q) {
   return q < r[3] ? a.g.bl[rpar].key[r[4] + q] : a.in.key[r[5] + q - r[3]];
 }
 
-__global__ void __launch_bounds__(kScanThreads) k_skew_plan(BucketArgs a, SkewArgs k) {
+static __global__ void __launch_bounds__(kScanThreads) k_skew_plan(BucketArgs a, SkewArgs k) {
   __shared__ uint32_t scratch[kScanThreads / kWave + 1];
   __shared__ unsigned long long s_tot;
   const uint32_t n = *a.skew_n, tid = threadIdx.x;
@@ -1835,7 +1836,7 @@ __device__ __forceinline__ bool sk_part(const BucketArgs& a, const SkewArgs& k, 
   return true;
 }
 
-__global__ void __launch_bounds__(kBThreads) k_skew_count(BucketArgs a, SkewArgs k) {
+static __global__ void __launch_bounds__(kBThreads) k_skew_count(BucketArgs a, SkewArgs k) {
   __shared__ uint32_t s_c[kBucket];
   __shared__ uint32_t s_q[3];
   const uint32_t tid = threadIdx.x, nparts = k.meta[0], rpar = (*a.pstep & 1u) ^ 1u, amask = (1u << a.bb) - 1u;
@@ -1863,10 +1864,11 @@ __global__ void __launch_bounds__(kBThreads) k_skew_count(BucketArgs a, SkewArgs
   }
 }
 
-__global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, SkewArgs k) {
+static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, SkewArgs k) {
   __shared__ uint32_t scratch[2 * (kBWaves + 1)];
   const DevParams& P = a.P;
   const uint32_t tid = threadIdx.x, n = *a.skew_n, T = P.T, C = P.C;
+  if (k.meta[0] > k.max_parts) return;  // (plan and buffer disagree: k_skew_count reported it; no pc access)
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     uint32_t* r = k.rec + (size_t)i * kSkRec;
     const uint32_t b = r[0], pb = r[6], np = r[7];
@@ -1914,7 +1916,7 @@ __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, SkewArgs 
   }
 }
 
-__global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a, SkewArgs k) {
+static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a, SkewArgs k) {
   __shared__ __attribute__((aligned(16))) uint16_t whist[kBWaves * kBucket];  // 32 KB
   __shared__ uint32_t s_run[kBucket], s_keep[kBucket], s_ds[kBucket], s_bs[kBucket], s_tmp[kBucket];
   uint32_t* const s_first = s_tmp;  // backlog parts: first position of each actor's run in the part
@@ -2042,7 +2044,7 @@ __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a, SkewAr
 }
 
 template <bool kWide, uint32_t KM, bool kGather, bool kSkew, bool kOwner = false>
-__global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
+static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
   constexpr bool kDefer = !kSkew;  // large inboxes are appended to the skew list
   // key/src/pay carved from one array: group_tells reuses key+src as a 16 KB histogram
   __shared__ __attribute__((aligned(16))) uint32_t s_ksp[3 * kBucket];
@@ -2562,7 +2564,7 @@ __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
 // Bucket starts after a multi-pass sort: bstart[x] = first index with bucket >= x
 // (one thread per bucket, binary search over the sorted keys; the top levels of every
 // search hit the same cached lines).
-__global__ void __launch_bounds__(kThreads) k_bucket_bounds(const uint32_t* key, const uint32_t* d_n, uint32_t nb,
+static __global__ void __launch_bounds__(kThreads) k_bucket_bounds(const uint32_t* key, const uint32_t* d_n, uint32_t nb,
                                                             uint32_t bb, uint32_t* bstart) {
   const uint32_t n = *d_n;
   for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x <= nb; x += gridDim.x * kThreads) {
@@ -2576,7 +2578,7 @@ __global__ void __launch_bounds__(kThreads) k_bucket_bounds(const uint32_t* key,
 }
 
 // Sum the per-block counters of k_bucket_apply into out[0..kBStats).
-__global__ void __launch_bounds__(kScanThreads) k_stats_reduce(const unsigned long long* bstats, uint32_t nslots,
+static __global__ void __launch_bounds__(kScanThreads) k_stats_reduce(const unsigned long long* bstats, uint32_t nslots,
                                                                unsigned long long* out) {
   __shared__ unsigned long long s[kBStats];
   if (threadIdx.x < kBStats) s[threadIdx.x] = 0;
@@ -2592,7 +2594,7 @@ __global__ void __launch_bounds__(kScanThreads) k_stats_reduce(const unsigned lo
 }
 
 // Histogram columns of the host-staged chunks (one block per staged chunk).
-__global__ void __launch_bounds__(kThreads) k_chunk_hist(const uint32_t* key, uint32_t n, uint32_t* hist,
+static __global__ void __launch_bounds__(kThreads) k_chunk_hist(const uint32_t* key, uint32_t n, uint32_t* hist,
                                                          uint32_t stride, uint32_t col0, uint32_t shift, uint32_t bits,
                                                          uint32_t* chunk_off, uint32_t* chunk_cnt, uint32_t chunk0) {
   __shared__ uint32_t h[kRadix];
@@ -2639,7 +2641,7 @@ struct McompactArgs {
   uint32_t R, tstride, n_staged;
 };
 
-__global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactArgs a) {
+static __global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactArgs a) {
   __shared__ uint32_t scratch[kScanThreads / kWave + 1];
   __shared__ uint32_t s_obase[AGX_MAX_RANKS + 1];
   begin_step(a.step, a.heap_top);
@@ -2685,7 +2687,7 @@ __device__ __forceinline__ void copy_run(const CMsgs& s, uint32_t so, const Msgs
   }
 }
 
-__global__ void __launch_bounds__(kThreads) k_mcompact_copy(McompactArgs a) {
+static __global__ void __launch_bounds__(kThreads) k_mcompact_copy(McompactArgs a) {
   const bool go = a.d_total[0] != 0 || a.d_total[1] != 0;
   for (uint32_t c = blockIdx.x; c < a.ch.nb; c += gridDim.x) {
     const uint32_t n = a.ch.cnt[c];
@@ -2705,7 +2707,7 @@ __global__ void __launch_bounds__(kThreads) k_mcompact_copy(McompactArgs a) {
 }
 
 // messages in flight after the last apply = all chunk counts
-__global__ void __launch_bounds__(kScanThreads) k_inflight(const uint32_t* chunk_cnt, uint32_t nchunks,
+static __global__ void __launch_bounds__(kScanThreads) k_inflight(const uint32_t* chunk_cnt, uint32_t nchunks,
                                                            unsigned long long* out) {
   __shared__ unsigned long long s;
   if (threadIdx.x == 0) s = 0;
@@ -2729,7 +2731,7 @@ __device__ __forceinline__ uint32_t rmat_dst(uint64_t e, uint32_t bits, uint32_t
   return (uint32_t)(col % n);
 }
 
-__global__ void __launch_bounds__(kThreads) k_gen_rmat(const uint64_t* lrow, const uint64_t* gstart, uint32_t* col,
+static __global__ void __launch_bounds__(kThreads) k_gen_rmat(const uint64_t* lrow, const uint64_t* gstart, uint32_t* col,
                                                        uint32_t n_local, uint32_t bits, uint32_t ta, uint32_t tb,
                                                        uint32_t tc, uint64_t seed, uint32_t n_global) {
   for (uint32_t l = blockIdx.x * kThreads + threadIdx.x; l < n_local; l += gridDim.x * kThreads) {
@@ -2741,7 +2743,7 @@ __global__ void __launch_bounds__(kThreads) k_gen_rmat(const uint64_t* lrow, con
 // End of a fused superstep graph: the replay's per-superstep inbox sizes (and strict abort marks)
 // into ring slot (*ctr % 4) of the device-mapped pinned host ring -- one block, so the counter it
 // reads and bumps is never raced.  The host knows the slot of every replay (same counter).
-__global__ void __launch_bounds__(kScanThreads) k_replay_out(const uint32_t* cntb, uint32_t n, const uint32_t* abort,
+static __global__ void __launch_bounds__(kScanThreads) k_replay_out(const uint32_t* cntb, uint32_t n, const uint32_t* abort,
                                                             uint32_t* ring, uint32_t* ctr, uint32_t stride) {
   const uint32_t c = *ctr;
   uint32_t* dst = ring + (size_t)(c % 4u) * stride;
@@ -2753,7 +2755,7 @@ __global__ void __launch_bounds__(kScanThreads) k_replay_out(const uint32_t* cnt
 
 // Multi-rank exchange: the owner-major tells (SoA) interleaved as (key, src, payload) triples, so
 // each peer's run is ONE contiguous ncclSend instead of three; and back to SoA after the receive.
-__global__ void __launch_bounds__(kThreads) k_pack_aos(CMsgs s, const uint32_t* d_total, uint32_t* out) {
+static __global__ void __launch_bounds__(kThreads) k_pack_aos(CMsgs s, const uint32_t* d_total, uint32_t* out) {
   const uint32_t n = d_total[1];
   for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
     const uint32_t k = s.key[i], sv = s.src[i], pv = s.pay[i];
@@ -2762,7 +2764,7 @@ __global__ void __launch_bounds__(kThreads) k_pack_aos(CMsgs s, const uint32_t* 
     out[3 * (size_t)i + 2] = pv;
   }
 }
-__global__ void __launch_bounds__(kThreads) k_unpack_aos(const uint32_t* in, uint32_t n, Msgs d, uint32_t dof) {
+static __global__ void __launch_bounds__(kThreads) k_unpack_aos(const uint32_t* in, uint32_t n, Msgs d, uint32_t dof) {
   for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
     const uint32_t k = in[3 * (size_t)i], sv = in[3 * (size_t)i + 1], pv = in[3 * (size_t)i + 2];
     d.key[dof + i] = k;
@@ -2771,12 +2773,12 @@ __global__ void __launch_bounds__(kThreads) k_unpack_aos(const uint32_t* in, uin
   }
 }
 
-__global__ void k_set_u32(uint32_t* p, uint32_t v) {
+static __global__ void k_set_u32(uint32_t* p, uint32_t v) {
   if (threadIdx.x == 0) *p = v;
 }
 
 // fused mode: messages in flight after the last superstep = its backlog + tells + staged
-__global__ void __launch_bounds__(kScanThreads) k_inflight_fused(const uint32_t* blc0, const uint32_t* blc1,
+static __global__ void __launch_bounds__(kScanThreads) k_inflight_fused(const uint32_t* blc0, const uint32_t* blc1,
                                                                  const uint32_t* emc0, const uint32_t* emc1,
                                                                  const uint32_t* stg_cnt, uint32_t last_par,
                                                                  uint32_t nb, unsigned long long* out) {
@@ -2800,7 +2802,7 @@ namespace agx {
 // Multi-rank CRDT rows.  After the owner partition, the rows of state gossips that
 // leave this rank are packed in the order of the partitioned tells (row i <-> tell i);
 // they travel beside the envelopes and land in `rx` at the receiver's sort-input index.
-__global__ void __launch_bounds__(kThreads) k_pack_rows(CMsgs s2, const uint32_t* d_total, DevParams P,
+static __global__ void __launch_bounds__(kThreads) k_pack_rows(CMsgs s2, const uint32_t* d_total, DevParams P,
                                                         uint32_t* out) {
   const uint32_t n = d_total[1];
   const CrdtHeap H = crdt_heap(P);
@@ -2811,7 +2813,7 @@ __global__ void __launch_bounds__(kThreads) k_pack_rows(CMsgs s2, const uint32_t
 
 // Received gossips from other ranks [lo, hi) minus this rank's own segment: point
 // their handles at the rx rows (handle = heap_rows + sort-input index).
-__global__ void __launch_bounds__(kThreads) k_fix_rx(Msgs a, uint32_t lo, uint32_t hi, uint32_t self_lo,
+static __global__ void __launch_bounds__(kThreads) k_fix_rx(Msgs a, uint32_t lo, uint32_t hi, uint32_t self_lo,
                                                      uint32_t self_hi, uint32_t heap_rows) {
   for (uint32_t i = lo + blockIdx.x * kThreads + threadIdx.x; i < hi; i += gridDim.x * kThreads)
     if ((i < self_lo || i >= self_hi) && is_wide(a.src[i])) a.pay[i] = (a.pay[i] & ~kHandleMask) | (heap_rows + i);

@@ -334,6 +334,13 @@ class Tables:
     def n_behaviors(self) -> int:
         return len(self.behaviors)
 
+    @property
+    def max_tells(self) -> int:
+        """The most tells one message can emit (the largest tell count of any case): the engine's
+        max_emit must be at least this (agx_set_behaviors rejects the tables otherwise)."""
+        return max((sum(1 for i in range(c.act_first, c.act_first + c.act_count) if self.acts[i].op == A_TELL)
+                    for c in self.cases[:int(self.first[-1])]), default=0)
+
     def kind_of(self, b: Behavior) -> int:
         """The actor kind that starts in behaviour `b`."""
         for i, x in enumerate(self.behaviors):
@@ -355,8 +362,10 @@ def _reachable(roots) -> list:
     return order
 
 
-def compile_behaviors(roots) -> Tables:
-    """Lower `roots` and every behaviour they become into the engine's tables."""
+def compile_behaviors(roots, max_emit: int | None = None) -> Tables:
+    """Lower `roots` and every behaviour they become into the engine's tables.  With `max_emit`
+    (the engine's agx_cfg.max_emit), a case that tells more often than that is a CompileError:
+    the apply kernels reserve max_emit tell slots per message."""
     behs = _reachable(roots)
     if len(behs) > MAX_BEHAVIORS:
         raise CompileError(f"more than {MAX_BEHAVIORS} behaviours")
@@ -381,8 +390,11 @@ def compile_behaviors(roots) -> Tables:
         first.append(len(cases))
     if len(cases) > MAX_CASES or len(acts) > MAX_ACTS:
         raise CompileError("tables too large")
-    return Tables(behs, (AgxCase * max(len(cases), 1))(*cases), (AgxAct * max(len(acts), 1))(*acts),
-                  np.asarray(first, dtype=np.uint32))
+    t = Tables(behs, (AgxCase * max(len(cases), 1))(*cases), (AgxAct * max(len(acts), 1))(*acts),
+               np.asarray(first, dtype=np.uint32))
+    if max_emit is not None and t.max_tells > max(1, max_emit):
+        raise CompileError(f"a case tells {t.max_tells} times per message but max_emit is {max_emit}")
+    return t
 
 
 # ------------------------------------------------------------------ the built-in kinds, as typed behaviours

@@ -168,17 +168,105 @@ def test_c4_gcounter_as_benched_window(built):
     _assert_same(sg, so, a, b, "C4 GCounter 28 supersteps")
 
 
-# ------------------------------------------------------------------ C3 as benched
+# ------------------------------------------------------------------ C3
 @pytest.mark.parametrize("variant", ["tree", "steady"])
-def test_c3_zipf_as_benched(built, variant):
-    """bench C3 (SURVEY.md §8(d)): Zipf(1.1) FANOUT, 1/64 roots, unbounded, throughput 5;
-    'tree' = k 4, ttl 3; 'steady' = k 1, ttl 64 -- 2M actors, the bench's supersteps window."""
+def test_c3_zipf_unbounded_shapes(built, variant):
+    """SURVEY.md §8(d)'s C3 shapes with an UNBOUNDED mailbox (the bench's own parameters are in
+    test_c3_zipf_as_benched): Zipf(1.1) FANOUT, 1/64 roots, throughput 5; 'tree' = k 4, ttl 3;
+    'steady' = k 1, ttl 64 -- 2M actors, 24 supersteps."""
     if variant == "tree":
         w = wl.zipf_fanout(2_000_000, k=4, ttl=3, root_every=64, throughput=5)
     else:
         w = wl.zipf_fanout(2_000_000, k=1, ttl=64, root_every=64, throughput=5)
     sg, so, a, b = _run_both(w, max_steps=24)
-    _assert_same(sg, so, a, b, f"C3 {variant}")
+    _assert_same(sg, so, a, b, f"C3 unbounded {variant}")
+
+
+@pytest.mark.parametrize("variant", ["steady", "tree"])
+def test_c3_zipf_as_benched(built, variant):
+    """bench.py's two C3 lines at their own parameters, at 2.2M actors (> 2^20: the multi-pass
+    grouping, in-place backlog, tiny-wave and skewed-bucket paths of the 10M bench):
+    'steady' = zipf_fanout(k=1, ttl=15, root_every=1, BoundedMailbox(1000)), throughput 5, timed
+    from superstep 2 for 10 supersteps; 'tree' = zipf_fanout(k=4, ttl=3, root_every=64,
+    BoundedMailbox(1000)), timed from superstep 0 for 8.  Checked after the bench's window and
+    again to quiescence (the hot actors' bounded backlogs drain at 5 per superstep)."""
+    if variant == "steady":
+        w, window = wl.zipf_fanout(2_200_000, k=1, ttl=15, root_every=1, capacity=1000), 12
+    else:
+        w, window = wl.zipf_fanout(2_200_000, k=4, ttl=3, root_every=64, capacity=1000), 8
+    assert w.throughput == 5 and w.capacity == 1000
+    sg, so, a, b = _run_both(w, max_steps=window)
+    _assert_same(sg, so, a, b, f"C3 {variant} bench window")
+    assert sg.dead_letters > 0 and sg.in_flight > 0  # hot actors tail-drop at 1000 and keep backlogs
+    sg, so, a, b = _run_both(w)
+    _assert_same(sg, so, a, b, f"C3 {variant} to quiescence")
+    assert sg.in_flight == 0
+
+
+# ------------------------------------------------------------------ 8-way sharding (loopback)
+def _run_sharded(w, ranks):
+    from oracle import BspOracle
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.gpu_kwargs())) for r in range(ranks)]
+    for e in engs:
+        w.apply_to(e)
+    sg = GpuEngine.group_run(engs)
+    ref = BspOracle(n_ranks=ranks, **w.engine_kwargs())
+    w.apply_to(ref)
+    so = ref.run()
+    wo, ao = ref.read_state()
+    ref.close()
+    own_of = np.array([owner(i, 1000, ranks) for i in range(w.n_actors)])
+    wg = np.zeros_like(wo)
+    ag = np.zeros_like(ao)
+    for e in engs:
+        x, y = e.read_state()
+        own = own_of == e.cfg.rank
+        wg[own] = x[own]
+        ag[own] = y[own]
+        e.close()
+    return sg, so, (wg, ag), (wo, ao)
+
+
+@pytest.mark.parametrize("case", ["zipf", "zipf_bounded", "orset", "orset_delta", "gcounter_delta"])
+def test_sharded_8_ranks(built, case):
+    """C3 Zipf fan-out and C4 ORSet (full-state and delta-CRDT) hash-sharded over 8 ranks
+    (ShardRegion extractShardId ownership, SH/ShardRegion.scala:154-158; loopback exchange of the
+    RCCL path's kernels), bit-exact against the oracle in the sharded canonical order."""
+    w = {
+        "zipf": lambda: wl.zipf_fanout(60_000, k=4, ttl=3, root_every=16, throughput=3),
+        "zipf_bounded": lambda: wl.zipf_fanout(60_000, k=1, ttl=8, root_every=1, capacity=64),
+        "orset": lambda: wl.crdt_gossip(4_000, Kind.ORSET, rounds=8, throughput=2),
+        "orset_delta": lambda: wl.crdt_delta(8 * 400, Kind.ORSET, rounds=8, write=True, gossip_rounds=2,
+                                             throughput=3),
+        "gcounter_delta": lambda: wl.crdt_delta(8 * 400, Kind.GCOUNTER, rounds=8, write=True, throughput=3),
+    }[case]()
+    sg, so, a, b = _run_sharded(w, 8)
+    for k in ("delivered", "dead_letters", "unhandled", "emitted", "staged", "in_flight"):
+        assert getattr(sg, k) == so[k], f"{case}: {k} gpu={getattr(sg, k)} oracle={so[k]}"
+    assert np.array_equal(a[1], b[1]), f"{case}: alive differs"
+    diff = np.nonzero((a[0] != b[0]).any(axis=1))[0]
+    assert diff.size == 0, f"{case}: state differs at {diff[:10]}"
+    assert sg.delivered > 0
+
+
+# ------------------------------------------------------------------ skewed-bucket partitions
+def test_skew_parts_many_saturated_buckets(built):
+    """Many skewed buckets just over one LDS tile, each with a backlog, on a multi-pass population
+    with a small message capacity: k_skew_plan rounds every bucket's backlog parts and new-mail
+    parts up separately, so the parts reach budget + 2 x (skewed buckets) -- the pc table must
+    hold them (k_skew_scan wrote past it).  800 of 1075 buckets hold 2048 + 60 tokens
+    that RING-forward to themselves (stride 0) at throughput 1: every superstep each of them has
+    a 60-message backlog and 2048 new messages."""
+    n, hot, extra, hops = 2_200_000, 800, 60, 5
+    base = np.arange(hot * 2048, dtype=np.uint32)
+    dup = (np.arange(hot, dtype=np.uint32)[:, None] * 2048 + np.arange(extra, dtype=np.uint32)[None, :] * 31).reshape(-1)
+    dst = np.concatenate([base, dup])
+    pay = np.full(dst.size, hops, np.uint32)
+    src = np.full(dst.size, 0xFFFFFFFF, np.uint32)
+    w = wl.Workload("skew_parts", n, 1, 1, 1, 0, [(0, n, Kind.RING, None)], ring_stride=0, tells=(dst, src, pay))
+    sg, so, a, b = _run_both(w, msg_capacity=3_200_000)
+    _assert_same(sg, so, a, b, "skew parts")
+    assert sg.delivered == dst.size * (hops + 1)
 
 
 def test_c1_ping_pong_as_benched(built):

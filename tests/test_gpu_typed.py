@@ -58,3 +58,30 @@ def test_compiled_rejects_crdt_mix(built):
     with pytest.raises(Exception):
         eng.register_range(32, 32, t.kind_of(t.behaviors[0]))
     eng.close()
+
+
+def test_compiled_tells_beyond_max_emit_rejected(built):
+    """A case that tells twice per message needs max_emit >= 2 (the apply reserves max_emit tell
+    slots per message): agx_set_behaviors rejects it with AGX_EINVAL at max_emit 1, and accepts it,
+    bit-exact against the oracle, at max_emit 2."""
+    from akka_amd import typed
+    from akka_amd._lib import AgxError
+    st = typed.State("count")
+    two = (typed.ReceiveBuilder.create(st)
+           .on_any_message(lambda m, s: [s.count.inc(), typed.self_ref(1).tell(m.payload - 1),
+                                         typed.self_ref(2).tell(m.payload - 1), typed.Behaviors.same],
+                           test=lambda m: m.payload > 0)
+           .on_any_message(lambda m, s: [s.count.inc(), typed.Behaviors.same])
+           .build("two_tells"))
+    tables = typed.compile_behaviors([two])
+    assert tables.max_tells == 2
+    eng = GpuEngine(EngineConfig(n_actors=64, n_words=2, max_emit=1))
+    with pytest.raises(AgxError):
+        eng.set_behaviors(tables)
+    eng.close()
+    n = 4096
+    w = wl.Workload("two_tells", n, 2, 2, 3, 0, [(0, n, tables.kind_of(two), None)], behaviors=tables,
+                    tells=(np.arange(0, n, 97, dtype=np.uint32), np.full(43, 0xFFFFFFFF, np.uint32),
+                           np.full(43, 6, np.uint32)))
+    sg, so, a, b = run_both(w)
+    assert_same(sg, so, a, b, "two tells")

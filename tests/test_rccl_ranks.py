@@ -19,6 +19,8 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
     ("orset", 2, 6_000, 6),
     ("power", 4, 60_000, 8),
     ("zipf", 2, 30_000, 3),
+    ("zipf", 8, 40_000, 3),     # 8 ranks = the node's 8 GPUs (C3 sharded)
+    ("orset", 8, 4_000, 5),     # C4 ORSet rows over 8 ranks
 ])
 def test_rccl_ranks_parity(built, workload, world, n, hops):
     cmd = [sys.executable, "-u", str(ROOT / "tools" / "rccl_two_rank.py"), "--split-hosts", "--world", str(world),

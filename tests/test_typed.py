@@ -94,3 +94,18 @@ def test_switch_become_semantics():
     assert st["delivered"] == 6 and st["unhandled"] == 2 and st["emitted"] == 1
     assert list(ws[0]) == [2, 2]                 # flips, sum
     assert list(ws[1]) == [1, P(1)]              # the reply Ping(1)
+
+
+def test_compile_rejects_tells_beyond_max_emit():
+    """compile_behaviors(max_emit=k) refuses a case that tells more than k times per message
+    (the engine reserves max_emit tell slots per message, agx_set_behaviors checks the same)."""
+    st = typed.State("count")
+    two = (typed.ReceiveBuilder.create(st)
+           .on_any_message(lambda m, s: [typed.self_ref(1).tell(m.payload), m.sender.tell(m.payload),
+                                         typed.Behaviors.same])
+           .build("two"))
+    assert typed.compile_behaviors([two]).max_tells == 2
+    assert typed.compile_behaviors([two], max_emit=2).max_tells == 2
+    with pytest.raises(typed.CompileError):
+        typed.compile_behaviors([two], max_emit=1)
+    assert typed.compile_behaviors([typed.library()["ring"]], max_emit=1).max_tells == 1
