@@ -150,6 +150,12 @@ struct agx_engine {
   uint32_t *d_s2p = nullptr, *d_rcvp = nullptr;    // multi-rank: tells as (key, src, payload) triples, sent / received
 
   DevMsgs A, B, scr, bl, em, stg, s2;
+  // single-rank multi-pass: the tell arena by superstep parity (em = even, em2 = odd superstep
+  // counter): the apply writes one while identity grouping reads the other in place
+  DevMsgs em2;
+  bool ident_on = false;        // identity grouping enabled (multi-pass, > 1 radix pass; AGX_NO_IDENT=1 disables)
+  uint4* d_emmeta = nullptr;    // [nb] per tell chunk: first key, last key, descents, descent position
+  uint32_t *d_slsum = nullptr, *d_ident = nullptr;  // slice summaries; {on, rotation, total}
   uint64_t stg_cap = 0;
   uint32_t nb = 1, nchunks = 3;                // buckets; chunks = 2 nb + kStagedChunks
   uint32_t G = 1, ng = 1, nunits = 3, cstride = 4;  // first-pass histogram units (G buckets each)
@@ -354,10 +360,14 @@ DevParams make_params(agx_engine* e) {
 uint32_t grid_for(uint64_t tiles, uint32_t cap) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, cap)); }
 
 // ------------------------------------------------------------ kernel steps
+bool bypass_mode(const agx_engine* e) { return !e->fused && e->R == 1; }
+// single-rank multi-pass: the tell arena the superstep of parity `par` writes
+const DevMsgs& em_arena(const agx_engine* e, uint32_t par) { return par ? e->em2 : e->em; }
+
 Chunks make_chunks(agx_engine* e) {
   Chunks c{};
   c.bl = e->bl.c();
-  c.em = e->em.c();
+  c.em = bypass_mode(e) ? em_arena(e, e->par ^ 1u).c() : e->em.c();  // (the previous apply's tells)
   c.st = e->stg.c();
   c.off = e->d_chunk_off;
   c.cnt = e->d_chunk_cnt;
@@ -379,6 +389,7 @@ agx_status launch_dense_pass(agx_engine* e, const DevMsgs& in, const DevMsgs& ou
   sa.super = e->dsuper;
   sa.shift = shift;
   sa.bits = bits;
+  sa.ident = e->ident_on ? e->d_ident : nullptr;
   const uint32_t g = grid_for(e->max_supers, 4096);
   {
     Scope s(e, K_UPSWEEP);
@@ -430,10 +441,19 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     ca.G = e->G;
     ca.shift = e->plan.shift[0];
     ca.bits = e->plan.bits[0];
+    const uint32_t nsl = (e->nb + kBlSlice - 1) / kBlSlice;
+    if (e->ident_on) {
+      ca.emmeta = e->d_emmeta;
+      ca.slsum = e->d_slsum;
+      ca.ident = e->d_ident;
+    }
     {
       Scope s(e, K_CROWSCAN);
-      hipLaunchKernelGGL(k_chunk_rowscan, dim3((1u << ca.bits) + (e->nb + kBlSlice - 1) / kBlSlice), dim3(kThreads), 0,
+      hipLaunchKernelGGL(k_chunk_rowscan, dim3((1u << ca.bits) + nsl + (e->ident_on ? nsl + 1 : 0)), dim3(kThreads), 0,
                          e->stream, ca);
+      if (e->ident_on)  // this superstep's grouping: identity (no pass) or the radix passes
+        hipLaunchKernelGGL(k_ident_combine, dim3(1), dim3(kWave), 0, e->stream, e->d_slsum, nsl, e->d_ident,
+                           reinterpret_cast<unsigned long long*>(e->d_stats + ST_IDENT));
     }
     {
       Scope s(e, K_CDOWN);
@@ -448,8 +468,10 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
   }
   if (e->plan.npass > 1) {  // digits of the last pass are not buckets: find the bucket starts
     Scope s(e, K_BOUNDS);
+    const bool idn = e->ident_on && first_from_chunks;
     hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((e->nb + kThreads) / kThreads, 4096)), dim3(kThreads), 0,
-                       e->stream, src->key, e->d_n, e->nb, e->bb, e->d_bstart);
+                       e->stream, src->key, e->d_n, e->nb, e->bb, e->d_bstart, idn ? e->d_ident : nullptr,
+                       idn ? em_arena(e, e->par ^ 1u).key : nullptr);
     HIP_TRY(hipGetLastError());
   }
   *result = src;
@@ -549,6 +571,12 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     g.region = e->region;
   }
   if (!e->fused && e->R == 1) {  // multi-pass: the backlog stays in place (parity arenas bl / bl2)
+    ba.em = em_arena(e, e->par).m();  // (tells by superstep parity: identity grouping reads the other one)
+    if (e->ident_on) {
+      ba.ident = e->d_ident;
+      ba.in_alt = em_arena(e, e->par ^ 1u).c();
+      ba.emmeta = e->d_emmeta;
+    }
     ba.pstep = e->d_step;
     ba.cap = e->cap;
     ba.blpre = e->d_blpre;
@@ -585,7 +613,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
       HIP_TRY(agx_launch_apply(vid, mode, true, gs, e->stream, ba));
     }
   }
-  if (e->fused) e->par ^= 1u;  // the next superstep writes the other parity
+  if (e->R == 1) e->par ^= 1u;  // the next superstep writes the other parity (fused and multi-pass)
   HIP_TRY(hipGetLastError());
   return AGX_OK;
 }
@@ -893,7 +921,7 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     return si < max_si ? si : max_si;
   };
   auto graph = [&](uint32_t si) -> hipGraphExec_t& {
-    return e->fused ? e->gx[strict][e->par][si] : e->gx[0][0][si];
+    return e->fused ? e->gx[strict][e->par][si] : e->gx[0][e->par][si];
   };
   // every replay size (and, fused, both starting parities) is captured at first use, so no
   // capture ever lands in the middle of a later budget
@@ -902,9 +930,9 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     const uint32_t p0 = e->par;  // capturing advances the host parity: restore it
     e->strict_cap = strict;
     agx_status s2 = AGX_OK;
-    for (uint32_t p = 0; p < (e->fused ? 2u : 1u) && s2 == AGX_OK; ++p)
+    for (uint32_t p = 0; p < 2u && s2 == AGX_OK; ++p)  // (both starting parities: arenas are kernel arguments)
       for (uint32_t si = 0; si < agx_engine::kNSizes && s2 == AGX_OK; ++si) {
-        hipGraphExec_t& g = e->fused ? e->gx[strict][p][si] : e->gx[0][0][si];
+        hipGraphExec_t& g = e->fused ? e->gx[strict][p][si] : e->gx[0][p][si];
         if (g) continue;
         e->par = p;
         s2 = capture_steps(e, kGraphSizes[si], &g);
@@ -1019,7 +1047,7 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
         st = set_err(AGX_EDEVICE, "hipGraphLaunch: %s", hipGetErrorString(ge));
         break;
       }
-      if (e->fused && (cnt & 1u)) e->par ^= 1u;  // the replayed supersteps advanced the parity
+      if (cnt & 1u) e->par ^= 1u;  // the replayed supersteps advanced the parity
     } else {
       cnt = 1;
       st = launch_step_single(e);
@@ -1306,6 +1334,9 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
 
   // fused superstep when one radix digit covers every bucket of a single rank
   e->fused = e->R == 1 && e->plan.npass == 1 && getenv("AGX_NO_FUSED") == nullptr;
+  // identity grouping (k_ident_combine): single-rank multi-pass with a bucket-bounds search
+  e->ident_on = !e->fused && e->R == 1 && e->plan.npass > 1 && getenv("AGX_IDENT") != nullptr;
+  if (!e->fused && e->R == 1) e->par = 1u;  // multi-pass: parity of the first superstep's counter value (1)
   e->tstride = (e->nb + 3) & ~3u;
   // fused: bucket b's inbox (and its backlog / tell slices) live at [b*region, ...) of the
   // arenas; an inbox larger than the region (skew) takes a slot of the overflow area that
@@ -1367,8 +1398,16 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(dalloc(&e->d_moff0, e->nb));
     CREATE_TRY(dalloc(&e->d_moff1, tsz));
   }
-  if (!e->fused && e->R == 1) {  // multi-pass: backlog arenas by superstep parity
+  if (!e->fused && e->R == 1) {  // multi-pass: backlog and tell arenas by superstep parity
     CREATE_TRY(alloc_msgs(e->bl2, e->acap));
+    CREATE_TRY(alloc_msgs(e->em2, e->acap * e->kmax));
+    if (e->ident_on) {
+      CREATE_TRY(dalloc(&e->d_emmeta, e->nb));
+      CREATE_TRY(dalloc(&e->d_slsum, (uint64_t)(kMaxBlSlices + 1) * kSlSum));
+      CREATE_TRY(dalloc(&e->d_ident, 4));
+      CREATE_TRY(hipMemset(e->d_emmeta, 0, e->nb * sizeof(uint4)) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+      CREATE_TRY(hipMemset(e->d_ident, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    }
     CREATE_TRY(dalloc(&e->d_blpre, e->nb + 2 * kMaxBlSlices));  // [nb] prefixes, [64] slice totals, [64] bases
     CREATE_TRY(dalloc(&e->d_ninbox, 1));
     CREATE_TRY(hipMemset(e->d_ninbox, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
@@ -1473,7 +1512,8 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_kind); hipFree(e->d_alive); hipFree(e->d_stopq); hipFree(e->d_nstop); hipFree(e->d_state); hipFree(e->d_gid); hipFree(e->d_route);
   hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_zidx); hipFree(e->d_row); hipFree(e->d_col);
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
-  free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1);
+  free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1); free_msgs(e->em2);
+  hipFree(e->d_emmeta); hipFree(e->d_slsum); hipFree(e->d_ident);
   hipFree(e->d_s2p); hipFree(e->d_rcvp);
   for (int q = 0; q < 2; ++q) {
     hipFree(e->d_tcnt[q]); hipFree(e->d_toff[q]); hipFree(e->d_blo[q]); hipFree(e->d_blc[q]); hipFree(e->d_emc[q]);

@@ -40,9 +40,11 @@ constexpr int kRadixBits = 9;  // max digit width of one pass
 constexpr int kRadix = 1 << kRadixBits;
 
 constexpr int kScanThreads = 1024;
+constexpr int kStagedChunks = 256;  // host-staged tells are split over this many chunks
 
 // stats slots (u64) on device
-enum { ST_DELIVERED = 0, ST_DEAD = 1, ST_UNHANDLED = 2, ST_EMITTED = 3, ST_STEPS = 4, ST_ERROR = 5, ST_ACTIVE = 6, ST_N = 8 };
+enum { ST_DELIVERED = 0, ST_DEAD = 1, ST_UNHANDLED = 2, ST_EMITTED = 3, ST_STEPS = 4, ST_ERROR = 5, ST_ACTIVE = 6,
+       ST_IDENT = 7, ST_N = 8 };
 constexpr uint64_t kErrCapacity = 1;
 constexpr uint64_t kErrRange = 2;  // a counter slot wrapped past 2^64 - 1 (AGX_ERANGE)
 // per-block counters of k_bucket_apply: delivered, dead, unhandled, emitted, active
@@ -397,7 +399,147 @@ struct ChunkSortArgs {
   uint64_t cap;
   uint32_t stride, nunits, ng, G, shift, bits;
   uint32_t bypass;     // backlog chunks are read in place by the apply (not sorted; units < ng skipped)
+  // identity grouping (single-rank multi-pass; null = off): per tell chunk the apply's key summary
+  // {first, last, descents, descent position}; the rowscan's extra blocks reduce it per slice of
+  // kBlSlice chunks into slsum, k_ident_combine decides, ident[0..2] = {on, rotation, total}
+  const uint4* emmeta;
+  uint32_t* slsum;     // [kMaxBlSlices + 1][kSlSum]; row kMaxBlSlices = the host-staged total
+  uint32_t* ident;
+  uint64_t* istats;    // stats[ST_IDENT]: supersteps grouped by identity
 };
+constexpr uint32_t kSlSum = 8;  // per slice: total, flags, delta, descents, position, first key, last key, -
+
+// ---- identity grouping (single-rank multi-pass).  If the previous apply's tell chunks, read in
+// bucket order, are already in key order -- up to one rotation -- and lie densely at [0, total) of
+// its tell arena, that arena IS the sorted new mail: no radix pass runs, k_bucket_bounds searches
+// it in place and the apply reads it there (InView).  Bucket d's inbox then holds exactly the mail
+// for d, each actor's in (sender bucket, sender, emission) order -- the canonical order of a stable
+// sort.  The rotation case (a ring's wrap-around: the last sender bucket's tells to actor 0) needs
+// the wrapped keys strictly below the first key, so no actor receives from both ends.
+// SURVEY.md §7 hard part 2: skipping the sort for a static topology is legitimate if the inbox
+// order is identical (akka-actor/src/main/scala/akka/dispatch/Mailbox.scala:89 enqueue order).
+__device__ __forceinline__ void ident_slice(const ChunkSortArgs& a, uint32_t sl, uint32_t nsl, uint32_t* scratch) {
+  __shared__ uint32_t s_tlast[kThreads], s_tfirst[kThreads];
+  __shared__ int s_iscr[kWaves + 1];
+  __shared__ uint32_t s_red[4];  // delta min / max, first / last thread with a non-empty chunk
+  const uint32_t tid = threadIdx.x;
+  if (sl >= nsl) {  // host-staged tells this superstep (any -> no identity)
+    uint32_t v = 0;
+    for (uint32_t i = tid; i < kStagedChunks; i += kThreads) v += a.ch.cnt[2 * a.ch.nb + i];
+    uint32_t t;
+    block_excl_sum<kThreads>(v, scratch, &t);
+    if (tid == 0) a.slsum[kMaxBlSlices * kSlSum] = t;
+    return;
+  }
+  if (tid == 0) {
+    s_red[0] = 0xFFFFFFFFu;
+    s_red[1] = 0u;
+    s_red[2] = 0xFFFFFFFFu;
+    s_red[3] = 0u;
+  }
+  const uint32_t c0 = sl * kBlSlice + tid * 8, nb = a.ch.nb;
+  uint32_t cnt[8], off[8], sum = 0;
+  uint4 m[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t c = c0 + j;
+    cnt[j] = c < nb ? a.ch.cnt[nb + c] : 0u;
+    off[j] = c < nb ? a.ch.off[nb + c] : 0u;
+    sum += cnt[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m[j] = cnt[j] ? a.emmeta[c0 + j] : make_uint4(0, 0, 0, 0);
+  uint32_t tot;
+  uint32_t p = block_excl_sum<kThreads>(sum, scratch, &tot);  // slice-local stream position (syncs s_red)
+  uint32_t dmin = 0xFFFFFFFFu, dmax = 0, nd = 0, pos = 0, tfirst = 0, tlast = 0, fpos = 0;
+  bool thas = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (cnt[j]) {
+      const uint32_t dv = off[j] - p;  // dense: off == slice base + position, for every chunk
+      dmin = min(dmin, dv);
+      dmax = max(dmax, dv);
+      if (m[j].z) pos = p + m[j].w;  // an internal descent (its position, used when it is the only one)
+      nd += min(m[j].z, 2u);
+      if (thas && m[j].x < tlast) {  // a descent where this chunk starts
+        ++nd;
+        pos = p;
+      }
+      if (!thas) {
+        tfirst = m[j].x;
+        fpos = p;
+      }
+      thas = true;
+      tlast = m[j].y;
+    }
+    p += cnt[j];
+  }
+  s_tlast[tid] = tlast;
+  s_tfirst[tid] = tfirst;
+  if (thas) {
+    atomicMin(&s_red[0], dmin);
+    atomicMax(&s_red[1], dmax);
+    atomicMin(&s_red[2], tid);
+    atomicMax(&s_red[3], tid);
+  }
+  const int prev = block_excl_max<kThreads>(thas ? (int)tid : -1, s_iscr);  // (syncs: s_tlast, s_red)
+  if (thas && prev >= 0 && tfirst < s_tlast[prev]) {  // a descent between the previous thread's chunks and ours
+    ++nd;
+    pos = fpos;
+  }
+  uint32_t tnd, tpos;
+  block_excl_sum2<kThreads>(min(nd, 2u), nd ? pos : 0u, scratch, &tnd, &tpos);  // (tpos valid when tnd == 1)
+  if (tid == 0) {
+    uint32_t* o = a.slsum + (size_t)sl * kSlSum;
+    const bool ne = s_red[2] != 0xFFFFFFFFu;
+    o[0] = tot;
+    o[1] = (ne ? 1u : 0u) | (ne && s_red[0] == s_red[1] ? 2u : 0u);
+    o[2] = s_red[0];  // every non-empty chunk sits at (this delta) + its stream position
+    o[3] = min(tnd, 2u);
+    o[4] = tpos;
+    o[5] = ne ? s_tfirst[s_red[2]] : 0u;
+    o[6] = ne ? s_tlast[s_red[3]] : 0u;
+  }
+}
+
+// The superstep's decision, one wave over the <= kMaxBlSlices slice summaries: ident = {on, rotation,
+// total}.  On iff no host-staged tells, every non-empty chunk at (stream position) in the arena
+// (dense from 0), and the stream in key order up to one descent whose wrapped keys stay strictly
+// below the first key (then sorted item i is stream item (i + rotation) mod total).
+static __global__ void __launch_bounds__(kWave) k_ident_combine(const uint32_t* slsum, uint32_t nsl, uint32_t* ident,
+                                                               unsigned long long* istats) {
+  const uint32_t s = lane_id();
+  const bool in = s < nsl;
+  const uint32_t* S = slsum + (size_t)(in ? s : 0u) * kSlSum;
+  const uint32_t tot = in ? S[0] : 0u, fl = in ? S[1] : 0u, s2 = S[2], s3 = S[3], s4 = S[4], s5 = S[5], s6 = S[6];
+  const bool ne = (fl & 1u) != 0;
+  const uint32_t inc = wave_incl_sum(tot), base = inc - tot;
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+  const bool dense = !ne || ((fl & 2u) != 0 && s2 == base);
+  uint32_t nd = ne ? s3 : 0u, pos = ne && s3 ? base + s4 : 0u;
+  const uint64_t nem = __ballot(ne);
+  const uint64_t before = nem & lanemask_lt();
+  const int prev = before ? 63 - __clzll((long long)before) : 0;
+  const uint32_t plast = (uint32_t)__shfl((int)s6, prev, kWave);
+  if (ne && before && s5 < plast) {  // a descent where this slice's mail starts
+    ++nd;
+    pos = base;
+  }
+  nd = min(nd, 2u);
+  const uint32_t ndt = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nd), kWave - 1);
+  const uint32_t post = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nd ? pos : 0u), kWave - 1);
+  const bool all_dense = __ballot(!dense) == 0;
+  const int fl0 = nem ? __builtin_ctzll(nem) : 0, fl1 = nem ? 63 - __clzll((long long)nem) : 0;
+  const uint32_t first_key = (uint32_t)__shfl((int)s5, fl0, kWave), last_key = (uint32_t)__shfl((int)s6, fl1, kWave);
+  if (s == 0) {
+    const uint32_t staged = slsum[kMaxBlSlices * kSlSum];
+    const bool on = all_dense && staged == 0 && total > 0 && (ndt == 0 || (ndt == 1 && last_key < first_key));
+    ident[0] = on ? 1u : 0u;
+    ident[1] = on && ndt ? post : 0u;
+    ident[2] = total;
+    if (on) atomicAdd(istats, 1ull);
+  }
+}
 
 // one block per digit: exclusive prefix over units (in place) + digit total;
 // block 0 also commits the previous step's stops.
@@ -409,6 +551,11 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs
     if (threadIdx.x == 0) *a.skew_n = 0u;
   }
   const uint32_t d = blockIdx.x;
+  const uint32_t nsl = (a.ch.nb + kBlSlice - 1) / kBlSlice;
+  if (a.emmeta && d >= (1u << a.bits) + nsl) {  // identity grouping: tell-chunk slices, then the staged total
+    ident_slice(a, d - (1u << a.bits) - nsl, nsl, scratch);
+    return;
+  }
   if (d >= (1u << a.bits) && a.bypass) {  // extra blocks: backlog prefix, one slice of kBlSlice buckets each
     const uint32_t sl = d - (1u << a.bits), i0 = sl * kBlSlice + threadIdx.x * 8;
     uint32_t v[8], sum = 0;
@@ -443,6 +590,7 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortAr
   const uint32_t nd = 1u << a.bits;
   const uint32_t total = digit_bases(a.tot, nd, s_dbase, scratch);
   const bool over = total > a.cap;  // the sorted mail must fit A (the apply checks mail + backlog)
+  const bool idn = a.ident && a.ident[0];  // identity grouping: nothing to move (histogram columns still zeroed)
   if (blockIdx.x == 0) {
     for (uint32_t d = tid; d < nd; d += kThreads) a.bstart[d] = s_dbase[d];
     if (tid == 0) {
@@ -481,6 +629,7 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortAr
       s_base[d] = s_dbase[d] + *hp;
       *hp = 0u;
     }
+    if (idn) continue;
     // the unit's chunks as one stream (tiles cross chunk boundaries: small chunks — skewed
     // or sparse supersteps — do not cost a tile each); chunk j of the unit holds stream
     // items [s_cpre[j], s_cpre[j+1])
@@ -540,6 +689,7 @@ struct SortArgs {
   uint32_t stride;
   uint32_t shift, bits;
   uint32_t super;  // envelopes per super-tile (kTile * 1..kSub): small inputs get more workgroups
+  const uint32_t* ident;  // single-rank multi-pass: [0] != 0 = identity grouping this superstep (no pass runs)
 };
 
 // Digit counts of four keys into a wave's LDS histogram.  Sorted-by-lower-bits input
@@ -564,6 +714,7 @@ __device__ __forceinline__ void count4(uint32_t* h, const uint4& v, uint32_t shi
 }
 
 static __global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
+  if (a.ident && a.ident[0]) return;  // identity grouping: the mail is already in key order
   __shared__ uint32_t h[kWaves][kRadix];
   const uint32_t n = *a.d_n, nt = div_up(n, a.super);
   const int tid = threadIdx.x, w = tid / kWave;
@@ -598,6 +749,7 @@ static __global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
 }
 
 static __global__ void __launch_bounds__(kThreads) k_sort_rowscan(SortArgs a) {
+  if (a.ident && a.ident[0]) return;
   __shared__ uint32_t scratch[kWaves + 1];
   const uint32_t d = blockIdx.x;
   if (d >= (1u << a.bits)) return;
@@ -606,6 +758,7 @@ static __global__ void __launch_bounds__(kThreads) k_sort_rowscan(SortArgs a) {
 }
 
 static __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) {
+  if (a.ident && a.ident[0]) return;
   __shared__ uint32_t whist[kWaves][kRadix];
   __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
   __shared__ uint32_t scratch[kWaves + 1];
@@ -678,7 +831,6 @@ constexpr int kBWaves = kBThreads / kWave;
 constexpr int kBIpt = kBucket / kBThreads;      // items per thread per sub-tile (4)
 constexpr int kBAct = kBucket / kBThreads;      // actors per thread (4)
 static_assert(kBAct == 4 && kBIpt == 4, "bucket_apply assumes 4 actors and 4 inbox items per thread");
-constexpr int kStagedChunks = 256;              // host-staged tells are split over this many chunks
 #ifndef AGX_NO_MONO
 constexpr bool kMonoShortcut = true;
 #else
@@ -773,7 +925,29 @@ struct BucketArgs {
   // bypass, plain behaviours: skewed buckets pre-partitioned by k_skew_* (see there); [i] = skew index
   const uint32_t* sk_rec;  // [i][kSkRec] bucket, bounds, parts, drained and queued totals
   const uint32_t* sk_act;  // [i][3][kBucket] per actor: admitted, drained-segment start, backlog start
+  // single-rank multi-pass, identity grouping (k_ident_combine): when ident[0] != 0 the sorted new mail
+  // is the previous apply's tell arena in_alt itself, rotated by ident[1] (n = ident[2]); emmeta
+  // (non-null in this mode) receives this superstep's per-chunk key summary for the next decision
+  const uint32_t* ident;
+  CMsgs in_alt;
+  uint4* emmeta;
 };
+
+// The sorted new mail of a single-rank multi-pass superstep: the radix passes' output, or --
+// identity grouping -- the previous apply's tell arena in place, whose concatenated chunks were
+// already in key order up to one rotation (a ring's wrap-around: sorted item i at (i + rot) mod n).
+struct InView {
+  CMsgs m;
+  uint32_t rot, n;
+  __device__ __forceinline__ uint32_t at(uint32_t i) const {
+    const uint32_t j = i + rot;
+    return j >= n ? j - n : j;
+  }
+};
+__device__ __forceinline__ InView in_view(const BucketArgs& a) {
+  if (a.ident && a.ident[0]) return InView{a.in_alt, a.ident[1], a.ident[2]};
+  return InView{a.in, 0u, 0xFFFFFFFFu};
+}
 
 #define AGX_STAMP(a, idx)                                                                         \
   do {                                                                                            \
@@ -1212,6 +1386,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       group_tells<true>(a, L, b, w, embase, emtot, a.em);
     } else {
       // compact the staged tells into the bucket's tell chunk (lane-consecutive actors: coalesced)
+      constexpr bool kMeta = !kGather && !kOwner && kLds;  // bypass fast path: the chunk's key summary
+      uint32_t* const ck = reinterpret_cast<uint32_t*>(L.U);  // (free: the state was written back)
       auto compact = [&](int j) {
         const uint32_t la = j * kBThreads + tid;
         const uint32_t s0 = L.seg[la], o = L.ecnt[la];
@@ -1219,6 +1395,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           a.em.key[embase + o + e] = stk[s0 + e];
           a.em.src[embase + o + e] = sts[s0 + e];
           a.em.pay[embase + o + e] = stp[s0 + e];
+          if constexpr (kMeta) ck[o + e] = stk[s0 + e];
         }
       };
       if constexpr (kUnrollActors) {
@@ -1230,6 +1407,25 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       if constexpr (kGather || kOwner) {  // (skew launch) grouped by destination from the em arena
         __syncthreads();
         group_tells<false>(a, L, b, w, embase, emtot, a.em);
+      }
+      if constexpr (kMeta) {
+        // identity grouping (k_ident_combine): first / last key of the chunk and its descents
+        // (positions i with key[i] < key[i - 1]) in sender order
+        if (a.emmeta) {
+          __syncthreads();
+          uint32_t nd = 0, dp = 0;
+#pragma unroll
+          for (uint32_t i = 4 * tid; i < 4 * tid + 4; ++i)
+            if (i > 0 && i < emtot && ck[i] < ck[i - 1]) {
+              ++nd;
+              dp = i;
+            }
+          uint32_t tnd, tdp;
+          block_excl_sum2<kBThreads>(nd, nd ? dp : 0u, L.scratch, &tnd, &tdp);  // (tdp is THE position if tnd == 1)
+          if (tid == 0) a.emmeta[b] = make_uint4(emtot ? ck[0] : 0u, emtot ? ck[emtot - 1] : 0u, tnd, tdp);
+        }
+      } else if constexpr (!kGather && !kOwner) {
+        if (a.emmeta && tid == 0) a.emmeta[b] = make_uint4(0u, 0u, 2u, 0u);  // (not summarised: forces a sort)
       }
     }
   } else {
@@ -1380,6 +1576,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   if (!kGather && tid == 0) {
     a.chunk_off[a.nb + b] = (uint32_t)embase;
     a.chunk_cnt[a.nb + b] = emtot;
+    if (!kOwner && !(!kWide && a.kmax == 1) && a.emmeta) a.emmeta[b] = make_uint4(0u, 0u, 2u, 0u);  // (phase A/B path)
   }
   __syncthreads();
   AGX_STAMP(a, 7);
@@ -1538,8 +1735,8 @@ struct TinyStageEmitter {
 };
 
 template <uint32_t KM>
-__device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uint32_t b, uint32_t lo, uint32_t cnt,
-                                            uint32_t xblc, uint32_t xblo, uint32_t xbst, uint32_t rpar,
+__device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& iv, TinyLds& T, uint32_t b, uint32_t lo,
+                                            uint32_t cnt, uint32_t xblc, uint32_t xblo, uint32_t xbst, uint32_t rpar,
                                             uint32_t wpar) {
   const DevParams& P = a.P;
   const uint32_t lane = lane_id();
@@ -1553,10 +1750,10 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uin
     for (uint32_t r = 0; r < kTinyIpl; ++r) {
       const uint32_t q = r * kWave + lane;
       const bool bl = q < xblc, ok = q < cnt;
-      const uint32_t i = !ok ? 0u : bl ? xblo + q : xbst + q - xblc;
-      k[r] = ldg(bl || !ok ? Bk : a.in.key, i);
-      sv[r] = ldg(bl || !ok ? Bs : a.in.src, i);
-      pv[r] = ldg(bl || !ok ? Bp : a.in.pay, i);
+      const uint32_t i = !ok ? 0u : bl ? xblo + q : iv.at(xbst + q - xblc);
+      k[r] = ldg(bl || !ok ? Bk : iv.m.key, i);
+      sv[r] = ldg(bl || !ok ? Bs : iv.m.src, i);
+      pv[r] = ldg(bl || !ok ? Bp : iv.m.pay, i);
     }
 #pragma unroll
     for (uint32_t r = 0; r < kTinyIpl; ++r) la[r] = r * kWave + lane < cnt ? k[r] & amask : 0xFFFFFFFFu;
@@ -1704,6 +1901,7 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, TinyLds& T, uin
     a.chunk_cnt[b] = bltot;
     a.chunk_off[a.nb + b] = (uint32_t)embase;
     a.chunk_cnt[a.nb + b] = emtot;
+    if (a.emmeta) a.emmeta[b] = make_uint4(0u, 0u, 2u, 0u);  // (wave path: not summarised, forces a sort)
   }
   const uint32_t v0 = wave_incl_sum(ndel), v1 = wave_incl_sum(ndead), v2 = wave_incl_sum(nunh),
                  v3 = wave_incl_sum(nall), v4 = wave_incl_sum(nact);
@@ -1756,8 +1954,9 @@ struct SkewArgs {
                       // rounded up separately: at most two parts beyond the budget each)
 };
 
-__device__ __forceinline__ uint32_t sk_key(const BucketArgs& a, const uint32_t* r, uint32_t rpar, uint32_t q) {
-  return q < r[3] ? a.g.bl[rpar].key[r[4] + q] : a.in.key[r[5] + q - r[3]];
+__device__ __forceinline__ uint32_t sk_key(const BucketArgs& a, const InView& iv, const uint32_t* r, uint32_t rpar,
+                                           uint32_t q) {
+  return q < r[3] ? a.g.bl[rpar].key[r[4] + q] : iv.m.key[iv.at(r[5] + q - r[3])];
 }
 
 static __global__ void __launch_bounds__(kScanThreads) k_skew_plan(BucketArgs a, SkewArgs k) {
@@ -1844,6 +2043,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_count(BucketArgs a, S
     if (blockIdx.x == 0 && tid == 0) atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
     return;
   }
+  const InView iv = in_view(a);
   for (uint32_t t = blockIdx.x; t < nparts; t += gridDim.x) {
     for (uint32_t i = tid; i < kBucket; i += kBThreads) s_c[i] = 0;
     sk_part(a, k, t, s_q);
@@ -1852,7 +2052,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_count(BucketArgs a, S
     for (uint32_t q = q0 + tid; q < q1; q += 8 * kBThreads) {  // 8 loads in flight
       uint32_t kk[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) kk[j] = q + j * kBThreads < q1 ? sk_key(a, r, rpar, q + j * kBThreads) : 0u;
+      for (int j = 0; j < 8; ++j) kk[j] = q + j * kBThreads < q1 ? sk_key(a, iv, r, rpar, q + j * kBThreads) : 0u;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (q + j * kBThreads < q1) lds_hist_inc(s_c, kk[j] & amask);
@@ -1927,6 +2127,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
   const uint64_t ltm = lanemask_lt();
   const Msgs blw = a.g.bl[wpar];
   if (nparts > k.max_parts) return;
+  const InView iv = in_view(a);
   for (uint32_t t = blockIdx.x; t < nparts; t += gridDim.x) {
     sk_part(a, k, t, s_q);
     const uint32_t i = s_q[0], q0 = s_q[1], q1 = s_q[2];
@@ -1979,7 +2180,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
 #pragma unroll
       for (int u = 0; u < kBIpt; ++u) {
         const uint32_t q = wbase + u * kWave + lane;
-        kk[u] = q < q1 ? sk_key(a, r, rpar, q) : 0u;
+        kk[u] = q < q1 ? sk_key(a, iv, r, rpar, q) : 0u;
       }
 #pragma unroll
       for (int u = 0; u < kBIpt; ++u) {
@@ -1997,8 +2198,9 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
             sv[u] = a.g.bl[rpar].src[blo + q];
             pv[u] = a.g.bl[rpar].pay[blo + q];
           } else {
-            sv[u] = a.in.src[bst + q - blc];
-            pv[u] = a.in.pay[bst + q - blc];
+            const uint32_t x = iv.at(bst + q - blc);
+            sv[u] = iv.m.src[x];
+            pv[u] = iv.m.pay[x];
           }
         }
       }
@@ -2071,6 +2273,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
   const GatherArgs& g = a.g;
   // (kBypass: single-rank multi-pass — the previous backlog is read in place, not sorted)
   constexpr bool kBypass = !kGather && !kOwner;
+  const InView iv = kBypass ? in_view(a) : InView{a.in, 0u, 0xFFFFFFFFu};  // (identity grouping: rotated tells)
   // fused / bypass: write parity w, read parity w ^ 1
   const uint32_t wpar = kGather ? a.par : kBypass ? (*a.pstep & 1u) : 0u, rpar = wpar ^ 1u;
   uint32_t* const skew_n = a.skew_n + (kGather ? wpar : 0u);  // (non-fused: one list, reset by the sort)
@@ -2126,7 +2329,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         blo = (uint32_t)__builtin_amdgcn_readlane((int)blo, 0);
         tiny = hi_w - lo_w <= a.tiny_max && (uint64_t)hi_w <= a.cap;  // (over capacity: the block path reports it)
         if (tiny)
-          tiny_bucket<KM>(a, reinterpret_cast<TinyLds*>(U)[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
+          tiny_bucket<KM>(a, iv, reinterpret_cast<TinyLds*>(U)[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
       }
       if (lane == 0) s_tiny[w] = tiny || bw >= a.nb;
       __syncthreads();
@@ -2291,7 +2494,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
               idx[r] = xblo + q;
             } else {
               sel[r] = 1;
-              idx[r] = xbst + q - xblc;
+              idx[r] = iv.at(xbst + q - xblc);
             }
           }
         }
@@ -2316,9 +2519,9 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
             ps = sel[r] == 0 ? Bs : sel[r] == 1 ? Es : g.stg.src;
             pp = sel[r] == 0 ? Bp : sel[r] == 1 ? Ep : g.stg.pay;
           } else if (kBypass) {
-            pk = sel[r] == 0 ? Bk : a.in.key;
-            ps = sel[r] == 0 ? Bs : a.in.src;
-            pp = sel[r] == 0 ? Bp : a.in.pay;
+            pk = sel[r] == 0 ? Bk : iv.m.key;
+            ps = sel[r] == 0 ? Bs : iv.m.src;
+            pp = sel[r] == 0 ? Bp : iv.m.pay;
           } else {
             pk = a.in.key;
             ps = a.in.src;
@@ -2425,7 +2628,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
       auto gkey = [&](uint32_t q) -> uint32_t {
         if (kGather) return gv.key(g, rpar, q);
         if (kBypass && q < xblc) return g.bl[rpar].key[xblo + q];
-        return a.in.key[xbst + q - xblc];
+        return iv.m.key[iv.at(xbst + q - xblc)];
       };
       if constexpr (kBypass && !kWide) {
         // pre-partitioned by k_skew_* (above): the drained messages are in the scratch copy at
@@ -2516,8 +2719,9 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
               sv[r] = g.bl[rpar].src[xblo + q];
               pv[r] = g.bl[rpar].pay[xblo + q];
             } else {
-              sv[r] = a.in.src[xbst + q - xblc];
-              pv[r] = a.in.pay[xbst + q - xblc];
+              const uint32_t x = iv.at(xbst + q - xblc);
+              sv[r] = iv.m.src[x];
+              pv[r] = iv.m.pay[x];
             }
           }
         }
@@ -2564,14 +2768,20 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
 // Bucket starts after a multi-pass sort: bstart[x] = first index with bucket >= x
 // (one thread per bucket, binary search over the sorted keys; the top levels of every
 // search hit the same cached lines).
+// Identity grouping (ident[0] != 0): the same search over the previous apply's tell arena in place,
+// sorted item i at (i + ident[1]) mod ident[2].
 static __global__ void __launch_bounds__(kThreads) k_bucket_bounds(const uint32_t* key, const uint32_t* d_n, uint32_t nb,
-                                                            uint32_t bb, uint32_t* bstart) {
-  const uint32_t n = *d_n;
+                                                            uint32_t bb, uint32_t* bstart, const uint32_t* ident,
+                                                            const uint32_t* key_alt) {
+  const bool idn = ident && ident[0];
+  const uint32_t n = idn ? ident[2] : *d_n, rot = idn ? ident[1] : 0u;
+  const uint32_t* k = idn ? key_alt : key;
   for (uint32_t x = blockIdx.x * kThreads + threadIdx.x; x <= nb; x += gridDim.x * kThreads) {
     uint32_t lo = 0, hi = n;
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (((key[mid] & kLocalMask) >> bb) < x) lo = mid + 1; else hi = mid;
+      const uint32_t j = mid + rot;
+      if (((k[j >= n ? j - n : j] & kLocalMask) >> bb) < x) lo = mid + 1; else hi = mid;
     }
     bstart[x] = lo;
   }
