@@ -13,8 +13,9 @@ export TMPDIR=/tmp
 TAG=${1:-run}
 fail() { echo "$1 failed"; tail -40 "$2"; exit 1; }
 if [ -n "$BUILD" ]; then
-  /usr/bin/time -f "build %e s" timeout -k 10 600 python -c "import __graft_entry__ as g; g.build_native(force=True)" > gpurun_out/${TAG}_build.log 2>&1 || fail build gpurun_out/${TAG}_build.log
-  tail -1 gpurun_out/${TAG}_build.log
+  t0=$(date +%s)
+  timeout -k 10 600 python -c "import __graft_entry__ as g; g.build_native(force=True)" > gpurun_out/${TAG}_build.log 2>&1 || fail build gpurun_out/${TAG}_build.log
+  echo "build on the box: $(( $(date +%s) - t0 )) s" | tee -a gpurun_out/${TAG}_build.log
 fi
 if [ -n "$TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 280 --timeout-method thread ${TEST_ARGS} > gpurun_out/${TAG}_pytest.log 2>&1 || fail pytest gpurun_out/${TAG}_pytest.log
