@@ -79,6 +79,10 @@ SIGNATURES = {
     "agx_register_range": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.c_void_p, ctypes.c_size_t]),
     "agx_set_ring": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32]),
+    "agx_set_mailbox_class": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]),
+    "agx_set_mailbox": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]),
+    "agx_set_outbound": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]),
+    "agx_take_outbound": (ctypes.c_int32, [ctypes.c_void_p, c_u32p, c_u32p, c_u32p, ctypes.c_uint64, c_u64p]),
     "agx_set_gossip": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64]),
     "agx_set_delta_crdt": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32]),
     "agx_set_behaviors": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,

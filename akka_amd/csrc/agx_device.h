@@ -46,7 +46,47 @@ struct DevParams {
   const agx_act* bact;
   const uint32_t* bfirst;
   uint32_t n_beh;
+  // the reply path (agx_set_outbound): tells to ids [host_lo, host_lo + host_n) go to the outbox
+  uint32_t host_lo, host_n, outbox_cap;
+  uint32_t* outbox;     // [outbox_cap][3] dst, src, payload
+  uint32_t* outbox_n;   // envelopes appended (may pass outbox_cap: reported as a capacity error)
+  // mailbox classes (agx_set_mailbox_class): the class of an actor is bits 1..3 of its alive byte;
+  // nmc == 0 -> every actor uses class 0 (C, T above); else capacity mcap[class], drain
+  // min(Tr, capacity) (Tr = the dispatcher throughput, >= 1)
+  uint32_t nmc, Tr;
+  uint32_t mcap[AGX_MAX_MAILBOX_CLASSES];
 };
+
+// An actor's bounded capacity (0 = unbounded) and drain limit from its alive byte (bit 0 = alive,
+// bits 1..3 = mailbox class): Mailboxes.lookupConfigurator per actor (Mailboxes.scala:204-260).
+__device__ __forceinline__ void mbox_limits(const DevParams& P, uint32_t abyte, uint32_t& C, uint32_t& T) {
+  if (P.nmc == 0) {  // (uniform: one mailbox type for the whole dispatcher)
+    C = P.C;
+    T = P.T;
+    return;
+  }
+  C = P.mcap[(abyte >> 1) & (AGX_MAX_MAILBOX_CLASSES - 1)];
+  T = C && P.Tr > C ? C : P.Tr;
+}
+
+// A tell to a host-side actor (agx_set_outbound): appended to the outbox (when `write`); returns
+// false for any other id.  One thread's appends are ordered (same counter, program order), so each
+// sender's outbound tells keep their emission order.
+__device__ __forceinline__ bool outbound_tell(const DevParams& P, uint32_t dst, uint32_t src, uint32_t pay,
+                                              bool write) {
+  if (dst - P.host_lo >= P.host_n) return false;
+  if (write) {
+    const uint32_t i = atomicAdd(P.outbox_n, 1u);
+    if (i < P.outbox_cap) {
+      P.outbox[3 * (size_t)i] = dst;
+      P.outbox[3 * (size_t)i + 1] = src;
+      P.outbox[3 * (size_t)i + 2] = pay;
+    } else {
+      atomicOr(P.err, 1ull);  // kErrCapacity
+    }
+  }
+  return true;
+}
 
 // ------------------------------------------------------------------ RNG
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {

@@ -111,6 +111,16 @@ struct agx_engine {
   uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0;
   uint32_t max_supers = 1, dstride = 4, dsuper = kSuper;  // dense passes: super-tiles, table row stride, tile size
   uint32_t T = 1, C = 0, W = 1, kmax = 1, R = 1, rank = 0, num_shards = 1000, key_bits = 1;
+  uint32_t Traw = 1;  // dispatcher throughput (>= 1); T = min(Traw, C) for the default mailbox class
+  // mailbox classes (agx_set_mailbox_class): capacity per class, class 0 = cfg.capacity
+  uint32_t mcap[AGX_MAX_MAILBOX_CLASSES] = {0};
+  uint32_t mclass_set = 1u;  // bit c: class c configured (class 0 always)
+  bool mclasses = false;     // some class other than 0 configured: kernels look up per-actor limits
+  // the reply path (agx_set_outbound): host-side actor ids and the outbox
+  uint32_t host_lo = 0, host_n = 0;
+  uint64_t outbox_cap = 0;
+  uint32_t *d_outbox = nullptr, *d_outbox_n = nullptr;
+  std::vector<uint32_t> outq;  // taken from the device, not yet handed to the host (dst, src, payload)
   uint32_t bb = kBucketBits;  // bucket bits (agx_cfg.bucket_actors)
 
   // sharding tables (R > 1)
@@ -321,6 +331,14 @@ DevParams make_params(agx_engine* e) {
   P.W = e->W;
   P.T = e->T;
   P.C = e->C;
+  P.Tr = e->Traw;
+  P.nmc = e->mclasses ? 1u : 0u;
+  for (uint32_t c = 0; c < AGX_MAX_MAILBOX_CLASSES; ++c) P.mcap[c] = e->mcap[c];
+  P.host_lo = e->host_lo;
+  P.host_n = e->host_n;
+  P.outbox = e->d_outbox;
+  P.outbox_n = e->d_outbox_n;
+  P.outbox_cap = (uint32_t)e->outbox_cap;
   P.R = e->R;
   P.rank = e->rank;
   P.kmax = e->kmax;
@@ -1258,7 +1276,9 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->cfg = *cfg;
   e->n_global = cfg->n_actors;
   e->T = cfg->throughput == 0 || (int32_t)cfg->throughput < 0 ? 1u : cfg->throughput;  // Mailbox.scala:261
+  e->Traw = e->T;
   e->C = cfg->capacity;
+  e->mcap[0] = e->C;
   if (e->C && e->T > e->C) e->T = e->C;  // a bounded queue never holds more than C: drain <= min(T, C)
   e->W = cfg->n_words;
   e->kmax = std::max<uint32_t>(1, cfg->max_emit);
@@ -1419,7 +1439,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     e->sk_budget = (uint32_t)std::min<uint64_t>(8192, e->cap / kSkSpan + 1);
     e->sk_rows = e->sk_budget + 2 * (uint32_t)nsk;
     CREATE_TRY(dalloc(&e->d_sk_rec, (uint64_t)e->nb * kSkRec));
-    CREATE_TRY(dalloc(&e->d_sk_act, nsk * 3 * kBucket));
+    CREATE_TRY(dalloc(&e->d_sk_act, nsk * kSkActPlanes * kBucket));
     CREATE_TRY(dalloc(&e->d_sk_pc, (uint64_t)e->sk_rows * kBucket));
     CREATE_TRY(dalloc(&e->d_sk_meta, 4));
   }
@@ -1514,6 +1534,7 @@ agx_status agx_destroy(agx_engine* e) {
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
   free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1); free_msgs(e->em2);
   hipFree(e->d_emmeta); hipFree(e->d_slsum); hipFree(e->d_ident);
+  hipFree(e->d_outbox); hipFree(e->d_outbox_n);
   hipFree(e->d_s2p); hipFree(e->d_rcvp);
   for (int q = 0; q < 2; ++q) {
     hipFree(e->d_tcnt[q]); hipFree(e->d_toff[q]); hipFree(e->d_blo[q]); hipFree(e->d_blc[q]); hipFree(e->d_emc[q]);
@@ -1570,7 +1591,7 @@ agx_status agx_register_range(agx_engine* e, uint64_t first_id, uint64_t count, 
       l = id;
     }
     e->h_kind[l] = (uint8_t)kind;
-    e->h_alive[l] = kind != AGX_KIND_NONE;
+    e->h_alive[l] = (uint8_t)((e->h_alive[l] & 0xFEu) | (kind != AGX_KIND_NONE ? 1u : 0u));  // (bits 1..3: mailbox class)
     for (uint32_t w = 0; w < e->W; ++w) {
       uint64_t v = 0;
       if (ib) memcpy(&v, ib + i * stride + w * 8, 8);
@@ -1578,6 +1599,96 @@ agx_status agx_register_range(agx_engine* e, uint64_t first_id, uint64_t count, 
     }
   }
   e->actors_dirty = true;
+  return AGX_OK;
+}
+
+agx_status agx_set_mailbox_class(agx_engine* e, uint32_t cls, uint32_t capacity) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  if (cls == 0 || cls >= AGX_MAX_MAILBOX_CLASSES)
+    return set_err(AGX_EINVAL, "mailbox class %u: classes 1..%u are configurable (0 is agx_cfg.capacity)", cls,
+                   AGX_MAX_MAILBOX_CLASSES - 1);
+  e->mcap[cls] = capacity;
+  e->mclass_set |= 1u << cls;
+  e->mclasses = true;
+  drop_graphs(e);  // the class table is a kernel parameter captured in the superstep graphs
+  return AGX_OK;
+}
+
+agx_status agx_set_mailbox(agx_engine* e, uint64_t first_id, uint64_t count, uint32_t cls) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  if (cls >= AGX_MAX_MAILBOX_CLASSES || !((e->mclass_set >> cls) & 1u))
+    return set_err(AGX_EINVAL, "mailbox class %u is not configured (agx_set_mailbox_class)", cls);
+  if (first_id + count > e->n_global) return set_err(AGX_EINVAL, "bad actor range");
+  AGX_TRY(ensure_dev(e));
+  AGX_TRY(sync_mirrors(e));  // device state is authoritative after a run
+  for (uint64_t i = 0; i < count; ++i) {
+    const uint64_t id = first_id + i;
+    uint64_t l = id;
+    if (e->R > 1) {
+      const uint32_t r = e->h_route[id];
+      if ((r >> kOwnerShift) != e->rank) continue;
+      l = r & kLocalMask;
+    }
+    e->h_alive[l] = (uint8_t)((e->h_alive[l] & 1u) | (cls << 1));
+  }
+  e->actors_dirty = true;
+  return AGX_OK;
+}
+
+agx_status agx_set_outbound(agx_engine* e, uint32_t first_host_id, uint32_t n_host, uint64_t capacity) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  if (n_host && (first_host_id < e->n_global || (uint64_t)first_host_id + n_host > (1ull << 31)))
+    return set_err(AGX_EINVAL, "host ids must lie in [n_actors, 2^31) (bit 31 of a sender tags CRDT state gossips)");
+  if (n_host && (capacity == 0 || capacity > 0x3FFFFFFFull))
+    return set_err(AGX_EINVAL, "outbox capacity must be in [1, 2^30)");
+  AGX_TRY(ensure_dev(e));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (!e->d_outbox_n) {
+    AGX_TRY(dalloc(&e->d_outbox_n, 1));
+    HIP_TRY(hipMemset(e->d_outbox_n, 0, 4));
+  }
+  if (n_host && capacity != e->outbox_cap) {
+    hipFree(e->d_outbox);
+    e->d_outbox = nullptr;
+    AGX_TRY(dalloc(&e->d_outbox, 3 * capacity));
+    e->outbox_cap = capacity;
+  }
+  HIP_TRY(hipDeviceSynchronize());  // (null-stream allocation / memset before the engine stream uses them)
+  e->host_lo = first_host_id;
+  e->host_n = n_host;
+  drop_graphs(e);  // the host-id range is a kernel parameter captured in the superstep graphs
+  return AGX_OK;
+}
+
+agx_status agx_take_outbound(agx_engine* e, uint32_t* dst, uint32_t* src, uint32_t* payload, uint64_t cap,
+                             uint64_t* n) {
+  if (!e || !n || (cap && (!dst || !src || !payload))) return set_err(AGX_EINVAL, "bad take_outbound args");
+  *n = 0;
+  AGX_TRY(ensure_dev(e));
+  if (e->d_outbox_n) {  // move the device outbox to the host queue (the engine is idle between calls)
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    uint32_t cnt = 0;
+    HIP_TRY(hipMemcpy(&cnt, e->d_outbox_n, 4, hipMemcpyDeviceToHost));
+    const uint64_t m = std::min<uint64_t>(cnt, e->outbox_cap);
+    if (m) {
+      const size_t o = e->outq.size();
+      e->outq.resize(o + 3 * m);
+      HIP_TRY(hipMemcpy(e->outq.data() + o, e->d_outbox, 12 * m, hipMemcpyDeviceToHost));
+    }
+    if (cnt) HIP_TRY(hipMemset(e->d_outbox_n, 0, 4));
+    HIP_TRY(hipDeviceSynchronize());
+    if (cnt > e->outbox_cap)
+      return set_err(AGX_ECAPACITY, "%u outbound tells since the last agx_take_outbound, outbox capacity %llu",
+                     cnt, (unsigned long long)e->outbox_cap);
+  }
+  const uint64_t k = std::min<uint64_t>(cap, e->outq.size() / 3);
+  for (uint64_t i = 0; i < k; ++i) {
+    dst[i] = e->outq[3 * i];
+    src[i] = e->outq[3 * i + 1];
+    payload[i] = e->outq[3 * i + 2];
+  }
+  e->outq.erase(e->outq.begin(), e->outq.begin() + 3 * k);
+  *n = k;
   return AGX_OK;
 }
 
@@ -1849,7 +1960,7 @@ agx_status agx_read_state(agx_engine* e, uint64_t first_id, uint64_t count, uint
     }
     if (words)
       for (uint32_t w = 0; w < e->W; ++w) words[i * e->W + w] = e->h_state[(uint64_t)w * e->n_local + l];
-    if (alive) alive[i] = e->h_alive[l];
+    if (alive) alive[i] = e->h_alive[l] & 1u;
   }
   return AGX_OK;
 }

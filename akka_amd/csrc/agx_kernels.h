@@ -79,7 +79,7 @@ __device__ __forceinline__ void begin_step(uint32_t* step, uint32_t* heap_top) {
 // alive-at-step-start value — deterministic across block schedules.)
 __device__ __forceinline__ void commit_stops(uint8_t* alive, const uint32_t* stopq, uint32_t* nstop) {
   const uint32_t ns = *nstop;
-  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) alive[stopq[i]] = 0;
+  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) alive[stopq[i]] &= 0xFEu;  // (bits 1..3: mailbox class)
   __syncthreads();
   if (threadIdx.x == 0) *nstop = 0;
 }
@@ -795,8 +795,11 @@ struct Emitter {
   uint32_t* nh;       // next-pass digit histogram (LDS)
   uint32_t nh_shift, nh_mask;
   __device__ __forceinline__ void operator()(uint32_t dst, uint32_t pay) {
+    if (dst >= P->n_global) {  // a host-side actor (the reply path: outbox) or an unknown ref -> deadLetters
+      if (!outbound_tell(*P, dst, self, pay, kWrite)) ++n_all;
+      return;
+    }
     ++n_all;
-    if (dst >= P->n_global) return;  // unknown ref -> deadLetters
     ++n_valid;
     if (kWrite) {
       const uint32_t key = (P->R > 1) ? P->route[dst] : dst;
@@ -853,8 +856,11 @@ struct EmitterLds {
   uint32_t* nh;
   uint32_t nh_shift, nh_mask;
   __device__ __forceinline__ void operator()(uint32_t dst, uint32_t p) {
+    if (dst >= P->n_global) {  // a host-side actor (the reply path: outbox) or an unknown ref -> deadLetters
+      if (!outbound_tell(*P, dst, self, p, true)) ++n_all;
+      return;
+    }
     ++n_all;
-    if (dst >= P->n_global) return;  // unknown ref -> deadLetters
     ++n_valid;
     const uint32_t k = (P->R > 1) ? P->route[dst] : dst;
     key[slot] = k;
@@ -1095,7 +1101,6 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
                                               uint32_t (&acc)[kBStats], uint32_t bl_given = 0xFFFFFFFFu) {
   const DevParams& P = a.P;
   const int tid = threadIdx.x;
-  const uint32_t T = P.T, C = P.C;
   const uint32_t nhmask = (1u << a.nx_bits) - 1u;
   auto ikey = [&](uint32_t q) -> uint32_t { return kLds ? L.key[q] : a.scr.key[lo + q]; };
   auto isrc = [&](uint32_t q) -> uint32_t { return kLds ? L.src[q] : a.scr.src[lo + q]; };
@@ -1123,9 +1128,12 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     const uint32_t len = L.seg[la + 1] - L.seg[la];
     uint32_t q = 0;
     if (len) {
-      if (!L.alive[la]) {
+      const uint32_t ab = L.alive[la];
+      if (!(ab & 1u)) {
         ndead += len;
       } else {
+        uint32_t C, T;
+        mbox_limits(P, ab, C, T);
         const uint32_t keep = (C == 0 || len < C) ? len : C;  // admitted (tail-drop beyond C)
         ndead += len - keep;
         q = keep > T ? keep - T : 0u;
@@ -1159,8 +1167,11 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       const uint32_t la = key & ((1u << a.bb) - 1u);
       const uint32_t p = q - L.seg[la];
       const uint32_t len = L.seg[la + 1] - L.seg[la];
+      const uint32_t ab = L.alive[la];
+      uint32_t C, T;
+      mbox_limits(P, ab, C, T);
       const uint32_t keep = (C == 0 || len < C) ? len : C;
-      const bool queued = L.alive[la] && p >= T && p < keep;
+      const bool queued = (ab & 1u) && p >= T && p < keep;
       const uint32_t sv = isrc(q);
       uint32_t pv = ipay(q);
       if (kWide) {  // a queued state gossip outlives its row's superstep: copy the row forward
@@ -1209,7 +1220,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
 #pragma unroll
       for (int j = 0; j < kBAct; ++j) {
         const uint32_t la = j * kBThreads + tid;
-        const bool has = la < na && L.alive[la] && L.seg[la + 1] != L.seg[la];
+        const bool has = la < na && (L.alive[la] & 1u) && L.seg[la + 1] != L.seg[la];
         const uint32_t l = a0 + la;
         kd[j] = has && kKindNeeded ? P.kind[l] : 0u;  // single-kind variants never read it
         x0[j] = has ? ldg64(P.state, l) : 0ull;  // (32-bit offsets: one VGPR per address)
@@ -1224,7 +1235,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
       const uint32_t la = j * kBThreads + tid;
-      const bool has = la < na && L.alive[la] && L.seg[la + 1] != L.seg[la];
+      const bool has = la < na && (L.alive[la] & 1u) && L.seg[la + 1] != L.seg[la];
       hasm |= has ? 1u << j : 0u;
       li[j] = has ? a0 + la : 0u;
     }
@@ -1286,12 +1297,14 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       const uint32_t la = j * kBThreads + tid;
       const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
       ecl[j] = 0;
-      if (la >= na || !len || !L.alive[la]) return;
+      if (la >= na || !len || !(L.alive[la] & 1u)) return;
       const uint32_t l = a0 + la;
       const uint32_t self = P.R > 1 ? P.gid[l] : l;
       EmitterLds em{&P, stk, sts, stp, s0, self, 0, 0, L.nh, a.nx_shift, nhmask};
       uint64_t wv[2] = {w0s[la], w1s[la]};
-      const uint32_t nd = min(len, T);
+      uint32_t Ca, Ta;
+      mbox_limits(P, L.alive[la], Ca, Ta);
+      const uint32_t nd = min(len, Ta);
       uint32_t kcur = L.kind[la];  // (a compiled behaviour's become changes it)
       ++nact;
       uint64_t hb = 0;
@@ -1321,7 +1334,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         ++ndel;
         if (r == AGX_RES_UNHANDLED) ++nunh;
         if (r == AGX_RES_STOPPED) {
-          if constexpr (kGather) P.alive[l] = 0;  // fused: only this block reads this bucket's flags
+          if constexpr (kGather) P.alive[l] = L.alive[la] & 0xFEu;  // fused: only this block reads this bucket's flags
           else P.stopq[atomicAdd(P.nstop, 1u)] = l;
           ndead += nd - q - 1;  // drained-but-unprocessed after the stop
           break;
@@ -1435,12 +1448,14 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     for (int j = 0; j < kBAct; ++j) {
       const uint32_t la = j * kBThreads + tid;
       const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
-      if (la >= na || !len || !L.alive[la]) continue;
+      if (la >= na || !len || !(L.alive[la] & 1u)) continue;
       const uint32_t l = a0 + la;
       const uint32_t self = P.R > 1 ? P.gid[l] : l;
       Emitter<false> em{&P, {}, 0, self, 0, 0, L.nh, a.nx_shift, nhmask};
       uint64_t wv[2] = {w0s[la], w1s[la]};  // behaviours read/write state words 0-1 only
-      const uint32_t nd = min(len, T);
+      uint32_t Ca, Ta;
+      mbox_limits(P, L.alive[la], Ca, Ta);
+      const uint32_t nd = min(len, Ta);
       uint32_t kd = L.kind[la];
       if (kWide && is_crdt(kd)) {
         DeltaSim ds;
@@ -1512,12 +1527,14 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     for (int j = 0; j < kBAct; ++j) {
       const uint32_t la = j * kBThreads + tid;
       const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
-      if (la >= na || !len || !L.alive[la]) continue;
+      if (la >= na || !len || !(L.alive[la] & 1u)) continue;
       const uint32_t l = a0 + la;
       const uint32_t self = P.R > 1 ? P.gid[l] : l;
       Emitter<true> em{&P, a.em, embase + L.ecnt[la], self, 0, 0, L.nh, a.nx_shift, nhmask};
       uint64_t wv[2] = {w0s[la], w1s[la]};  // behaviours read/write state words 0-1 only
-      const uint32_t nd = min(len, T);
+      uint32_t Ca, Ta;
+      mbox_limits(P, L.alive[la], Ca, Ta);
+      const uint32_t nd = min(len, Ta);
       uint32_t kd = L.kind[la];
       ++nact;
       if (kWide && is_crdt(kd)) {
@@ -1553,7 +1570,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
             const uint32_t r = apply_msg<KM>(P, kd, self, l, wv, svb[u], pvb[u], em);
             if (r == AGX_RES_UNHANDLED) ++nunh;
             if (r == AGX_RES_STOPPED) {
-              if constexpr (kGather) P.alive[l] = 0;  // fused: only this block reads this bucket's flags
+              if constexpr (kGather) P.alive[l] = L.alive[la] & 0xFEu;  // fused: only this block reads this bucket's flags
               else P.stopq[atomicAdd(P.nstop, 1u)] = l;
               ndead += nd - (q0 + u) - 1;  // drained-but-unprocessed after the stop
               stop = true;
@@ -1704,8 +1721,11 @@ struct TinyEmitter {
   uint32_t self, col, nhmask;
   uint32_t n_valid, n_all;
   __device__ __forceinline__ void operator()(uint32_t dst, uint32_t pay) {
+    if (dst >= P->n_global) {  // the reply path (outbox) or an unknown ref -> deadLetters
+      if (!outbound_tell(*P, dst, self, pay, true)) ++n_all;
+      return;
+    }
     ++n_all;
-    if (dst >= P->n_global) return;  // unknown ref -> deadLetters
     ++n_valid;
     a->em.key[pos] = dst;  // (single rank: key = local id = global id)
     a->em.src[pos] = self;
@@ -1723,8 +1743,11 @@ struct TinyStageEmitter {
   uint32_t slot, self;
   uint32_t n_valid, n_all;
   __device__ __forceinline__ void operator()(uint32_t dst, uint32_t pay) {
+    if (dst >= P->n_global) {  // the reply path (outbox) or an unknown ref -> deadLetters
+      if (!outbound_tell(*P, dst, self, pay, true)) ++n_all;
+      return;
+    }
     ++n_all;
-    if (dst >= P->n_global) return;  // unknown ref -> deadLetters
     ++n_valid;
     T->key[slot] = dst;
     T->src[slot] = self;
@@ -1741,7 +1764,6 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
   const DevParams& P = a.P;
   const uint32_t lane = lane_id();
   const uint32_t amask = (1u << a.bb) - 1u, a0 = b << a.bb;
-  const uint32_t Tt = P.T, C = P.C;
   // ---- items, and their stable rank by (actor, inbox position) over the whole inbox
   uint32_t k[kTinyIpl], sv[kTinyIpl], pv[kTinyIpl], la[kTinyIpl];
   {  // all loads back to back (selected SGPR bases, no branch around the loads)
@@ -1783,7 +1805,8 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // ---- per actor (the head of its run of sorted positions; lane l owns positions 2l, 2l + 1,
   // so lane order is actor order)
-  uint32_t hl[kTinyIpl], hlen[kTinyIpl], hkeep[kTinyIpl], hkind[kTinyIpl], nd[kTinyIpl];
+  uint32_t hl[kTinyIpl], hlen[kTinyIpl], hkeep[kTinyIpl], hkind[kTinyIpl], nd[kTinyIpl], hab[kTinyIpl],
+      hT[kTinyIpl];
   uint64_t hw0[kTinyIpl], hw1[kTinyIpl];
   bool head[kTinyIpl], hal[kTinyIpl];
 #pragma unroll
@@ -1795,7 +1818,7 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
   }
 #pragma unroll
   for (uint32_t i = 0; i < kTinyIpl; ++i) {  // (all loads in flight together)
-    hal[i] = head[i] && P.alive[hl[i]];
+    hab[i] = head[i] ? P.alive[hl[i]] : 0u;
     hkind[i] = head[i] ? P.kind[hl[i]] : 0u;
     hw0[i] = head[i] ? ldg64(P.state, hl[i]) : 0ull;
     hw1[i] = head[i] && P.W > 1 ? ldg64(P.state, P.n_local + hl[i]) : 0ull;
@@ -1803,8 +1826,12 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
   uint32_t ndead = 0, nq = 0;
 #pragma unroll
   for (uint32_t i = 0; i < kTinyIpl; ++i) {
+    uint32_t C, Tt;
+    mbox_limits(P, hab[i], C, Tt);
+    hal[i] = (hab[i] & 1u) != 0;
     const uint32_t keep = !hal[i] ? 0u : (C == 0 || hlen[i] < C) ? hlen[i] : C;  // tail-drop beyond C
     hkeep[i] = keep;
+    hT[i] = Tt;
     ndead += hlen[i] - keep;
     nd[i] = hal[i] ? min(hlen[i], Tt) : 0u;
     nq += keep > Tt ? keep - Tt : 0u;
@@ -1817,7 +1844,7 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
 #pragma unroll
   for (uint32_t i = 0; i < kTinyIpl; ++i) {  // queued beyond the throughput cap, in order
     const uint32_t p0 = lane * kTinyIpl + i;
-    for (uint32_t q = Tt; q < hkeep[i]; ++q, ++qoff) {
+    for (uint32_t q = hT[i]; q < hkeep[i]; ++q, ++qoff) {
       blw.key[lo + qoff] = T.key[p0 + q];
       blw.src[lo + qoff] = T.src[p0 + q];
       blw.pay[lo + qoff] = T.pay[p0 + q];
@@ -1943,10 +1970,11 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
 // =========================================================================
 constexpr uint32_t kSkRec = 12;    // b, lo, cnt, blc, blo, bst, pbase, np, ndrain, bltot, npb, -
 constexpr uint32_t kSkSpan = 4 * kBucket;  // minimum inbox positions per part
+constexpr uint32_t kSkActPlanes = 4;       // per actor of a skewed bucket: admitted, drained start, backlog start, drain limit
 
 struct SkewArgs {
   uint32_t* rec;      // [nb][kSkRec]
-  uint32_t* act;      // [nb][3][kBucket]: keep, dseg, blp
+  uint32_t* act;      // [nb][kSkActPlanes][kBucket]: keep, dseg, blp, drain limit (its mailbox class)
   uint32_t* pc;       // [max_parts][kBucket] arrivals per actor -> prefix over the bucket's parts
   uint32_t* meta;     // [0] parts, [1] span
   uint32_t budget;    // target number of parts (the span grows beyond kSkSpan to stay near it)
@@ -2067,7 +2095,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_count(BucketArgs a, S
 static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, SkewArgs k) {
   __shared__ uint32_t scratch[2 * (kBWaves + 1)];
   const DevParams& P = a.P;
-  const uint32_t tid = threadIdx.x, n = *a.skew_n, T = P.T, C = P.C;
+  const uint32_t tid = threadIdx.x, n = *a.skew_n;
   if (k.meta[0] > k.max_parts) return;  // (plan and buffer disagree: k_skew_count reported it; no pc access)
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     uint32_t* r = k.rec + (size_t)i * kSkRec;
@@ -2081,13 +2109,16 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, Sk
       *row = make_uint4(len[0], len[1], len[2], len[3]);
       len[0] += v.x; len[1] += v.y; len[2] += v.z; len[3] += v.w;
     }
-    uint32_t keep[kBAct], dr[kBAct], qd[kBAct], sd = 0, sq = 0, ndead = 0;
+    uint32_t keep[kBAct], dr[kBAct], qd[kBAct], tl[kBAct], sd = 0, sq = 0, ndead = 0;
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
       const uint32_t la = la0 + j;
-      const bool alive = la < na && P.alive[a0 + la];
-      keep[j] = alive ? ((C == 0 || len[j] < C) ? len[j] : C) : 0u;
+      const uint32_t ab = la < na ? P.alive[a0 + la] : 0u;
+      uint32_t C, T;
+      mbox_limits(P, ab, C, T);
+      keep[j] = (ab & 1u) ? ((C == 0 || len[j] < C) ? len[j] : C) : 0u;
       ndead += len[j] - keep[j];
+      tl[j] = T;
       dr[j] = min(keep[j], T);
       qd[j] = keep[j] - dr[j];
       sd += dr[j];
@@ -2095,7 +2126,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, Sk
     }
     uint32_t td, tq;
     const uint2 ex = block_excl_sum2<kBThreads>(sd, sq, scratch, &td, &tq);
-    uint32_t* act = k.act + (size_t)i * 3 * kBucket;
+    uint32_t* act = k.act + (size_t)i * kSkActPlanes * kBucket;
     uint32_t ds[kBAct], bs[kBAct], ed = ex.x, eq = ex.y;
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
@@ -2107,6 +2138,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, Sk
     reinterpret_cast<uint4*>(act)[tid] = make_uint4(keep[0], keep[1], keep[2], keep[3]);
     reinterpret_cast<uint4*>(act + kBucket)[tid] = make_uint4(ds[0], ds[1], ds[2], ds[3]);
     reinterpret_cast<uint4*>(act + 2 * kBucket)[tid] = make_uint4(bs[0], bs[1], bs[2], bs[3]);
+    reinterpret_cast<uint4*>(act + 3 * kBucket)[tid] = make_uint4(tl[0], tl[1], tl[2], tl[3]);
     if (tid == 0) {
       r[8] = td;
       r[9] = tq;
@@ -2118,12 +2150,12 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, Sk
 
 static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a, SkewArgs k) {
   __shared__ __attribute__((aligned(16))) uint16_t whist[kBWaves * kBucket];  // 32 KB
-  __shared__ uint32_t s_run[kBucket], s_keep[kBucket], s_ds[kBucket], s_bs[kBucket], s_tmp[kBucket];
+  __shared__ uint32_t s_run[kBucket], s_keep[kBucket], s_ds[kBucket], s_bs[kBucket], s_tmp[kBucket], s_T[kBucket];
   uint32_t* const s_first = s_tmp;  // backlog parts: first position of each actor's run in the part
   __shared__ uint32_t s_q[3];
   const DevParams& P = a.P;
   const uint32_t tid = threadIdx.x, w = tid / kWave, lane = lane_id(), nparts = k.meta[0];
-  const uint32_t wpar = *a.pstep & 1u, rpar = wpar ^ 1u, amask = (1u << a.bb) - 1u, T = P.T;
+  const uint32_t wpar = *a.pstep & 1u, rpar = wpar ^ 1u, amask = (1u << a.bb) - 1u;
   const uint64_t ltm = lanemask_lt();
   const Msgs blw = a.g.bl[wpar];
   if (nparts > k.max_parts) return;
@@ -2133,13 +2165,14 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
     const uint32_t i = s_q[0], q0 = s_q[1], q1 = s_q[2];
     const uint32_t* r = k.rec + (size_t)i * kSkRec;
     const uint32_t lo = r[1], blc = r[3], blo = r[4], bst = r[5];
-    const uint32_t* act = k.act + (size_t)i * 3 * kBucket;
+    const uint32_t* act = k.act + (size_t)i * kSkActPlanes * kBucket;
     const uint32_t* pc = k.pc + (size_t)t * kBucket;
     for (uint32_t la = tid; la < kBucket; la += kBThreads) {
       s_run[la] = pc[la];
       s_keep[la] = act[la];
       s_ds[la] = act[kBucket + la];
       s_bs[la] = act[2 * kBucket + la];
+      s_T[la] = act[3 * kBucket + la];  // the actor's drain limit (mailbox class)
     }
     __syncthreads();
     if (q1 <= blc) {  // a part of the previous backlog: grouped by actor, every item admitted unless
@@ -2162,6 +2195,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
           const uint32_t rank = s_run[la] + (q - s_first[la]);
           if (rank >= s_keep[la]) continue;
           const uint32_t sv = a.g.bl[rpar].src[blo + q], pv = a.g.bl[rpar].pay[blo + q];
+          const uint32_t T = s_T[la];
           const uint32_t pos = rank < T ? lo + s_ds[la] + rank : lo + s_bs[la] + rank - T;
           const Msgs& d = rank < T ? a.scr : blw;
           d.key[pos] = kk[u];
@@ -2224,6 +2258,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
         if (!live[u]) continue;
         const uint32_t la = kk[u] & amask;
         const uint32_t rank = s_run[la] + whist[w * kBucket + la] + rk[u];  // among this actor's arrivals
+        const uint32_t T = s_T[la];
         if (rank < s_keep[la]) {
           if (rank < T) {  // drained this superstep: the skew launch's scratch copy
             const uint32_t pos = lo + s_ds[la] + rank;
@@ -2634,7 +2669,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         // pre-partitioned by k_skew_* (above): the drained messages are in the scratch copy at
         // [lo, lo + ndrain) in actor order, the queued ones already in this superstep's backlog
         const uint32_t* r = a.sk_rec + (size_t)it * kSkRec;
-        const uint32_t* act = a.sk_act + (size_t)it * 3 * kBucket;
+        const uint32_t* act = a.sk_act + (size_t)it * kSkActPlanes * kBucket;
         for (uint32_t la = tid; la < kBucket; la += kBThreads) s_seg[la] = act[kBucket + la];
         if (tid == 0) s_seg[kBucket] = r[8];
         __syncthreads();
@@ -2663,7 +2698,10 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         for (int j = 0; j < kBAct; ++j) {
           const uint32_t la = tid * kBAct + j;
           const uint32_t len = s_seg[la];
-          const uint32_t keep = !s_alive[la] ? 0u : ((P.C == 0 || len < P.C) ? len : P.C);
+          const uint32_t ab = s_alive[la];
+          uint32_t Cc, Tc;
+          mbox_limits(P, ab, Cc, Tc);
+          const uint32_t keep = !(ab & 1u) ? 0u : ((Cc == 0 || len < Cc) ? len : Cc);
           ndead0 += len - keep;
           v[j] = keep;
           s_keep[la] = keep;

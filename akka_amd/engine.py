@@ -160,6 +160,29 @@ class GpuEngine:
     def set_ring(self, stride: int = 1) -> None:
         check(self.lib.agx_set_ring(self._h, stride))
 
+    def set_mailbox_class(self, cls: int, capacity: int) -> None:
+        """A further mailbox type of this dispatcher (agx_set_mailbox_class): bounded-capacity:N -> N,
+        an unbounded type -> 0 (Mailboxes.lookupConfigurator, Mailboxes.scala:204-260)."""
+        check(self.lib.agx_set_mailbox_class(self._h, cls, capacity))
+
+    def set_mailbox(self, first: int, count: int, cls: int) -> None:
+        """Bind actors [first, first + count) to mailbox class `cls` (agx_set_mailbox)."""
+        check(self.lib.agx_set_mailbox(self._h, first, count, cls))
+
+    def set_outbound(self, first_host_id: int, n_host: int, capacity: int = 1 << 20) -> None:
+        """Host-side actor ids [first_host_id, +n_host): GPU tells to them go to the outbox
+        (agx_set_outbound; the reply path of sender() ! reply, ActorCell.scala:583-587)."""
+        check(self.lib.agx_set_outbound(self._h, first_host_id, n_host, capacity))
+
+    def take_outbound(self, cap: int = 1 << 24):
+        """agx_take_outbound: (dst, src, payload) arrays, each sender's tells in emission order."""
+        d, s, p = (np.zeros(cap, np.uint32) for _ in range(3))
+        n = ctypes.c_uint64()
+        check(self.lib.agx_take_outbound(self._h, _ptr(d, ctypes.c_uint32), _ptr(s, ctypes.c_uint32),
+                                         _ptr(p, ctypes.c_uint32), cap, ctypes.byref(n)))
+        k = int(n.value)
+        return d[:k], s[:k], p[:k]
+
     def set_gossip(self, fanout: int, seed: int) -> None:
         check(self.lib.agx_set_gossip(self._h, fanout, seed))
 

@@ -43,6 +43,9 @@ class Workload:
     graph: tuple | None = None   # (row_ptr, col)
     tells: tuple | None = None   # (dst, src, payload)
     bucket_actors: int = 0       # GPU engine hint (agx_cfg.bucket_actors): deep mailboxes want small buckets
+    mailbox_classes: dict = field(default_factory=dict)  # class -> capacity (agx_set_mailbox_class)
+    mailboxes: list = field(default_factory=list)         # (first, count, class) (agx_set_mailbox)
+    outbound: tuple | None = None                         # (first_host_id, n_host) (agx_set_outbound)
 
     def engine_kwargs(self) -> dict:
         """Semantic parameters (shared by the GPU engine and the CPU oracles)."""
@@ -56,6 +59,12 @@ class Workload:
     def apply_to(self, target, stage_tells: bool = True) -> None:
         for first, count, kind, init in self.ranges:
             target.register_range(first, count, kind, init)
+        for cls, cap in self.mailbox_classes.items():
+            target.set_mailbox_class(cls, cap)
+        for first, count, cls in self.mailboxes:
+            target.set_mailbox(first, count, cls)
+        if self.outbound is not None:
+            target.set_outbound(*self.outbound)
         if self.ring_stride is not None:
             target.set_ring(self.ring_stride)
         if self.gossip is not None:
@@ -391,4 +400,30 @@ def compiled_ring(n: int = 1_000_000, hops: int = 256, throughput: int = 5) -> W
     tables = typed.compile_behaviors([ring])
     w = token_ring(n, hops, throughput)
     w.name, w.ranges, w.behaviors = "compiled_ring", [(0, n, tables.kind_of(ring), None)], tables
+    return w
+
+
+# ------------------------------------------------------------------ per-actor mailboxes + the reply path
+def mailbox_mix(n: int = 4096, seed: int = 7, throughput: int = 3, capacity: int = 0, n_host: int = 32,
+                tells_per_actor: int = 3) -> Workload:
+    """mixed() with several mailbox types in one dispatcher (Mailboxes.lookupConfigurator per actor,
+    Mailboxes.scala:204-260): quarters of the population bound to bounded-capacity:2, an unbounded
+    type, bounded-capacity:16 and the dispatcher default (`capacity`); plus `n_host` host-side actors
+    (ids n..n+n_host-1, e.g. JVM TestProbes) that tell GPU actors -- PINGPONG actors answer them
+    through the outbox (sender() ! reply, ActorCell.scala:583-587)."""
+    w = mixed(n, seed=seed, throughput=throughput, capacity=capacity, tells_per_actor=tells_per_actor)
+    q = n // 4
+    w.name = "mailbox_mix"
+    w.mailbox_classes = {1: 2, 2: 0, 3: 16}
+    w.mailboxes = [(0, q, 1), (q, q, 2), (2 * q, q, 3)]
+    if n_host:
+        w.outbound = (n, n_host)
+        rng = np.random.default_rng(seed + 101)
+        m = max(1, n // 4)
+        dst, src, pay = w.tells
+        hs = rng.integers(n, n + n_host, m).astype(np.uint32)
+        hd = rng.integers(0, n, m).astype(np.uint32)
+        hp = rng.integers(0, 12, m).astype(np.uint32)
+        # host senders to every kind; the PINGPONG range answers them
+        w.tells = (np.concatenate([dst, hd]), np.concatenate([src, hs]), np.concatenate([pay, hp]))
     return w

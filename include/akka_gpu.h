@@ -28,6 +28,12 @@
  *                          (Dispatcher.scala:120-143, Mailbox.scala:227-277)
  *   agx_read_state      <- (no reference counterpart: actor state is private to the
  *                          JVM object; the GPU engine exposes it for the host/oracle)
+ *   agx_set_mailbox_class / agx_set_mailbox
+ *                       <- Mailboxes.lookupConfigurator / getMailboxType per actor
+ *                          (akka-actor/.../dispatch/Mailboxes.scala:140-191,204-260)
+ *   agx_set_outbound / agx_take_outbound
+ *                       <- sender() ! reply to a JVM actor (akka-actor/.../actor/ActorCell.scala:583-587):
+ *                          GPU tells to host-side actors leave the engine through an outbox
  *   agx_destroy         <- MessageDispatcher.shutdown (AbstractDispatcher.scala:325)
  *
  * Threading: an engine handle is driven by one host thread at a time (the
@@ -294,6 +300,30 @@ agx_status agx_stage_tells(agx_engine* eng, const uint32_t* dst, const uint32_t*
  * was recorded meanwhile).                                                    */
 agx_status agx_run(agx_engine* eng, uint32_t max_supersteps, agx_stats* out);
 agx_status agx_get_stats(agx_engine* eng, agx_stats* out);
+
+/* --- per-actor mailboxes (Mailboxes.lookupConfigurator, Mailboxes.scala:204-260) -------------
+ * An actor's mailbox type is resolved per actor in the reference (props, then dispatcher, then
+ * requirement; ActorMailboxSpec.scala:245-450).  Here a dispatcher's actors use one of
+ * AGX_MAX_MAILBOX_CLASSES mailbox classes: class 0 is agx_cfg.capacity, classes 1..7 are set by
+ * agx_set_mailbox_class (bounded-capacity:N -> N; an unbounded mailbox type -> 0), and
+ * agx_set_mailbox binds a range of actors to a class (default: class 0).  A bounded class drains at
+ * most min(throughput, capacity) messages per mailbox run, as a bounded queue never holds more.    */
+#define AGX_MAX_MAILBOX_CLASSES 8u
+agx_status agx_set_mailbox_class(agx_engine* eng, uint32_t mailbox_class, uint32_t capacity);
+agx_status agx_set_mailbox(agx_engine* eng, uint64_t first_id, uint64_t count, uint32_t mailbox_class);
+
+/* --- the reply path: actors that live on the host ------------------------------------------
+ * Ids [first_host_id, first_host_id + n_host) -- outside the population (>= n_actors, < 2^31) --
+ * name host-side actors, e.g. the JVM ActorRefs that told GPU actors (their sender() ids).  A GPU
+ * behaviour's tell to one of them is not a dead letter: it is appended to the engine's outbox
+ * (each sender's tells in emission order; different senders interleave arbitrarily, as on the
+ * JVM) and the host takes it with agx_take_outbound and delivers it.  Outbound tells leave the
+ * engine: they are not counted in agx_stats.emitted.  More than `capacity` outbound tells between
+ * two agx_take_outbound calls is AGX_ECAPACITY.  agx_take_outbound copies up to `cap` envelopes
+ * (dst host id, src GPU actor id, payload) and removes them; *n = how many.                   */
+agx_status agx_set_outbound(agx_engine* eng, uint32_t first_host_id, uint32_t n_host, uint64_t capacity);
+agx_status agx_take_outbound(agx_engine* eng, uint32_t* dst, uint32_t* src, uint32_t* payload, uint64_t cap,
+                             uint64_t* n);
 
 /* --- state readback ----------------------------------------------------------- */
 /* words: count x n_words u64 (actor-major); alive: count bytes (may be NULL).

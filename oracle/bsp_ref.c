@@ -157,6 +157,16 @@ typedef struct bsp_sim {
   /* mail */
   envvec backlog, emitted, staged;
   agx_stats st;
+  /* per-actor mailboxes (Mailboxes.lookupConfigurator, Mailboxes.scala:204-260): class per actor,
+   * capacity per class (class 0 = the dispatcher default), Tr = throughput before the bound clamp */
+  uint8_t* mcls;
+  uint32_t mcap[AGX_MAX_MAILBOX_CLASSES];
+  uint32_t Tr;
+  /* the reply path: tells to host-side ids [host_lo, host_lo + host_n) go to the outbox
+   * (sender() ! reply to a JVM actor, ActorCell.scala:583-587) */
+  uint32_t host_lo, host_n;
+  uint32_t* outbox;
+  uint64_t outbox_n, outbox_cap;
 } bsp_sim;
 
 bsp_sim* bsp_create(uint64_t n_actors, uint32_t throughput, uint32_t capacity, uint32_t n_words,
@@ -167,7 +177,9 @@ bsp_sim* bsp_create(uint64_t n_actors, uint32_t throughput, uint32_t capacity, u
   s->n = n_actors;
   s->T = throughput == 0 ? 1 : throughput; /* max(throughput, 1), Mailbox.scala:261 */
   if ((int32_t)throughput < 0) s->T = 1;
+  s->Tr = s->T;
   s->C = capacity;
+  s->mcap[0] = capacity;
   /* a bounded queue never holds more than C messages: drain <= min(T, C) */
   if (capacity && s->T > capacity) s->T = capacity;
   s->W = n_words;
@@ -177,10 +189,11 @@ bsp_sim* bsp_create(uint64_t n_actors, uint32_t throughput, uint32_t capacity, u
   s->alive = (uint8_t*)calloc(n_actors, 1);
   s->state = (uint64_t*)calloc(n_actors * n_words, 8);
   s->order = (uint32_t*)malloc(n_actors * 4);
+  s->mcls = (uint8_t*)calloc(n_actors, 1);
   s->P.n = n_actors;
   s->P.W = n_words;
   s->P.ring_stride = 1;
-  if (!s->kind || !s->alive || !s->state || !s->order) return NULL;
+  if (!s->kind || !s->alive || !s->state || !s->order || !s->mcls) return NULL;
   if (s->n_ranks == 1) {
     for (uint64_t a = 0; a < n_actors; ++a) s->order[a] = (uint32_t)a;
   } else {
@@ -201,7 +214,7 @@ bsp_sim* bsp_create(uint64_t n_actors, uint32_t throughput, uint32_t capacity, u
 
 void bsp_destroy(bsp_sim* s) {
   if (!s) return;
-  free(s->kind); free(s->alive); free(s->state); free(s->order);
+  free(s->kind); free(s->alive); free(s->state); free(s->order); free(s->mcls); free(s->outbox);
   free(s->zipf_cdf); free(s->zipf_perm); free(s->row_ptr); free(s->col);
   free(s->bcase); free(s->bact); free(s->bfirst);
   free(s->backlog.v); free(s->emitted.v); free(s->staged.v);
@@ -229,6 +242,38 @@ int bsp_register_range(bsp_sim* s, uint64_t first, uint64_t count, uint32_t kind
 }
 
 void bsp_set_ring(bsp_sim* s, uint32_t stride) { s->P.ring_stride = stride; }
+
+/* agx_set_mailbox_class / agx_set_mailbox: a mailbox type per actor */
+int bsp_set_mailbox_class(bsp_sim* s, uint32_t cls, uint32_t capacity) {
+  if (cls == 0 || cls >= AGX_MAX_MAILBOX_CLASSES) return 1;
+  s->mcap[cls] = capacity;
+  return 0;
+}
+int bsp_set_mailbox(bsp_sim* s, uint64_t first, uint64_t count, uint32_t cls) {
+  if (cls >= AGX_MAX_MAILBOX_CLASSES || first + count > s->n) return 1;
+  for (uint64_t i = 0; i < count; ++i) s->mcls[first + i] = (uint8_t)cls;
+  return 0;
+}
+
+/* agx_set_outbound / agx_take_outbound (the outbox keeps the canonical emission order) */
+int bsp_set_outbound(bsp_sim* s, uint32_t first, uint32_t n, uint64_t cap) {
+  if (n && first < s->n) return 1;
+  s->host_lo = first;
+  s->host_n = n;
+  s->outbox_cap = cap;
+  return 0;
+}
+uint64_t bsp_take_outbound(bsp_sim* s, uint32_t* dst, uint32_t* src, uint32_t* pay, uint64_t cap) {
+  const uint64_t k = s->outbox_n < cap ? s->outbox_n : cap;
+  for (uint64_t i = 0; i < k; ++i) {
+    dst[i] = s->outbox[3 * i];
+    src[i] = s->outbox[3 * i + 1];
+    pay[i] = s->outbox[3 * i + 2];
+  }
+  memmove(s->outbox, s->outbox + 3 * k, (size_t)(s->outbox_n - k) * 12);
+  s->outbox_n -= k;
+  return k;
+}
 
 void bsp_set_gossip(bsp_sim* s, uint32_t fanout, uint64_t seed) {
   s->P.gossip_f = fanout;
@@ -313,6 +358,17 @@ int bsp_stage(bsp_sim* s, const uint32_t* dst, const uint32_t* src, const uint32
 /* emit: tell(dst, payload) from `self`; unknown dst -> deadLetters now. */
 static void emit_cb(void* ctx, uint32_t dst, uint32_t self, uint32_t payload, const uint64_t* row, uint32_t rw) {
   bsp_sim* s = (bsp_sim*)ctx;
+  if (dst >= s->n && dst - s->host_lo < s->host_n) { /* a host-side actor: the outbox (not emitted here) */
+    if (s->outbox_n >= s->outbox_cap) { s->P.error = 1; return; }
+    uint32_t* o = (uint32_t*)realloc(s->outbox, (size_t)(s->outbox_n + 1) * 12);
+    if (!o) { s->P.error = 1; return; }
+    s->outbox = o;
+    o[3 * s->outbox_n] = dst;
+    o[3 * s->outbox_n + 1] = self;
+    o[3 * s->outbox_n + 2] = payload;
+    s->outbox_n++;
+    return;
+  }
   s->st.emitted++;
   if (dst >= s->n) { s->st.dead_letters++; return; }
   ev_push(&s->emitted, dst, row ? (self | AGX_WIDE_BIT) : self, payload, row, rw);
@@ -351,7 +407,10 @@ static int bsp_step(bsp_sim* s) {
     uint64_t b = off[a], L = off[a + 1] - b;
     if (!L) continue;
     if (!s->alive[a]) { s->st.dead_letters += L; continue; }
-    uint64_t nd = L < s->T ? L : s->T;
+    /* this actor's mailbox: capacity C (0 = unbounded), drain <= min(throughput, C) */
+    const uint32_t C = s->mcap[s->mcls[a]];
+    const uint32_t T = C && s->Tr > C ? C : s->Tr;
+    uint64_t nd = L < T ? L : T;
     uint32_t kcur = s->kind[a];
     for (uint64_t p = 0; p < nd; ++p) {
       uint32_t r = ref_apply(&s->P, &kcur, a, &s->state[(uint64_t)a * s->W], in[b + p].src, in[b + p].payload,
@@ -366,7 +425,7 @@ static int bsp_step(bsp_sim* s) {
       }
     }
     for (uint64_t p = nd; p < L; ++p) {
-      if (s->C == 0 || p < s->C)
+      if (C == 0 || p < C)
         ev_push(&s->backlog, in[b + p].dst, in[b + p].src, in[b + p].payload, rw ? inrows + (b + p) * rw : 0, rw);
       else s->st.dead_letters++;
     }

@@ -61,6 +61,10 @@ def _load_bsp():
             "bsp_destroy": (None, [vp]),
             "bsp_register_range": (ctypes.c_int, [vp, u64, u64, u32, P64, u64]),
             "bsp_set_ring": (None, [vp, u32]),
+            "bsp_set_mailbox_class": (ctypes.c_int, [vp, u32, u32]),
+            "bsp_set_mailbox": (ctypes.c_int, [vp, u64, u64, u32]),
+            "bsp_set_outbound": (ctypes.c_int, [vp, u32, u32, u64]),
+            "bsp_take_outbound": (u64, [vp, P32, P32, P32, u64]),
             "bsp_set_gossip": (None, [vp, u32, u64]),
             "bsp_set_delta_crdt": (ctypes.c_int, [vp, u32]),
             "bsp_set_behaviors": (ctypes.c_int, [vp, vp, u32, vp, u32, P32, u32]),
@@ -161,6 +165,25 @@ class BspOracle(_Base):
 
     def set_ring(self, stride):
         self.lib.bsp_set_ring(self.h, stride)
+
+    def set_mailbox_class(self, cls, capacity):
+        if self.lib.bsp_set_mailbox_class(self.h, cls, capacity):
+            raise ValueError("bsp_set_mailbox_class failed")
+
+    def set_mailbox(self, first, count, cls):
+        if self.lib.bsp_set_mailbox(self.h, first, count, cls):
+            raise ValueError("bsp_set_mailbox failed")
+
+    def set_outbound(self, first_host_id, n_host, capacity=1 << 20):
+        if self.lib.bsp_set_outbound(self.h, first_host_id, n_host, capacity):
+            raise ValueError("bsp_set_outbound failed")
+
+    def take_outbound(self, cap=1 << 24):
+        """(dst, src, payload) arrays of the outbox, canonical emission order."""
+        d, s, p = (np.zeros(cap, np.uint32) for _ in range(3))
+        n = self.lib.bsp_take_outbound(self.h, _p(d, ctypes.c_uint32), _p(s, ctypes.c_uint32),
+                                       _p(p, ctypes.c_uint32), cap)
+        return d[:n], s[:n], p[:n]
 
     def set_gossip(self, fanout, seed):
         self.lib.bsp_set_gossip(self.h, fanout, seed)

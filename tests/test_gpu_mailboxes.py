@@ -1,0 +1,98 @@
+"""GPU parity of per-actor mailbox types and of the reply path (the HIP engine through the C ABI vs
+the BSP oracle, bit-exact): a population with bounded-capacity:2 / unbounded / bounded-capacity:16 /
+default mailboxes in one dispatcher (Mailboxes.lookupConfigurator per actor, akka-actor/src/main/
+scala/akka/dispatch/Mailboxes.scala:204-260), host-side senders answered through the outbox
+(ActorCell.scala:583-587), on the fused, multi-pass, tiny-wave, skew and sharded paths."""
+import numpy as np
+import pytest
+
+from akka_amd import workloads as wl
+from akka_amd.engine import EngineConfig, GpuEngine, owner
+from tests.test_gpu_parity import COUNT_KEYS
+
+pytestmark = pytest.mark.gpu
+
+
+def _per_sender(d, s, p):
+    """outbox -> canonical per-sender sequences (a stable sort by sender keeps each sender's order)"""
+    o = np.argsort(s, kind="stable")
+    return np.stack([s[o], d[o], p[o]])
+
+
+def _run(w, ranks=1, max_steps=1 << 30, **cfg):
+    from oracle import BspOracle
+    kw = dict(w.engine_kwargs(), **cfg)
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, bucket_actors=w.bucket_actors, **kw)) for r in range(ranks)]
+    for e in engs:
+        w.apply_to(e)
+    sg = engs[0].run(max_steps) if ranks == 1 else GpuEngine.group_run(engs, max_steps)
+    outs = [e.take_outbound() for e in engs]
+    ref = BspOracle(n_ranks=ranks, **kw)
+    w.apply_to(ref)
+    so = ref.run(max_steps)
+    od = ref.take_outbound()
+    wo, ao = ref.read_state()
+    ref.close()
+    own_of = np.array([owner(i, 1000, ranks) for i in range(w.n_actors)]) if ranks > 1 else np.zeros(w.n_actors, int)
+    wg, ag = np.zeros_like(wo), np.zeros_like(ao)
+    for e in engs:
+        x, y = e.read_state()
+        own = own_of == e.cfg.rank
+        wg[own], ag[own] = x[own], y[own]
+        e.close()
+    keys = COUNT_KEYS if ranks == 1 else tuple(k for k in COUNT_KEYS if k != "supersteps")
+    for k in keys:
+        assert getattr(sg, k) == so[k], f"{k}: gpu={getattr(sg, k)} oracle={so[k]}"
+    assert np.array_equal(ag, ao), "alive differs"
+    diff = np.nonzero((wg != wo).any(axis=1))[0]
+    assert diff.size == 0, f"state differs at {diff[:10]}"
+    d = np.concatenate([o[0] for o in outs])
+    s = np.concatenate([o[1] for o in outs])
+    p = np.concatenate([o[2] for o in outs])
+    assert d.size == od[0].size and d.size > 0, (d.size, od[0].size)
+    assert np.array_equal(_per_sender(d, s, p), _per_sender(*od)), "outbox differs"
+    return sg
+
+
+@pytest.mark.parametrize("T,C", [(1, 0), (3, 0), (5, 4), (50, 1)])
+def test_mailbox_classes_fused(built, T, C):
+    _run(wl.mailbox_mix(6000, seed=T + C, throughput=T, capacity=C))
+
+
+@pytest.mark.parametrize("tiny", ["0", "128"])
+def test_mailbox_classes_multipass(built, monkeypatch, tiny):
+    """multi-pass grouping (narrow radix digits), wave path on / off, skewed buckets (32-actor buckets)"""
+    monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    monkeypatch.setenv("AGX_TINY", tiny)
+    _run(wl.mailbox_mix(30_000, seed=5, throughput=2, capacity=6))
+    _run(wl.mailbox_mix(30_000, seed=6, throughput=3, capacity=0), bucket_actors=32)
+
+
+@pytest.mark.parametrize("ranks", [2, 5])
+def test_mailbox_classes_sharded(built, ranks):
+    _run(wl.mailbox_mix(5000, seed=ranks, throughput=2, capacity=3), ranks=ranks)
+
+
+def test_outbox_capacity_is_loud(built):
+    """More outbound tells than the outbox holds between two takes: AGX_ECAPACITY, not a silent drop."""
+    from akka_amd._lib import AgxError
+    w = wl.mailbox_mix(4096, seed=1, throughput=5)
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+    w.apply_to(eng)
+    eng.set_outbound(w.n_actors, 32, capacity=4)
+    with pytest.raises(AgxError):
+        eng.run()
+        eng.take_outbound()
+    eng.close()
+
+
+def test_set_mailbox_rejects_unconfigured_class(built):
+    from akka_amd._lib import AgxError
+    eng = GpuEngine(EngineConfig(n_actors=64))
+    with pytest.raises(AgxError):
+        eng.set_mailbox(0, 8, 3)
+    with pytest.raises(AgxError):
+        eng.set_mailbox_class(0, 5)  # class 0 is agx_cfg.capacity
+    with pytest.raises(AgxError):
+        eng.set_outbound(10, 4)      # host ids inside the population
+    eng.close()
