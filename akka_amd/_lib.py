@@ -95,6 +95,7 @@ SIGNATURES = {
     "agx_stage_tells": (ctypes.c_int32, [ctypes.c_void_p, c_u32p, c_u32p, c_u32p, ctypes.c_size_t]),
     "agx_run": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(AgxStats)]),
     "agx_get_stats": (ctypes.c_int32, [ctypes.c_void_p, ctypes.POINTER(AgxStats)]),
+    "agx_identity_supersteps": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
     "agx_read_state": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_u64p, c_u8p]),
     "agx_comm_unique_id": (ctypes.c_int32, [ctypes.c_void_p]),
     "agx_comm_init": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p]),

@@ -1355,7 +1355,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   // fused superstep when one radix digit covers every bucket of a single rank
   e->fused = e->R == 1 && e->plan.npass == 1 && getenv("AGX_NO_FUSED") == nullptr;
   // identity grouping (k_ident_combine): single-rank multi-pass with a bucket-bounds search
-  e->ident_on = !e->fused && e->R == 1 && e->plan.npass > 1 && getenv("AGX_IDENT") != nullptr;
+  e->ident_on = !e->fused && e->R == 1 && e->plan.npass > 1 && getenv("AGX_NO_IDENT") == nullptr;
   if (!e->fused && e->R == 1) e->par = 1u;  // multi-pass: parity of the first superstep's counter value (1)
   e->tstride = (e->nb + 3) & ~3u;
   // fused: bucket b's inbox (and its backlog / tell slices) live at [b*region, ...) of the
@@ -1936,6 +1936,15 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
   // out == NULL: no counter read-back (one stream round trip less; agx_get_stats reads them
   // later), but the error word came back with the run's final sync
   return out ? collect_stats(e, out, true) : error_status(e, e->h_stat[ST_ERROR]);
+}
+
+agx_status agx_identity_supersteps(agx_engine* e, uint64_t* out) {
+  if (!e || !out) return set_err(AGX_EINVAL, "bad identity_supersteps args");
+  AGX_TRY(ensure_dev(e));
+  uint64_t s[kStatBlk];
+  AGX_TRY(read_counters(e, s));
+  *out = s[ST_IDENT];
+  return AGX_OK;
 }
 
 agx_status agx_get_stats(agx_engine* e, agx_stats* out) {

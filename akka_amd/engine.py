@@ -232,6 +232,12 @@ class GpuEngine:
         check(self.lib.agx_run(self._h, min(int(max_supersteps), 0xFFFFFFFF), ctypes.byref(st)))
         return Stats.from_c(st)
 
+    def identity_supersteps(self) -> int:
+        """Multi-pass supersteps grouped without a radix pass (agx_identity_supersteps)."""
+        v = ctypes.c_uint64()
+        check(self.lib.agx_identity_supersteps(self._h, ctypes.byref(v)))
+        return int(v.value)
+
     def stats(self) -> Stats:
         st = AgxStats()
         check(self.lib.agx_get_stats(self._h, ctypes.byref(st)))

@@ -300,6 +300,10 @@ agx_status agx_stage_tells(agx_engine* eng, const uint32_t* dst, const uint32_t*
  * was recorded meanwhile).                                                    */
 agx_status agx_run(agx_engine* eng, uint32_t max_supersteps, agx_stats* out);
 agx_status agx_get_stats(agx_engine* eng, agx_stats* out);
+/* Supersteps of a single-rank multi-pass engine (> 2^20 actors) whose mail needed no radix pass:
+ * the previous apply's tells were already in destination order (a ring, a stencil -- identity
+ * grouping).  Diagnostic; the grouping is the same either way.                  */
+agx_status agx_identity_supersteps(agx_engine* eng, uint64_t* out);
 
 /* --- per-actor mailboxes (Mailboxes.lookupConfigurator, Mailboxes.scala:204-260) -------------
  * An actor's mailbox type is resolved per actor in the reference (props, then dispatcher, then

