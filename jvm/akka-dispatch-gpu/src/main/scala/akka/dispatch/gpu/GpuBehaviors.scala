@@ -14,12 +14,11 @@
  *   val tables = GpuBehaviors.compile(Seq(counter))         // -> agx_set_behaviors
  *   engine.registerRange(0, n, tables.kindOf(counter))
  *
- * Not compiled in the build image (no JVM, SURVEY.md §8(c)).
+ * Not compiled in the build image (no JVM, SURVEY.md §8(c)); JDK 8+ (no java.lang.foreign).
  */
 package akka.dispatch.gpu
 
-import java.lang.foreign.{ Arena, MemorySegment }
-import java.lang.foreign.ValueLayout._
+import java.nio.{ ByteBuffer, ByteOrder }
 
 import scala.collection.mutable
 
@@ -109,13 +108,26 @@ object GpuBehaviors {
   }
   def receiveBuilder(state: State): Builder = new Builder(state)
 
-  /** The lowered tables (agx_set_behaviors arguments) in native memory. */
-  final class Tables(val behaviors: Vector[Behavior], val cases: MemorySegment, val nCases: Int,
-                     val acts: MemorySegment, val nActs: Int, val first: MemorySegment) {
-    def kindOf(b: Behavior): Int = AgxNative.KindCompiled + behaviors.indexWhere(_ eq b)
+  /** The lowered tables (agx_set_behaviors arguments): agx_case (48 B) and agx_act (32 B) entries
+   *  as little-endian bytes, and first[] -- handed to either binding (AgxBackend.setBehaviors). */
+  final class Tables(val behaviors: Vector[Behavior], val cases: Array[Byte], val nCases: Int,
+                     val acts: Array[Byte], val nActs: Int, val first: Array[Int]) {
+    def kindOf(b: Behavior): Int = Agx.KindCompiled + behaviors.indexWhere(_ eq b)
+    /** the most tells one message can emit: the dispatcher's gpu.max-emit must be at least this */
+    def maxTells: Int = {
+      var m = 0
+      var c = 0
+      while (c < nCases) {
+        val first = (cases(48 * c + 12) & 0xFF) | ((cases(48 * c + 13) & 0xFF) << 8)
+        val cnt = (cases(48 * c + 14) & 0xFF) | ((cases(48 * c + 15) & 0xFF) << 8)
+        m = math.max(m, (first until first + cnt).count(i => acts(32 * i) == ATell))
+        c += 1
+      }
+      m
+    }
   }
 
-  def compile(roots: Seq[Behavior], arena: Arena = Arena.global()): Tables = {
+  def compile(roots: Seq[Behavior]): Tables = {
     val order = mutable.ArrayBuffer.empty[Behavior]
     val todo = mutable.Queue(roots: _*)
     while (todo.nonEmpty) {
@@ -128,39 +140,38 @@ object GpuBehaviors {
     val index = order.zipWithIndex.map { case (b, i) => (b: AnyRef) -> i }.toMap
     val allCases = order.flatMap(_.cases)
     val nActs = allCases.map(_.actions.size).sum
-    val cs = arena.allocate(AgxNative.Case, math.max(allCases.size, 1).toLong)
-    val as = arena.allocate(AgxNative.Act, math.max(nActs, 1).toLong)
-    val first = arena.allocate(JAVA_INT, (order.size + 1).toLong)
+    val cs = ByteBuffer.allocate(48 * math.max(allCases.size, 1)).order(ByteOrder.LITTLE_ENDIAN)
+    val as = ByteBuffer.allocate(32 * math.max(nActs, 1)).order(ByteOrder.LITTLE_ENDIAN)
+    val first = new Array[Int](order.size + 1)
     var ci = 0; var ai = 0
-    first.setAtIndex(JAVA_INT, 0, 0)
     order.zipWithIndex.foreach { case (b, bi) =>
       b.cases.foreach { c =>
         val t = c.tests ++ Seq.fill(2 - c.tests.size)(Always)
-        val base = ci * 48L
+        val base = ci * 48
         val bytes = Array(t(0).lhs.src, t(0).lhs.word, t(0).cmp, t(0).rhs.src, t(0).rhs.word, t(1).lhs.src,
                           t(1).lhs.word, t(1).cmp, t(1).rhs.src, t(1).rhs.word,
                           c.next match { case Same => 0; case Stopped => 1; case Unhandled => 2; case _ => 3 },
                           c.next match { case nb: Behavior => index(nb); case _ => 0 })
-        bytes.zipWithIndex.foreach { case (v, i) => cs.set(JAVA_BYTE, base + i, v.toByte) }
-        cs.set(JAVA_SHORT_UNALIGNED, base + 12, ai.toShort)
-        cs.set(JAVA_SHORT_UNALIGNED, base + 14, c.actions.size.toShort)
+        bytes.zipWithIndex.foreach { case (v, i) => cs.put(base + i, v.toByte) }
+        cs.putShort(base + 12, ai.toShort)
+        cs.putShort(base + 14, c.actions.size.toShort)
         Seq(t(0).lhs.k, t(0).rhs.k, t(1).lhs.k, t(1).rhs.k).zipWithIndex.foreach { case (k, i) =>
-          cs.set(JAVA_LONG_UNALIGNED, base + 16 + 8 * i, k)
+          cs.putLong(base + 16 + 8 * i, k)
         }
         c.actions.foreach { a =>
-          val ab = ai * 32L
+          val ab = ai * 32
           Array(a.op, a.word, a.v.src, a.v.word, a.dst.src, a.dst.word, 0, 0).zipWithIndex.foreach { case (v, i) =>
-            as.set(JAVA_BYTE, ab + i, v.toByte)
+            as.put(ab + i, v.toByte)
           }
-          as.set(JAVA_INT_UNALIGNED, ab + 8, a.orMask)
-          as.set(JAVA_LONG_UNALIGNED, ab + 16, a.v.k)
-          as.set(JAVA_LONG_UNALIGNED, ab + 24, a.dst.k)
+          as.putInt(ab + 8, a.orMask)
+          as.putLong(ab + 16, a.v.k)
+          as.putLong(ab + 24, a.dst.k)
           ai += 1
         }
         ci += 1
       }
-      first.setAtIndex(JAVA_INT, (bi + 1).toLong, ci)
+      first(bi + 1) = ci
     }
-    new Tables(order.toVector, cs, ci, as, ai, first)
+    new Tables(order.toVector, cs.array(), ci, as.array(), ai, first)
   }
 }

@@ -113,11 +113,14 @@ class GpuDispatcher(
 
   /** Large populations: `count` fixed-layout actors without a JVM ActorCell each; returns the
    *  first id (tell to them with tellRange / GpuRef). */
-  def spawnRange(kind: Int, count: Int): Int = engine.registerRange(count, kind)
+  def spawnRange(kind: Int, count: Int, mailboxCapacity: Int = defaultCapacity): Int =
+    engine.registerRange(count, kind, mailboxCapacity)
+
+  private def defaultCapacity: Int = if (config.hasPath("gpu.mailbox-capacity")) config.getInt("gpu.mailbox-capacity") else 0
 
   def tellRange(first: Int, count: Int, payload: Int): Unit = {
     var i = 0
-    while (i < count) { engine.stage(first + i, AgxNative.NoSender, payload); i += 1 }
+    while (i < count) { engine.stage(first + i, Agx.NoSender, payload); i += 1 }
     schedulePump()
   }
 

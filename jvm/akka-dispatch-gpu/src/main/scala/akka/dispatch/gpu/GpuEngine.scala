@@ -1,11 +1,16 @@
 /*
- * One engine (one agx_engine handle = one GPU rank) per GpuDispatcher instance: actor ids,
- * the MPSC staging buffer that ActorRef.! appends to, and the pump that runs supersteps.
+ * One engine (one agx_engine handle = one GPU rank) per GpuDispatcher instance: actor ids, the
+ * MPSC staging buffer that ActorRef.! appends to, the pump that runs supersteps, and the reply
+ * path back to JVM actors.  All native calls go through an AgxBackend (JNI on JDK 8/11, Panama on
+ * JDK 22+, AgxBackend.scala).
+ *
+ * Ids: GPU actors are [0, gpu.actors); a JVM actor that tells a GPU actor gets a host id in
+ * [gpu.actors, gpu.actors + gpu.host-actors) (agx_set_outbound), so the GPU actor's sender() is a
+ * real id: `sender() ! reply` (ActorCell.scala:583-587) lands in the engine's outbox, and the pump
+ * delivers it to the JVM ActorRef with the replying GPU actor as sender.
  */
 package akka.dispatch.gpu
 
-import java.lang.foreign._
-import java.lang.foreign.ValueLayout._
 import java.util.concurrent.ConcurrentHashMap
 import java.util.concurrent.atomic.{ AtomicBoolean, AtomicInteger }
 
@@ -14,59 +19,110 @@ import com.typesafe.config.Config
 import akka.actor.ActorRef
 
 final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int) {
-  import AgxNative._
+  private val native: AgxBackend = AgxBackend.load()
+  if (native.abiVersion != Agx.AbiVersion)
+    throw new akka.ConfigurationException(s"akka-gpu: native ABI ${native.abiVersion}, shim ABI ${Agx.AbiVersion}")
 
-  private val arena = Arena.ofShared()
+  private def opt(path: String, default: Int): Int = if (config.hasPath(path)) config.getInt(path) else default
   val maxActors: Long = config.getLong("gpu.actors")
-  private val capacity: Int = if (config.hasPath("gpu.mailbox-capacity")) config.getInt("gpu.mailbox-capacity") else 0
+  private val defaultCapacity: Int = opt("gpu.mailbox-capacity", 0)
+  val stateWords: Int = config.getInt("gpu.state-words")
+  private val nHost: Int = opt("gpu.host-actors", 65536)
 
   /** agx_create from the dispatcher's HOCON block (throughput: reference.conf:541, <= 0 behaves as 1) */
-  val handle: MemorySegment = {
-    val cfg = arena.allocate(Cfg)
-    cfg.set(JAVA_INT, 0, AbiVersion)
-    cfg.set(JAVA_INT, 4, if (config.hasPath("gpu.device")) config.getInt("gpu.device") else 0)
-    cfg.set(JAVA_LONG, 8, maxActors)
-    cfg.set(JAVA_INT, 16, math.max(throughput, 0))
-    cfg.set(JAVA_INT, 20, capacity)
-    cfg.set(JAVA_INT, 24, config.getInt("gpu.state-words"))
-    cfg.set(JAVA_INT, 28, config.getInt("gpu.max-emit"))
-    cfg.set(JAVA_INT, 32, 1)
-    cfg.set(JAVA_INT, 36, 0)
-    cfg.set(JAVA_INT, 40, 1000) // akka.cluster.sharding number-of-shards (typed reference.conf:10)
-    cfg.set(JAVA_INT, 44, if (config.hasPath("gpu.bucket-actors")) config.getInt("gpu.bucket-actors") else 0)
-    cfg.set(JAVA_LONG, 48, 0L)
-    val out = arena.allocate(ADDRESS)
-    check(create.invokeExact(cfg, out).asInstanceOf[Int])
-    out.get(ADDRESS, 0)
+  val handle: Long = native.create(
+    opt("gpu.device", 0),
+    maxActors,
+    math.max(throughput, 0),
+    defaultCapacity,
+    stateWords,
+    config.getInt("gpu.max-emit"),
+    1,
+    0,
+    1000, // akka.cluster.sharding number-of-shards (typed reference.conf:10)
+    opt("gpu.bucket-actors", 0),
+    0L)
+  native.setOutbound(handle, maxActors.toInt, nHost, opt("gpu.outbox-capacity", 1 << 20).toLong)
+
+  // ---------------------------------------------------------------- mailbox types (per actor)
+  // Mailboxes.lookupConfigurator resolves a mailbox per actor (Mailboxes.scala:204-260): each distinct
+  // capacity among this dispatcher's GPU mailbox types becomes one engine mailbox class (class 0 =
+  // gpu.mailbox-capacity; at most Agx.MaxMailboxClasses - 1 further ones).
+  private val classes = new ConcurrentHashMap[Integer, Integer]()
+  classes.put(defaultCapacity, 0)
+  def mailboxClass(capacity: Int): Int = synchronized {
+    val c = classes.get(capacity)
+    if (c != null) c.intValue
+    else {
+      val cls = classes.size
+      if (cls >= Agx.MaxMailboxClasses)
+        throw new akka.ConfigurationException(
+          s"GPU dispatcher [$dispatcherId]: more than ${Agx.MaxMailboxClasses} distinct mailbox capacities")
+      native.setMailboxClass(handle, cls, capacity)
+      classes.put(capacity, cls)
+      cls
+    }
   }
 
   // ---------------------------------------------------------------- actor ids
   private val nextId = new AtomicInteger(0)
   private val ids = new ConcurrentHashMap[ActorRef, Integer]()
+  private val refs = new ConcurrentHashMap[Integer, ActorRef]() // GPU id -> its ActorRef (individually created)
+  private val nextHost = new AtomicInteger(0)
+  private val hostIds = new ConcurrentHashMap[ActorRef, Integer]()
+  private val hostRefs = new ConcurrentHashMap[Integer, ActorRef]()
+  private[gpu] val queues = new ConcurrentHashMap[Integer, GpuMessageQueue]() // numberOfMessages bookkeeping
 
-  /** actorOf: one fixed-layout actor (GpuMailboxType.create) */
-  def register(ref: ActorRef, kind: Int, init: Array[Long]): Int = {
+  /** actorOf: one fixed-layout actor (GpuMailboxType.create) with its mailbox class */
+  def register(ref: ActorRef, kind: Int, init: Array[Long], mailboxCapacity: Int): Int = {
     val id = nextId.getAndIncrement()
     if (id >= maxActors) throw new IllegalStateException(s"GPU dispatcher [$dispatcherId] is full ($maxActors actors)")
-    val st = if (init == null) MemorySegment.NULL else arena.allocateFrom(JAVA_LONG, init: _*)
-    synchronized { check(registerRange.invokeExact(handle, id.toLong, 1L, kind, st, init.length.toLong * 8).asInstanceOf[Int]) }
+    val cls = mailboxClass(mailboxCapacity)
+    synchronized {
+      native.registerRange(handle, id.toLong, 1L, kind, init, stateWords)
+      if (cls != 0) native.setMailbox(handle, id.toLong, 1L, cls)
+    }
     ids.put(ref, id)
+    refs.put(id, ref)
     id
   }
 
   /** a contiguous range of fixed-layout actors with no JVM ActorCell each (GpuDispatcher.spawnRange) */
-  def registerRange(count: Int, kind: Int): Int = {
+  def registerRange(count: Int, kind: Int, mailboxCapacity: Int): Int = {
     val first = nextId.getAndAdd(count)
     if (first.toLong + count > maxActors) throw new IllegalStateException(s"GPU dispatcher [$dispatcherId] is full")
+    val cls = mailboxClass(mailboxCapacity)
     synchronized {
-      check(AgxNative.registerRange.invokeExact(handle, first.toLong, count.toLong, kind, MemorySegment.NULL, 0L).asInstanceOf[Int])
+      native.registerRange(handle, first.toLong, count.toLong, kind, null, stateWords)
+      if (cls != 0) native.setMailbox(handle, first.toLong, count.toLong, cls)
     }
     first
   }
 
+  def setBehaviors(t: GpuBehaviors.Tables): Unit = synchronized(native.setBehaviors(handle, t))
+
+  /** sender id of a tell: a GPU actor's own id, a host id for a JVM actor (the reply path), or
+   *  noSender (deadLetters) when the host-id range is exhausted */
   def idOf(ref: ActorRef): Int = {
+    if (ref == null || ref == ActorRef.noSender) return Agx.NoSender
     val i = ids.get(ref)
-    if (i == null) NoSender else i.intValue
+    if (i != null) return i.intValue
+    val h = hostIds.get(ref)
+    if (h != null) return h.intValue
+    synchronized {
+      val again = hostIds.get(ref)
+      if (again != null) again.intValue
+      else {
+        val k = nextHost.getAndIncrement()
+        if (k >= nHost) Agx.NoSender
+        else {
+          val id = maxActors.toInt + k
+          hostIds.put(ref, id)
+          hostRefs.put(id, ref)
+          id
+        }
+      }
+    }
   }
 
   // ---------------------------------------------------------------- staging (MPSC)
@@ -90,9 +146,13 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
   }
 
   private val pumping = new AtomicBoolean(false)
+  private val outD = new Array[Int](4096)
+  private val outS = new Array[Int](4096)
+  private val outP = new Array[Int](4096)
 
-  /** Run supersteps until the engine is quiescent.  One host thread drives the handle at a time
-   *  (include/akka_gpu.h threading rule); returns false if another pump is running. */
+  /** Run supersteps until the engine is quiescent, delivering outbound replies to JVM actors after
+   *  each run.  One host thread drives the handle at a time (include/akka_gpu.h threading rule);
+   *  returns false if another pump is running. */
   def pump(maxSupersteps: Int): Boolean = {
     if (!pumping.compareAndSet(false, true)) return false
     try {
@@ -105,45 +165,50 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
           r
         }
         if (k > 0) {
-          val a = Arena.ofConfined()
-          try {
-            check(stageTells.invokeExact(handle, a.allocateFrom(JAVA_INT, d.take(k): _*),
-              a.allocateFrom(JAVA_INT, s.take(k): _*), a.allocateFrom(JAVA_INT, p.take(k): _*), k.toLong).asInstanceOf[Int])
-          } finally a.close()
+          native.stageTells(handle, d, s, p, k)
+          var i = 0
+          while (i < k) { val q = queues.get(d(i)); if (q != null) q.handedOver(); i += 1 }
         }
-        check(run.invokeExact(handle, maxSupersteps, MemorySegment.NULL).asInstanceOf[Int])
+        native.run(handle, maxSupersteps, null)
+        deliverOutbound()
         more = synchronized(n > 0)
       }
       true
     } finally pumping.set(false)
   }
 
+  /** outbox -> JVM actors: `jvmRef ! GpuTell(payload)` with the replying GPU actor as sender
+   *  (each GPU sender's replies in emission order, the only order Akka guarantees) */
+  private def deliverOutbound(): Unit = {
+    var k = native.takeOutbound(handle, outD, outS, outP, outD.length)
+    while (k > 0) {
+      var i = 0
+      while (i < k) {
+        val to = hostRefs.get(outD(i))
+        if (to != null) to.tell(GpuTell(outP(i)), refs.getOrDefault(outS(i), ActorRef.noSender))
+        i += 1
+      }
+      k = native.takeOutbound(handle, outD, outS, outP, outD.length)
+    }
+  }
+
   def hasStaged: Boolean = synchronized(n > 0)
 
   /** delivered, dead letters, unhandled, emitted, staged, supersteps, in flight, bytes */
   def stats(): Array[Long] = {
-    val a = Arena.ofConfined()
-    try {
-      val st = a.allocate(Stats)
-      check(getStats.invokeExact(handle, st).asInstanceOf[Int])
-      st.toArray(JAVA_LONG)
-    } finally a.close()
+    val st = new Array[Long](8)
+    native.getStats(handle, st)
+    st
   }
 
-  def state(id: Int, words: Int): (Array[Long], Boolean) = {
-    val a = Arena.ofConfined()
-    try {
-      val w = a.allocate(JAVA_LONG, words.toLong)
-      val alive = a.allocate(JAVA_BYTE, 1)
-      check(readState.invokeExact(handle, id.toLong, 1L, w, alive).asInstanceOf[Int])
-      (w.toArray(JAVA_LONG), alive.get(JAVA_BYTE, 0) != 0)
-    } finally a.close()
+  def state(id: Int): (Array[Long], Boolean) = {
+    val w = new Array[Long](stateWords)
+    val alive = new Array[Byte](1)
+    native.readState(handle, id.toLong, 1L, w, alive)
+    (w, alive(0) != 0)
   }
 
-  def close(): Unit = {
-    check(destroy.invokeExact(handle).asInstanceOf[Int])
-    arena.close()
-  }
+  def close(): Unit = native.destroy(handle)
 }
 
 object GpuEngine {

@@ -2,9 +2,14 @@
  * mailbox-type = "akka.dispatch.gpu.GpuMailboxType": Mailboxes.lookupConfigurator instantiates
  * it reflectively with the (ActorSystem.Settings, Config) constructor (akka-actor/src/main/
  * scala/akka/dispatch/Mailboxes.scala:222-236); MailboxType.create (Mailbox.scala:638-640)
- * registers the owner as one fixed-layout actor of the dispatcher's engine.
+ * registers the owner as one fixed-layout actor of the dispatcher's engine, bound to the engine
+ * mailbox class of this mailbox type's capacity -- so bounded and unbounded GPU mailboxes coexist
+ * on one dispatcher, each actor with its own (Mailboxes.scala:204-260, ActorMailboxSpec.scala:245-450).
  */
 package akka.dispatch.gpu
+
+import java.util.concurrent.atomic.AtomicInteger
+
 
 import com.typesafe.config.Config
 
@@ -20,34 +25,50 @@ class GpuMailboxType(settings: ActorSystem.Settings, config: Config)
 
   private val dispatcherId = config.getString("gpu.dispatcher")
   private val kind: Int = config.getString("gpu.behavior") match {
-    case "counter"    => AgxNative.KindCounter
-    case "ring"       => AgxNative.KindRing
-    case "fanout"     => AgxNative.KindFanout
-    case "forward-rr" => AgxNative.KindForwardRR
-    case "stop-after" => AgxNative.KindStopAfter
-    case "ping-pong"  => AgxNative.KindPingPong
-    case "even"       => AgxNative.KindEven
-    case "gcounter"   => AgxNative.KindGCounter
-    case "pncounter"  => AgxNative.KindPNCounter
-    case "orset"      => AgxNative.KindORSet
+    case "counter"    => Agx.KindCounter
+    case "ring"       => Agx.KindRing
+    case "fanout"     => Agx.KindFanout
+    case "forward-rr" => Agx.KindForwardRR
+    case "stop-after" => Agx.KindStopAfter
+    case "ping-pong"  => Agx.KindPingPong
+    case "even"       => Agx.KindEven
+    case "gcounter"   => Agx.KindGCounter
+    case "pncounter"  => Agx.KindPNCounter
+    case "orset"      => Agx.KindORSet
     case other        => throw new akka.ConfigurationException(s"Unknown GPU behavior [$other] in mailbox config")
   }
+
+  /** BoundedMailbox's keys (Mailbox.scala:699-720): mailbox-capacity, mailbox-push-timeout-time.
+   *  The GPU mailbox tail-drops at capacity (pushTimeOut 0, AbstractBoundedNodeQueue.java:92-113);
+   *  a positive push timeout would block the sender, which a superstep cannot do. */
+  private val capacity: Int = if (config.hasPath("mailbox-capacity")) config.getInt("mailbox-capacity") else 0
+  if (capacity < 0) throw new IllegalArgumentException("The capacity for GpuMailboxType can not be negative")
+  if (capacity > 0 && config.hasPath("mailbox-push-timeout-time") &&
+      config.getDuration("mailbox-push-timeout-time").toNanos != 0L)
+    throw new akka.ConfigurationException(
+      "GpuMailboxType is a non-blocking bounded mailbox: mailbox-push-timeout-time must be 0")
 
   override def create(owner: Option[ActorRef], system: Option[ActorSystem]): MessageQueue = {
     val engine = GpuEngine.forDispatcher(dispatcherId)
     val id = owner match {
-      case Some(ref) => engine.register(ref, kind, Array.fill(config.getInt("gpu.state-words"))(0L))
-      case None      => AgxNative.NoSender // the dummy queue of a top-level actor under construction
+      case Some(ref) => engine.register(ref, kind, Array.fill(engine.stateWords)(0L), capacity)
+      case None      => Agx.NoSender // the dummy queue of a top-level actor under construction
     }
-    new GpuMessageQueue(id, engine, system)
+    val q = new GpuMessageQueue(id, engine, system)
+    if (id != Agx.NoSender) engine.queues.put(id, q)
+    q
   }
 }
 
 /** The device-side mailbox of one actor.  enqueue stages the tell for the engine; nothing is
- *  ever dequeued on the JVM (MessageQueue contract, Mailbox.scala:359-390). */
+ *  ever dequeued on the JVM (MessageQueue contract, Mailbox.scala:359-390).  numberOfMessages
+ *  counts this actor's tells staged on the JVM and not yet handed to the engine; the messages on
+ *  the device are in the engine's in-flight count (GpuEngine.stats()(6)). */
 final class GpuMessageQueue(val id: Int, engine: GpuEngine, system: Option[ActorSystem])
     extends MessageQueue
     with UnboundedMessageQueueSemantics {
+
+  private val staged = new AtomicInteger(0)
 
   def enqueue(receiver: ActorRef, handle: Envelope): Unit = {
     val payload = handle.message match {
@@ -59,10 +80,14 @@ final class GpuMessageQueue(val id: Int, engine: GpuEngine, system: Option[Actor
         return
     }
     engine.stage(id, engine.idOf(handle.sender), payload)
+    staged.incrementAndGet()
   }
 
+  /** the pump took this actor's staged tells (GpuDispatcher.pumpTask) */
+  private[gpu] def handedOver(): Unit = staged.set(0)
+
   def dequeue(): Envelope = null
-  def numberOfMessages: Int = 0 // messages live on the device (agx_get_stats in_flight)
-  def hasMessages: Boolean = false
+  def numberOfMessages: Int = staged.get
+  def hasMessages: Boolean = staged.get > 0
   def cleanUp(owner: ActorRef, deadLetters: MessageQueue): Unit = () // the engine dead-letters them
 }
