@@ -206,7 +206,7 @@ __device__ __forceinline__ uint32_t dl_record(const DevParams& P, const St32& s,
 
 // DeltaPropagation row of seqNrs (j, ctr]: collectPropagations' merged group (DeltaOp.merge: runs of
 // AddDeltaOps coalesce) or a NoDeltaPlaceholder (max-delta-size reached / a no-delta update).
-__device__ __forceinline__ void dl_group_row(const DevParams& P, const St32& s, uint32_t kind, uint32_t node, uint32_t j,
+__device__ __forceinline__ bool dl_group_row(const DevParams& P, const St32& s, uint32_t kind, uint32_t node, uint32_t j,
                                              uint32_t* row) {
   const uint32_t e0 = dl_env(kind), ctr = s.ld(e0 + 8);
   row[0] = 0;  // (rows are recycled: every field the receiver reads is written)
@@ -279,6 +279,7 @@ __device__ __forceinline__ void dl_group_row(const DevParams& P, const St32& s, 
     row[0] = nops;
   }
   if (ph) row[0] = 0x80000000u;
+  return ph;
 }
 
 // ORSet: apply one received DeltaPropagation group (mergeDelta, DD/ORSet.scala:455-501)
@@ -409,9 +410,13 @@ __device__ __forceinline__ void dl_tick(const DevParams& P, const CrdtHeap& H, u
       const uint32_t j = s.ld(e0 + 10 + x);
       if (ctr <= j) continue;  // deltaEntriesAfter(j) is empty
       const uint32_t h = row_cursor++;
-      if (h < H.rows) dl_group_row(P, s, kind, node, j, H.wrow(h));
+      const bool ph = h < H.rows && dl_group_row(P, s, kind, node, j, H.wrow(h));
       s.put(e0 + 10 + x, ctr);  // deltaSentToNode(node) = last seqNr (also for a placeholder)
-      em.wide(self - node + x, tag | h);
+      // createDeltaPropagation leaves NoDeltaPlaceholder out (DD/Replicator.scala:1364) and nothing is
+      // sent for an empty propagation (:1957): the group's slot (counted by phase A) stays void and
+      // is compacted out of the bucket's tells (bucket_finish)
+      if (ph) em.void_slot();
+      else em.wide(self - node + x, tag | h);
     }
     s.put(e0 + 9, rr + sz);  // deltaNodeRoundRobinCounter += sliceSize
   }

@@ -784,6 +784,8 @@ static __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) 
 // =========================================================================
 // Bucket apply: in-bucket sort + segmented drain + behaviour + emission
 // =========================================================================
+constexpr uint32_t kVoidKey = 0xFFFFFFFFu;  // never a key: local ids < 2^28 - 1, owners < 16
+
 template <bool kWrite>
 struct Emitter {
   const DevParams* P;
@@ -827,7 +829,50 @@ struct Emitter {
     n_all += k;
     n_valid += k;
   }
+  // delta-CRDT: a NoDeltaPlaceholder group's slot (phase A counted it): a void tell, compacted out
+  // of the bucket's tells after phase B (compact_void); not emitted, not in the next-pass histogram
+  uint32_t n_void = 0;
+  __device__ __forceinline__ void void_slot() {
+    ++n_void;
+    if (kWrite) {
+      out.key[pos] = kVoidKey;
+      ++pos;
+    }
+  }
 };
+
+// Remove the void tells (kVoidKey) from a bucket's tell chunk [base, base + n) in place, keeping the
+// sender order (tile by tile: every write lands at or below the positions still to be read).
+__device__ __forceinline__ uint32_t compact_void(const Msgs& m, uint64_t base, uint32_t n, uint32_t* scratch) {
+  constexpr uint32_t NT = 512, IPT = 4;
+  uint32_t out = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += NT * IPT) {
+    uint32_t k[IPT], sv[IPT], pv[IPT], c = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < IPT; ++r) {
+      const uint32_t i = t0 + threadIdx.x * IPT + r;
+      k[r] = i < n ? m.key[base + i] : kVoidKey;
+      if (k[r] != kVoidKey) {
+        sv[r] = m.src[base + i];
+        pv[r] = m.pay[base + i];
+        ++c;
+      }
+    }
+    uint32_t tot;
+    uint32_t o = out + block_excl_sum<NT>(c, scratch, &tot);  // (barriers: every load of the tile is done)
+#pragma unroll
+    for (uint32_t r = 0; r < IPT; ++r)
+      if (k[r] != kVoidKey) {
+        m.key[base + o] = k[r];
+        m.src[base + o] = sv[r];
+        m.pay[base + o] = pv[r];
+        ++o;
+      }
+    out += tot;
+    __syncthreads();
+  }
+  return out;
+}
 
 constexpr int kBThreads = 512;                 // bucket_apply block: 8 waves
 constexpr int kBWaves = kBThreads / kWave;
@@ -1443,6 +1488,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     }
   } else {
   uint32_t nrows_t = 0;  // snapshot rows this thread's actors will write (kWide)
+  uint32_t nvoid = 0;    // delta-CRDT: void tells (NoDeltaPlaceholder groups) this thread left
   // ---- phase A: emissions per actor (drain min(len, T) messages in order)
   #pragma unroll 1
     for (int j = 0; j < kBAct; ++j) {
@@ -1584,6 +1630,12 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       }
       nall += em.n_all;
       ndead += em.n_all - em.n_valid;
+      nvoid += em.n_void;
+    }
+    if constexpr ((KM & kDeltaKM) != 0) {  // NoDeltaPlaceholder groups are not told: drop their void slots
+      uint32_t tv;
+      block_excl_sum<kBThreads>(nvoid, L.scratch, &tv);
+      if (tv) emtot = compact_void(a.em, embase, emtot, L.scratch);
     }
     if constexpr (kGather || kOwner) {
       __syncthreads();  // phase B's tells are in the em scratch arena (sender order)

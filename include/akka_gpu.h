@@ -196,7 +196,8 @@ typedef struct agx_act {
  *   a DeltaPropagation is applied with causal delivery for ORSet (skip if already handled or a
  *   seqNr is missing, DD/Replicator.scala:1965-2027) and ORSet.mergeDelta (DD/ORSet.scala:455-501);
  *   counters merge it (no causal delivery needed).  A group that is a NoDeltaPlaceholder
- *   (too large, or a no-op update in range) is still told, empty, and ignored by the receiver.  */
+ *   (too large, or a no-op update in range) is not told (createDeltaPropagation leaves it out,
+ *   DD/Replicator.scala:1364,1957); deltaSentToNode still advances.                           */
 #define AGX_DELTA_WRITE 0x800000u
 #define AGX_DELTA_LOG 64u            /* ring entries per replica (seqNrs not yet sent to every node) */
 #define AGX_DELTA_ENV_WORDS 12u      /* u64 words of the envelope / selector area */

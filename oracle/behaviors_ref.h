@@ -282,10 +282,13 @@ static inline void dref_tick(ref_params* P, uint32_t kind, uint32_t a, uint64_t*
     for (uint32_t i = 0; i < s; ++i) {
       const uint32_t j = env[10 + sl[i]];
       if (env[8] <= j) continue; /* deltaEntriesAfter(j) is empty */
-      dref_group_row(P, w, kind, a, j, (uint32_t*)rowbuf);
+      const uint32_t ph = dref_group_row(P, w, kind, a, j, (uint32_t*)rowbuf);
       env[10 + sl[i]] = env[8]; /* deltaSentToNode(node) = last seqNr, also for a placeholder */
-      emit(ctx, a - a % AGX_CRDT_NODES + sl[i], a, ((kind - AGX_KIND_GCOUNTER) << 30) | AGX_DELTA_ROW_BIT, rowbuf,
-           ref_row_words(kind, 1));
+      /* createDeltaPropagation leaves NoDeltaPlaceholder out (DD/Replicator.scala:1364) and nothing is
+         sent for an empty propagation (:1957): a placeholder group is not told */
+      if (!ph)
+        emit(ctx, a - a % AGX_CRDT_NODES + sl[i], a, ((kind - AGX_KIND_GCOUNTER) << 30) | AGX_DELTA_ROW_BIT, rowbuf,
+             ref_row_words(kind, 1));
     }
     env[9] += s; /* deltaNodeRoundRobinCounter += sliceSize */
   }
