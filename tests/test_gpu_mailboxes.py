@@ -21,8 +21,9 @@ def _per_sender(d, s, p):
 
 def _run(w, ranks=1, max_steps=1 << 30, **cfg):
     from oracle import BspOracle
+    ba = cfg.pop("bucket_actors", w.bucket_actors)
     kw = dict(w.engine_kwargs(), **cfg)
-    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, bucket_actors=w.bucket_actors, **kw)) for r in range(ranks)]
+    engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, bucket_actors=ba, **kw)) for r in range(ranks)]
     for e in engs:
         w.apply_to(e)
     sg = engs[0].run(max_steps) if ranks == 1 else GpuEngine.group_run(engs, max_steps)
