@@ -197,6 +197,16 @@ struct agx_engine {
   // multi-pass, plain behaviours: skewed buckets split over workgroups (k_skew_*, agx_kernels.h)
   uint32_t *d_sk_rec = nullptr, *d_sk_act = nullptr, *d_sk_pc = nullptr, *d_sk_meta = nullptr;
   uint32_t sk_budget = 0, sk_rows = 0;
+  // bounded-mailbox rings (multi-pass, plain behaviours, every mailbox class bounded by <= kRingMaxC):
+  // a skewed bucket's queued messages stay in per-actor rings instead of the backlog arena.
+  // ring_res: pool slots whose drain scratch / tell slices were reserved after the arenas at
+  // create (ring_lo0 = acap); the pool itself is allocated at the first run whose mailbox classes
+  // allow it, with ring_c = the largest capacity, and fixes the classes from then on.
+  uint32_t ring_res = 0, ring_slots = 0, ring_c = 0;
+  bool ring_live = false;
+  uint32_t *d_ring_of = nullptr, *d_ring_state = nullptr, *d_ring_src = nullptr, *d_ring_pay = nullptr;
+  uint32_t* d_ring_next = nullptr;
+  unsigned long long* d_ring_total = nullptr;
   uint32_t tstride = 4, region = 0;
   uint64_t acap = 0;  // arena capacity (fused: regions + overflow area)
   uint32_t apply_grid = kMaxApplyGrid;  // AGX_APPLY_GRID test knob: fewer blocks, each looping over buckets
@@ -449,6 +459,7 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     ca.bl_stot = e->d_blpre + e->nb;
     ca.bl_sbase = e->d_blpre + e->nb + kMaxBlSlices;
     ca.d_ninbox = e->d_ninbox;
+    ca.ring_total = e->ring_live ? e->d_ring_total : nullptr;
     ca.bypass = 1;
     ca.heap_top = e->d_heap_top;
     ca.skew_n = e->d_skew_n;
@@ -615,6 +626,18 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   ba.tiny_max = e->tiny_max;
   ba.sk_rec = e->d_sk_rec;
   ba.sk_act = e->d_sk_act;
+  if (e->ring_live) {
+    ba.ring_of = e->d_ring_of;
+    ba.ring_state = e->d_ring_state;
+    ba.ring_src = e->d_ring_src;
+    ba.ring_pay = e->d_ring_pay;
+    ba.ring_next = e->d_ring_next;
+    ba.ring_total = e->d_ring_total;
+    ba.ring_slots = e->ring_slots;
+    ba.ring_c = e->ring_c;
+    ba.ring_t = e->Traw;
+    ba.ring_lo0 = (uint32_t)e->acap;
+  }
   SkewArgs ska{e->d_sk_rec, e->d_sk_act, e->d_sk_pc, e->d_sk_meta, e->sk_budget, e->sk_rows};
   {
     const uint32_t vid = apply_variant(e);
@@ -644,6 +667,43 @@ agx_status launch_staged_chunk(agx_engine* e) {
                      e->d_chunk_cnt, 2 * e->nb);
   HIP_TRY(hipGetLastError());
   e->n_staged_dev = 0;
+  return AGX_OK;
+}
+
+// Bounded-mailbox rings: allocate the pool at the first run whose configuration allows it (plain
+// behaviours, every configured mailbox class bounded by <= kRingMaxC); from then on the classes
+// are fixed (agx_set_mailbox_class refuses a capacity the rings cannot hold).
+agx_status setup_rings(agx_engine* e) {
+  if (e->ring_live || !e->ring_res || e->pw) return AGX_OK;
+  uint32_t cmax = 0;
+  for (uint32_t c = 0; c < AGX_MAX_MAILBOX_CLASSES; ++c) {
+    if (!((e->mclass_set >> c) & 1u)) continue;
+    if (e->mcap[c] == 0 || e->mcap[c] > kRingMaxC) return AGX_OK;  // an unbounded (or large) mailbox class
+    cmax = std::max(cmax, e->mcap[c]);
+  }
+  uint64_t budget = kRingPoolBytes;
+  if (const char* s = getenv("AGX_RING_MB")) budget = (uint64_t)std::max(0, atoi(s)) << 20;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) == hipSuccess) budget = std::min<uint64_t>(budget, fr / 4);
+  const uint64_t per = (uint64_t)kBucket * (2ull * cmax + 1) * 4;
+  const uint32_t slots = (uint32_t)std::min<uint64_t>(e->ring_res, budget / per);
+  if (!slots) return AGX_OK;
+  const uint64_t nst = (uint64_t)slots * kBucket, nmsg = nst * cmax;
+  AGX_TRY(dalloc(&e->d_ring_of, e->nb));
+  AGX_TRY(dalloc(&e->d_ring_state, nst));
+  AGX_TRY(dalloc(&e->d_ring_src, nmsg));
+  AGX_TRY(dalloc(&e->d_ring_pay, nmsg));
+  AGX_TRY(dalloc(&e->d_ring_next, 1));
+  AGX_TRY(dalloc(&e->d_ring_total, 2));
+  HIP_TRY(hipMemsetAsync(e->d_ring_of, 0, e->nb * 4ull, e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_ring_state, 0, nst * 4, e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_ring_next, 0, 4, e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_ring_total, 0, 8, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->ring_slots = slots;
+  e->ring_c = cmax;
+  e->ring_live = true;
+  drop_graphs(e);  // the ring arrays are kernel arguments of the captured supersteps
   return AGX_OK;
 }
 
@@ -821,7 +881,7 @@ agx_status read_counters(agx_engine* e, uint64_t* s) {
                        e->d_emc[0], e->d_emc[1], e->d_stg_cnt, e->par ^ 1u, e->nb, (unsigned long long*)e->d_inflight);
   else
     hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_chunk_cnt, e->nchunks,
-                       (unsigned long long*)e->d_inflight);
+                       (unsigned long long*)e->d_inflight, e->ring_live ? e->d_ring_total : nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(e->h_stat, e->d_stats, kStatBlk * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1373,6 +1433,17 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     e->apply_grid = (uint32_t)std::min<int>(kMaxApplyGrid, std::max(1, atoi(s)));
   e->acap = e->fused ? (uint64_t)e->nb * e->region + e->cap : e->cap;
   if (e->acap * e->kmax >= (1ull << 32)) { delete e; return set_err(AGX_EINVAL, "msg_capacity * max_emit too large"); }
+  // bounded-mailbox rings: drain scratch / tell slices of kBucket x throughput messages per pool slot
+  // after the arenas (AGX_RING_SLOTS: how many, 0 = off; CRDT kinds are registered later and turn
+  // the pool off at the first run; class 0 is agx_cfg.capacity, so an unbounded default never has rings)
+  if (!e->fused && e->R == 1 && e->Traw <= kRingMaxT && e->mcap[0] && e->mcap[0] <= kRingMaxC) {
+    uint64_t want = kRingSlots;
+    if (const char* s = getenv("AGX_RING_SLOTS")) want = (uint64_t)std::max(0, atoi(s));
+    const uint64_t per = (uint64_t)kBucket * e->Traw;
+    const uint64_t room = ((1ull << 32) / e->kmax - 1 - e->acap) / per;
+    e->ring_res = (uint32_t)std::min<uint64_t>({want, e->nb, room});
+  }
+  const uint64_t ring_extra = (uint64_t)e->ring_res * kBucket * e->Traw;
 
   e->h_kind.assign(e->n_local, 0);
   e->h_alive.assign(e->n_local, 0);
@@ -1403,9 +1474,9 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   }
   CREATE_TRY(alloc_msgs(e->A, e->acap));
   CREATE_TRY(alloc_msgs(e->B, e->fused ? 1 : e->cap));
-  CREATE_TRY(alloc_msgs(e->scr, e->acap));
+  CREATE_TRY(alloc_msgs(e->scr, e->acap + ring_extra));
   CREATE_TRY(alloc_msgs(e->bl, e->acap));
-  CREATE_TRY(alloc_msgs(e->em, e->acap * e->kmax));
+  CREATE_TRY(alloc_msgs(e->em, (e->acap + ring_extra) * e->kmax));
   if (e->R > 1) {  // tells grouped by owner per bucket (eg0 + [R][tstride] tables), send buffer s2
     const uint64_t tsz = (uint64_t)e->R * e->tstride;
     CREATE_TRY(alloc_msgs(e->eg0, e->cap_emit));
@@ -1420,7 +1491,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   }
   if (!e->fused && e->R == 1) {  // multi-pass: backlog and tell arenas by superstep parity
     CREATE_TRY(alloc_msgs(e->bl2, e->acap));
-    CREATE_TRY(alloc_msgs(e->em2, e->acap * e->kmax));
+    CREATE_TRY(alloc_msgs(e->em2, (e->acap + ring_extra) * e->kmax));
     if (e->ident_on) {
       CREATE_TRY(dalloc(&e->d_emmeta, e->nb));
       CREATE_TRY(dalloc(&e->d_slsum, (uint64_t)(kMaxBlSlices + 1) * kSlSum));
@@ -1545,6 +1616,8 @@ agx_status agx_destroy(agx_engine* e) {
   if (e->h_abort) hipHostFree(e->h_abort);
   hipFree(e->d_skew_list); hipFree(e->d_skew_n);
   hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);
+  hipFree(e->d_ring_of); hipFree(e->d_ring_state); hipFree(e->d_ring_src); hipFree(e->d_ring_pay);
+  hipFree(e->d_ring_next); hipFree(e->d_ring_total);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_blpre); hipFree(e->d_ninbox); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_cvec); hipFree(e->d_cmat);
@@ -1607,6 +1680,10 @@ agx_status agx_set_mailbox_class(agx_engine* e, uint32_t cls, uint32_t capacity)
   if (cls == 0 || cls >= AGX_MAX_MAILBOX_CLASSES)
     return set_err(AGX_EINVAL, "mailbox class %u: classes 1..%u are configurable (0 is agx_cfg.capacity)", cls,
                    AGX_MAX_MAILBOX_CLASSES - 1);
+  if (e->ring_live && (capacity == 0 || capacity > e->ring_c))
+    return set_err(AGX_EINVAL,
+                   "mailbox class %u capacity %u: this engine keeps queued messages in rings of %u (set every "
+                   "mailbox class before the first run, or AGX_RING_SLOTS=0)", cls, capacity, e->ring_c);
   e->mcap[cls] = capacity;
   e->mclass_set |= 1u << cls;
   e->mclasses = true;
@@ -1902,6 +1979,7 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
   AGX_TRY(ensure_dev(e));
   if (e->R > 1 && !e->comm) return set_err(AGX_ESTATE, "n_ranks > 1 needs agx_comm_init (or agx_group_run)");
   AGX_TRY(prepare_run(e));
+  AGX_TRY(setup_rings(e));
   e->started = true;
   if (e->R > 1) {
     AGX_TRY(run_multi_rccl(e, max_supersteps));
@@ -1944,6 +2022,18 @@ agx_status agx_identity_supersteps(agx_engine* e, uint64_t* out) {
   uint64_t s[kStatBlk];
   AGX_TRY(read_counters(e, s));
   *out = s[ST_IDENT];
+  return AGX_OK;
+}
+
+agx_status agx_ring_buckets(agx_engine* e, uint64_t* out) {
+  if (!e || !out) return set_err(AGX_EINVAL, "bad ring_buckets args");
+  AGX_TRY(ensure_dev(e));
+  *out = 0;
+  if (!e->ring_live) return AGX_OK;
+  uint32_t n = 0;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  HIP_TRY(hipMemcpy(&n, e->d_ring_next, 4, hipMemcpyDeviceToHost));
+  *out = std::min(n, e->ring_slots);
   return AGX_OK;
 }
 

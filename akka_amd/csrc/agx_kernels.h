@@ -395,7 +395,8 @@ struct ChunkSortArgs {
   uint32_t* blpre;     // bypass: [nb] slice-local exclusive scan of the backlog chunk counts (rowscan blocks >= nd)
   uint32_t* bl_stot;   // bypass: [slices] backlog total per slice of kBlSlice buckets
   uint32_t* bl_sbase;  // bypass: out: [slices] exclusive scan of bl_stot (downsweep block 0)
-  uint32_t* d_ninbox;  // bypass: out: messages in this superstep's inboxes (sorted + backlog)
+  uint32_t* d_ninbox;  // bypass: out: messages in this superstep's inboxes (sorted + backlog + rings)
+  const unsigned long long* ring_total;  // bypass: messages held in bounded-mailbox rings (null: none)
   uint64_t cap;
   uint32_t stride, nunits, ng, G, shift, bits;
   uint32_t bypass;     // backlog chunks are read in place by the apply (not sorted; units < ng skipped)
@@ -603,7 +604,10 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortAr
       const uint32_t v = (uint32_t)tid < nsl ? a.bl_stot[tid] : 0u;
       const uint32_t inc = wave_incl_sum(v);
       if ((uint32_t)tid < nsl) a.bl_sbase[tid] = inc - v;
-      if (tid == kWave - 1) *a.d_ninbox = over ? 0u : total + inc;
+      if (tid == kWave - 1) {  // (rings: clamped, only "any mail at all" is read from it)
+        const unsigned long long rt = a.ring_total ? *a.ring_total : 0ull;
+        *a.d_ninbox = over ? 0u : total + inc + (uint32_t)(rt < (1ull << 30) ? rt : (1ull << 30));
+      }
     }
   }
   if (over) return;
@@ -982,6 +986,19 @@ struct BucketArgs {
   const uint32_t* ident;
   CMsgs in_alt;
   uint4* emmeta;
+  // bounded-mailbox rings (single-rank multi-pass, plain behaviours, every mailbox class bounded;
+  // null = off).  A bucket that reaches the skew path takes a pool slot (k_skew_plan) for good: its
+  // actors' queued messages then stay in per-actor rings of ring_c slots -- a queued message is
+  // written once and read once, when it is drained (AbstractBoundedNodeQueue.java:92-113: a queued
+  // node does not move) -- instead of being copied forward every superstep.
+  uint32_t* ring_of;        // [nb] pool slot + 1 (0 = the bucket's backlog is in the bl arena)
+  uint32_t* ring_state;     // [slots][kBucket] head | len << 16
+  uint32_t* ring_src;       // [slots][kBucket][ring_c]
+  uint32_t* ring_pay;
+  uint32_t* ring_next;      // pool slots handed out
+  unsigned long long* ring_total;  // messages held in rings (in flight)
+  uint32_t ring_slots, ring_c, ring_t;
+  uint32_t ring_lo0;        // drain scratch / tell slice of slot k: ring_lo0 + k * kBucket * ring_t
 };
 
 // The sorted new mail of a single-rank multi-pass superstep: the radix passes' output, or --
@@ -2022,6 +2039,10 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
 // =========================================================================
 constexpr uint32_t kSkRec = 12;    // b, lo, cnt, blc, blo, bst, pbase, np, ndrain, bltot, npb, -
 constexpr uint32_t kSkSpan = 4 * kBucket;  // minimum inbox positions per part
+constexpr uint32_t kRingMaxC = 256;  // bounded-mailbox rings: largest mailbox capacity they hold (16-bit state)
+constexpr uint32_t kRingMaxT = 64;   // largest throughput with rings (drain scratch of kBucket x T per slot)
+constexpr uint32_t kRingSlots = 8192;  // pool slots (buckets) reserved at create (AGX_RING_SLOTS)
+constexpr unsigned long long kRingPoolBytes = 16ull << 30;  // ring pool budget (AGX_RING_MB; <= free HBM / 4)
 constexpr uint32_t kSkActPlanes = 4;       // per actor of a skewed bucket: admitted, drained start, backlog start, drain limit
 
 struct SkewArgs {
@@ -2051,8 +2072,20 @@ static __global__ void __launch_bounds__(kScanThreads) k_skew_plan(BucketArgs a,
     const uint32_t bs = a.bstart[b], be = a.bstart[b + 1], bp = a.blpre[b] + a.bl_sbase[b / kBlSlice];
     const uint32_t blc = a.chunk_cnt[b], blo = a.chunk_off[b];
     uint32_t* r = k.rec + (size_t)i * kSkRec;
+    uint32_t rs = 0;  // ring pool slot + 1: a skewed bucket keeps its queued messages in place from now on
+    if (a.ring_of) {
+      rs = a.ring_of[b];
+      if (!rs && *a.ring_next < a.ring_slots) {
+        const uint32_t sl = atomicAdd(a.ring_next, 1u);
+        if (sl < a.ring_slots) {
+          rs = sl + 1u;
+          a.ring_of[b] = rs;
+        }
+      }
+    }
     r[0] = b;
-    r[1] = bs + bp;
+    r[1] = rs ? a.ring_lo0 + (rs - 1u) * (uint32_t)kBucket * a.ring_t : bs + bp;
+    r[11] = rs;
     r[2] = blc + (be - bs);
     r[3] = blc;
     r[4] = blo;
@@ -2162,6 +2195,78 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, Sk
       len[0] += v.x; len[1] += v.y; len[2] += v.z; len[3] += v.w;
     }
     uint32_t keep[kBAct], dr[kBAct], qd[kBAct], tl[kBAct], sd = 0, sq = 0, ndead = 0;
+    const uint32_t rs = r[11];  // ring bucket: its queued messages stay in the per-actor rings
+    if (rs) {
+      // ring of actor la: head h, length Lr (messages queued earlier, in arrival order, ahead of this
+      // superstep's arrivals).  Tail-drop over the concatenation ring ++ arrivals, as bucket_finish:
+      // keep = alive ? min(Lr + arr, C) : 0; Lk = min(Lr, keep) ring messages stay, keep - Lk arrivals
+      // are admitted; drained = min(keep, T): the first rr = min(Lk, drained) from the ring, then
+      // drained - rr arrivals; the other admitted arrivals are appended to the ring.
+      // Planes: [0] arrivals admitted, [1] drained segment start, [2] ring slot of the first queued
+      // arrival, [3] arrivals drained (the scatter's drain limit).
+      const uint32_t cs = a.ring_c, sbase = (rs - 1u) * (uint32_t)kBucket;
+      uint32_t* st = a.ring_state + sbase;
+      uint32_t hd[kBAct], rr[kBAct], nl[kBAct];
+      int dl = 0;
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        const uint32_t la = la0 + j;
+        const uint32_t ab = la < na ? P.alive[a0 + la] : 0u;
+        uint32_t C, T;
+        mbox_limits(P, ab, C, T);
+        const uint32_t sv = st[la], h = sv & 0xFFFFu, lr = sv >> 16, tot = lr + len[j];
+        const uint32_t kp = (ab & 1u) ? ((C == 0 || tot < C) ? tot : C) : 0u;
+        const uint32_t lk = min(lr, kp), drn = min(kp, T);
+        rr[j] = min(lk, drn);
+        hd[j] = h;
+        keep[j] = kp - lk;          // arrivals admitted
+        tl[j] = drn - rr[j];        // arrivals drained
+        dr[j] = drn;
+        qd[j] = h + lk < cs ? h + lk : h + lk - cs;  // ring slot of the first queued arrival
+        nl[j] = kp - drn;           // ring length after this superstep
+        ndead += tot - kp;
+        dl += (int)nl[j] - (int)lr;
+        sd += drn;
+      }
+      uint32_t td;
+      uint32_t ed = block_excl_sum<kBThreads>(sd, scratch, &td);
+      uint32_t* act = k.act + (size_t)i * kSkActPlanes * kBucket;
+      uint32_t ds[kBAct];
+      const uint32_t lo = r[1];
+      const uint32_t* rsrc = a.ring_src + (size_t)sbase * cs;
+      const uint32_t* rpay = a.ring_pay + (size_t)sbase * cs;
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        const uint32_t la = la0 + j;
+        ds[j] = ed;
+        for (uint32_t q = 0; q < rr[j]; ++q) {  // the ring's drained head -> the drain scratch, first
+          uint32_t x = hd[j] + q;
+          x = x < cs ? x : x - cs;
+          a.scr.key[lo + ed + q] = a0 + la;
+          a.scr.src[lo + ed + q] = rsrc[(size_t)la * cs + x];
+          a.scr.pay[lo + ed + q] = rpay[(size_t)la * cs + x];
+        }
+        ed += dr[j];
+        uint32_t h2 = hd[j] + rr[j];
+        h2 = h2 < cs ? h2 : h2 - cs;
+        st[la] = (nl[j] ? h2 : 0u) | nl[j] << 16;
+      }
+      reinterpret_cast<uint4*>(act)[tid] = make_uint4(keep[0], keep[1], keep[2], keep[3]);
+      reinterpret_cast<uint4*>(act + kBucket)[tid] = make_uint4(ds[0], ds[1], ds[2], ds[3]);
+      reinterpret_cast<uint4*>(act + 2 * kBucket)[tid] = make_uint4(qd[0], qd[1], qd[2], qd[3]);
+      reinterpret_cast<uint4*>(act + 3 * kBucket)[tid] = make_uint4(tl[0], tl[1], tl[2], tl[3]);
+      if (tid == 0) {
+        r[8] = td;
+        r[9] = 0u;  // (nothing in the backlog arena)
+      }
+      const uint32_t wd = wave_incl_sum(ndead);
+      if (lane_id() == kWave - 1 && wd) atomicAdd(&a.bstats[(size_t)blockIdx.x * kBStats + 1], (unsigned long long)wd);
+      // ring length change of the block (two's complement into the u64 total)
+      const uint32_t gp = wave_incl_sum(dl > 0 ? (uint32_t)dl : 0u), gn = wave_incl_sum(dl < 0 ? (uint32_t)-dl : 0u);
+      if (lane_id() == kWave - 1 && gp != gn)
+        atomicAdd(a.ring_total, (unsigned long long)((long long)gp - (long long)gn));
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
       const uint32_t la = la0 + j;
@@ -2202,7 +2307,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, Sk
 
 static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a, SkewArgs k) {
   __shared__ __attribute__((aligned(16))) uint16_t whist[kBWaves * kBucket];  // 32 KB
-  __shared__ uint32_t s_run[kBucket], s_keep[kBucket], s_ds[kBucket], s_bs[kBucket], s_tmp[kBucket], s_T[kBucket];
+  __shared__ uint32_t s_run[kBucket], s_keep[kBucket], s_ds[kBucket + 1], s_bs[kBucket], s_tmp[kBucket], s_T[kBucket];
   uint32_t* const s_first = s_tmp;  // backlog parts: first position of each actor's run in the part
   __shared__ uint32_t s_q[3];
   const DevParams& P = a.P;
@@ -2216,7 +2321,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
     sk_part(a, k, t, s_q);
     const uint32_t i = s_q[0], q0 = s_q[1], q1 = s_q[2];
     const uint32_t* r = k.rec + (size_t)i * kSkRec;
-    const uint32_t lo = r[1], blc = r[3], blo = r[4], bst = r[5];
+    const uint32_t lo = r[1], blc = r[3], blo = r[4], bst = r[5], rs = r[11];
     const uint32_t* act = k.act + (size_t)i * kSkActPlanes * kBucket;
     const uint32_t* pc = k.pc + (size_t)t * kBucket;
     for (uint32_t la = tid; la < kBucket; la += kBThreads) {
@@ -2224,9 +2329,34 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
       s_keep[la] = act[la];
       s_ds[la] = act[kBucket + la];
       s_bs[la] = act[2 * kBucket + la];
-      s_T[la] = act[3 * kBucket + la];  // the actor's drain limit (mailbox class)
+      s_T[la] = act[3 * kBucket + la];  // the actor's drain limit (mailbox class; ring: arrivals drained)
     }
+    if (tid == 0) s_ds[kBucket] = r[8];
     __syncthreads();
+    // an admitted arrival of rank `rank` among its actor's arrivals: drained (the scratch copy, in
+    // canonical order) or queued (the backlog arena at the canonical position; ring bucket: the
+    // actor's ring, behind the messages it already holds)
+    const uint32_t cs = a.ring_c;
+    const size_t rbase = rs ? (size_t)(rs - 1u) * kBucket * cs : 0;
+    auto place = [&](uint32_t la, uint32_t rank, uint32_t kv, uint32_t sv, uint32_t pv) {
+      const uint32_t T = s_T[la];
+      if (rank < T) {
+        const uint32_t pos = rs ? lo + s_ds[la + 1] - T + rank : lo + s_ds[la] + rank;  // (ring: after its drained head)
+        a.scr.key[pos] = kv;
+        a.scr.src[pos] = sv;
+        a.scr.pay[pos] = pv;
+      } else if (rs) {
+        uint32_t x = s_bs[la] + rank - T;
+        x = x < cs ? x : x - cs;
+        a.ring_src[rbase + (size_t)la * cs + x] = sv;
+        a.ring_pay[rbase + (size_t)la * cs + x] = pv;
+      } else {
+        const uint32_t pos = lo + s_bs[la] + rank - T;
+        blw.key[pos] = kv;
+        blw.src[pos] = sv;
+        blw.pay[pos] = pv;
+      }
+    };
     if (q1 <= blc) {  // a part of the previous backlog: grouped by actor, every item admitted unless
                       // its actor stopped; rank = earlier parts' count + distance to the run start
       for (uint32_t sub = q0; sub < q1; sub += kBucket) {
@@ -2246,13 +2376,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
           if (q >= q1) continue;
           const uint32_t rank = s_run[la] + (q - s_first[la]);
           if (rank >= s_keep[la]) continue;
-          const uint32_t sv = a.g.bl[rpar].src[blo + q], pv = a.g.bl[rpar].pay[blo + q];
-          const uint32_t T = s_T[la];
-          const uint32_t pos = rank < T ? lo + s_ds[la] + rank : lo + s_bs[la] + rank - T;
-          const Msgs& d = rank < T ? a.scr : blw;
-          d.key[pos] = kk[u];
-          d.src[pos] = sv;
-          d.pay[pos] = pv;
+          place(la, rank, kk[u], a.g.bl[rpar].src[blo + q], a.g.bl[rpar].pay[blo + q]);
         }
       }
       __syncthreads();
@@ -2310,20 +2434,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
         if (!live[u]) continue;
         const uint32_t la = kk[u] & amask;
         const uint32_t rank = s_run[la] + whist[w * kBucket + la] + rk[u];  // among this actor's arrivals
-        const uint32_t T = s_T[la];
-        if (rank < s_keep[la]) {
-          if (rank < T) {  // drained this superstep: the skew launch's scratch copy
-            const uint32_t pos = lo + s_ds[la] + rank;
-            a.scr.key[pos] = kk[u];
-            a.scr.src[pos] = sv[u];
-            a.scr.pay[pos] = pv[u];
-          } else {         // queued beyond the throughput cap: the backlog, in canonical order
-            const uint32_t pos = lo + s_bs[la] + rank - T;
-            blw.key[pos] = kk[u];
-            blw.src[pos] = sv[u];
-            blw.pay[pos] = pv[u];
-          }
-        }
+        if (rank < s_keep[la]) place(la, rank, kk[u], sv[u], pv[u]);
       }
       __syncthreads();
       for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] += s_tmp[la];
@@ -2414,7 +2525,8 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         hi_w = (uint32_t)__builtin_amdgcn_readlane((int)hi_w, 0);
         blc = (uint32_t)__builtin_amdgcn_readlane((int)blc, 0);
         blo = (uint32_t)__builtin_amdgcn_readlane((int)blo, 0);
-        tiny = hi_w - lo_w <= a.tiny_max && (uint64_t)hi_w <= a.cap;  // (over capacity: the block path reports it)
+        tiny = hi_w - lo_w <= a.tiny_max && (uint64_t)hi_w <= a.cap &&  // (over capacity: the block path reports it)
+               !(a.ring_of && a.ring_of[bw]);                         // (a ring bucket: skew path)
         if (tiny)
           tiny_bucket<KM>(a, iv, reinterpret_cast<TinyLds*>(U)[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
       }
@@ -2459,7 +2571,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
           s_lo = a.bstart[b];
           s_hi = a.bstart[b + 1];
         }
-        s_g[5] = s_hi - s_lo > (uint32_t)kBucket;
+        s_g[5] = s_hi - s_lo > (uint32_t)kBucket || (kBypass && a.ring_of && a.ring_of[b]);  // (a ring bucket: skew path)
         if (kDefer && s_g[5]) a.skew_list[atomicAdd(skew_n, 1u)] = b;
       }
     } else {
@@ -2531,7 +2643,8 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
       if (tid == 0 && s_g[2]) g.stg_cnt[b] = 0u;
     }
     const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
-    if (cnt == 0) {  // no mail (most buckets of a sparse superstep at 10^7+ actors): write the empty
+    const bool ringb = kBypass && !kWide && kSkew && a.ring_of && a.ring_of[b];  // (its rings may hold mail)
+    if (cnt == 0 && !ringb) {  // no mail (most buckets of a sparse superstep at 10^7+ actors): write the empty
                      // backlog / tell-chunk entries bucket_finish would write, skip the pipeline
       if (tid == 0) {
         if constexpr (kGather) {
@@ -2725,7 +2838,8 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         for (uint32_t la = tid; la < kBucket; la += kBThreads) s_seg[la] = act[kBucket + la];
         if (tid == 0) s_seg[kBucket] = r[8];
         __syncthreads();
-        bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, r[8], a0, na, wpar, 0u, acc, r[9]);
+        // (r[1]: the bucket's inbox index space, or a ring bucket's drain scratch / tell slice)
+        bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, r[1], r[8], a0, na, wpar, 0u, acc, r[9]);
         continue;
       }
       uint32_t* s_run = s_key;   // LDS items are unused on this path
@@ -3006,11 +3120,12 @@ static __global__ void __launch_bounds__(kThreads) k_mcompact_copy(McompactArgs 
   }
 }
 
-// messages in flight after the last apply = all chunk counts
+// messages in flight after the last apply = all chunk counts (+ the bounded-mailbox rings)
 static __global__ void __launch_bounds__(kScanThreads) k_inflight(const uint32_t* chunk_cnt, uint32_t nchunks,
-                                                           unsigned long long* out) {
+                                                           unsigned long long* out,
+                                                           const unsigned long long* ring_total) {
   __shared__ unsigned long long s;
-  if (threadIdx.x == 0) s = 0;
+  if (threadIdx.x == 0) s = ring_total ? *ring_total : 0ull;  // (+ messages queued in rings)
   __syncthreads();
   unsigned long long v = 0;
   for (uint32_t i = threadIdx.x; i < nchunks; i += blockDim.x) v += chunk_cnt[i];

@@ -238,6 +238,12 @@ class GpuEngine:
         check(self.lib.agx_identity_supersteps(self._h, ctypes.byref(v)))
         return int(v.value)
 
+    def ring_buckets(self) -> int:
+        """Buckets whose queued messages live in bounded-mailbox rings (agx_ring_buckets)."""
+        v = ctypes.c_uint64()
+        check(self.lib.agx_ring_buckets(self._h, ctypes.byref(v)))
+        return v.value
+
     def stats(self) -> Stats:
         st = AgxStats()
         check(self.lib.agx_get_stats(self._h, ctypes.byref(st)))

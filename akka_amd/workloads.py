@@ -405,16 +405,17 @@ def compiled_ring(n: int = 1_000_000, hops: int = 256, throughput: int = 5) -> W
 
 # ------------------------------------------------------------------ per-actor mailboxes + the reply path
 def mailbox_mix(n: int = 4096, seed: int = 7, throughput: int = 3, capacity: int = 0, n_host: int = 32,
-                tells_per_actor: int = 3) -> Workload:
+                tells_per_actor: int = 3, classes: dict | None = None) -> Workload:
     """mixed() with several mailbox types in one dispatcher (Mailboxes.lookupConfigurator per actor,
     Mailboxes.scala:204-260): quarters of the population bound to bounded-capacity:2, an unbounded
-    type, bounded-capacity:16 and the dispatcher default (`capacity`); plus `n_host` host-side actors
+    type, bounded-capacity:16 and the dispatcher default (`capacity`) -- or `classes` {class: capacity}
+    for classes 1..3; plus `n_host` host-side actors
     (ids n..n+n_host-1, e.g. JVM TestProbes) that tell GPU actors -- PINGPONG actors answer them
     through the outbox (sender() ! reply, ActorCell.scala:583-587)."""
     w = mixed(n, seed=seed, throughput=throughput, capacity=capacity, tells_per_actor=tells_per_actor)
     q = n // 4
     w.name = "mailbox_mix"
-    w.mailbox_classes = {1: 2, 2: 0, 3: 16}
+    w.mailbox_classes = dict(classes) if classes else {1: 2, 2: 0, 3: 16}
     w.mailboxes = [(0, q, 1), (q, q, 2), (2 * q, q, 3)]
     if n_host:
         w.outbound = (n, n_host)

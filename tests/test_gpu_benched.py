@@ -26,7 +26,7 @@ def _load(name):
     return json.loads((GOLD / name).read_text())
 
 
-def _run_both(w, max_steps=1 << 30, bucket_actors=None, **cfg):
+def _run_both(w, max_steps=1 << 30, bucket_actors=None, probe=None, **cfg):
     from oracle import BspOracle
     kw = w.engine_kwargs()
     kw.update(cfg)
@@ -36,6 +36,8 @@ def _run_both(w, max_steps=1 << 30, bucket_actors=None, **cfg):
     w.apply_to(eng)
     sg = eng.run(max_steps)
     wg, ag = eng.read_state()
+    if probe is not None:
+        probe(eng)
     eng.close()
     ref = BspOracle(**kw)
     w.apply_to(ref)
@@ -108,15 +110,24 @@ def test_throughput_zero_behaves_as_one(built, C):
 
 
 # ------------------------------------------------------------------ C5 as benched
-def test_c5_power_law_bounded_as_benched(built):
+@pytest.mark.parametrize("ring_slots", [None, "0", "5"])
+def test_c5_power_law_bounded_as_benched(built, monkeypatch, ring_slots):
     """bench C5: FORWARD_RR over the device-generated R-MAT power-law graph, BoundedMailbox(64),
     throughput 5, one message per actor with ttl 15 -- at 2.2M actors (> 2^20: the multi-pass
     grouping + in-place backlog path of the 100M bench) and the bench's 2 + 10 superstep window,
-    then to quiescence."""
+    then to quiescence.  ring_slots: the bounded-mailbox ring pool as benched (None), off (backlog
+    arena only), or 5 slots (ring and backlog buckets side by side)."""
+    if ring_slots is not None:
+        monkeypatch.setenv("AGX_RING_SLOTS", ring_slots)
     w = wl.power_law_forward(2_200_000, ttl=15, capacity=64, throughput=5, device_graph=True)
-    sg, so, a, b = _run_both(w, max_steps=12)
+    rings = []
+    sg, so, a, b = _run_both(w, max_steps=12, probe=lambda e: rings.append(e.ring_buckets()))
     _assert_same(sg, so, a, b, "C5 12 supersteps")
     assert sg.dead_letters > 0 and sg.in_flight > 0
+    if ring_slots is None:
+        assert rings[0] > 5, rings
+    else:
+        assert rings[0] == min(int(ring_slots), rings[0]) and (ring_slots == "0") == (rings[0] == 0), rings
     sg, so, a, b = _run_both(w)
     _assert_same(sg, so, a, b, "C5 to quiescence")
 

@@ -19,7 +19,7 @@ def _per_sender(d, s, p):
     return np.stack([s[o], d[o], p[o]])
 
 
-def _run(w, ranks=1, max_steps=1 << 30, **cfg):
+def _run(w, ranks=1, max_steps=1 << 30, probe=None, **cfg):
     from oracle import BspOracle
     ba = cfg.pop("bucket_actors", w.bucket_actors)
     kw = dict(w.engine_kwargs(), **cfg)
@@ -28,6 +28,8 @@ def _run(w, ranks=1, max_steps=1 << 30, **cfg):
         w.apply_to(e)
     sg = engs[0].run(max_steps) if ranks == 1 else GpuEngine.group_run(engs, max_steps)
     outs = [e.take_outbound() for e in engs]
+    if probe is not None:
+        probe(engs[0])
     ref = BspOracle(n_ranks=ranks, **kw)
     w.apply_to(ref)
     so = ref.run(max_steps)
@@ -67,6 +69,37 @@ def test_mailbox_classes_multipass(built, monkeypatch, tiny):
     monkeypatch.setenv("AGX_TINY", tiny)
     _run(wl.mailbox_mix(30_000, seed=5, throughput=2, capacity=6))
     _run(wl.mailbox_mix(30_000, seed=6, throughput=3, capacity=0), bucket_actors=32)
+
+
+@pytest.mark.parametrize("slots", ["8192", "3"])
+def test_bounded_rings_multipass(built, monkeypatch, slots):
+    """Every mailbox class bounded: buckets that reach the skew path keep their actors' queued
+    messages in per-actor rings (a 3-slot pool: ring and backlog buckets side by side), with stops,
+    replies to host senders and capacity classes 2 / 5 / 16 / 40 in one population."""
+    monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    monkeypatch.setenv("AGX_RING_SLOTS", slots)
+    rings = []
+    w = wl.mailbox_mix(30_000, seed=9, throughput=3, capacity=5, classes={1: 2, 2: 40, 3: 16},
+                       tells_per_actor=12)
+    _run(w, bucket_actors=32, probe=lambda e: rings.append(e.ring_buckets()))
+    assert 0 < rings[0] <= int(slots), rings
+    _run(w, bucket_actors=32, max_steps=3)  # stopped with messages in the rings
+
+
+def test_rings_fix_mailbox_classes(built, monkeypatch):
+    """Once the rings are allocated (first run), a class they cannot hold is refused loudly."""
+    from akka_amd._lib import AgxError
+    monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    w = wl.mailbox_mix(30_000, seed=3, throughput=3, capacity=5, classes={1: 2, 2: 40, 3: 16})
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+    w.apply_to(eng)
+    eng.run(2)
+    eng.set_mailbox_class(1, 30)  # within the ring capacity (40)
+    with pytest.raises(AgxError):
+        eng.set_mailbox_class(2, 0)
+    with pytest.raises(AgxError):
+        eng.set_mailbox_class(3, 41)
+    eng.close()
 
 
 @pytest.mark.parametrize("ranks", [2, 5])
