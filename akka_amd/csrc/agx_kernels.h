@@ -2039,7 +2039,7 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
 // =========================================================================
 constexpr uint32_t kSkRec = 12;    // b, lo, cnt, blc, blo, bst, pbase, np, ndrain, bltot, npb, -
 constexpr uint32_t kSkSpan = 4 * kBucket;  // minimum inbox positions per part
-constexpr uint32_t kRingMaxC = 256;  // bounded-mailbox rings: largest mailbox capacity they hold (16-bit state)
+constexpr uint32_t kRingMaxC = 4096;  // bounded-mailbox rings: largest mailbox capacity they hold (16-bit head / length)
 constexpr uint32_t kRingMaxT = 64;   // largest throughput with rings (drain scratch of kBucket x T per slot)
 constexpr uint32_t kRingSlots = 8192;  // pool slots (buckets) reserved at create (AGX_RING_SLOTS)
 constexpr unsigned long long kRingPoolBytes = 16ull << 30;  // ring pool budget (AGX_RING_MB; <= free HBM / 4)

@@ -209,13 +209,14 @@ def timed_workload(w, warmup: int, steps: int, prof_steps: int = 8, msg_capacity
     eng.profile_reset()
     eng.run(prof_steps)
     prof = eng.profile_read()
+    rings = eng.ring_buckets()
     eng.close()
     d = s1.delivered - s0.delivered
     ss = s1.supersteps - s0.supersteps
     bytes_alg = s1.bytes_alg - s0.bytes_alg
     return {"value": d / el, "unit": "msg/s", "delivered": d, "dead_letters": s1.dead_letters - s0.dead_letters,
             "supersteps_timed": ss, "ms_per_step": el / max(ss, 1) * 1e3, "setup_s": round(setup, 2),
-            "alg_bytes_per_msg": bytes_alg / max(d, 1),
+            "alg_bytes_per_msg": bytes_alg / max(d, 1), "ring_buckets": rings,
             "superstep_frac": bytes_alg / el / 1e9 / PEAK_HBM_GBS,
             "kernel_ms_per_step": {k: round(v["total_ms"] / max(v["launches"], 1), 4) for k, v in prof.items()
                                    if v["launches"]}}
