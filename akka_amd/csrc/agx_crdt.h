@@ -15,8 +15,9 @@
 //     receiveDeltaPropagation         DD/Replicator.scala:1965-2027 (causal delivery for ORSet)
 //     ORSet.mergeDelta / mergeRemoveDelta / DeltaOp.merge  DD/ORSet.scala:43-120,455-501
 //
-// State lives in the actor SoA (word-major u64, coalesced across the lanes of
-// a wave that drain consecutive actors).  A state gossip carries a handle to
+// A CRDT engine keeps the state actor-major (wide_state: a replica's words are one contiguous
+// row of P.pitch u64, 128-B aligned), so a replica's 2 KB of ORSet dots are whole cache lines
+// however its lanes diverge; plain engines keep the word-major SoA.  A state gossip carries a handle to
 // an immutable snapshot row (row-major, 16-B vector loads per lane).  Rows are
 // allocated per superstep in heap[step & 1] and read in the next superstep
 // from heap[(step - 1) & 1]; a gossip that stays queued beyond the
@@ -145,7 +146,7 @@ __device__ __forceinline__ uint32_t crdt_count(const DevParams& P, uint32_t kind
   const uint32_t op = pay >> 24, arg = pay & 0xFFFFFFu;
   const bool dm = (CM & kDeltaKM) != 0 && P.delta_max != 0;
   if (dm && (op == AGX_OP_DELTA_TICK || dl_records(kind, op, arg)) && !ds.on) {
-    const St32 s{P.state + l, P.n_local};
+    const St32 s{wide_state(P, l), 1};
     const uint32_t e0 = dl_env(kind);
     ds.on = true;
     ds.ctr = s.ld(e0 + 8);
@@ -436,8 +437,8 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
   if constexpr ((CM & ~kDeltaKM) == (1u << AGX_KIND_GCOUNTER)) kind = AGX_KIND_GCOUNTER;
   if constexpr ((CM & ~kDeltaKM) == (1u << AGX_KIND_PNCOUNTER)) kind = AGX_KIND_PNCOUNTER;
   if constexpr ((CM & ~kDeltaKM) == (1u << AGX_KIND_ORSET)) kind = AGX_KIND_ORSET;
-  const size_t nl = P.n_local;
-  uint64_t* st = P.state + l;  // word w at st[w * nl]
+  constexpr size_t nl = 1;
+  uint64_t* st = wide_state(P, l);  // word w at st[w * nl] (actor-major row)
   const uint32_t node = self % AGX_CRDT_NODES;
   const bool dm = (CM & kDeltaKM) != 0 && P.delta_max != 0;  // (the engine launches kDeltaKM variants then)
   const St32 s32{st, nl};
@@ -605,45 +606,41 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
   }
 }
 
-// ORSet-only populations with full-state gossip: one replica's whole drain run (nd messages in
-// order) applied element-batch-outer, so its 2 KB of dots are read and written once per run
-// instead of once per message (crdt_apply's per-message loop re-reads them for every merge and
-// snapshot: C4's tick + 2 gossips per replica read the state 3x).  Same results as nd calls of
-// crdt_apply<kb(ORSET)>: message q sees the state left by messages < q, per element.  The version
-// vector chain (merge: max with the row's; add: vvector(node) + 1) is recomputed in every batch
-// from the first one (the rows' vvectors are hot in the cache); messages are re-read from the
-// inbox (LDS or scratch).  Emissions and snapshot-row allocation happen once, in message order.
-// Returns the unhandled count.
+// ORSet-only populations with full-state gossip: one replica's drain run (nd messages in order)
+// in two passes.  orset_protocol (one lane per replica): emissions and snapshot-row allocation in
+// message order, the unhandled count.  orset_merge_wave (the whole wave on one replica, lane e =
+// element e of the 64-element universe): the replica's 2 KB of dots, every merged row and every
+// snapshot row move as whole contiguous rows (one 32-B slice per lane), and each message of the run
+// is applied to all elements at once -- message q sees the state left by messages < q (per element;
+// the version-vector chain is uniform across the lanes).  Same results as nd calls of
+// crdt_apply<kb(ORSET)>.
+constexpr uint32_t kOrMerge = 1, kOrAdd = 2, kOrRemove = 3, kOrClear = 4, kOrSnap = 5;
+__device__ __forceinline__ uint32_t orset_code(uint32_t sv, uint32_t pv) {
+  if (is_wide(sv)) return (pv >> 30) == (uint32_t)(AGX_KIND_ORSET - AGX_KIND_GCOUNTER) && !(pv & AGX_DELTA_ROW_BIT) ? kOrMerge : 0u;
+  const uint32_t op = pv >> 24, arg = pv & 0xFFFFFFu;
+  if (op == AGX_OP_ADD) return arg < AGX_ORSET_ELEMS ? kOrAdd : 0u;
+  if (op == AGX_OP_REMOVE) return arg < AGX_ORSET_ELEMS ? kOrRemove : 0u;
+  if (op == AGX_OP_CLEAR) return kOrClear;
+  if (op == AGX_OP_GOSSIP) return kOrSnap;
+  return 0u;
+}
+
+// pass 1 (per lane): returns the unhandled count; *state_work: the run reads or writes the state
 template <typename Emit, typename Src, typename Pay>
-__device__ __forceinline__ uint32_t orset_run(const DevParams& P, const CrdtHeap& H, uint32_t self, uint32_t l,
-                                              uint32_t s0, uint32_t nd, const Src& isrc, const Pay& ipay,
-                                              uint32_t& row_cursor, Emit& em) {
-  const size_t nl = P.n_local;
-  uint64_t* st = P.state + l;  // word w at st[w * nl]
-  const uint32_t node = self % AGX_CRDT_NODES;
-  constexpr uint32_t vw = AGX_ORSET_ELEMS * AGX_CRDT_NODES / 2;  // first vvector word
-  constexpr uint32_t kMerge = 1, kAdd = 2, kRemove = 3, kClear = 4, kSnap = 5;
+__device__ __forceinline__ uint32_t orset_protocol(const DevParams& P, uint32_t self, uint32_t s0, uint32_t nd,
+                                                   const Src& isrc, const Pay& ipay, uint32_t& row_cursor, Emit& em,
+                                                   bool* state_work) {
   const uint32_t f = P.n_global > 1 ? P.gossip_f : 0u;
-  auto code_of = [&](uint32_t sv, uint32_t pv) -> uint32_t {
-    if (is_wide(sv)) return (pv >> 30) == (uint32_t)(AGX_KIND_ORSET - AGX_KIND_GCOUNTER) && !(pv & AGX_DELTA_ROW_BIT) ? kMerge : 0u;
-    const uint32_t op = pv >> 24, arg = pv & 0xFFFFFFu;
-    if (op == AGX_OP_ADD) return arg < AGX_ORSET_ELEMS ? kAdd : 0u;
-    if (op == AGX_OP_REMOVE) return arg < AGX_ORSET_ELEMS ? kRemove : 0u;
-    if (op == AGX_OP_CLEAR) return kClear;
-    if (op == AGX_OP_GOSSIP) return kSnap;
-    return 0u;
-  };
-  // pass 1: protocol, emissions and snapshot rows, in message order
   uint32_t nunh = 0, nmod = 0;
   const uint32_t rc0 = row_cursor;
   for (uint32_t q = 0; q < nd; ++q) {
     const uint32_t sv = isrc(s0 + q), pv = ipay(s0 + q);
-    const uint32_t c = code_of(sv, pv);
+    const uint32_t c = orset_code(sv, pv);
     if (c == 0) {
       ++nunh;
       continue;
     }
-    if (c != kSnap) {
+    if (c != kOrSnap) {
       ++nmod;
       continue;
     }
@@ -654,100 +651,85 @@ __device__ __forceinline__ uint32_t orset_run(const DevParams& P, const CrdtHeap
     }
     if (arg > 0) em(self, AGX_OP(AGX_OP_GOSSIP, arg - 1u));
   }
-  if (nmod == 0 && row_cursor == rc0) return nunh;  // no state read or write
-  uint32_t vv0[AGX_CRDT_NODES];
+  *state_work = nmod != 0 || row_cursor != rc0;
+  return nunh;
+}
+
+// pass 2 (wave-uniform arguments, all 64 lanes converged): the run's state effects, rows from rc0
+template <typename Src, typename Pay>
+__device__ __forceinline__ void orset_merge_wave(const DevParams& P, const CrdtHeap& H, uint32_t l, uint32_t node,
+                                                 uint32_t s0, uint32_t nd, uint32_t rc0, const Src& isrc,
+                                                 const Pay& ipay) {
+  static_assert(AGX_ORSET_ELEMS == kWave, "one lane per ORSet element");
+  constexpr uint32_t vw = AGX_ORSET_ELEMS * AGX_CRDT_NODES / 2;  // first vvector word
+  const uint32_t e = lane_id();
+  const uint32_t f = P.n_global > 1 ? P.gossip_f : 0u;
+  uint64_t* st = wide_state(P, l);
+  uint4* se = reinterpret_cast<uint4*>(st + 4 * e);  // element e: 8 u32 dots = 2 x 16 B
+  const uint4* sv4 = reinterpret_cast<const uint4*>(st + vw);
+  const uint4 a0 = se[0], a1 = se[1], v0 = sv4[0], v1 = sv4[1];
+  uint32_t d[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  const uint32_t vv0[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  uint32_t cur[8];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint64_t x = st[(size_t)(vw + k) * nl];
-    vv0[2 * k] = (uint32_t)x;
-    vv0[2 * k + 1] = (uint32_t)(x >> 32);
-  }
-  uint32_t cur[AGX_CRDT_NODES];
-  constexpr uint32_t kE = 2;  // elements per batch: 8 state words, 2 x 32 B of each row
-  for (uint32_t e0 = 0; e0 < AGX_ORSET_ELEMS; e0 += kE) {
-    uint32_t d[kE][AGX_CRDT_NODES];  // this batch's dots (element, node)
-    uint32_t dirty = 0;              // bit 4u + k: state word k of element e0 + u changed
+  for (int n = 0; n < 8; ++n) cur[n] = vv0[n];
+  bool dirty = false;
+  uint32_t h = rc0;
+  for (uint32_t q = 0; q < nd; ++q) {
+    const uint32_t sv = isrc(s0 + q), pv = ipay(s0 + q);
+    const uint32_t c = orset_code(sv, pv);
+    const uint32_t arg = pv & 0xFFFFFFu;
+    if (c == kOrMerge) {  // ORSet.merge: dots per (element, node) against both vvectors, then vvector max
+      const uint32_t* row = H.row(pv & kHandleMask);
+      const uint4 ra = *reinterpret_cast<const uint4*>(row + 8 * e), rb = *reinterpret_cast<const uint4*>(row + 8 * e + 4);
+      const uint4 va = *reinterpret_cast<const uint4*>(row + 2 * vw), vb = *reinterpret_cast<const uint4*>(row + 2 * vw + 4);
+      const uint32_t r[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+      const uint32_t rvv[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
-    for (uint32_t u = 0; u < kE; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint64_t x = st[(size_t)(4 * (e0 + u) + k) * nl];
-        d[u][2 * k] = (uint32_t)x;
-        d[u][2 * k + 1] = (uint32_t)(x >> 32);
+      for (int n = 0; n < 8; ++n) {
+        const uint32_t o = orset_merge_entry(d[n], r[n], cur[n], rvv[n]);
+        dirty |= o != d[n];
+        d[n] = o;
       }
 #pragma unroll
-    for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) cur[n] = vv0[n];
-    uint32_t h = rc0;
-    const bool last = e0 + kE == AGX_ORSET_ELEMS;
-    for (uint32_t q = 0; q < nd; ++q) {
-      const uint32_t sv = isrc(s0 + q), pv = ipay(s0 + q);
-      const uint32_t c = code_of(sv, pv);
-      const uint32_t arg = pv & 0xFFFFFFu;
-      if (c == kMerge) {  // ORSet.merge: dots per (element, node) against both vvectors, then vvector max
-        const uint32_t* row = H.row(pv & kHandleMask);
-        const uint4 va = *reinterpret_cast<const uint4*>(row + 2 * vw);
-        const uint4 vb = *reinterpret_cast<const uint4*>(row + 2 * vw + 4);
-        const uint32_t rvv[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
-        uint4 ra[kE], rb[kE];
+      for (int n = 0; n < 8; ++n) cur[n] = max(cur[n], rvv[n]);
+    } else if (c == kOrAdd || c == kOrRemove || c == kOrClear) {
+      uint32_t ver = 0;
+      if (c == kOrAdd) {  // vvector + node; birth dot (node -> new version)
 #pragma unroll
-        for (uint32_t u = 0; u < kE; ++u) {
-          ra[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u));
-          rb[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u) + 4);
-        }
+        for (uint32_t n = 0; n < 8; ++n)
+          if (n == node) ver = cur[n] = cur[n] + 1u;
+      }
+      if (c == kOrClear || arg == e) {
 #pragma unroll
-        for (uint32_t u = 0; u < kE; ++u) {
-          const uint32_t r[8] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w, rb[u].x, rb[u].y, rb[u].z, rb[u].w};
-#pragma unroll
-          for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
-            const uint32_t o = orset_merge_entry(d[u][n], r[n], cur[n], rvv[n]);
-            dirty |= (o != d[u][n] ? 1u : 0u) << (4 * u + n / 2);
-            d[u][n] = o;
-          }
-        }
-#pragma unroll
-        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) cur[n] = max(cur[n], rvv[n]);
-      } else if (c == kAdd || c == kRemove || c == kClear) {
-        uint32_t ver = 0;
-        if (c == kAdd) {  // vvector + node; birth dot (node -> new version)
-#pragma unroll
-          for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n)
-            if (n == node) ver = cur[n] = cur[n] + 1u;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kE; ++u)
-          if (c == kClear || arg == e0 + u) {
-#pragma unroll
-            for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) d[u][n] = (c == kAdd && n == node) ? ver : 0u;
-            dirty |= 0xFu << (4 * u);
-          }
-      } else if (c == kSnap && f) {  // this batch of the snapshot row (and its vvector, once)
-        const uint32_t hr = h++;
-        if (hr < H.rows) {
-          uint32_t* row = H.wrow(hr);
-#pragma unroll
-          for (uint32_t u = 0; u < kE; ++u) {
-            *reinterpret_cast<uint4*>(row + 8 * (e0 + u)) = make_uint4(d[u][0], d[u][1], d[u][2], d[u][3]);
-            *reinterpret_cast<uint4*>(row + 8 * (e0 + u) + 4) = make_uint4(d[u][4], d[u][5], d[u][6], d[u][7]);
-          }
-          if (last) {
-            *reinterpret_cast<uint4*>(row + 2 * vw) = make_uint4(cur[0], cur[1], cur[2], cur[3]);
-            *reinterpret_cast<uint4*>(row + 2 * vw + 4) = make_uint4(cur[4], cur[5], cur[6], cur[7]);
-          }
+        for (uint32_t n = 0; n < 8; ++n) d[n] = (c == kOrAdd && n == node) ? ver : 0u;
+        dirty = true;
+      }
+    } else if (c == kOrSnap && f) {  // snapshot row: element e per lane, the vvector from lane 0
+      const uint32_t hr = h++;
+      if (hr < H.rows) {
+        uint32_t* row = H.wrow(hr);
+        *reinterpret_cast<uint4*>(row + 8 * e) = make_uint4(d[0], d[1], d[2], d[3]);
+        *reinterpret_cast<uint4*>(row + 8 * e + 4) = make_uint4(d[4], d[5], d[6], d[7]);
+        if (e == 0) {
+          *reinterpret_cast<uint4*>(row + 2 * vw) = make_uint4(cur[0], cur[1], cur[2], cur[3]);
+          *reinterpret_cast<uint4*>(row + 2 * vw + 4) = make_uint4(cur[4], cur[5], cur[6], cur[7]);
         }
       }
     }
-#pragma unroll
-    for (uint32_t u = 0; u < kE; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if ((dirty >> (4 * u + k)) & 1u) st[(size_t)(4 * (e0 + u) + k) * nl] = ((uint64_t)d[u][2 * k + 1] << 32) | d[u][2 * k];
   }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint64_t o = ((uint64_t)cur[2 * k + 1] << 32) | cur[2 * k];
-    if (cur[2 * k] != vv0[2 * k] || cur[2 * k + 1] != vv0[2 * k + 1]) st[(size_t)(vw + k) * nl] = o;
+  if (dirty) {
+    se[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    se[1] = make_uint4(d[4], d[5], d[6], d[7]);
   }
-  return nunh;
+  bool vch = false;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) vch |= cur[n] != vv0[n];
+  if (vch && e == 0) {
+    uint4* vo = reinterpret_cast<uint4*>(st + vw);
+    vo[0] = make_uint4(cur[0], cur[1], cur[2], cur[3]);
+    vo[1] = make_uint4(cur[4], cur[5], cur[6], cur[7]);
+  }
 }
 
 }  // namespace agx

@@ -29,7 +29,9 @@ struct DevParams {
   uint8_t* alive;           // read-only inside k_apply; stops are committed after it
   uint32_t* stopq;          // actors that returned Behaviors.stopped this step
   uint32_t* nstop;
-  uint64_t* state;          // word-major SoA: state[w * n_local + l]
+  uint64_t* state;          // word-major SoA: state[w * n_local + l]; CRDT engines (pw > 0): actor-major,
+                            // state[l * pitch + w] (wide_state)
+  uint32_t pitch;           // u64 words per actor row of a CRDT engine (0: word-major)
   // CRDT state gossips (agx_crdt.h): snapshot rows, row-major, `pw` u32 each.
   // heap = 2 x heap_rows rows (ping-pong by superstep parity); rx = rows
   // received from other ranks this superstep (handle - heap_rows).
@@ -59,6 +61,11 @@ struct DevParams {
 
 // An actor's bounded capacity (0 = unbounded) and drain limit from its alive byte (bit 0 = alive,
 // bits 1..3 = mailbox class): Mailboxes.lookupConfigurator per actor (Mailboxes.scala:204-260).
+// actor l's state row in a CRDT engine (actor-major, P.pitch u64 words per row)
+__device__ __forceinline__ uint64_t* wide_state(const DevParams& P, uint32_t l) {
+  return P.state + (size_t)l * P.pitch;
+}
+
 __device__ __forceinline__ void mbox_limits(const DevParams& P, uint32_t abyte, uint32_t& C, uint32_t& T) {
   if (P.nmc == 0) {  // (uniform: one mailbox type for the whole dispatcher)
     C = P.C;

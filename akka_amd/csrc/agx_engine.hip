@@ -137,6 +137,9 @@ struct agx_engine {
   uint8_t *d_kind = nullptr, *d_alive = nullptr;
   uint32_t *d_stopq = nullptr, *d_nstop = nullptr;
   uint64_t* d_state = nullptr;
+  // CRDT engines (pw > 0 at the first upload) keep the device state actor-major, `pitch` u64 per
+  // actor (a replica's words are one contiguous, 128-B aligned row); the host mirror stays word-major
+  uint32_t pitch = 0;
   uint32_t *d_gid = nullptr, *d_route = nullptr;
   uint32_t ring_stride = 1, fan_k = 0;
   uint64_t fan_seed = 0, zipf_n = 0;
@@ -366,6 +369,7 @@ DevParams make_params(agx_engine* e) {
   P.kind = e->d_kind;
   P.alive = e->d_alive;
   P.state = e->d_state;
+  P.pitch = e->pitch;
   P.stopq = e->d_stopq;
   P.nstop = e->d_nstop;
   P.heap = e->d_heap;
@@ -712,7 +716,24 @@ agx_status prepare_run(agx_engine* e) {
   if (e->actors_dirty) {
     HIP_TRY(hipMemcpyAsync(e->d_kind, e->h_kind.data(), e->n_local, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemcpyAsync(e->d_alive, e->h_alive.data(), e->n_local, hipMemcpyHostToDevice, e->stream));
-    HIP_TRY(hipMemcpyAsync(e->d_state, e->h_state.data(), e->n_local * e->W * 8, hipMemcpyHostToDevice, e->stream));
+    if (e->pw && !e->pitch) {  // first upload of a CRDT engine: actor-major rows from now on
+      const uint32_t pitch = e->W <= 16 ? (e->W + 1u) & ~1u : (e->W + 15u) & ~15u;
+      uint64_t* d = nullptr;
+      AGX_TRY(dalloc(&d, (uint64_t)e->n_local * pitch));
+      HIP_TRY(hipFree(e->d_state));
+      e->d_state = d;
+      e->pitch = pitch;
+      drop_graphs(e);  // (the state array is a kernel argument)
+    }
+    if (e->pitch) {  // word-major mirror -> actor-major rows
+      std::vector<uint64_t> rows((size_t)e->n_local * e->pitch, 0);
+      for (uint64_t w = 0; w < e->W; ++w)
+        for (uint64_t l = 0; l < e->n_local; ++l) rows[l * e->pitch + w] = e->h_state[w * e->n_local + l];
+      HIP_TRY(hipMemcpyAsync(e->d_state, rows.data(), rows.size() * 8, hipMemcpyHostToDevice, e->stream));
+      HIP_TRY(hipStreamSynchronize(e->stream));
+    } else {
+      HIP_TRY(hipMemcpyAsync(e->d_state, e->h_state.data(), e->n_local * e->W * 8, hipMemcpyHostToDevice, e->stream));
+    }
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->actors_dirty = false;
   }
@@ -867,7 +888,14 @@ agx_status sync_mirrors(agx_engine* e) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(e->h_alive.data(), e->d_alive, e->n_local, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(e->h_state.data(), e->d_state, e->n_local * e->W * 8, hipMemcpyDeviceToHost));
+  if (e->pitch) {  // actor-major rows -> word-major mirror
+    std::vector<uint64_t> rows((size_t)e->n_local * e->pitch);
+    HIP_TRY(hipMemcpy(rows.data(), e->d_state, rows.size() * 8, hipMemcpyDeviceToHost));
+    for (uint64_t w = 0; w < e->W; ++w)
+      for (uint64_t l = 0; l < e->n_local; ++l) e->h_state[w * e->n_local + l] = rows[l * e->pitch + w];
+  } else {
+    HIP_TRY(hipMemcpy(e->h_state.data(), e->d_state, e->n_local * e->W * 8, hipMemcpyDeviceToHost));
+  }
   return AGX_OK;
 }
 

@@ -1285,8 +1285,13 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         const bool has = la < na && (L.alive[la] & 1u) && L.seg[la + 1] != L.seg[la];
         const uint32_t l = a0 + la;
         kd[j] = has && kKindNeeded ? P.kind[l] : 0u;  // single-kind variants never read it
-        x0[j] = has ? ldg64(P.state, l) : 0ull;  // (32-bit offsets: one VGPR per address)
-        x1[j] = has && P.W > 1 ? ldg64(P.state, P.n_local + l) : 0ull;
+        if constexpr (kWide) {  // (CRDT engines: actor-major rows, wide_state)
+          x0[j] = has ? wide_state(P, l)[0] : 0ull;
+          x1[j] = has && P.W > 1 ? wide_state(P, l)[1] : 0ull;
+        } else {
+          x0[j] = has ? ldg64(P.state, l) : 0ull;  // (32-bit offsets: one VGPR per address)
+          x1[j] = has && P.W > 1 ? ldg64(P.state, P.n_local + l) : 0ull;
+        }
         if constexpr (kFwd) {
           frb[j] = has ? P.row_ptr[l] : 0ull;
           fre[j] = has ? P.row_ptr[l + 1] : ~0ull;  // (no mail: deg out of range -> no hint)
@@ -1308,8 +1313,13 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
       kd[j] = kKindNeeded ? P.kind[li[j]] : 0u;  // single-kind variants never read it
-      x0[j] = ldg64(P.state, li[j]);  // (32-bit offsets: one VGPR per address)
-      x1[j] = ldg64(P.state, w1off + li[j]);
+      if constexpr (kWide) {
+        x0[j] = wide_state(P, li[j])[0];
+        x1[j] = wide_state(P, li[j])[w1off ? 1 : 0];
+      } else {
+        x0[j] = ldg64(P.state, li[j]);  // (32-bit offsets: one VGPR per address)
+        x1[j] = ldg64(P.state, w1off + li[j]);
+      }
       if constexpr (kFwd) {
         frb[j] = P.row_ptr[li[j]];
         fre[j] = P.row_ptr[li[j] + 1];
@@ -1586,11 +1596,17 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   
     AGX_STAMP(a, 6);
     // ---- phase B: apply for real, write tells (sender order) and state
+    // (ORSet-only full-state variant: the state effects of each replica's run are applied by the
+    // whole wave afterwards, orset_merge_wave; L.ecnt[la] = the run's first snapshot row, or ~0)
+    constexpr bool kOrWave = kWide && KM == kb(AGX_KIND_ORSET);
   #pragma unroll 1
     for (int j = 0; j < kBAct; ++j) {
       const uint32_t la = j * kBThreads + tid;
       const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
-      if (la >= na || !len || !(L.alive[la] & 1u)) continue;
+      if (la >= na || !len || !(L.alive[la] & 1u)) {
+        if constexpr (kOrWave) L.ecnt[la] = 0xFFFFFFFFu;
+        continue;
+      }
       const uint32_t l = a0 + la;
       const uint32_t self = P.R > 1 ? P.gid[l] : l;
       Emitter<true> em{&P, a.em, embase + L.ecnt[la], self, 0, 0, L.nh, a.nx_shift, nhmask};
@@ -1601,9 +1617,12 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       uint32_t kd = L.kind[la];
       ++nact;
       if (kWide && is_crdt(kd)) {
-        if constexpr (KM == kb(AGX_KIND_ORSET)) {  // whole run element-batch-outer (agx_crdt.h)
-          nunh += orset_run(P, H, self, l, s0, nd, isrc, ipay, row_cursor, em);
+        if constexpr (kOrWave) {  // protocol here, state effects by the wave below (agx_crdt.h)
+          bool work = false;
+          const uint32_t rc0 = row_cursor;
+          nunh += orset_protocol(P, self, s0, nd, isrc, ipay, row_cursor, em, &work);
           ndel += nd;
+          L.ecnt[la] = work ? rc0 : 0xFFFFFFFFu;  // (this actor's tell offset is no longer needed)
         } else {
           for (uint32_t q = 0; q < nd; ++q) {
             const uint32_t r = crdt_apply<KM>(P, H, kd, self, l, isrc(s0 + q), ipay(s0 + q), row_cursor, em);
@@ -1640,14 +1659,37 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
             }
           }
         }
-        stg64(P.state, l, wv[0]);
-        if (P.W > 1) stg64(P.state, P.n_local + l, wv[1]);
+        if constexpr (kWide) {
+          wide_state(P, l)[0] = wv[0];
+          if (P.W > 1) wide_state(P, l)[1] = wv[1];
+        } else {
+          stg64(P.state, l, wv[0]);
+          if (P.W > 1) stg64(P.state, P.n_local + l, wv[1]);
+        }
         if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
           if (kd != L.kind[la]) P.kind[l] = (uint8_t)kd;
+        if constexpr (kOrWave) L.ecnt[la] = 0xFFFFFFFFu;
       }
       nall += em.n_all;
       ndead += em.n_all - em.n_valid;
       nvoid += em.n_void;
+    }
+    if constexpr (kOrWave) {  // each wave takes its lanes' replicas one at a time (lane = element)
+      const uint32_t wbase = tid & ~(kWave - 1u);
+  #pragma unroll 1
+      for (int j = 0; j < kBAct; ++j) {
+        uint64_t m = __ballot(L.ecnt[j * kBThreads + tid] != 0xFFFFFFFFu);
+        while (m) {
+          const uint32_t lb = j * kBThreads + wbase + (uint32_t)__builtin_ctzll(m);
+          m &= m - 1;
+          const uint32_t s0 = L.seg[lb], len = L.seg[lb + 1] - s0;
+          uint32_t Ca, Ta;
+          mbox_limits(P, L.alive[lb], Ca, Ta);
+          const uint32_t l = a0 + lb;
+          const uint32_t self = P.R > 1 ? P.gid[l] : l;
+          orset_merge_wave(P, H, l, self % AGX_CRDT_NODES, s0, min(len, Ta), L.ecnt[lb], isrc, ipay);
+        }
+      }
     }
     if constexpr ((KM & kDeltaKM) != 0) {  // NoDeltaPlaceholder groups are not told: drop their void slots
       uint32_t tv;
