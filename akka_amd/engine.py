@@ -215,7 +215,7 @@ class GpuEngine:
     # -- tell / run
     def tell(self, dst, payload, src=None) -> None:
         dst = _u32(dst)
-        pay = _u32(payload)
+        pay = _u32(np.broadcast_to(np.asarray(payload, dtype=np.uint32), dst.shape))  # (a scalar: every tell)
         srcp = None
         if src is not None:
             s = _u32(np.broadcast_to(np.asarray(src, dtype=np.uint32), dst.shape))

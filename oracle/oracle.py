@@ -209,7 +209,8 @@ class BspOracle(_Base):
         self.lib.bsp_set_graph(self.h, _p(rp, ctypes.c_uint64), _p(cl, ctypes.c_uint32))
 
     def tell(self, dst, payload, src=None):
-        dst, pay = _u32(dst), _u32(payload)
+        dst = _u32(dst)
+        pay = _u32(np.broadcast_to(np.asarray(payload, dtype=np.uint32), dst.shape))  # (a scalar: every tell)
         s = _u32(np.broadcast_to(np.asarray(NO_SENDER if src is None else src, dtype=np.uint32), dst.shape))
         if self.lib.bsp_stage(self.h, _p(dst, ctypes.c_uint32), _p(s, ctypes.c_uint32), _p(pay, ctypes.c_uint32),
                               dst.size):
@@ -282,7 +283,8 @@ class FjpOracle(_Base):
         self.lib.fjp_set_graph(self.h, _p(rp, ctypes.c_uint64), _p(cl, ctypes.c_uint32))
 
     def tell(self, dst, payload, src=None):
-        dst, pay = _u32(dst), _u32(payload)
+        dst = _u32(dst)
+        pay = _u32(np.broadcast_to(np.asarray(payload, dtype=np.uint32), dst.shape))  # (a scalar: every tell)
         s = _u32(np.broadcast_to(np.asarray(NO_SENDER if src is None else src, dtype=np.uint32), dst.shape))
         self.lib.fjp_stage(self.h, _p(dst, ctypes.c_uint32), _p(s, ctypes.c_uint32), _p(pay, ctypes.c_uint32),
                            dst.size)
