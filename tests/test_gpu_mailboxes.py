@@ -79,8 +79,13 @@ def test_bounded_rings_multipass(built, monkeypatch, slots):
     monkeypatch.setenv("AGX_RADIX_BITS", "3")
     monkeypatch.setenv("AGX_RING_SLOTS", slots)
     rings = []
-    w = wl.mailbox_mix(30_000, seed=9, throughput=3, capacity=5, classes={1: 2, 2: 40, 3: 16},
-                       tells_per_actor=12)
+    w = wl.mailbox_mix(30_000, seed=9, throughput=3, capacity=5, classes={1: 2, 2: 40, 3: 16})
+    # a hot spot: 6000 more tells to the 64 actors from 7500 (class 2) -- two buckets over one LDS tile
+    rng = np.random.default_rng(9)
+    dst, src, pay = w.tells
+    hd = rng.integers(7500, 7564, 6000).astype(np.uint32)
+    w.tells = (np.concatenate([dst, hd]), np.concatenate([src, rng.integers(0, 30_000, 6000).astype(np.uint32)]),
+               np.concatenate([pay, rng.integers(0, 12, 6000).astype(np.uint32)]))
     _run(w, bucket_actors=32, probe=lambda e: rings.append(e.ring_buckets()))
     assert 0 < rings[0] <= int(slots), rings
     _run(w, bucket_actors=32, max_steps=3)  # stopped with messages in the rings
