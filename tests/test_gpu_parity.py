@@ -449,7 +449,9 @@ def test_identity_grouping(built, monkeypatch, bits):
     (forwarders at first; host tells staged mid-run)."""
     monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
     from oracle import BspOracle
-    for w in (wl.token_ring(100_000, 12), _ring_and_forwarders()):
+    # (9-bit digits: the production plan, multi-pass only above 2^20 actors)
+    big = bits >= 9
+    for w in (wl.token_ring(1_200_000 if big else 100_000, 12), _ring_and_forwarders(1_300_000 if big else 120_000)):
         res = {}
         for ident in (True, False):
             if ident:
