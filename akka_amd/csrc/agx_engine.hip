@@ -2015,6 +2015,18 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
     AGX_TRY(run_single(e, max_supersteps));
   }
   prof_collect(e);
+  if (e->ident_on && getenv("AGX_IDENT_DEBUG")) {  // diagnostic: the last superstep's slice summaries
+    const uint32_t nsl = (e->nb + kBlSlice - 1) / kBlSlice;
+    std::vector<uint32_t> h((kMaxBlSlices + 1) * kSlSum), id(4);
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipMemcpy(h.data(), e->d_slsum, h.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(id.data(), e->d_ident, 16, hipMemcpyDeviceToHost));
+    fprintf(stderr, "[agx ident] on=%u rot=%u total=%u staged=%u |", id[0], id[1], id[2], h[kMaxBlSlices * kSlSum]);
+    for (uint32_t i = 0; i < nsl; ++i)
+      fprintf(stderr, " s%u{tot=%u fl=%u d=%u nd=%u pos=%u first=%u last=%u}", i, h[i * kSlSum], h[i * kSlSum + 1],
+              h[i * kSlSum + 2], h[i * kSlSum + 3], h[i * kSlSum + 4], h[i * kSlSum + 5], h[i * kSlSum + 6]);
+    fprintf(stderr, "\n");
+  }
   if (e->d_dbg) {  // diagnostic: mean phase durations of k_bucket_apply blocks (last superstep)
     const uint64_t nbk = std::min<uint64_t>(e->nb, 4096);
     std::vector<unsigned long long> h(nbk * 16);
