@@ -208,7 +208,8 @@ struct agx_engine {
   uint32_t ring_res = 0, ring_slots = 0, ring_c = 0;
   bool ring_live = false;
   uint32_t *d_ring_of = nullptr, *d_ring_state = nullptr, *d_ring_src = nullptr, *d_ring_pay = nullptr;
-  uint32_t* d_ring_next = nullptr;
+  uint32_t* d_ring_next = nullptr;  // [0] slots handed out, [1] free-stack depth
+  uint32_t* d_ring_free = nullptr;
   unsigned long long* d_ring_total = nullptr;
   uint32_t tstride = 4, region = 0;
   uint64_t acap = 0;  // arena capacity (fused: regions + overflow area)
@@ -636,6 +637,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     ba.ring_src = e->d_ring_src;
     ba.ring_pay = e->d_ring_pay;
     ba.ring_next = e->d_ring_next;
+    ba.ring_free = e->d_ring_free;
     ba.ring_total = e->d_ring_total;
     ba.ring_slots = e->ring_slots;
     ba.ring_c = e->ring_c;
@@ -647,7 +649,8 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     const uint32_t vid = apply_variant(e);
     const uint32_t mode = e->fused ? M_FUSED : e->R > 1 ? M_OWNER : M_BYPASS;
     const dim3 g(grid_for(e->nb, e->apply_grid));
-    const dim3 gs(grid_for(e->nb, std::min(e->apply_grid, e->skew_grid)));  // skew list (grid-stride)
+    // skew list (grid-stride); ring buckets take the skew launch every superstep: a wider grid then
+    const dim3 gs(grid_for(e->nb, std::min(e->apply_grid, e->ring_live ? std::max(e->skew_grid, 2048u) : e->skew_grid)));
     if (!e->skew_only) {
       Scope s(e, K_APPLY);
       HIP_TRY(agx_launch_apply(vid, mode, false, g, e->stream, ba));
@@ -697,11 +700,12 @@ agx_status setup_rings(agx_engine* e) {
   AGX_TRY(dalloc(&e->d_ring_state, nst));
   AGX_TRY(dalloc(&e->d_ring_src, nmsg));
   AGX_TRY(dalloc(&e->d_ring_pay, nmsg));
-  AGX_TRY(dalloc(&e->d_ring_next, 1));
+  AGX_TRY(dalloc(&e->d_ring_next, 2));
+  AGX_TRY(dalloc(&e->d_ring_free, slots));
   AGX_TRY(dalloc(&e->d_ring_total, 2));
   HIP_TRY(hipMemsetAsync(e->d_ring_of, 0, e->nb * 4ull, e->stream));
   HIP_TRY(hipMemsetAsync(e->d_ring_state, 0, nst * 4, e->stream));
-  HIP_TRY(hipMemsetAsync(e->d_ring_next, 0, 4, e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_ring_next, 0, 8, e->stream));
   HIP_TRY(hipMemsetAsync(e->d_ring_total, 0, 8, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->ring_slots = slots;
@@ -1645,7 +1649,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_skew_list); hipFree(e->d_skew_n);
   hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);
   hipFree(e->d_ring_of); hipFree(e->d_ring_state); hipFree(e->d_ring_src); hipFree(e->d_ring_pay);
-  hipFree(e->d_ring_next); hipFree(e->d_ring_total);
+  hipFree(e->d_ring_next); hipFree(e->d_ring_free); hipFree(e->d_ring_total);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_blpre); hipFree(e->d_ninbox); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_cvec); hipFree(e->d_cmat);
@@ -2070,7 +2074,7 @@ agx_status agx_ring_buckets(agx_engine* e, uint64_t* out) {
   AGX_TRY(ensure_dev(e));
   *out = 0;
   if (!e->ring_live) return AGX_OK;
-  uint32_t n = 0;
+  uint32_t n = 0;  // pool slots handed out (high-water mark: released slots are reused first)
   HIP_TRY(hipStreamSynchronize(e->stream));
   HIP_TRY(hipMemcpy(&n, e->d_ring_next, 4, hipMemcpyDeviceToHost));
   *out = std::min(n, e->ring_slots);

@@ -995,7 +995,8 @@ struct BucketArgs {
   uint32_t* ring_state;     // [slots][kBucket] head | len << 16
   uint32_t* ring_src;       // [slots][kBucket][ring_c]
   uint32_t* ring_pay;
-  uint32_t* ring_next;      // pool slots handed out
+  uint32_t* ring_next;      // [0] pool slots handed out, [1] released slots on the free stack
+  uint32_t* ring_free;      // [slots] free stack (slots of buckets that cooled down)
   unsigned long long* ring_total;  // messages held in rings (in flight)
   uint32_t ring_slots, ring_c, ring_t;
   uint32_t ring_lo0;        // drain scratch / tell slice of slot k: ring_lo0 + k * kBucket * ring_t
@@ -2109,22 +2110,26 @@ static __global__ void __launch_bounds__(kScanThreads) k_skew_plan(BucketArgs a,
   if (tid == 0) s_tot = 0;
   __syncthreads();
   unsigned long long part = 0;
-  for (uint32_t i = tid; i < n; i += kScanThreads) {
-    const uint32_t b = a.skew_list[i];
+  // ring pool slots for skewed buckets without one: the free stack first, then fresh slots
+  const uint32_t nfree = a.ring_of ? a.ring_next[1] : 0u, nnext = a.ring_of ? a.ring_next[0] : 0u;
+  uint32_t taken = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += kScanThreads) {
+    const uint32_t i = i0 + tid;
+    const uint32_t b = i < n ? a.skew_list[i] : 0u;
+    uint32_t rs = i < n && a.ring_of ? a.ring_of[b] : 0u;  // ring pool slot + 1
+    const bool need = i < n && a.ring_of && !rs;
+    uint32_t tn;
+    const uint32_t g = taken + block_excl_sum<kScanThreads>(need ? 1u : 0u, scratch, &tn);
+    taken += tn;
+    if (need) {
+      if (g < nfree) rs = a.ring_free[nfree - 1u - g] + 1u;
+      else if (nnext + (g - nfree) < a.ring_slots) rs = nnext + (g - nfree) + 1u;
+      if (rs) a.ring_of[b] = rs;
+    }
+    if (i >= n) continue;
     const uint32_t bs = a.bstart[b], be = a.bstart[b + 1], bp = a.blpre[b] + a.bl_sbase[b / kBlSlice];
     const uint32_t blc = a.chunk_cnt[b], blo = a.chunk_off[b];
     uint32_t* r = k.rec + (size_t)i * kSkRec;
-    uint32_t rs = 0;  // ring pool slot + 1: a skewed bucket keeps its queued messages in place from now on
-    if (a.ring_of) {
-      rs = a.ring_of[b];
-      if (!rs && *a.ring_next < a.ring_slots) {
-        const uint32_t sl = atomicAdd(a.ring_next, 1u);
-        if (sl < a.ring_slots) {
-          rs = sl + 1u;
-          a.ring_of[b] = rs;
-        }
-      }
-    }
     r[0] = b;
     r[1] = rs ? a.ring_lo0 + (rs - 1u) * (uint32_t)kBucket * a.ring_t : bs + bp;
     r[11] = rs;
@@ -2135,6 +2140,11 @@ static __global__ void __launch_bounds__(kScanThreads) k_skew_plan(BucketArgs a,
     part += blc + (be - bs);
   }
   atomicAdd(&s_tot, part);
+  if (tid == 0 && a.ring_of && taken) {
+    const uint32_t fu = min(taken, nfree);
+    a.ring_next[1] = nfree - fu;
+    a.ring_next[0] = min(a.ring_slots, nnext + (taken - fu));
+  }
   __syncthreads();
   // parts of at least kSkSpan positions, sum over buckets of ceil(cnt / span) <= budget + n
   const unsigned long long tot = s_tot;
@@ -2270,8 +2280,23 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, Sk
         dl += (int)nl[j] - (int)lr;
         sd += drn;
       }
-      uint32_t td;
-      uint32_t ed = block_excl_sum<kBThreads>(sd, scratch, &td);
+      uint32_t td, tl2;
+      uint32_t nlt = 0, arr = 0;
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        nlt += nl[j];
+        arr += len[j];
+      }
+      const uint2 ex2 = block_excl_sum2<kBThreads>(sd, nlt, scratch, &td, &tl2);
+      uint32_t ed = ex2.x;
+      uint32_t ta;
+      block_excl_sum<kBThreads>(arr, scratch, &ta);
+      if (tid == 0 && tl2 == 0 && ta <= (uint32_t)kBucket) {
+        // cooled down: rings empty and this superstep's mail fits one tile -- the slot goes back to
+        // the pool (the drain scratch / tell slice is still this superstep's; the next plan reuses it)
+        a.ring_of[b] = 0u;
+        a.ring_free[atomicAdd(&a.ring_next[1], 1u)] = rs - 1u;
+      }
       uint32_t* act = k.act + (size_t)i * kSkActPlanes * kBucket;
       uint32_t ds[kBAct];
       const uint32_t lo = r[1];

@@ -305,10 +305,11 @@ agx_status agx_get_stats(agx_engine* eng, agx_stats* out);
  * the previous apply's tells were already in destination order (a ring, a stencil -- identity
  * grouping).  Diagnostic; the grouping is the same either way.                  */
 agx_status agx_identity_supersteps(agx_engine* eng, uint64_t* out);
-/* Buckets whose queued messages live in bounded-mailbox rings (single-rank multi-pass engine whose
- * mailbox classes are all bounded): a bucket that once held more than one LDS
- * tile of mail keeps its actors' queued messages in per-actor rings of the largest capacity, so a
- * queued message is written once and read once.  Diagnostic; the semantics are the same either way. */
+/* Bounded-mailbox ring slots handed out so far (high-water mark; single-rank multi-pass engine whose
+ * mailbox classes are all bounded): a bucket that holds more than one LDS tile of
+ * mail keeps its actors' queued messages in per-actor rings of the largest capacity -- a queued
+ * message is written once and read once -- until its rings are empty and its mail fits one tile
+ * again (the slot is then reused).  Diagnostic; the semantics are the same either way. */
 agx_status agx_ring_buckets(agx_engine* eng, uint64_t* out);
 
 /* --- per-actor mailboxes (Mailboxes.lookupConfigurator, Mailboxes.scala:204-260) -------------

@@ -127,7 +127,7 @@ def test_c5_power_law_bounded_as_benched(built, monkeypatch, ring_slots):
     if ring_slots is None:
         assert rings[0] > 5, rings
     else:
-        assert rings[0] == min(int(ring_slots), rings[0]) and (ring_slots == "0") == (rings[0] == 0), rings
+        assert rings[0] <= int(ring_slots) and (ring_slots == "0") == (rings[0] == 0), rings
     sg, so, a, b = _run_both(w)
     _assert_same(sg, so, a, b, "C5 to quiescence")
 
