@@ -210,6 +210,10 @@ struct agx_engine {
   uint32_t *d_ring_of = nullptr, *d_ring_state = nullptr, *d_ring_src = nullptr, *d_ring_pay = nullptr;
   uint32_t* d_ring_next = nullptr;  // [0] slots handed out, [1] free-stack depth
   uint32_t* d_ring_free = nullptr;
+  // ORSet-only full-state populations: the apply's work list for k_orset_merge
+  uint4* d_orw = nullptr;
+  uint2* d_orm = nullptr;
+  uint32_t* d_orw_n = nullptr;
   unsigned long long* d_ring_total = nullptr;
   uint32_t tstride = 4, region = 0;
   uint64_t acap = 0;  // arena capacity (fused: regions + overflow area)
@@ -647,6 +651,14 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   SkewArgs ska{e->d_sk_rec, e->d_sk_act, e->d_sk_pc, e->d_sk_meta, e->sk_budget, e->sk_rows};
   {
     const uint32_t vid = apply_variant(e);
+    const bool orm = vid == V_OR;  // ORSet-only full state: state effects in k_orset_merge
+    if (orm) {
+      if (!e->d_orw) return set_err(AGX_ESTATE, "ORSet work list not allocated (setup_orset)");
+      ba.orw = e->d_orw;
+      ba.orm = e->d_orm;
+      ba.orw_n = e->d_orw_n;
+      HIP_TRY(hipMemsetAsync(e->d_orw_n, 0, 8, e->stream));
+    }
     const uint32_t mode = e->fused ? M_FUSED : e->R > 1 ? M_OWNER : M_BYPASS;
     const dim3 g(grid_for(e->nb, e->apply_grid));
     // skew list (grid-stride); ring buckets take the skew launch every superstep: a wider grid then
@@ -659,6 +671,11 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
       Scope s(e, K_SKEW);
       if (!kVariants[vid].wide && mode == M_BYPASS) skew_prepass(e, ba, ska);
       HIP_TRY(agx_launch_apply(vid, mode, true, gs, e->stream, ba));
+    }
+    if (orm) {
+      Scope s(e, K_APPLY);
+      hipLaunchKernelGGL(k_orset_merge, dim3(grid_for(e->n_local / 4 + 1, 4096)), dim3(kThreads), 0, e->stream, ba.P,
+                         (const uint4*)e->d_orw, (const uint2*)e->d_orm, (const uint32_t*)e->d_orw_n);
     }
   }
   if (e->R == 1) e->par ^= 1u;  // the next superstep writes the other parity (fused and multi-pass)
@@ -712,6 +729,15 @@ agx_status setup_rings(agx_engine* e) {
   e->ring_c = cmax;
   e->ring_live = true;
   drop_graphs(e);  // the ring arrays are kernel arguments of the captured supersteps
+  return AGX_OK;
+}
+
+// ORSet-only full-state populations: k_orset_merge's work list (before any graph capture)
+agx_status setup_orset(agx_engine* e) {
+  if (e->d_orw || apply_variant(e) != V_OR) return AGX_OK;
+  AGX_TRY(dalloc(&e->d_orw, e->n_local));
+  AGX_TRY(dalloc(&e->d_orm, e->acap));
+  AGX_TRY(dalloc(&e->d_orw_n, 2));
   return AGX_OK;
 }
 
@@ -1650,6 +1676,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);
   hipFree(e->d_ring_of); hipFree(e->d_ring_state); hipFree(e->d_ring_src); hipFree(e->d_ring_pay);
   hipFree(e->d_ring_next); hipFree(e->d_ring_free); hipFree(e->d_ring_total);
+  hipFree(e->d_orw); hipFree(e->d_orm); hipFree(e->d_orw_n);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
   hipFree(e->d_moff0); hipFree(e->d_moff1); hipFree(e->d_blpre); hipFree(e->d_ninbox); hipFree(e->d_n); hipFree(e->d_total);
   hipFree(e->d_stats); hipFree(e->d_bstats); hipFree(e->d_cvec); hipFree(e->d_cmat);
@@ -2012,6 +2039,7 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
   if (e->R > 1 && !e->comm) return set_err(AGX_ESTATE, "n_ranks > 1 needs agx_comm_init (or agx_group_run)");
   AGX_TRY(prepare_run(e));
   AGX_TRY(setup_rings(e));
+  AGX_TRY(setup_orset(e));
   e->started = true;
   if (e->R > 1) {
     AGX_TRY(run_multi_rccl(e, max_supersteps));
@@ -2136,6 +2164,7 @@ agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_steps, agx_
       return set_err(AGX_EINVAL, "group engines differ in row pitch / delta mode / max_emit / n_words");
     AGX_TRY(ensure_dev(engs[i]));
     AGX_TRY(prepare_run(engs[i]));
+    AGX_TRY(setup_orset(engs[i]));
     engs[i]->started = true;
   }
   const uint32_t S = n + 2;

@@ -997,6 +997,11 @@ struct BucketArgs {
   uint32_t* ring_pay;
   uint32_t* ring_next;      // [0] pool slots handed out, [1] released slots on the free stack
   uint32_t* ring_free;      // [slots] free stack (slots of buckets that cooled down)
+  // ORSet-only full-state populations: the state effects of each replica's run are left to
+  // k_orset_merge (a lean kernel, lane = element): one item per replica with work, and its run
+  uint4* orw;               // [n_local] {l, node, message offset, first snapshot row}
+  uint2* orm;               // [cap] (src, payload) of the runs
+  uint32_t* orw_n;          // [0] items, [1] messages (reset before the apply)
   unsigned long long* ring_total;  // messages held in rings (in flight)
   uint32_t ring_slots, ring_c, ring_t;
   uint32_t ring_lo0;        // drain scratch / tell slice of slot k: ring_lo0 + k * kBucket * ring_t
@@ -1597,8 +1602,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   
     AGX_STAMP(a, 6);
     // ---- phase B: apply for real, write tells (sender order) and state
-    // (ORSet-only full-state variant: the state effects of each replica's run are applied by the
-    // whole wave afterwards, orset_merge_wave; L.ecnt[la] = the run's first snapshot row, or ~0)
+    // (ORSet-only full-state variant: the state effects of each replica's run are applied by
+    // k_orset_merge after the apply; L.ecnt[la] = the run's first snapshot row, or ~0)
     constexpr bool kOrWave = kWide && KM == kb(AGX_KIND_ORSET);
   #pragma unroll 1
     for (int j = 0; j < kBAct; ++j) {
@@ -1618,7 +1623,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       uint32_t kd = L.kind[la];
       ++nact;
       if (kWide && is_crdt(kd)) {
-        if constexpr (kOrWave) {  // protocol here, state effects by the wave below (agx_crdt.h)
+        if constexpr (kOrWave) {  // protocol here, state effects by k_orset_merge (agx_crdt.h)
           bool work = false;
           const uint32_t rc0 = row_cursor;
           nunh += orset_protocol(P, self, s0, nd, isrc, ipay, row_cursor, em, &work);
@@ -1675,20 +1680,33 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       ndead += em.n_all - em.n_valid;
       nvoid += em.n_void;
     }
-    if constexpr (kOrWave) {  // each wave takes its lanes' replicas one at a time (lane = element)
-      const uint32_t wbase = tid & ~(kWave - 1u);
+    if constexpr (kOrWave) {  // the runs with state work -> k_orset_merge's list (wave-aggregated slots)
+      const uint32_t lane = lane_id();
   #pragma unroll 1
       for (int j = 0; j < kBAct; ++j) {
-        uint64_t m = __ballot(L.ecnt[j * kBThreads + tid] != 0xFFFFFFFFu);
-        while (m) {
-          const uint32_t lb = j * kBThreads + wbase + (uint32_t)__builtin_ctzll(m);
-          m &= m - 1;
-          const uint32_t s0 = L.seg[lb], len = L.seg[lb + 1] - s0;
+        const uint32_t la = j * kBThreads + tid;
+        const uint32_t rc0 = L.ecnt[la];
+        const bool work = rc0 != 0xFFFFFFFFu;
+        uint32_t nd = 0;
+        if (work) {
           uint32_t Ca, Ta;
-          mbox_limits(P, L.alive[lb], Ca, Ta);
-          const uint32_t l = a0 + lb;
-          const uint32_t self = P.R > 1 ? P.gid[l] : l;
-          orset_merge_wave(P, H, l, self % AGX_CRDT_NODES, s0, min(len, Ta), L.ecnt[lb], isrc, ipay);
+          mbox_limits(P, L.alive[la], Ca, Ta);
+          nd = min(L.seg[la + 1] - L.seg[la], Ta);
+        }
+        const uint64_t m = __ballot(work);
+        if (!m) continue;
+        const uint32_t mi = wave_incl_sum(nd), mtot = (uint32_t)__builtin_amdgcn_readlane((int)mi, kWave - 1);
+        uint32_t ib = 0, mb = 0;
+        if (lane == 0) {
+          ib = atomicAdd(&a.orw_n[0], (uint32_t)__popcll(m));
+          mb = atomicAdd(&a.orw_n[1], mtot);
+        }
+        ib = (uint32_t)__builtin_amdgcn_readlane((int)ib, 0) + (uint32_t)__popcll(m & lanemask_lt());
+        mb = (uint32_t)__builtin_amdgcn_readlane((int)mb, 0) + mi - nd;
+        if (work) {
+          const uint32_t l = a0 + la, self = P.R > 1 ? P.gid[l] : l, s0 = L.seg[la];
+          a.orw[ib] = make_uint4(l, (self % AGX_CRDT_NODES) | (nd << 8), mb, rc0);
+          for (uint32_t q = 0; q < nd; ++q) a.orm[mb + q] = make_uint2(isrc(s0 + q), ipay(s0 + q));
         }
       }
     }
@@ -3184,6 +3202,23 @@ static __global__ void __launch_bounds__(kThreads) k_mcompact_copy(McompactArgs 
       __syncthreads();  // every thread has read the count before it is cleared
       if (threadIdx.x == 0) a.tcnt[x] = 0u;  // the apply writes non-zero entries only
     }
+  }
+}
+
+// ORSet-only full-state populations: the state effects of every replica run the apply listed
+// (orset_protocol did its tells and snapshot-row allocation): one wave per replica, lane = element
+// (orset_merge_wave).  A separate, lean kernel: far more waves in flight than the apply's 4 per
+// SIMD to cover the replica's state / row round trips.
+static __global__ void __launch_bounds__(kThreads) k_orset_merge(DevParams P, const uint4* orw, const uint2* orm,
+                                                             const uint32_t* orw_n) {
+  const uint32_t n = orw_n[0];
+  const CrdtHeap H = crdt_heap(P);
+  const uint32_t nw = gridDim.x * (kThreads / kWave);
+  for (uint32_t it = blockIdx.x * (kThreads / kWave) + threadIdx.x / kWave; it < n; it += nw) {
+    const uint4 w = orw[it];
+    const uint2* msg = orm + w.z;
+    orset_merge_wave(P, H, w.x, w.y & 0xFFu, 0u, w.y >> 8, w.w, [&](uint32_t q) { return msg[q].x; },
+                     [&](uint32_t q) { return msg[q].y; });
   }
 }
 
