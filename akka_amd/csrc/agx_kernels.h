@@ -419,6 +419,7 @@ constexpr uint32_t kSlSum = 8;  // per slice: total, flags, delta, descents, pos
 // the wrapped keys strictly below the first key, so no actor receives from both ends.
 // SURVEY.md §7 hard part 2: skipping the sort for a static topology is legitimate if the inbox
 // order is identical (akka-actor/src/main/scala/akka/dispatch/Mailbox.scala:89 enqueue order).
+// (scratch: 2 * (kWaves + 1) u32)
 __device__ __forceinline__ void ident_slice(const ChunkSortArgs& a, uint32_t sl, uint32_t nsl, uint32_t* scratch) {
   __shared__ uint32_t s_tlast[kThreads], s_tfirst[kThreads];
   __shared__ int s_iscr[kWaves + 1];
@@ -545,7 +546,7 @@ static __global__ void __launch_bounds__(kWave) k_ident_combine(const uint32_t* 
 // one block per digit: exclusive prefix over units (in place) + digit total;
 // block 0 also commits the previous step's stops.
 static __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs a) {
-  __shared__ uint32_t scratch[kWaves + 1];
+  __shared__ uint32_t scratch[2 * (kWaves + 1)];  // (block_excl_sum2 in ident_slice needs both halves)
   if (blockIdx.x == 0) {
     begin_step(a.step, a.heap_top);
     commit_stops(a.alive, a.stopq, a.nstop);

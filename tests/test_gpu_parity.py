@@ -441,12 +441,13 @@ def _ring_and_forwarders(n=120_000, seed=3):
                        graph=(row, col), tells=(dst, src, pay))
 
 
-@pytest.mark.parametrize("bits", [3, 9])
-def test_identity_grouping(built, monkeypatch, bits):
+@pytest.mark.parametrize("bits,ba", [(3, 0), (9, 0), (3, 32)])
+def test_identity_grouping(built, monkeypatch, bits, ba):
     """Multi-pass supersteps whose tells are already in destination order skip the radix passes
     (identity grouping; a ring's wrap-around is a rotation) -- bit-exact against the oracle and
     against the same engine with identity grouping off, through transitions in both directions
-    (forwarders at first; host tells staged mid-run)."""
+    (forwarders at first; host tells staged mid-run).  ba = 32: 32-actor buckets, so the chunk
+    summaries span several slices of 2048 chunks (the 10^8-actor shape)."""
     monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
     from oracle import BspOracle
     # (9-bit digits: the production plan, multi-pass only above 2^20 actors)
@@ -458,7 +459,7 @@ def test_identity_grouping(built, monkeypatch, bits):
                 monkeypatch.delenv("AGX_NO_IDENT", raising=False)
             else:
                 monkeypatch.setenv("AGX_NO_IDENT", "1")
-            eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+            eng = GpuEngine(EngineConfig(**dict(w.gpu_kwargs(), bucket_actors=ba or w.bucket_actors)))
             w.apply_to(eng)
             s1 = eng.run(9)
             eng.tell(np.arange(0, w.n_actors, 97, dtype=np.uint32), 2)  # a staged burst: sort path once
