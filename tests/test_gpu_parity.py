@@ -449,6 +449,8 @@ def test_identity_grouping(built, monkeypatch, bits, ba):
     (forwarders at first; host tells staged mid-run).  ba = 32: 32-actor buckets, so the chunk
     summaries span several slices of 2048 chunks (the 10^8-actor shape)."""
     monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
+    if ba:
+        monkeypatch.setenv("AGX_TINY", "0")  # (a wave-path bucket is never summarised: no identity)
     from oracle import BspOracle
     # (9-bit digits: the production plan, multi-pass only above 2^20 actors)
     big = bits >= 9
