@@ -2729,7 +2729,9 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
       if (tid == 0 && s_g[2]) g.stg_cnt[b] = 0u;
     }
     const uint32_t lo = s_lo, cnt = s_hi > s_lo ? s_hi - s_lo : 0u;
-    const bool ringb = kBypass && !kWide && kSkew && a.ring_of && a.ring_of[b];  // (its rings may hold mail)
+    // (a ring bucket's rings may hold mail; the plan's record, not ring_of: k_skew_scan may have
+    // just returned the slot -- its drained ring messages are still in this superstep's scratch)
+    const bool ringb = kBypass && !kWide && kSkew && a.ring_of && a.sk_rec[(size_t)it * kSkRec + 11] != 0u;
     if (cnt == 0 && !ringb) {  // no mail (most buckets of a sparse superstep at 10^7+ actors): write the empty
                      // backlog / tell-chunk entries bucket_finish would write, skip the pipeline
       if (tid == 0) {
