@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--cpu-hops", type=int, default=96, help="hop budget of the bounded CPU sample")
     ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (N=1 only)")
     ap.add_argument("--quick-configs", action="store_true", help="C5 at 10M instead of 100M actors")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_r02.json"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_r03.json"),
                     help="PMC traffic summary written by profiles/collect_pmc.py")
     return ap.parse_args()
 
@@ -60,11 +60,19 @@ def kernel_bytes_per_msg(W: int) -> dict:
     }
 
 
-def kernel_rooflines(prof: dict, per_msg: dict, msgs_per_launch: int) -> dict:
+SORT_CLASSES = ("chunk_downsweep", "sort_upsweep", "sort_downsweep")
+
+
+def kernel_rooflines(prof: dict, per_msg: dict, msgs_per_launch: int, identity: bool = False) -> dict:
     """HBM roofline of every kernel class with algorithmic bytes: achieved = bytes per message x
-    messages per launch / average launch time (HIP events); `dominant` = largest total time."""
+    messages per launch / average launch time (HIP events); `dominant` = largest total time.
+    identity: every profiled superstep was grouped without a radix pass -- the
+    pass kernels were launched but returned at entry, so they move no bytes and get no roofline."""
     out = {}
     for k, v in prof.items():
+        if identity and k in SORT_CLASSES and v["launches"]:
+            out[k] = {"returned_at_entry": True, "avg_launch_ms": round(v["total_ms"] / v["launches"], 4)}
+            continue
         if not v["launches"] or not per_msg.get(k):
             continue
         avg_ms = v["total_ms"] / v["launches"]
@@ -363,6 +371,7 @@ def main():
         eng_l.profile_reset()
         eng_l.run(prof_l)
         pl = eng_l.profile_read()
+        prof_ident = eng_l.identity_supersteps() - ident_l == prof_l
         eng_l.close()
         el_l, dl_l = reduce_ranks(el_l, dl_l, world)
         large = {"actors": n_l, "actors_per_gpu": per, "steps": steps_l, "warmup": args.large_warmup,
@@ -370,7 +379,7 @@ def main():
                  "ms_per_step": el_l / steps_l * 1e3, "scaling": "strong",
                  "superstep_frac": (12 + 12 + 16 * cfg_words + 2) * per / (el_l / steps_l) / 1e9 / PEAK_HBM_GBS,
                  "identity_supersteps": int(ident_l),
-                 "roofline": kernel_rooflines(pl, kernel_bytes_per_msg(cfg_words), per)}
+                 "roofline": kernel_rooflines(pl, kernel_bytes_per_msg(cfg_words), per, identity=prof_ident)}
 
     value = delivered / elapsed
     # roofline of the dominant kernel (largest total time in the timed region)
