@@ -31,7 +31,11 @@ struct DevParams {
   uint32_t* nstop;
   uint64_t* state;          // word-major SoA: state[w * n_local + l]; CRDT engines (pw > 0): actor-major,
                             // state[l * pitch + w] (wide_state)
-  uint32_t pitch;           // u64 words per actor row of a CRDT engine (0: word-major)
+  uint32_t pitch;           // u64 words per actor row of an actor-major engine (0: word-major)
+  // words 0 / 1 of a plain behaviour: state[l * sa + w * sw] -- word-major (sa 1, sw n_local), or
+  // actor-major pairs of a two-word engine (sa 2, sw 1: one line holds both words of 8 actors, so
+  // a sparse superstep touches one state line per activation instead of two)
+  uint32_t sa, sw;
   // CRDT state gossips (agx_crdt.h): snapshot rows, row-major, `pw` u32 each.
   // heap = 2 x heap_rows rows (ping-pong by superstep parity); rx = rows
   // received from other ranks this superstep (handle - heap_rows).
@@ -65,6 +69,9 @@ struct DevParams {
 __device__ __forceinline__ uint64_t* wide_state(const DevParams& P, uint32_t l) {
   return P.state + (size_t)l * P.pitch;
 }
+
+// word w (0 or 1) of a plain behaviour's state (P.sa / P.sw above; 32-bit offsets)
+__device__ __forceinline__ uint32_t sidx(const DevParams& P, uint32_t l, uint32_t w) { return l * P.sa + w * P.sw; }
 
 __device__ __forceinline__ void mbox_limits(const DevParams& P, uint32_t abyte, uint32_t& C, uint32_t& T) {
   if (P.nmc == 0) {  // (uniform: one mailbox type for the whole dispatcher)

@@ -161,6 +161,11 @@ struct agx_engine {
   uint32_t *d_heap = nullptr, *d_heap_top = nullptr, *d_step = nullptr;
   uint32_t *d_rx = nullptr, *d_s2rows = nullptr;  // multi-rank: received rows / rows packed for sending
   uint32_t *d_s2p = nullptr, *d_rcvp = nullptr;    // multi-rank: tells as (key, src, payload) triples, sent / received
+  // device-resident multi-rank replays (run_multi_rccl, plain behaviours): fixed per-peer slabs of
+  // `slab` envelopes, the replay's stop word halt[2] (k_mr_pack); h_halt = its pinned copy
+  uint32_t *d_sslab = nullptr, *d_rslab = nullptr, *d_halt = nullptr, *h_halt = nullptr;
+  uint32_t slab = 0;
+  uint64_t mr_exact = 0;  // supersteps whose exchange the host redid exactly (a count over the slab)
 
   DevMsgs A, B, scr, bl, em, stg, s2;
   // single-rank multi-pass: the tell arena by superstep parity (em = even, em2 = odd superstep
@@ -375,6 +380,8 @@ DevParams make_params(agx_engine* e) {
   P.alive = e->d_alive;
   P.state = e->d_state;
   P.pitch = e->pitch;
+  P.sa = e->pitch ? e->pitch : 1u;
+  P.sw = e->pitch ? 1u : (uint32_t)e->n_local;
   P.stopq = e->d_stopq;
   P.nstop = e->d_nstop;
   P.heap = e->d_heap;
@@ -426,7 +433,8 @@ agx_status launch_dense_pass(agx_engine* e, const DevMsgs& in, const DevMsgs& ou
   sa.super = e->dsuper;
   sa.shift = shift;
   sa.bits = bits;
-  sa.ident = e->ident_on ? e->d_ident : nullptr;
+  // (multi-rank: the device-resident replays' stop word -- [0] != 0 makes the pass return, like identity)
+  sa.ident = e->ident_on ? e->d_ident : e->R > 1 ? e->d_halt : nullptr;
   const uint32_t g = grid_for(e->max_supers, 4096);
   {
     Scope s(e, K_UPSWEEP);
@@ -487,11 +495,22 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     }
     {
       Scope s(e, K_CROWSCAN);
-      hipLaunchKernelGGL(k_chunk_rowscan, dim3((1u << ca.bits) + nsl + (e->ident_on ? nsl + 1 : 0)), dim3(kThreads), 0,
-                         e->stream, ca);
-      if (e->ident_on)  // this superstep's grouping: identity (no pass) or the radix passes
+      if (e->ident_on && e->plan.npass > 1) {
+        // the decision first (slice summaries, k_ident_combine), then the rowscan proper, whose digit
+        // rows are skipped under identity (k_bucket_bounds finds the bucket starts in place)
+        ca.part = 1;
+        hipLaunchKernelGGL(k_chunk_rowscan, dim3(nsl + 1), dim3(kThreads), 0, e->stream, ca);
         hipLaunchKernelGGL(k_ident_combine, dim3(1), dim3(kWave), 0, e->stream, e->d_slsum, nsl, e->d_ident,
                            reinterpret_cast<unsigned long long*>(e->d_stats + ST_IDENT));
+        ca.part = 2;
+        hipLaunchKernelGGL(k_chunk_rowscan, dim3((1u << ca.bits) + nsl), dim3(kThreads), 0, e->stream, ca);
+      } else {
+        hipLaunchKernelGGL(k_chunk_rowscan, dim3((1u << ca.bits) + nsl + (e->ident_on ? nsl + 1 : 0)), dim3(kThreads), 0,
+                           e->stream, ca);
+        if (e->ident_on)  // this superstep's grouping: identity (no pass) or the radix passes
+          hipLaunchKernelGGL(k_ident_combine, dim3(1), dim3(kWave), 0, e->stream, e->d_slsum, nsl, e->d_ident,
+                             reinterpret_cast<unsigned long long*>(e->d_stats + ST_IDENT));
+      }
     }
     {
       Scope s(e, K_CDOWN);
@@ -507,9 +526,9 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
   if (e->plan.npass > 1) {  // digits of the last pass are not buckets: find the bucket starts
     Scope s(e, K_BOUNDS);
     const bool idn = e->ident_on && first_from_chunks;
-    hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((e->nb + kThreads) / kThreads, 4096)), dim3(kThreads), 0,
+    hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((e->nb + kThreads / 8) / (kThreads / 8), 8192)), dim3(kThreads), 0,
                        e->stream, src->key, e->d_n, e->nb, e->bb, e->d_bstart, idn ? e->d_ident : nullptr,
-                       idn ? em_arena(e, e->par ^ 1u).key : nullptr);
+                       idn ? em_arena(e, e->par ^ 1u).key : nullptr, e->R > 1 ? e->d_halt : nullptr);
     HIP_TRY(hipGetLastError());
   }
   *result = src;
@@ -632,6 +651,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     ba.g.tstride = e->tstride;
   }
   ba.dbg = e->d_dbg;
+  ba.halt = e->R > 1 ? e->d_halt : nullptr;
   ba.tiny_max = e->tiny_max;
   ba.sk_rec = e->d_sk_rec;
   ba.sk_act = e->d_sk_act;
@@ -853,6 +873,7 @@ agx_status phase1(agx_engine* e) {
   m.R = e->R;
   m.tstride = e->tstride;
   m.n_staged = e->n_staged_dev;
+  m.halt = e->d_halt;  // (multi-rank only; zero outside device-resident replays)
   {
     Scope s(e, K_MCOMPACT);
     hipLaunchKernelGGL(k_mcompact_scan, dim3(1), dim3(kScanThreads), 0, e->stream, m);
@@ -911,20 +932,29 @@ void make_plan(agx_engine* e, const uint64_t* mat, Plan& p) {
   p.n_recv = ro - p.n_bl;
 }
 
+// host <-> device copies of the agx_set_* / read-back entry points: on the engine stream, waited for
+// (ordered after any work still queued there -- never a null-stream copy racing the non-blocking
+// engine stream)
+agx_status copy_sync(agx_engine* e, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, kind, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return AGX_OK;
+}
+
 // bring the host mirrors up to date with the device (commits pending stops)
 agx_status sync_mirrors(agx_engine* e) {
   if (e->actors_dirty) return AGX_OK;  // host mirror is newer than the device
   hipLaunchKernelGGL(k_commit_stops, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_alive, e->d_stopq, e->d_nstop);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipMemcpy(e->h_alive.data(), e->d_alive, e->n_local, hipMemcpyDeviceToHost));
+  AGX_TRY(copy_sync(e, e->h_alive.data(), e->d_alive, e->n_local, hipMemcpyDeviceToHost));
   if (e->pitch) {  // actor-major rows -> word-major mirror
     std::vector<uint64_t> rows((size_t)e->n_local * e->pitch);
-    HIP_TRY(hipMemcpy(rows.data(), e->d_state, rows.size() * 8, hipMemcpyDeviceToHost));
+    AGX_TRY(copy_sync(e, rows.data(), e->d_state, rows.size() * 8, hipMemcpyDeviceToHost));
     for (uint64_t w = 0; w < e->W; ++w)
       for (uint64_t l = 0; l < e->n_local; ++l) e->h_state[w * e->n_local + l] = rows[l * e->pitch + w];
   } else {
-    HIP_TRY(hipMemcpy(e->h_state.data(), e->d_state, e->n_local * e->W * 8, hipMemcpyDeviceToHost));
+    AGX_TRY(copy_sync(e, e->h_state.data(), e->d_state, e->n_local * e->W * 8, hipMemcpyDeviceToHost));
   }
   return AGX_OK;
 }
@@ -1263,6 +1293,71 @@ agx_status exchange_rccl(agx_engine* e, Plan& p) {
   return AGX_OK;
 }
 
+// ---- device-resident multi-rank supersteps (k_mr_pack / k_mr_unpack, agx_kernels.h)
+// first slab: 5/4 of an even share of one superstep's tells per (sender, receiver) pair, + 1024.
+// Every rank must size it alike (the sends and receives are fixed-size): it depends on n_global,
+// max_emit and R only, which the layout check compares (AGX_MR_SLAB overrides, on every rank).
+uint32_t mr_initial_slab(const agx_engine* e) {
+  if (const char* s = getenv("AGX_MR_SLAB")) return (uint32_t)std::max(1, atoi(s));
+  const uint64_t share = e->n_global * e->kmax / ((uint64_t)e->R * e->R);
+  return (uint32_t)std::min<uint64_t>(share + share / 4 + 1024, 1u << 30);
+}
+
+// (re)allocate the per-peer send / receive slabs (the same size on every rank: the decision to grow
+// comes from the all-gathered counts, which every rank reads alike)
+agx_status mr_slabs(agx_engine* e, uint64_t want) {
+  const uint32_t n = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 64), 1u << 30);
+  if (n <= e->slab) return AGX_OK;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  hipFree(e->d_sslab);
+  hipFree(e->d_rslab);
+  e->d_sslab = e->d_rslab = nullptr;
+  e->slab = 0;
+  AGX_TRY(dalloc(&e->d_sslab, (uint64_t)e->R * n * 3));
+  AGX_TRY(dalloc(&e->d_rslab, (uint64_t)e->R * n * 3));
+  e->slab = n;
+  return AGX_OK;
+}
+
+// one superstep with no host round trip: phase 1, count all-gather, the decision and the send
+// slabs (k_mr_pack), one fixed-size send / receive per peer, unpack, bucket passes, apply
+agx_status mr_step_dev(agx_engine* e, uint32_t idx) {
+  const uint32_t S = e->R + 2;
+  AGX_TRY(phase1(e));
+  MrArgs a{};
+  a.cmat = e->d_cmat;
+  a.s2 = e->s2.c();
+  a.sslab = e->d_sslab;
+  a.rslab = e->d_rslab;
+  a.A = e->A.m();
+  a.d_n = e->d_n;
+  a.halt = e->d_halt;
+  a.stats = e->d_stats;
+  a.cap = e->cap;
+  a.R = e->R;
+  a.rank = e->rank;
+  a.slab = e->slab;
+  a.step = idx;
+  const dim3 g(grid_for((uint64_t)e->R * e->slab / kThreads + 1, 2048));
+  {
+    Scope sc(e, K_EXCHANGE);
+    NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, S, ncclUint64, e->comm, e->stream));
+    hipLaunchKernelGGL(k_mr_pack, g, dim3(kThreads), 0, e->stream, a);
+    NCCL_TRY(ncclGroupStart());
+    for (uint32_t q = 0; q < e->R; ++q) {
+      if (q == e->rank) continue;
+      NCCL_TRY(ncclSend(e->d_sslab + (size_t)q * e->slab * 3, 3ull * e->slab, ncclUint32, (int)q, e->comm, e->stream));
+      NCCL_TRY(ncclRecv(e->d_rslab + (size_t)q * e->slab * 3, 3ull * e->slab, ncclUint32, (int)q, e->comm, e->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    hipLaunchKernelGGL(k_mr_unpack, g, dim3(kThreads), 0, e->stream, a);
+  }
+  HIP_TRY(hipGetLastError());
+  DevMsgs* sorted = nullptr;
+  AGX_TRY(launch_bucket_sort(e, false, &sorted));
+  return launch_apply(e, *sorted);
+}
+
 agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
   const uint32_t S = e->R + 2;
   Plan p;
@@ -1282,16 +1377,14 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
                        "(make the same register_range and set_* calls on every rank)", e->rank, r);
     e->layout_checked = true;
   }
-  for (uint32_t s = 0; s < max_steps; ++s) {
-    AGX_TRY(phase1(e));
-    {
-      Scope sc(e, K_EXCHANGE);
-      NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, S, ncclUint64, e->comm, e->stream));
-    }
+  // the host-planned exchange of a superstep whose phase 1 and count all-gather have run:
+  // exact sizes from the count matrix (one host round trip); *quiet: nothing was in flight
+  auto exact_rest = [&](bool* quiet) -> agx_status {
     HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_cmat, (size_t)e->R * S * 8, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     make_plan(e, e->h_pin64, p);
-    if (p.total_inflight == 0) break;
+    *quiet = p.total_inflight == 0;
+    if (*quiet) return AGX_OK;
     if (p.n_bl + p.n_recv + p.n_staged > e->cap)
       return set_err(AGX_ECAPACITY, "rank %u: %llu messages in flight exceed capacity %llu", e->rank,
                      (unsigned long long)(p.n_bl + p.n_recv + p.n_staged), (unsigned long long)e->cap);
@@ -1300,7 +1393,56 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
       AGX_TRY(exchange_rccl(e, p));
     }
     AGX_TRY(fix_rx(e, p));
-    AGX_TRY(phase2(e, p.n_bl + p.n_recv + p.n_staged, p.n_bl + p.n_recv));
+    return phase2(e, p.n_bl + p.n_recv + p.n_staged, p.n_bl + p.n_recv);
+  };
+  auto host_step = [&](bool* quiet) -> agx_status {
+    AGX_TRY(phase1(e));
+    {
+      Scope sc(e, K_EXCHANGE);
+      NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, S, ncclUint64, e->comm, e->stream));
+    }
+    return exact_rest(quiet);
+  };
+  uint32_t left = max_steps;
+  bool quiet = false;
+  // device-resident replays (plain behaviours: CRDT rows keep the host-planned exchange); a staged
+  // burst enters through one host-planned superstep (its staged count is a host number)
+  const bool dev = e->pw == 0 && !getenv("AGX_MR_HOST");
+  if (dev && e->n_staged_dev && left) {
+    AGX_TRY(host_step(&quiet));
+    --left;
+  }
+  if (dev) {
+    if (!e->slab) AGX_TRY(mr_slabs(e, mr_initial_slab(e)));
+    constexpr uint32_t kMrReplay = 8;  // supersteps enqueued before the host reads the stop word
+    while (left && !quiet) {
+      const uint32_t k = std::min(left, kMrReplay);
+      for (uint32_t i = 0; i < k; ++i) AGX_TRY(mr_step_dev(e, i));
+      HIP_TRY(hipMemcpyAsync(e->h_halt, e->d_halt, 8, hipMemcpyDeviceToHost, e->stream));
+      HIP_TRY(hipStreamSynchronize(e->stream));
+      const uint32_t code = e->h_halt[0], at = e->h_halt[1];
+      if (!code) {
+        left -= k;
+        continue;
+      }
+      left -= at;  // supersteps completed before the one that stopped (its phase 1 and all-gather ran)
+      HIP_TRY(hipMemsetAsync(e->d_halt, 0, 8, e->stream));
+      if (code == 2u) break;  // nothing in flight (the host path's quiescence, same point)
+      if (code == 3u)
+        return set_err(AGX_ECAPACITY, "rank %u: messages in flight exceed capacity %llu", e->rank,
+                       (unsigned long long)e->cap);
+      // a sender -> receiver count over the slab: this superstep's exchange exactly, bigger slabs
+      AGX_TRY(exact_rest(&quiet));
+      ++e->mr_exact;
+      --left;
+      uint64_t mx = 0;
+      for (uint32_t r = 0; r < e->R; ++r)
+        for (uint32_t q = 0; q < e->R; ++q)
+          if (q != r) mx = std::max<uint64_t>(mx, e->h_pin64[r * S + q]);
+      AGX_TRY(mr_slabs(e, mx + mx / 4 + 1024));
+    }
+  } else {
+    for (; left && !quiet; --left) AGX_TRY(host_step(&quiet));
   }
   HIP_TRY(hipMemcpyAsync(e->h_stat + ST_ERROR, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1492,10 +1634,12 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->acap = e->fused ? (uint64_t)e->nb * e->region + e->cap : e->cap;
   if (e->acap * e->kmax >= (1ull << 32)) { delete e; return set_err(AGX_EINVAL, "msg_capacity * max_emit too large"); }
   // bounded-mailbox rings: drain scratch / tell slices of kBucket x throughput messages per pool slot
-  // after the arenas (AGX_RING_SLOTS: how many, 0 = off; CRDT kinds are registered later and turn
-  // the pool off at the first run; class 0 is agx_cfg.capacity, so an unbounded default never has rings)
+  // after the arenas (AGX_RING_SLOTS: how many; CRDT kinds are registered later and turn the pool off
+  // at the first run; class 0 is agx_cfg.capacity, so an unbounded default never has rings).
+  // Opt-in: measured same-box against the backlog arena they cost C5 -2 % and C3 -6 % (every ring
+  // bucket takes the four-kernel skew path each superstep)
   if (!e->fused && e->R == 1 && e->Traw <= kRingMaxT && e->mcap[0] && e->mcap[0] <= kRingMaxC) {
-    uint64_t want = kRingSlots;
+    uint64_t want = 0;
     if (const char* s = getenv("AGX_RING_SLOTS")) want = (uint64_t)std::max(0, atoi(s));
     const uint64_t per = (uint64_t)kBucket * e->Traw;
     const uint64_t room = ((1ull << 32) / e->kmax - 1 - e->acap) / per;
@@ -1524,6 +1668,10 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(dalloc(&e->d_nstop, 4));
   CREATE_TRY(hipMemset(e->d_nstop, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_state, nl * e->W));
+  // two-word engines (the plain behaviours' count + cursor / sum): actor-major pairs on the device
+  // (DevParams::sa / sw; the host mirror stays word-major, transposed at upload / read-back).
+  // A CRDT kind needs n_words >= 8, so a two-word engine never becomes a CRDT engine.
+  if (e->W == 2 && !getenv("AGX_STATE_SOA")) e->pitch = 2;
   if (e->R > 1) {
     CREATE_TRY(dalloc(&e->d_gid, nl));
     CREATE_TRY(dalloc(&e->d_route, e->n_global));
@@ -1541,6 +1689,9 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(alloc_msgs(e->s2, e->cap_emit));
     CREATE_TRY(dalloc(&e->d_s2p, 3 * e->cap_emit));
     CREATE_TRY(dalloc(&e->d_rcvp, 3 * e->cap));
+    CREATE_TRY(dalloc(&e->d_halt, 2));
+    CREATE_TRY(hipMemset(e->d_halt, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    CREATE_TRY(hipHostMalloc((void**)&e->h_halt, 8, hipHostMallocDefault) == hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
     CREATE_TRY(dalloc(&e->d_tcnt[0], tsz));
     CREATE_TRY(dalloc(&e->d_toff[0], tsz));
     CREATE_TRY(hipMemset(e->d_tcnt[0], 0, tsz * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
@@ -1664,7 +1815,8 @@ agx_status agx_destroy(agx_engine* e) {
   free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1); free_msgs(e->em2);
   hipFree(e->d_emmeta); hipFree(e->d_slsum); hipFree(e->d_ident);
   hipFree(e->d_outbox); hipFree(e->d_outbox_n);
-  hipFree(e->d_s2p); hipFree(e->d_rcvp);
+  hipFree(e->d_s2p); hipFree(e->d_rcvp); hipFree(e->d_sslab); hipFree(e->d_rslab); hipFree(e->d_halt);
+  if (e->h_halt) hipHostFree(e->h_halt);
   for (int q = 0; q < 2; ++q) {
     hipFree(e->d_tcnt[q]); hipFree(e->d_toff[q]); hipFree(e->d_blo[q]); hipFree(e->d_blc[q]); hipFree(e->d_emc[q]);
   }
@@ -1781,7 +1933,7 @@ agx_status agx_set_outbound(agx_engine* e, uint32_t first_host_id, uint32_t n_ho
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (!e->d_outbox_n) {
     AGX_TRY(dalloc(&e->d_outbox_n, 1));
-    HIP_TRY(hipMemset(e->d_outbox_n, 0, 4));
+    HIP_TRY(hipMemsetAsync(e->d_outbox_n, 0, 4, e->stream));
   }
   if (n_host && capacity != e->outbox_cap) {
     hipFree(e->d_outbox);
@@ -1804,14 +1956,14 @@ agx_status agx_take_outbound(agx_engine* e, uint32_t* dst, uint32_t* src, uint32
   if (e->d_outbox_n) {  // move the device outbox to the host queue (the engine is idle between calls)
     HIP_TRY(hipStreamSynchronize(e->stream));
     uint32_t cnt = 0;
-    HIP_TRY(hipMemcpy(&cnt, e->d_outbox_n, 4, hipMemcpyDeviceToHost));
+    AGX_TRY(copy_sync(e, &cnt, e->d_outbox_n, 4, hipMemcpyDeviceToHost));
     const uint64_t m = std::min<uint64_t>(cnt, e->outbox_cap);
     if (m) {
       const size_t o = e->outq.size();
       e->outq.resize(o + 3 * m);
-      HIP_TRY(hipMemcpy(e->outq.data() + o, e->d_outbox, 12 * m, hipMemcpyDeviceToHost));
+      AGX_TRY(copy_sync(e, e->outq.data() + o, e->d_outbox, 12 * m, hipMemcpyDeviceToHost));
     }
-    if (cnt) HIP_TRY(hipMemset(e->d_outbox_n, 0, 4));
+    if (cnt) HIP_TRY(hipMemsetAsync(e->d_outbox_n, 0, 4, e->stream));
     HIP_TRY(hipDeviceSynchronize());
     if (cnt > e->outbox_cap)
       return set_err(AGX_ECAPACITY, "%u outbound tells since the last agx_take_outbound, outbox capacity %llu",
@@ -1882,9 +2034,9 @@ agx_status agx_set_behaviors(agx_engine* e, const agx_case* cases, uint32_t n_ca
   AGX_TRY(dalloc(&e->d_bcase, std::max<uint32_t>(n_cases, 1)));
   AGX_TRY(dalloc(&e->d_bact, std::max<uint32_t>(n_acts, 1)));
   AGX_TRY(dalloc(&e->d_bfirst, n_beh + 1));
-  if (n_cases) HIP_TRY(hipMemcpy(e->d_bcase, cases, n_cases * sizeof(agx_case), hipMemcpyHostToDevice));
-  if (n_acts) HIP_TRY(hipMemcpy(e->d_bact, acts, n_acts * sizeof(agx_act), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_bfirst, first, (n_beh + 1) * 4ull, hipMemcpyHostToDevice));
+  if (n_cases) AGX_TRY(copy_sync(e, e->d_bcase, cases, n_cases * sizeof(agx_case), hipMemcpyHostToDevice));
+  if (n_acts) AGX_TRY(copy_sync(e, e->d_bact, acts, n_acts * sizeof(agx_act), hipMemcpyHostToDevice));
+  AGX_TRY(copy_sync(e, e->d_bfirst, first, (n_beh + 1) * 4ull, hipMemcpyHostToDevice));
   e->n_beh = n_beh;
   drop_graphs(e);  // the tables are kernel parameters captured in the superstep graphs
   return AGX_OK;
@@ -1938,9 +2090,9 @@ agx_status agx_set_fanout(agx_engine* e, uint32_t k, uint64_t seed, const uint32
   AGX_TRY(dalloc(&e->d_zcdf, n));
   AGX_TRY(dalloc(&e->d_zperm, n));
   AGX_TRY(dalloc(&e->d_zidx, Z + 1));
-  HIP_TRY(hipMemcpy(e->d_zidx, zidx.data(), (Z + 1) * 4, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_zcdf, cdf, n * 4, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_zperm, perm, n * 4, hipMemcpyHostToDevice));
+  AGX_TRY(copy_sync(e, e->d_zidx, zidx.data(), (Z + 1) * 4, hipMemcpyHostToDevice));
+  AGX_TRY(copy_sync(e, e->d_zcdf, cdf, n * 4, hipMemcpyHostToDevice));
+  AGX_TRY(copy_sync(e, e->d_zperm, perm, n * 4, hipMemcpyHostToDevice));
   e->fan_k = k;
   e->fan_seed = seed;
   e->zipf_n = n;
@@ -1967,8 +2119,8 @@ agx_status agx_set_graph(agx_engine* e, const uint64_t* row_ptr, const uint32_t*
   e->d_col = nullptr;
   AGX_TRY(dalloc(&e->d_row, row.size()));
   AGX_TRY(dalloc(&e->d_col, c.size()));
-  HIP_TRY(hipMemcpy(e->d_row, row.data(), row.size() * 8, hipMemcpyHostToDevice));
-  if (!c.empty()) HIP_TRY(hipMemcpy(e->d_col, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+  AGX_TRY(copy_sync(e, e->d_row, row.data(), row.size() * 8, hipMemcpyHostToDevice));
+  if (!c.empty()) AGX_TRY(copy_sync(e, e->d_col, c.data(), c.size() * 4, hipMemcpyHostToDevice));
   e->graph_set = true;
   drop_graphs(e);
   return AGX_OK;
@@ -1994,8 +2146,8 @@ agx_status agx_set_graph_rmat(agx_engine* e, const uint64_t* row_ptr, uint32_t b
   AGX_TRY(dalloc(&e->d_row, lrow.size()));
   AGX_TRY(dalloc(&e->d_col, lrow.back()));
   AGX_TRY(dalloc(&d_gs, gstart.size()));
-  HIP_TRY(hipMemcpy(e->d_row, lrow.data(), lrow.size() * 8, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(d_gs, gstart.data(), gstart.size() * 8, hipMemcpyHostToDevice));
+  AGX_TRY(copy_sync(e, e->d_row, lrow.data(), lrow.size() * 8, hipMemcpyHostToDevice));
+  AGX_TRY(copy_sync(e, d_gs, gstart.data(), gstart.size() * 8, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_gen_rmat, dim3(grid_for(e->n_local / kThreads + 1, 8192)), dim3(kThreads), 0, e->stream,
                      e->d_row, d_gs, e->d_col, (uint32_t)e->n_local, bits, ta, tb, tc, seed, (uint32_t)e->n_global);
   hipError_t le = hipGetLastError();
@@ -2081,7 +2233,7 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
     for (size_t i = 0; i < std::min<size_t>(6, slow.size()); ++i)
       fprintf(stderr, " %llu:%llu:%llu", slow[i].first, h[slow[i].second * 16 + 11], h[slow[i].second * 16 + 12]);
     fprintf(stderr, "\n");
-    HIP_TRY(hipMemset(e->d_dbg, 0, h.size() * 8));
+    HIP_TRY(hipMemsetAsync(e->d_dbg, 0, h.size() * 8, e->stream));
   }
   // out == NULL: no counter read-back (one stream round trip less; agx_get_stats reads them
   // later), but the error word came back with the run's final sync
@@ -2104,7 +2256,7 @@ agx_status agx_ring_buckets(agx_engine* e, uint64_t* out) {
   if (!e->ring_live) return AGX_OK;
   uint32_t n = 0;  // pool slots handed out (high-water mark: released slots are reused first)
   HIP_TRY(hipStreamSynchronize(e->stream));
-  HIP_TRY(hipMemcpy(&n, e->d_ring_next, 4, hipMemcpyDeviceToHost));
+  AGX_TRY(copy_sync(e, &n, e->d_ring_next, 4, hipMemcpyDeviceToHost));
   *out = std::min(n, e->ring_slots);
   return AGX_OK;
 }

@@ -110,13 +110,13 @@ def test_throughput_zero_behaves_as_one(built, C):
 
 
 # ------------------------------------------------------------------ C5 as benched
-@pytest.mark.parametrize("ring_slots", [None, "0", "5"])
+@pytest.mark.parametrize("ring_slots", [None, "8192", "5"])
 def test_c5_power_law_bounded_as_benched(built, monkeypatch, ring_slots):
     """bench C5: FORWARD_RR over the device-generated R-MAT power-law graph, BoundedMailbox(64),
     throughput 5, one message per actor with ttl 15 -- at 2.2M actors (> 2^20: the multi-pass
     grouping + in-place backlog path of the 100M bench) and the bench's 2 + 10 superstep window,
-    then to quiescence.  ring_slots: the bounded-mailbox ring pool as benched (None), off (backlog
-    arena only), or 5 slots (ring and backlog buckets side by side)."""
+    then to quiescence.  ring_slots: as benched (None: no ring pool, the backlog arena), the
+    bounded-mailbox ring pool (8192 slots), or 5 slots (ring and backlog buckets side by side)."""
     if ring_slots is not None:
         monkeypatch.setenv("AGX_RING_SLOTS", ring_slots)
     w = wl.power_law_forward(2_200_000, ttl=15, capacity=64, throughput=5, device_graph=True)
@@ -125,9 +125,11 @@ def test_c5_power_law_bounded_as_benched(built, monkeypatch, ring_slots):
     _assert_same(sg, so, a, b, "C5 12 supersteps")
     assert sg.dead_letters > 0 and sg.in_flight > 0
     if ring_slots is None:
+        assert rings[0] == 0, rings
+    elif ring_slots == "8192":
         assert rings[0] > 5, rings
     else:
-        assert rings[0] <= int(ring_slots) and (ring_slots == "0") == (rings[0] == 0), rings
+        assert 0 < rings[0] <= int(ring_slots), rings
     sg, so, a, b = _run_both(w)
     _assert_same(sg, so, a, b, "C5 to quiescence")
 

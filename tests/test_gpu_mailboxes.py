@@ -95,6 +95,7 @@ def test_rings_fix_mailbox_classes(built, monkeypatch):
     """Once the rings are allocated (first run), a class they cannot hold is refused loudly."""
     from akka_amd._lib import AgxError
     monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    monkeypatch.setenv("AGX_RING_SLOTS", "8192")
     w = wl.mailbox_mix(30_000, seed=3, throughput=3, capacity=5, classes={1: 2, 2: 40, 3: 16})
     eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
     w.apply_to(eng)

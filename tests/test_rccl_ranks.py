@@ -1,8 +1,12 @@
 """The real multi-process RCCL path on one GPU: N ranks (processes) with one engine each,
 agx_comm_init + run_multi_rccl (ncclAllGather of the count vectors, grouped
 ncclSend/ncclRecv of envelopes and CRDT rows), bit-exact against the BSP oracle in the
-sharded canonical order.  tools/rccl_two_rank.py gives every rank its own NCCL_HOSTID so
+sharded canonical order.  Plain behaviours run the device-resident replays (fixed per-peer
+slabs, k_mr_pack / k_mr_unpack, no host round trip per superstep); `env` forces the
+host-planned exchange (AGX_MR_HOST) or tiny slabs (AGX_MR_SLAB: the first superstep's counts
+overflow them -> the host redoes that exchange exactly, grows the slabs and the replays resume).  tools/rccl_two_rank.py gives every rank its own NCCL_HOSTID so
 RCCL accepts several ranks on one device (socket transport on loopback)."""
+import os
 import pathlib
 import subprocess
 import sys
@@ -13,23 +17,27 @@ pytestmark = pytest.mark.gpu
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 
 
-@pytest.mark.parametrize("workload,world,n,hops", [
-    ("ring", 2, 20_000, 8),
-    ("mixed", 3, 20_000, 8),
-    ("orset", 2, 6_000, 6),
-    ("power", 4, 60_000, 8),
-    ("zipf", 2, 30_000, 3),
-    ("zipf", 4, 40_000, 3),     # C3 sharded over 4 ranks
-    ("orset", 4, 4_000, 5),     # C4 ORSet rows over 4 ranks
+@pytest.mark.parametrize("workload,world,n,hops,env", [
+    ("ring", 2, 20_000, 8, {}),
+    ("ring", 2, 20_000, 8, {"AGX_MR_SLAB": "64"}),      # slab overflow -> exact exchange, bigger slabs
+    ("ring", 3, 20_000, 30, {"AGX_MR_SLAB": "6000"}),   # 3+ replays of 8 supersteps, budget not a multiple
+    ("mixed", 3, 20_000, 8, {"AGX_MR_HOST": "1"}),      # the host-planned exchange
+    ("power", 4, 60_000, 8, {"AGX_MR_SLAB": "64"}),
+    ("mixed", 3, 20_000, 8, {}),
+    ("orset", 2, 6_000, 6, {}),  # (CRDT rows: the host-planned exchange)
+    ("power", 4, 60_000, 8, {}),
+    ("zipf", 2, 30_000, 3, {}),
+    ("zipf", 4, 40_000, 3, {}),     # C3 sharded over 4 ranks
+    ("orset", 4, 4_000, 5, {}),     # C4 ORSet rows over 4 ranks
     # (8 RCCL ranks cannot share ONE device: with 8 processes' RCCL kernels spinning on one GPU the
     # run stalls after communicator setup -- measured on the 1-GPU box, gpurun_out/r03b_cmd.log;
     # the 8-rank exchange is covered by agx_group_run's loopback of the same kernels,
     # test_gpu_benched.py::test_sharded_8_ranks)
 ])
-def test_rccl_ranks_parity(built, workload, world, n, hops):
+def test_rccl_ranks_parity(built, workload, world, n, hops, env):
     cmd = [sys.executable, "-u", str(ROOT / "tools" / "rccl_two_rank.py"), "--split-hosts", "--world", str(world),
            "--n", str(n), "--hops", str(hops), "--workload", workload]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280, env=dict(os.environ, **env))
     tail = (r.stdout[-1500:] + "\n" + r.stderr[-1500:])
     assert r.returncode == 0, tail
     assert "parity: OK" in r.stdout, tail

@@ -11,3 +11,5 @@ AB_REPS=2 bash tools/ab_cfg.sh C5_power_law_bounded $L $L:AGX_STATE_SOA=1 $L:AGX
 bash tools/ab_cfg.sh C3_zipf_fanout $L $L:AGX_STATE_SOA=1 $L:AGX_RING_SLOTS=0 >> gpurun_out/${TAG}_ab.log 2>&1 || { cat gpurun_out/${TAG}_ab.log; exit 1; }
 bash tools/ab_cfg.sh C3_zipf_tree $L $L:AGX_STATE_SOA=1 $L:AGX_RING_SLOTS=0 >> gpurun_out/${TAG}_ab.log 2>&1 || { cat gpurun_out/${TAG}_ab.log; exit 1; }
 cat gpurun_out/${TAG}_ab.log
+AB_REPS=2 bash tools/ab.sh ${TAG}ring $L akka_amd/lib/var/noearly.so > gpurun_out/${TAG}_abring.log 2>&1 || { cat gpurun_out/${TAG}_abring.log; exit 1; }
+cat gpurun_out/${TAG}_abring.log
