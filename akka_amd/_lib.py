@@ -108,6 +108,8 @@ SIGNATURES = {
     "agx_profile_reset": (ctypes.c_int32, [ctypes.c_void_p]),
     "agx_exchange_plan": (ctypes.c_int32, [c_u64p, ctypes.c_uint32, ctypes.c_uint32, c_u64p, c_u64p, c_u64p, c_u64p,
                                            c_u64p]),
+    "agx_mr_plan": (ctypes.c_int32, [c_u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                     c_u32p, c_u64p, c_u64p, c_u64p]),
     "agx_shard_id": (ctypes.c_int32, [ctypes.c_uint32, ctypes.c_uint32]),
     "agx_owner": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
 }

@@ -526,7 +526,7 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
   if (e->plan.npass > 1) {  // digits of the last pass are not buckets: find the bucket starts
     Scope s(e, K_BOUNDS);
     const bool idn = e->ident_on && first_from_chunks;
-    hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((e->nb + kThreads / 8) / (kThreads / 8), 8192)), dim3(kThreads), 0,
+    hipLaunchKernelGGL(k_bucket_bounds, dim3(grid_for((e->nb + kThreads) / kThreads, 4096)), dim3(kThreads), 0,
                        e->stream, src->key, e->d_n, e->nb, e->bb, e->d_bstart, idn ? e->d_ident : nullptr,
                        idn ? em_arena(e, e->par ^ 1u).key : nullptr, e->R > 1 ? e->d_halt : nullptr);
     HIP_TRY(hipGetLastError());
@@ -2375,6 +2375,20 @@ agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_steps, agx_
     tot.bytes_alg += st.bytes_alg;
   }
   if (out) *out = tot;
+  return AGX_OK;
+}
+
+agx_status agx_mr_plan(const uint64_t* mat, uint32_t R, uint32_t rank, uint32_t slab, uint64_t cap, uint32_t* code,
+                       uint64_t* send_off, uint64_t* recv_off, uint64_t* n_backlog) {
+  if (!mat || !code || R == 0 || R > AGX_MAX_RANKS || rank >= R) return set_err(AGX_EINVAL, "bad mr_plan args");
+  MrPlan p;
+  mr_decide(mat, R, rank, slab, cap, p);
+  *code = p.code;
+  for (uint32_t q = 0; q <= R; ++q) {
+    if (send_off) send_off[q] = p.soff[q];
+    if (recv_off) recv_off[q] = p.roff[q];
+  }
+  if (n_backlog) *n_backlog = p.nbl;
   return AGX_OK;
 }
 

@@ -309,6 +309,27 @@ def owner(entity_id: int, num_shards: int, n_ranks: int) -> int:
     return int(_lib.load().agx_owner(entity_id, num_shards, n_ranks))
 
 
+MR_GO, MR_OVER_SLAB, MR_QUIET, MR_OVER_CAPACITY = 0, 1, 2, 3
+
+
+def mr_plan(mat, rank: int, slab: int, cap: int) -> dict:
+    """agx_mr_plan: the device-resident replays' decision for one superstep (the same code as
+    k_mr_pack): code (MR_*), this rank's send / receive offsets (R + 1 each) and backlog."""
+    m = np.ascontiguousarray(np.asarray(mat, dtype=np.uint64))
+    R = m.shape[0]
+    so, ro = np.zeros(R + 1, np.uint64), np.zeros(R + 1, np.uint64)
+    code, nbl = ctypes.c_uint32(), ctypes.c_uint64()
+    check(_lib.load().agx_mr_plan(_ptr(m, ctypes.c_uint64), R, rank, slab, cap, ctypes.byref(code),
+                                  _ptr(so, ctypes.c_uint64), _ptr(ro, ctypes.c_uint64), ctypes.byref(nbl)))
+    return {"code": int(code.value), "send_off": so, "recv_off": ro, "n_backlog": int(nbl.value)}
+
+
+def mr_initial_slab(n_global: int, max_emit: int, R: int) -> int:
+    """The first slab size of the device-resident replays (agx_engine.hip mr_initial_slab)."""
+    share = n_global * max_emit // (R * R)
+    return min(share + share // 4 + 1024, 1 << 30)
+
+
 def exchange_plan(mat, rank: int) -> dict:
     """agx_exchange_plan: this rank's send/recv counts and offsets (host only)."""
     m = np.ascontiguousarray(np.asarray(mat, dtype=np.uint64))

@@ -351,6 +351,19 @@ agx_status agx_comm_init(agx_engine* eng, const uint8_t id[128]);
  * Same kernels as the RCCL path; used to test sharding on a 1-GPU box.      */
 agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_supersteps, agx_stats* out);
 
+/* The device-resident replays' per-superstep decision (pure host function, no GPU; the device runs
+ * the same code in k_mr_pack / k_mr_unpack, agx_kernels.h mr_decide).  `mat` as below; `slab` =
+ * envelopes per fixed-size peer slab; `cap` = this rank's message capacity.  *code: 0 = exchange
+ * the slabs, 1 = some sender -> receiver count (off the diagonal) exceeds the slab (the host redoes
+ * this superstep's exchange exactly and grows the slabs), 2 = nothing in flight on any rank, 3 =
+ * backlog + received mail would exceed `cap`.  send_off / recv_off: R + 1 entries (exclusive
+ * prefixes of this rank's send counts and of its receive counts in sender-rank order; [R] = the
+ * total); *n_backlog = this rank's backlog (received mail is placed after it).
+ * Replaces: ShardRegion delivery to remote regions (akka-cluster-sharding/.../ShardRegion.scala:
+ * 154-158 routing), batched once per superstep. */
+agx_status agx_mr_plan(const uint64_t* mat, uint32_t n_ranks, uint32_t rank, uint32_t slab, uint64_t cap,
+                       uint32_t* code, uint64_t* send_off, uint64_t* recv_off, uint64_t* n_backlog);
+
 /* Exchange plan of one superstep (pure host function, no GPU).  `mat` is the
  * gathered R x (R+2) matrix, row r = rank r's [tells to rank 0..R-1,
  * n_backlog, n_staged].  Outputs (R entries each): this rank's send
