@@ -226,6 +226,7 @@ struct agx_engine {
   // blocks of the skew-list launch (grid-stride over the list; AGX_SKEW_GRID diagnostic knob): one
   // round of workgroups (2 per CU) -- an empty list at 10^8 actors cost 18 us with 4096 blocks
   uint32_t skew_grid = 512;
+  bool stamps_skew = false;  // AGX_STAMPS_SKEW (diagnostic): phase stamps of the skew launch only
   std::vector<uint32_t> hd_key, hd_src, hd_pay;  // staged tells on the device, not yet consumed (fused)
   bool stg_pending = false;
 
@@ -685,7 +686,9 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     const dim3 gs(grid_for(e->nb, std::min(e->apply_grid, e->ring_live ? std::max(e->skew_grid, 2048u) : e->skew_grid)));
     if (!e->skew_only) {
       Scope s(e, K_APPLY);
-      HIP_TRY(agx_launch_apply(vid, mode, false, g, e->stream, ba));
+      BucketArgs bf = ba;
+      if (e->stamps_skew) bf.dbg = nullptr;  // (diagnostic: stamps of the skew launch only)
+      HIP_TRY(agx_launch_apply(vid, mode, false, g, e->stream, bf));
     }
     if (!(mode == M_FUSED && e->strict_cap)) {
       Scope s(e, K_SKEW);
@@ -1627,6 +1630,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     const uint32_t m = (uint32_t)std::max(1, atoi(s));
     e->max_replay_si = m >= 16 ? 4u : m >= 8 ? 3u : m >= 4 ? 2u : m >= 2 ? 1u : 0u;
   }
+  e->stamps_skew = getenv("AGX_STAMPS_SKEW") != nullptr;
   if (const char* s = getenv("AGX_SKEW_GRID"))
     e->skew_grid = (uint32_t)std::min<int>(kMaxApplyGrid, std::max(1, atoi(s)));
   if (const char* s = getenv("AGX_APPLY_GRID"))
@@ -1768,7 +1772,11 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(dalloc(&e->d_hist_c, (uint64_t)kRadix * e->cstride));
   CREATE_TRY(hipMemset(e->d_hist_c, 0, (uint64_t)kRadix * e->cstride * 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_bstart, std::max<uint64_t>(kRadix, e->nb) + 1));
-  if (getenv("AGX_STAMPS")) CREATE_TRY(dalloc(&e->d_dbg, (uint64_t)std::min<uint64_t>(e->nb, 4096) * 16));
+  if (getenv("AGX_STAMPS")) {
+    CREATE_TRY(dalloc(&e->d_dbg, (uint64_t)std::min<uint64_t>(e->nb, 4096) * 16));
+    CREATE_TRY(hipMemset(e->d_dbg, 0, std::min<uint64_t>(e->nb, 4096) * 16 * 8) == hipSuccess ? AGX_OK
+                                                                                       : set_err(AGX_EDEVICE, "memset"));
+  }
   CREATE_TRY(dalloc(&e->d_hist_d, (uint64_t)kRadix * e->dstride));
   CREATE_TRY(dalloc(&e->d_tot, kRadix));
   CREATE_TRY(dalloc(&e->d_n, 4));
@@ -2217,14 +2225,18 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
     HIP_TRY(hipMemcpy(h.data(), e->d_dbg, h.size() * 8, hipMemcpyDeviceToHost));
     double acc[8] = {0};
     unsigned long long t0min = ~0ull, t8max = 0;
+    uint64_t nst = 0;  // blocks that recorded stamps (the skew launch runs fewer blocks)
     for (uint64_t b = 0; b < nbk; ++b) {
+      if (!h[b * 16] || !h[b * 16 + 8]) continue;
+      ++nst;
       for (int k = 0; k < 8; ++k) acc[k] += (double)(h[b * 16 + k + 1] - h[b * 16 + k]);
       t0min = std::min(t0min, h[b * 16]);
       t8max = std::max(t8max, h[b * 16 + 8]);
     }
-    fprintf(stderr, "[agx stamps] mean cycles per phase:");
+    fprintf(stderr, "[agx stamps%s] mean cycles per phase over %llu blocks:", e->stamps_skew ? " (skew launch)" : "",
+            (unsigned long long)nst);
     const char* nm[8] = {"range+alive", "sort", "->finish", "classify+backlog", "prefetch+phaseA", "scan", "phaseB", "hist+stats"};
-    for (int k = 0; k < 8; ++k) fprintf(stderr, " %s=%.0f", nm[k], acc[k] / nbk);
+    for (int k = 0; k < 8; ++k) fprintf(stderr, " %s=%.0f", nm[k], nst ? acc[k] / nst : 0.0);
     fprintf(stderr, " | kernel span=%llu cycles\n", t8max - t0min);
     std::vector<std::pair<unsigned long long, uint64_t>> slow;
     for (uint64_t b = 0; b < nbk; ++b) slow.push_back({h[b * 16 + 10], b});

@@ -23,6 +23,7 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
     ("ring", 3, 20_000, 30, {"AGX_MR_SLAB": "6000"}),   # 3+ replays of 8 supersteps, budget not a multiple
     ("mixed", 3, 20_000, 8, {"AGX_MR_HOST": "1"}),      # the host-planned exchange
     ("power", 4, 60_000, 8, {"AGX_MR_SLAB": "64"}),
+    ("zipf", 2, 30_000, 3, {"AGX_MR_SLAB": "2000"}),   # fan-out grows 4x: the slab overflows mid-replay
     ("mixed", 3, 20_000, 8, {}),
     ("orset", 2, 6_000, 6, {}),  # (CRDT rows: the host-planned exchange)
     ("power", 4, 60_000, 8, {}),

@@ -19,11 +19,17 @@ elif a.workload in ("c4g", "c4o"):
     from akka_amd.engine import Kind
     w = wl.crdt_gossip(a.n if a.n != 100_000_000 else 1_000_000, Kind.GCOUNTER if a.workload == "c4g" else Kind.ORSET,
                        rounds=40)
+elif a.workload in ("c4gd", "c4od"):  # delta-CRDT replication as benched
+    from akka_amd.engine import Kind
+    w = wl.crdt_delta(a.n if a.n != 100_000_000 else 1_000_000, Kind.GCOUNTER if a.workload == "c4gd" else Kind.ORSET,
+                      rounds=40, write=True)
 else:
     w = wl.ping_pong(1000, messages_per_pair=2_000_000, throughput=50)
 cfg = EngineConfig(**w.gpu_kwargs())
 if a.workload == "c1":
     cfg.msg_capacity = 1 << 20
+if a.workload in ("c4gd", "c4od"):
+    cfg.msg_capacity = 8_000_000
 eng = GpuEngine(cfg)
 w.apply_to(eng)
 eng.run(2)
