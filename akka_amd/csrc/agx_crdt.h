@@ -146,7 +146,7 @@ __device__ __forceinline__ uint32_t crdt_count(const DevParams& P, uint32_t kind
   const uint32_t op = pay >> 24, arg = pay & 0xFFFFFFu;
   const bool dm = (CM & kDeltaKM) != 0 && P.delta_max != 0;
   if (dm && (op == AGX_OP_DELTA_TICK || dl_records(kind, op, arg)) && !ds.on) {
-    const St32 s{wide_state(P, l), 1};
+    const St32 s{wide_state(P, l), wide_nl(P)};
     const uint32_t e0 = dl_env(kind);
     ds.on = true;
     ds.ctr = s.ld(e0 + 8);
@@ -437,8 +437,8 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
   if constexpr ((CM & ~kDeltaKM) == (1u << AGX_KIND_GCOUNTER)) kind = AGX_KIND_GCOUNTER;
   if constexpr ((CM & ~kDeltaKM) == (1u << AGX_KIND_PNCOUNTER)) kind = AGX_KIND_PNCOUNTER;
   if constexpr ((CM & ~kDeltaKM) == (1u << AGX_KIND_ORSET)) kind = AGX_KIND_ORSET;
-  constexpr size_t nl = 1;
-  uint64_t* st = wide_state(P, l);  // word w at st[w * nl] (actor-major row)
+  const size_t nl = wide_nl(P);
+  uint64_t* st = wide_state(P, l);  // word w at st[w * nl] (actor-major row, or word-major: AGX_CRDT_WORDMAJOR)
   const uint32_t node = self % AGX_CRDT_NODES;
   const bool dm = (CM & kDeltaKM) != 0 && P.delta_max != 0;  // (the engine launches kDeltaKM variants then)
   const St32 s32{st, nl};

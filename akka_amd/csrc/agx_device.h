@@ -67,8 +67,10 @@ struct DevParams {
 // bits 1..3 = mailbox class): Mailboxes.lookupConfigurator per actor (Mailboxes.scala:204-260).
 // actor l's state row in a CRDT engine (actor-major, P.pitch u64 words per row)
 __device__ __forceinline__ uint64_t* wide_state(const DevParams& P, uint32_t l) {
-  return P.state + (size_t)l * P.pitch;
+  return P.pitch ? P.state + (size_t)l * P.pitch : P.state + l;
 }
+// the stride between consecutive words of one actor's state (1 actor-major, n_local word-major)
+__device__ __forceinline__ size_t wide_nl(const DevParams& P) { return P.pitch ? 1u : P.n_local; }
 
 // word w (0 or 1) of a plain behaviour's state (P.sa / P.sw above; 32-bit offsets)
 __device__ __forceinline__ uint32_t sidx(const DevParams& P, uint32_t l, uint32_t w) { return l * P.sa + w * P.sw; }

@@ -769,7 +769,15 @@ agx_status prepare_run(agx_engine* e) {
   if (e->actors_dirty) {
     HIP_TRY(hipMemcpyAsync(e->d_kind, e->h_kind.data(), e->n_local, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipMemcpyAsync(e->d_alive, e->h_alive.data(), e->n_local, hipMemcpyHostToDevice, e->stream));
-    if (e->pw && !e->pitch) {  // first upload of a CRDT engine: actor-major rows from now on
+    // first upload of a CRDT engine: actor-major rows from now on -- except delta-CRDT counter
+    // populations, which stay word-major: there a lane walks its own replica's envelope and log,
+    // and consecutive lanes then read consecutive words (same-box A/B: GCounter delta 3.25e9 ->
+    // 3.93e9 word-major; ORSet delta 1.29e9 actor-major vs 1.17e9 word-major, its element rows
+    // are read whole).  AGX_CRDT_LAYOUT=actor|word overrides.
+    const char* lay = getenv("AGX_CRDT_LAYOUT");
+    const bool word_major = apply_variant(e) != V_OR &&  // (k_orset_merge walks actor-major rows)
+                            (lay ? lay[0] == 'w' : (e->delta_max && !(e->kinds_mask & kb(AGX_KIND_ORSET))));
+    if (e->pw && !e->pitch && !word_major) {
       const uint32_t pitch = e->W <= 16 ? (e->W + 1u) & ~1u : (e->W + 15u) & ~15u;
       uint64_t* d = nullptr;
       AGX_TRY(dalloc(&d, (uint64_t)e->n_local * pitch));

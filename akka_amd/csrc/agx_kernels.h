@@ -1316,7 +1316,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         kd[j] = has && kKindNeeded ? P.kind[l] : 0u;  // single-kind variants never read it
         if constexpr (kWide) {  // (CRDT engines: actor-major rows, wide_state)
           x0[j] = has ? wide_state(P, l)[0] : 0ull;
-          x1[j] = has && P.W > 1 ? wide_state(P, l)[1] : 0ull;
+          x1[j] = has && P.W > 1 ? wide_state(P, l)[wide_nl(P)] : 0ull;
         } else {
           x0[j] = has ? ldg64(P.state, sidx(P, l, 0)) : 0ull;  // (32-bit offsets: one VGPR per address)
           x1[j] = has && P.W > 1 ? ldg64(P.state, sidx(P, l, 1)) : 0ull;
@@ -1347,7 +1347,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         x1[j] = pre1[j];
       } else if constexpr (kWide) {
         x0[j] = wide_state(P, li[j])[0];
-        x1[j] = wide_state(P, li[j])[w1off ? 1 : 0];
+        x1[j] = wide_state(P, li[j])[w1off ? wide_nl(P) : 0];
       } else {
         x0[j] = ldg64(P.state, li[j] * P.sa);  // (32-bit offsets: one VGPR per address)
         x1[j] = ldg64(P.state, li[j] * P.sa + w1off);
@@ -1693,7 +1693,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         }
         if constexpr (kWide) {
           wide_state(P, l)[0] = wv[0];
-          if (P.W > 1) wide_state(P, l)[1] = wv[1];
+          if (P.W > 1) wide_state(P, l)[wide_nl(P)] = wv[1];
         } else {
           stg64(P.state, sidx(P, l, 0), wv[0]);
           if (P.W > 1) stg64(P.state, sidx(P, l, 1), wv[1]);
