@@ -1861,12 +1861,16 @@ struct GatherView {
 // dependent round trips are per bucket, not per message).  Same semantics as the block path:
 // stable order by actor (inbox order within an actor), tail-drop at C, drain min(len, T), the
 // rest queued in order, Behaviors.stopped / unhandled, tells in sender (= actor) order.
-constexpr uint32_t kTinyIpl = 2;                 // inbox items per lane
+#ifndef AGX_TINY_IPL
+#define AGX_TINY_IPL 2  // (4 = 256-message wave path: measured slower, C3 -18 %, C5 -4 %: the rank loop is
+#endif                  // quadratic in the inbox and the bypass apply spills 44 -> 84 B/lane)
+constexpr uint32_t kTinyIpl = AGX_TINY_IPL;      // inbox items per lane
 constexpr uint32_t kTinyMax = kTinyIpl * kWave;  // 128
 struct TinyLds {                                 // one per wave (2.5 KB)
   uint32_t key[kTinyMax], src[kTinyMax], pay[kTinyMax];
   uint16_t st[kTinyMax], len[kTinyMax];
 };
+static_assert(kBWaves * sizeof(TinyLds) <= 2 * kBucket * sizeof(uint64_t), "the waves' TinyLds live in the apply's U");
 
 // Tells of the wave path: into the bucket's tell chunk, next-pass histogram column updated
 // directly (the block path stages it in LDS).
@@ -1937,14 +1941,18 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
     for (uint32_t r = 0; r < kTinyIpl; ++r) la[r] = r * kWave + lane < cnt ? k[r] & amask : 0xFFFFFFFFu;
   }
   uint32_t rank[kTinyIpl] = {}, st[kTinyIpl] = {}, len[kTinyIpl] = {};
-  for (uint32_t j = 0; j < cnt; ++j) {  // (uniform loop; v_readlane with a scalar lane, no LDS crossbar)
-    const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)((j >> 6) ? la[1] : la[0]), (int)(j & 63u));
 #pragma unroll
-    for (uint32_t r = 0; r < kTinyIpl; ++r) {
-      const bool lt = lj < la[r], eq = lj == la[r];
-      st[r] += lt;
-      len[r] += eq;
-      rank[r] += lt || (eq && j < r * kWave + lane);
+  for (uint32_t r2 = 0; r2 < kTinyIpl; ++r2) {  // item j = r2 * 64 + jj, held by lane jj in la[r2]
+    const uint32_t jn = cnt > r2 * kWave ? min(cnt - r2 * kWave, (uint32_t)kWave) : 0u;
+    for (uint32_t jj = 0; jj < jn; ++jj) {  // (uniform loop; v_readlane with a scalar lane, no LDS crossbar)
+      const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)la[r2], (int)jj), j = r2 * kWave + jj;
+#pragma unroll
+      for (uint32_t r = 0; r < kTinyIpl; ++r) {
+        const bool lt = lj < la[r], eq = lj == la[r];
+        st[r] += lt;
+        len[r] += eq;
+        rank[r] += lt || (eq && j < r * kWave + lane);
+      }
     }
   }
 #pragma unroll

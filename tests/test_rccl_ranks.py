@@ -24,6 +24,7 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
     ("mixed", 3, 20_000, 8, {"AGX_MR_HOST": "1"}),      # the host-planned exchange
     ("power", 4, 60_000, 8, {"AGX_MR_SLAB": "64"}),
     ("zipf", 2, 30_000, 3, {"AGX_MR_SLAB": "2000"}),   # fan-out grows 4x: the slab overflows mid-replay
+    ("ring", 2, 20_000, 12, {"RESTAGE": "5"}),         # a staged burst between device-resident replays
     ("mixed", 3, 20_000, 8, {}),
     ("orset", 2, 6_000, 6, {}),  # (CRDT rows: the host-planned exchange)
     ("power", 4, 60_000, 8, {}),
@@ -36,8 +37,9 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
     # test_gpu_benched.py::test_sharded_8_ranks)
 ])
 def test_rccl_ranks_parity(built, workload, world, n, hops, env):
+    env = dict(env)
     cmd = [sys.executable, "-u", str(ROOT / "tools" / "rccl_two_rank.py"), "--split-hosts", "--world", str(world),
-           "--n", str(n), "--hops", str(hops), "--workload", workload]
+           "--n", str(n), "--hops", str(hops), "--workload", workload, "--restage", env.pop("RESTAGE", "0")]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280, env=dict(os.environ, **env))
     tail = (r.stdout[-1500:] + "\n" + r.stderr[-1500:])
     assert r.returncode == 0, tail

@@ -8,7 +8,9 @@ socket transport on loopback -- the same ncclSend/ncclRecv/ncclAllGather calls a
 over xGMI on a multi-GPU node.  Exit 0 = parity, 1 = mismatch, 2 = a rank failed.
 
     python tools/rccl_two_rank.py --split-hosts [--world 2] [--n 20000] [--hops 8]
-                                  [--workload ring|mixed|orset|power|zipf]
+                                  [--workload ring|mixed|orset|power|zipf] [--restage K]
+--restage K: run K supersteps, stage a second burst of tells on every rank (each keeps the ones it
+owns), then run to quiescence -- a staged burst between device-resident replays.
 """
 import argparse
 import os
@@ -42,6 +44,13 @@ def _make(a):
     return wl.mixed(a.n, seed=3, throughput=2, capacity=6)
 
 
+def _burst(n):
+    """the second staged burst of --restage: every 7th actor, payload 3 (a hop budget / an op)"""
+    import numpy as np
+    d = np.arange(0, n, 7, dtype=np.uint32)
+    return d, np.full(d.size, 3, np.uint32)
+
+
 def _rank_main(rank, world, port, a, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -62,6 +71,10 @@ def _rank_main(rank, world, port, a, q):
         uid = [GpuEngine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(uid[0])
+        if a.restage:
+            eng.run(a.restage)
+            d, pay = _burst(w.n_actors)
+            eng.tell(d, pay)
         st = eng.run()
         ws, al = eng.read_state()
         eng.close()
@@ -79,6 +92,7 @@ def main():
     ap.add_argument("--workload", default="ring")
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--split-hosts", action="store_true", help="one NCCL_HOSTID per rank (one-GPU box)")
+    ap.add_argument("--restage", type=int, default=0, help="stage a second burst after this many supersteps")
     a = ap.parse_args()
     import numpy as np
     import torch.multiprocessing as mp
@@ -101,6 +115,10 @@ def main():
     w = _make(a)
     ref = BspOracle(n_ranks=world, **w.engine_kwargs())
     w.apply_to(ref)
+    if a.restage:
+        ref.run(a.restage)
+        d, pay = _burst(w.n_actors)
+        ref.tell(d, pay)
     so = ref.run()
     wo, ao = ref.read_state()
     wg = np.zeros_like(wo)
