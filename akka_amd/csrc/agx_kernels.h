@@ -1293,6 +1293,63 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   __syncthreads();
 
   AGX_STAMP(a, 4);
+  // ---- FANOUT with one tell per message (C3): every drained message's Zipf destination is looked
+  // up here, the four items of a thread in lockstep (index range, then each binary-search step's
+  // loads together, then the permutation), instead of ~5 dependent loads per message inside the
+  // serial per-actor drain.  The destination replaces the message's sender in LDS (FANOUT does not
+  // read it); the drain emits exactly what apply_msg would (same hash, same lookup).
+  constexpr bool kFanPre = !kWide && kLds && KM == kb(AGX_KIND_FANOUT);
+  const bool fan_pre = kFanPre && P.fan_k == 1 && a.kmax == 1;
+  if (kFanPre && fan_pre) {
+    uint32_t qi[kBIpt], lo[kBIpt], hi[kBIpt], uu[kBIpt];
+    bool need[kBIpt];
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r) {
+      const uint32_t q = r * kBThreads + tid;
+      qi[r] = q;
+      need[r] = false;
+      uu[r] = 0;
+      if (q < cnt) {
+        const uint32_t la = L.key[q] & ((1u << a.bb) - 1u), s0 = L.seg[la], len = L.seg[la + 1] - s0;
+        const uint32_t ab = L.alive[la], pv = L.pay[q];
+        uint32_t Ca, Ta;
+        mbox_limits(P, ab, Ca, Ta);
+        if (la < na && (ab & 1u) && q - s0 < min(len, Ta) && (pv >> 24) > 0) {
+          const uint32_t l = a0 + la, self = P.R > 1 ? P.gid[l] : l;
+          const uint64_t rr = fanout_rand(P.fan_seed, self, pv & 0x00FFFFFFu, 0);
+          need[r] = true;
+          uu[r] = (uint32_t)(rr >> 32);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r) {
+      const uint32_t t = uu[r] >> (32 - kZipfBits);
+      lo[r] = need[r] ? P.zipf_idx[t] : 0u;
+      hi[r] = need[r] ? P.zipf_idx[t + 1] : 0u;
+    }
+    for (;;) {  // zipf_index's binary search, one step of every item per round
+      bool more = false;
+      uint32_t c[kBIpt];
+#pragma unroll
+      for (int r = 0; r < kBIpt; ++r) c[r] = lo[r] < hi[r] ? P.zipf_cdf[(lo[r] + hi[r]) >> 1] : 0u;
+#pragma unroll
+      for (int r = 0; r < kBIpt; ++r)
+        if (lo[r] < hi[r]) {
+          const uint32_t mid = (lo[r] + hi[r]) >> 1;
+          if (c[r] >= uu[r]) hi[r] = mid; else lo[r] = mid + 1;
+          more |= lo[r] < hi[r];
+        }
+      if (!more) break;
+    }
+    uint32_t d[kBIpt];
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r) d[r] = need[r] ? P.zipf_perm[lo[r]] : 0u;
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r)
+      if (need[r]) L.src[qi[r]] = d[r];
+    __syncthreads();
+  }
   // ---- prefetch kind + state words 0/1 of actors with mail (striped: coalesced).  All loads
   // are issued before the LDS stores (the stores go through generic pointers).
   // FORWARD_RR (C5) single pass: each actor's out-edge row and the destination of its next
@@ -1422,7 +1479,16 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       for (uint32_t q = 0; q < nd; ++q) {
         const uint32_t sv = sts[s0 + q], pv = stp[s0 + q];
         uint32_t r;
-        if (kFwd && hdeg != kNoHint && wv[1] <= 0xFFFFFFFFull) {
+        if (kFanPre && fan_pre) {  // apply_msg's FANOUT with the destination looked up above (in sv)
+          wv[0] += 1;
+          wv[1] += pv;
+          const uint32_t ttl = pv >> 24;
+          if (ttl > 0) {
+            const uint64_t rr = fanout_rand(P.fan_seed, self, pv & 0x00FFFFFFu, 0);
+            em(sv, ((ttl - 1) << 24) | ((uint32_t)rr & 0x00FFFFFFu));
+          }
+          r = AGX_RES_SAME;
+        } else if (kFwd && hdeg != kNoHint && wv[1] <= 0xFFFFFFFFull) {
           // apply_msg's FORWARD_RR with the prefetched row (same cursor arithmetic)
           wv[0] += 1;
           if (pv > 0 && hdeg) {
