@@ -2080,6 +2080,58 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
       blw.pay[lo + qoff] = T.pay[p0 + q];
     }
   }
+  // FANOUT with one tell per message: every drained position's Zipf destination first, the lane's
+  // positions in lockstep, into the position's sender slot (as the block path does)
+  constexpr bool kFanPre = KM == kb(AGX_KIND_FANOUT);
+  const bool fan_pre = kFanPre && P.fan_k == 1 && a.kmax == 1;
+  if (kFanPre && fan_pre) {
+    uint32_t uu[kTinyIpl], lo2[kTinyIpl], hi2[kTinyIpl];
+    bool need[kTinyIpl];
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i) {
+      const uint32_t p = lane * kTinyIpl + i;
+      need[i] = false;
+      uu[i] = 0;
+      if (p < cnt) {
+        const uint32_t lp = a0 + (T.key[p] & amask), pv = T.pay[p], ab = P.alive[lp];
+        uint32_t C, Tt;
+        mbox_limits(P, ab, C, Tt);
+        if ((ab & 1u) && p - T.st[p] < min((uint32_t)T.len[p], Tt) && (pv >> 24) > 0) {
+          need[i] = true;
+          uu[i] = (uint32_t)(fanout_rand(P.fan_seed, lp, pv & 0x00FFFFFFu, 0) >> 32);
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i) {
+      const uint32_t t = uu[i] >> (32 - kZipfBits);
+      lo2[i] = need[i] ? P.zipf_idx[t] : 0u;
+      hi2[i] = need[i] ? P.zipf_idx[t + 1] : 0u;
+    }
+    for (;;) {
+      bool more = false;
+      uint32_t c[kTinyIpl];
+#pragma unroll
+      for (uint32_t i = 0; i < kTinyIpl; ++i) c[i] = lo2[i] < hi2[i] ? P.zipf_cdf[(lo2[i] + hi2[i]) >> 1] : 0u;
+#pragma unroll
+      for (uint32_t i = 0; i < kTinyIpl; ++i)
+        if (lo2[i] < hi2[i]) {
+          const uint32_t mid = (lo2[i] + hi2[i]) >> 1;
+          if (c[i] >= uu[i]) hi2[i] = mid; else lo2[i] = mid + 1;
+          more |= lo2[i] < hi2[i];
+        }
+      if (!more) break;
+    }
+    uint32_t dd[kTinyIpl];
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i) dd[i] = need[i] ? P.zipf_perm[lo2[i]] : 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i)
+      if (need[i]) T.src[lane * kTinyIpl + i] = dd[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
   // drain + apply.  Every message emits <= 1 tell (max_emit 1): one pass, tells staged over the
   // actor's consumed inbox slots, then compacted in actor order.  Otherwise: count the tells on
   // copies of the state first (phase A), then apply for real.
@@ -2090,7 +2142,16 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
     uint32_t kd = hkind[i];
     for (uint32_t q = 0; q < nd[i]; ++q) {
       ++ndel;
-      const uint32_t r = apply_msg<KM>(P, kd, l, l, wv, T.src[p0 + q], T.pay[p0 + q], em);
+      uint32_t r;
+      if (kFanPre && fan_pre) {  // apply_msg's FANOUT with the destination looked up above
+        const uint32_t pv = T.pay[p0 + q], ttl = pv >> 24;
+        wv[0] += 1;
+        wv[1] += pv;
+        if (ttl > 0) em(T.src[p0 + q], ((ttl - 1) << 24) | ((uint32_t)fanout_rand(P.fan_seed, l, pv & 0x00FFFFFFu, 0) & 0x00FFFFFFu));
+        r = AGX_RES_SAME;
+      } else {
+        r = apply_msg<KM>(P, kd, l, l, wv, T.src[p0 + q], T.pay[p0 + q], em);
+      }
       if (r == AGX_RES_UNHANDLED) ++nunh;
       if (r == AGX_RES_STOPPED) {
         P.stopq[atomicAdd(P.nstop, 1u)] = l;
