@@ -57,13 +57,6 @@ __device__ __forceinline__ CrdtHeap crdt_heap(const DevParams& P) {
   return {P.heap + (s & 1u) * half, P.heap + ((s + 1u) & 1u) * half, P.rx, P.heap_top + (s & 1u), P.heap_rows, P.pw};
 }
 
-// copy a row (pw u32, multiple of 4, 16-B aligned)
-__device__ __forceinline__ void copy_row(uint32_t* dst, const uint32_t* src, uint32_t pw) {
-  const uint4* s = reinterpret_cast<const uint4*>(src);
-  uint4* d = reinterpret_cast<uint4*>(dst);
-  for (uint32_t i = 0; i < pw / 4; ++i) d[i] = s[i];
-}
-
 // Gossip peer j of `self` at countdown `round` (Replicator.selectRandomNode with the counter RNG)
 __device__ __forceinline__ uint32_t crdt_peer(uint64_t seed, uint32_t self, uint32_t round, uint32_t j, uint32_t n) {
   const uint64_t r = fanout_rand(seed, self, round | 0x08000000u, j);
