@@ -45,24 +45,28 @@ fused = "agx::k_bucket_apply<false, 4u, true, false, false>"
 bypass = "agx::k_bucket_apply<false, 4u, false, false, false>"
 c4 = load("pmc3_C4_orset_gossip_p*")
 c5 = load("pmc3_C5_power_law_bounded_p*")
+c4d = load("pmc3_C4_orset_delta_gossip_p*")
 out = {
     "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE / SQ_* (separate passes, tools/gpu_pmc_r03.sh)",
     "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), KiB -> bytes; raw sums kept beside",
     "note": "round 3: bench.py --steps 20 --warmup 4 --no-configs --no-cpu-baseline --large-steps 8 (1M fused ring "
-            "+ 100M multi-pass ring with identity grouping); tools/cfg_one.py C4_orset_gossip / C5_power_law_bounded",
+            "+ 100M multi-pass ring with identity grouping); tools/cfg_one.py C4_orset_gossip / C4_orset_delta_gossip / C5_power_law_bounded",
     "kernels": {"bucket_apply": traffic(ring[fused], 42_000_000)},
     "ring_1M_fused_apply": dict(traffic(ring[fused], 42_000_000), sq=sq(ring[fused])),
     "ring_100M_apply": dict(traffic(ring[bypass], 4_200_000_000), sq=sq(ring[bypass])),
     "C4_orset_gossip": {k.replace("agx::", ""): traffic(v) for k, v in c4.items()
                         if v.get("FETCH_SIZE", 0) + v.get("WRITE_SIZE", 0) > 1000},
+    "C4_orset_delta_gossip": {k.replace("agx::", ""): traffic(v) for k, v in c4d.items()
+                              if v.get("FETCH_SIZE", 0) + v.get("WRITE_SIZE", 0) > 1000},
     "C5_power_law_bounded": {k.replace("agx::", ""): traffic(v) for k, v in c5.items()
                              if v.get("FETCH_SIZE", 0) + v.get("WRITE_SIZE", 0) > 1000 and "gen_rmat" not in k
                              and "chunk_hist" not in k},
 }
-for cfg in ("C4_orset_gossip", "C5_power_law_bounded"):
+for cfg in ("C4_orset_gossip", "C4_orset_delta_gossip", "C5_power_law_bounded"):
     t = out[cfg]
     t["per_superstep_total"] = {"hbm_bytes": sum(v["hbm_bytes_per_launch"] for v in t.values()),
                                 "hbm_bytes_raw": sum(v["hbm_bytes_raw"] for v in t.values())}
 (ROOT / "profiles" / "pmc_r03.json").write_text(json.dumps(out, indent=1) + "\n")
 print(json.dumps({k: out[k] for k in ("ring_1M_fused_apply", "ring_100M_apply")}, indent=1))
-print(out["C4_orset_gossip"]["per_superstep_total"], out["C5_power_law_bounded"]["per_superstep_total"])
+print(out["C4_orset_gossip"]["per_superstep_total"], out["C4_orset_delta_gossip"]["per_superstep_total"],
+      out["C5_power_law_bounded"]["per_superstep_total"])
