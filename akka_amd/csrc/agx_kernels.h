@@ -2287,6 +2287,10 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
 #define AGX_EARLY_STATE 1
 #endif
 constexpr bool kEarlyState = AGX_EARLY_STATE != 0;  // fused fast path: state loads at bucket start (A/B build knob)
+#ifndef AGX_TINY_BOUNDS
+#define AGX_TINY_BOUNDS 1
+#endif
+constexpr bool kTinyBounds = AGX_TINY_BOUNDS != 0;  // multi-pass: block path reuses the wave check's bounds (A/B knob)
 constexpr uint32_t kSkRec = 12;    // b, lo, cnt, blc, blo, bst, pbase, np, ndrain, bltot, npb, -
 constexpr uint32_t kSkSpan = 4 * kBucket;  // minimum inbox positions per part
 constexpr uint32_t kRingMaxC = 4096;  // bounded-mailbox rings: largest mailbox capacity they hold (16-bit head / length)
@@ -2789,6 +2793,9 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
   // bucket if it is tiny (wave path), then the block drains the group's other buckets
   constexpr bool kTiny = kBypass && !kSkew && !kWide;
   __shared__ uint32_t s_tiny[kBWaves];
+  // (kTiny) the bounds the wave check read for bucket w: [bs, lo, hi, blc, blo, valid] -- the block
+  // path takes them from here instead of a second round trip to global memory
+  __shared__ uint32_t s_tb[kBWaves][6];
   // (a group is kBWaves consecutive iterations of the block's grid-stride sequence, so the
   // bucket -> block assignment, and with it the load balance, is the block path's own)
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};  // this thread's counters over the block's buckets
@@ -2818,10 +2825,20 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         blo = (uint32_t)__builtin_amdgcn_readlane((int)blo, 0);
         tiny = hi_w - lo_w <= a.tiny_max && (uint64_t)hi_w <= a.cap &&  // (over capacity: the block path reports it)
                !(a.ring_of && a.ring_of[bw]);                         // (a ring bucket: skew path)
+        if (lane == 0 && kTinyBounds) {
+          s_tb[w][0] = bs;
+          s_tb[w][1] = lo_w;
+          s_tb[w][2] = hi_w;
+          s_tb[w][3] = blc;
+          s_tb[w][4] = blo;
+        }
         if (tiny)
           tiny_bucket<KM>(a, iv, reinterpret_cast<TinyLds*>(U)[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
       }
-      if (lane == 0) s_tiny[w] = tiny || bw >= a.nb;
+      if (lane == 0) {
+        s_tiny[w] = tiny || bw >= a.nb;
+        s_tb[w][5] = bw < a.nb && a.tiny_max;  // (bounds above valid)
+      }
       __syncthreads();
       todo = 0;
 #pragma unroll
@@ -2852,13 +2869,21 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
     if (!kGather) {
       if (tid == 0) {
         if constexpr (kBypass) {  // inbox = [previous backlog, in place][sorted new mail]
-          const uint32_t bs = a.bstart[b], be = a.bstart[b + 1], bp = a.blpre[b] + a.bl_sbase[b / kBlSlice];
-          const uint32_t blc = a.chunk_cnt[b], blo = a.chunk_off[b];
-          s_g[0] = blc;
-          s_g[1] = blo;
-          s_g[3] = bs;
-          s_lo = bs + bp;
-          s_hi = bs + bp + blc + (be - bs);
+          if (kTiny && kTinyBounds && s_tb[j][5]) {  // (read by the wave check of this group)
+            s_g[0] = s_tb[j][3];
+            s_g[1] = s_tb[j][4];
+            s_g[3] = s_tb[j][0];
+            s_lo = s_tb[j][1];
+            s_hi = s_tb[j][2];
+          } else {
+            const uint32_t bs = a.bstart[b], be = a.bstart[b + 1], bp = a.blpre[b] + a.bl_sbase[b / kBlSlice];
+            const uint32_t blc = a.chunk_cnt[b], blo = a.chunk_off[b];
+            s_g[0] = blc;
+            s_g[1] = blo;
+            s_g[3] = bs;
+            s_lo = bs + bp;
+            s_hi = bs + bp + blc + (be - bs);
+          }
           if ((uint64_t)s_hi > a.cap) {  // mail + backlog over the message capacity: report, drop
             atomicOr((unsigned long long*)&a.stats[ST_ERROR], (unsigned long long)kErrCapacity);
             s_lo = s_hi = 0u;
