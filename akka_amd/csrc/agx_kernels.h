@@ -2290,7 +2290,11 @@ constexpr bool kEarlyState = AGX_EARLY_STATE != 0;  // fused fast path: state lo
 #ifndef AGX_TINY_BOUNDS
 #define AGX_TINY_BOUNDS 1
 #endif
-constexpr bool kTinyBounds = AGX_TINY_BOUNDS != 0;  // multi-pass: block path reuses the wave check's bounds (A/B knob)
+constexpr bool kTinyBounds = AGX_TINY_BOUNDS != 0;
+#ifndef AGX_LATE_ALIVE
+#define AGX_LATE_ALIVE 1
+#endif
+constexpr bool kLateAlive = AGX_LATE_ALIVE != 0;  // alive flags stored to LDS after the inbox loads issue (A/B knob)  // multi-pass: block path reuses the wave check's bounds (A/B knob)
 constexpr uint32_t kSkRec = 12;    // b, lo, cnt, blc, blo, bst, pbase, np, ndrain, bltot, npb, -
 constexpr uint32_t kSkSpan = 4 * kBucket;  // minimum inbox positions per part
 constexpr uint32_t kRingMaxC = 4096;  // bounded-mailbox rings: largest mailbox capacity they hold (16-bit head / length)
@@ -2960,7 +2964,10 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         }
       }
     }
-    reinterpret_cast<uint32_t*>(s_alive)[tid] = alive4;
+    // (kLateAlive: the flags reach LDS after the inbox loads are issued, so the bucket's first
+    // barrier does not wait for their round trip; loads return in order, so the store's wait does
+    // not wait for the inbox)
+    if (!kLateAlive) reinterpret_cast<uint32_t*>(s_alive)[tid] = alive4;
     __syncthreads();
     AGX_STAMP(a, 1);
     const bool big = s_g[5] != 0;
@@ -3067,6 +3074,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         for (int r = 0; r < kBIpt; ++r)
           if (wbase + r * kWave + lane >= cnt) k[r] = 0xFFFFFFFFu;
       }
+      if (kLateAlive) reinterpret_cast<uint32_t*>(s_alive)[tid] = alive4;
       __syncthreads();  // (fused) the segment list in s_pay is read before the items overwrite it
       // in-order copy + sortedness check: local topologies (rings, stencils) arrive already in
       // actor order, and then the wave multisplit ranking is unnecessary (same result)
@@ -3170,6 +3178,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         const uint32_t* act = a.sk_act + (size_t)it * kSkActPlanes * kBucket;
         for (uint32_t la = tid; la < kBucket; la += kBThreads) s_seg[la] = act[kBucket + la];
         if (tid == 0) s_seg[kBucket] = r[8];
+        if (kLateAlive) reinterpret_cast<uint32_t*>(s_alive)[tid] = alive4;
         __syncthreads();
         // (r[1]: the bucket's inbox index space, or a ring bucket's drain scratch / tell slice)
         bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, r[1], r[8], a0, na, wpar, 0u, acc, r[9]);
@@ -3180,6 +3189,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
       uint32_t* s_keep = s_ecnt;  // (bucket_finish re-initialises ecnt)
       for (uint32_t i = tid; i < kBucket + 4; i += kBThreads) s_seg[i] = 0;
       for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] = 0;
+      if (kLateAlive) reinterpret_cast<uint32_t*>(s_alive)[tid] = alive4;
       __syncthreads();
       for (uint32_t q0 = 0; q0 < cnt; q0 += 4 * kBThreads) {  // arrivals per actor (4 loads in flight)
         uint32_t kk[4];
