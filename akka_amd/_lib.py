@@ -97,6 +97,7 @@ SIGNATURES = {
     "agx_get_stats": (ctypes.c_int32, [ctypes.c_void_p, ctypes.POINTER(AgxStats)]),
     "agx_identity_supersteps": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
     "agx_ring_buckets": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
+    "agx_get_shape": (ctypes.c_int32, [ctypes.c_void_p, c_u64p, c_u32p]),
     "agx_read_state": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_u64p, c_u8p]),
     "agx_comm_unique_id": (ctypes.c_int32, [ctypes.c_void_p]),
     "agx_comm_init": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p]),

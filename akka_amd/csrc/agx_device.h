@@ -92,13 +92,13 @@ __device__ __forceinline__ bool outbound_tell(const DevParams& P, uint32_t dst, 
                                               bool write) {
   if (dst - P.host_lo >= P.host_n) return false;
   if (write) {
+    // an append past outbox_cap is dropped and reported (then cleared) by agx_take_outbound from the
+    // count itself -- not through the sticky error word, so the engine stays usable
     const uint32_t i = atomicAdd(P.outbox_n, 1u);
     if (i < P.outbox_cap) {
       P.outbox[3 * (size_t)i] = dst;
       P.outbox[3 * (size_t)i + 1] = src;
       P.outbox[3 * (size_t)i + 2] = pay;
-    } else {
-      atomicOr(P.err, 1ull);  // kErrCapacity
     }
   }
   return true;

@@ -121,6 +121,7 @@ struct agx_engine {
   uint64_t outbox_cap = 0;
   uint32_t *d_outbox = nullptr, *d_outbox_n = nullptr;
   std::vector<uint32_t> outq;  // taken from the device, not yet handed to the host (dst, src, payload)
+  uint64_t outbox_lost = 0;    // outbound tells dropped at a full outbox, not reported yet (agx_take_outbound)
   uint32_t bb = kBucketBits;  // bucket bits (agx_cfg.bucket_actors)
 
   // sharding tables (R > 1)
@@ -949,6 +950,25 @@ void make_plan(agx_engine* e, const uint64_t* mat, Plan& p) {
 agx_status copy_sync(agx_engine* e, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, kind, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return AGX_OK;
+}
+
+// the reply path: move the device outbox to the host queue (the engine is idle between calls); the
+// appends past the outbox capacity were dropped on the device and are counted into outbox_lost
+agx_status drain_outbox(agx_engine* e) {
+  if (!e->d_outbox_n) return AGX_OK;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  uint32_t cnt = 0;
+  AGX_TRY(copy_sync(e, &cnt, e->d_outbox_n, 4, hipMemcpyDeviceToHost));
+  const uint64_t m = e->d_outbox ? std::min<uint64_t>(cnt, e->outbox_cap) : 0;
+  if (m) {
+    const size_t o = e->outq.size();
+    e->outq.resize(o + 3 * m);
+    AGX_TRY(copy_sync(e, e->outq.data() + o, e->d_outbox, 12 * m, hipMemcpyDeviceToHost));
+  }
+  e->outbox_lost += cnt - m;
+  const uint32_t zero = 0;
+  if (cnt) AGX_TRY(copy_sync(e, e->d_outbox_n, &zero, 4, hipMemcpyHostToDevice));
   return AGX_OK;
 }
 
@@ -1952,6 +1972,7 @@ agx_status agx_set_outbound(agx_engine* e, uint32_t first_host_id, uint32_t n_ho
     HIP_TRY(hipMemsetAsync(e->d_outbox_n, 0, 4, e->stream));
   }
   if (n_host && capacity != e->outbox_cap) {
+    AGX_TRY(drain_outbox(e));  // tells still in the old buffer move to the host queue first
     hipFree(e->d_outbox);
     e->d_outbox = nullptr;
     AGX_TRY(dalloc(&e->d_outbox, 3 * capacity));
@@ -1969,21 +1990,12 @@ agx_status agx_take_outbound(agx_engine* e, uint32_t* dst, uint32_t* src, uint32
   if (!e || !n || (cap && (!dst || !src || !payload))) return set_err(AGX_EINVAL, "bad take_outbound args");
   *n = 0;
   AGX_TRY(ensure_dev(e));
-  if (e->d_outbox_n) {  // move the device outbox to the host queue (the engine is idle between calls)
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    uint32_t cnt = 0;
-    AGX_TRY(copy_sync(e, &cnt, e->d_outbox_n, 4, hipMemcpyDeviceToHost));
-    const uint64_t m = std::min<uint64_t>(cnt, e->outbox_cap);
-    if (m) {
-      const size_t o = e->outq.size();
-      e->outq.resize(o + 3 * m);
-      AGX_TRY(copy_sync(e, e->outq.data() + o, e->d_outbox, 12 * m, hipMemcpyDeviceToHost));
-    }
-    if (cnt) HIP_TRY(hipMemsetAsync(e->d_outbox_n, 0, 4, e->stream));
-    HIP_TRY(hipDeviceSynchronize());
-    if (cnt > e->outbox_cap)
-      return set_err(AGX_ECAPACITY, "%u outbound tells since the last agx_take_outbound, outbox capacity %llu",
-                     cnt, (unsigned long long)e->outbox_cap);
+  AGX_TRY(drain_outbox(e));
+  if (e->outbox_lost) {  // reported once, then cleared: the engine stays usable after an overflow
+    const uint64_t lost = e->outbox_lost;
+    e->outbox_lost = 0;
+    return set_err(AGX_ECAPACITY, "%llu outbound tells dropped: more than the outbox capacity %llu between two "
+                   "agx_take_outbound calls", (unsigned long long)lost, (unsigned long long)e->outbox_cap);
   }
   const uint64_t k = std::min<uint64_t>(cap, e->outq.size() / 3);
   for (uint64_t i = 0; i < k; ++i) {
@@ -2285,6 +2297,13 @@ agx_status agx_get_stats(agx_engine* e, agx_stats* out) {
   if (!e) return set_err(AGX_EINVAL, "null engine");
   AGX_TRY(ensure_dev(e));
   return collect_stats(e, out, true);
+}
+
+agx_status agx_get_shape(agx_engine* e, uint64_t* n_actors, uint32_t* n_words) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  if (n_actors) *n_actors = e->n_global;
+  if (n_words) *n_words = e->W;
+  return AGX_OK;
 }
 
 agx_status agx_read_state(agx_engine* e, uint64_t first_id, uint64_t count, uint64_t* words, uint8_t* alive) {

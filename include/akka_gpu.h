@@ -337,6 +337,9 @@ agx_status agx_take_outbound(agx_engine* eng, uint32_t* dst, uint32_t* src, uint
                              uint64_t* n);
 
 /* --- state readback ----------------------------------------------------------- */
+/* The population (agx_cfg.n_actors, all ranks) and state words per actor: the sizes a binding
+ * checks caller arrays against before agx_set_graph / agx_read_state (whose pointers carry none). */
+agx_status agx_get_shape(agx_engine* eng, uint64_t* n_actors, uint32_t* n_words);
 /* words: count x n_words u64 (actor-major); alive: count bytes (may be NULL).
  * Only ids owned by this rank are written; others are left untouched.       */
 agx_status agx_read_state(agx_engine* eng, uint64_t first_id, uint64_t count, uint64_t* words,

@@ -192,10 +192,13 @@ JNIEXPORT void JNICALL Java_akka_dispatch_gpu_AgxJni_setFanout(JNIEnv* env, jcla
 JNIEXPORT void JNICALL Java_akka_dispatch_gpu_AgxJni_setGraph(JNIEnv* env, jclass k, jlong eng, jlongArray row_ptr,
                                                               jintArray col) {
   (void)k;
+  uint64_t n_actors = 0;
+  if (raise(env, agx_get_shape(ENG(eng), &n_actors, NULL))) return;
   jsize nr = 0, nc = 0;
   uint64_t* r = copy_longs(env, row_ptr, &nr);
   uint32_t* c = copy_ints(env, col, &nc);
-  if (!r || nr < 1 || (uint64_t)nc < r[nr - 1])
+  /* agx_set_graph reads row_ptr[0 .. n_actors] and col[0 .. row_ptr[n_actors]): both lengths exact */
+  if (!r || (uint64_t)nr != n_actors + 1 || (uint64_t)nc < r[n_actors] || (r[n_actors] && !c))
     raise(env, AGX_EINVAL);
   else
     raise(env, agx_set_graph(ENG(eng), r, c ? c : (const uint32_t*)r));
@@ -261,9 +264,13 @@ JNIEXPORT void JNICALL Java_akka_dispatch_gpu_AgxJni_getStats(JNIEnv* env, jclas
 JNIEXPORT void JNICALL Java_akka_dispatch_gpu_AgxJni_readState(JNIEnv* env, jclass k, jlong eng, jlong first,
                                                                jlong count, jlongArray words, jbyteArray alive) {
   (void)k;
+  uint32_t n_words = 0;
+  if (raise(env, agx_get_shape(ENG(eng), NULL, &n_words))) return;
   const jsize nw = words ? (*env)->GetArrayLength(env, words) : 0;
   const jsize na = alive ? (*env)->GetArrayLength(env, alive) : 0;
-  if (count < 0 || (alive && na < count) || (words && count && nw % count)) {
+  /* agx_read_state writes count x n_words u64: the array must hold exactly that */
+  if (count < 0 || count > 0x7FFFFFFFll || (alive && na < count) ||
+      (words && (jlong)nw != count * (jlong)n_words)) {
     raise(env, AGX_EINVAL);
     return;
   }

@@ -61,6 +61,7 @@ object AgxNative {
   val getStats: MethodHandle = h("agx_get_stats", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS))
   val readState: MethodHandle =
     h("agx_read_state", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, JAVA_LONG, ADDRESS, ADDRESS))
+  val getShape: MethodHandle = h("agx_get_shape", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS))
   val shardId: MethodHandle = h("agx_shard_id", FunctionDescriptor.of(JAVA_INT, JAVA_INT, JAVA_INT))
 
   /** status -> exception (errors never cross the C ABI as exceptions; the message is agx_last_error) */
@@ -171,6 +172,14 @@ object PanamaBackend extends AgxBackend {
   def readState(engine: Long, first: Long, count: Long, words: Array[Long], alive: Array[Byte]): Unit = {
     val a = Arena.ofConfined()
     try {
+      // agx_read_state writes count x n_words u64 and count bytes: the arrays must hold exactly that
+      val shape = a.allocate(JAVA_INT)
+      check(AgxNative.getShape.invokeExact(seg(engine), MemorySegment.NULL, shape).asInstanceOf[Int])
+      val nWords = shape.get(JAVA_INT, 0).toLong
+      if (count < 0 || (words != null && words.length.toLong != count * nWords) ||
+          (alive != null && alive.length.toLong < count))
+        throw new ConfigurationException(
+          s"akka-gpu: readState needs words.length == count * $nWords and alive.length >= count")
       val w = if (words == null) MemorySegment.NULL else a.allocate(JAVA_LONG, math.max(words.length, 1).toLong)
       val al = if (alive == null) MemorySegment.NULL else a.allocate(JAVA_BYTE, math.max(alive.length, 1).toLong)
       check(AgxNative.readState.invokeExact(seg(engine), first, count, w, al).asInstanceOf[Int])

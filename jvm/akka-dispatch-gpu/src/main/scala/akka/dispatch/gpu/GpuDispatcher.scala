@@ -94,7 +94,7 @@ class GpuDispatcher(
   /** ActorRef.! for every actor bound to this dispatcher (Dispatcher.scala:61-65). */
   override protected[akka] def dispatch(receiver: ActorCell, invocation: Envelope): Unit =
     receiver.mailbox.messageQueue match {
-      case q: GpuMessageQueue =>
+      case q: GpuQueue =>
         q.enqueue(receiver.self, invocation) // -> engine staging (dead letter if not fixed-layout)
         schedulePump()
       case _ =>
@@ -107,7 +107,7 @@ class GpuDispatcher(
       hasMessageHint: Boolean,
       hasSystemMessageHint: Boolean): Boolean =
     mbox.messageQueue match {
-      case _: GpuMessageQueue if !hasSystemMessageHint && !mbox.hasSystemMessages => false
+      case _: GpuQueue if !hasSystemMessageHint && !mbox.hasSystemMessages => false
       case _                                                                       => super.registerForExecution(mbox, hasMessageHint, hasSystemMessageHint)
     }
 

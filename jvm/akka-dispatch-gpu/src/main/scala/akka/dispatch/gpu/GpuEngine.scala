@@ -71,7 +71,7 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
   private val nextHost = new AtomicInteger(0)
   private val hostIds = new ConcurrentHashMap[ActorRef, Integer]()
   private val hostRefs = new ConcurrentHashMap[Integer, ActorRef]()
-  private[gpu] val queues = new ConcurrentHashMap[Integer, GpuMessageQueue]() // numberOfMessages bookkeeping
+  private[gpu] val queues = new ConcurrentHashMap[Integer, GpuQueue]() // numberOfMessages bookkeeping
 
   /** actorOf: one fixed-layout actor (GpuMailboxType.create) with its mailbox class */
   def register(ref: ActorRef, kind: Int, init: Array[Long], mailboxCapacity: Int): Int = {

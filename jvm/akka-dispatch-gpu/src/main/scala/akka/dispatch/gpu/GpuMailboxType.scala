@@ -5,6 +5,14 @@
  * registers the owner as one fixed-layout actor of the dispatcher's engine, bound to the engine
  * mailbox class of this mailbox type's capacity -- so bounded and unbounded GPU mailboxes coexist
  * on one dispatcher, each actor with its own (Mailboxes.scala:204-260, ActorMailboxSpec.scala:245-450).
+ *
+ * Two mailbox types, like the reference's UnboundedMailbox / BoundedMailbox (Mailbox.scala:647-720):
+ * GpuMailboxType (ProducesMessageQueue[GpuMessageQueue], UnboundedMessageQueueSemantics) and
+ * GpuBoundedMailboxType (ProducesMessageQueue[GpuBoundedMessageQueue], BoundedMessageQueueSemantics,
+ * mailbox-capacity > 0) -- Mailboxes.getMailboxType checks an actor's RequiresMessageQueue against
+ * the type's marker (Mailboxes.scala:122-135,164-175), so an actor that requires bounded semantics
+ * must be given the bounded type.  A GpuMailboxType with mailbox-capacity > 0 still tail-drops at
+ * that capacity and its queues are GpuBoundedMessageQueue at run time.
  */
 package akka.dispatch.gpu
 
@@ -13,15 +21,15 @@ import java.util.concurrent.atomic.AtomicInteger
 
 import com.typesafe.config.Config
 
+import scala.concurrent.duration.Duration
+
 import akka.actor.{ ActorRef, ActorSystem, DeadLetter }
 import akka.dispatch._
 
 /** The fixed-layout message of a GPU actor: one u32 payload word (the sender travels in the Envelope). */
 final case class GpuTell(payload: Int)
 
-class GpuMailboxType(settings: ActorSystem.Settings, config: Config)
-    extends MailboxType
-    with ProducesMessageQueue[GpuMessageQueue] {
+abstract class GpuMailboxTypeBase(settings: ActorSystem.Settings, config: Config) extends MailboxType {
 
   private val dispatcherId = config.getString("gpu.dispatcher")
   private val kind: Int = config.getString("gpu.behavior") match {
@@ -41,7 +49,7 @@ class GpuMailboxType(settings: ActorSystem.Settings, config: Config)
   /** BoundedMailbox's keys (Mailbox.scala:699-720): mailbox-capacity, mailbox-push-timeout-time.
    *  The GPU mailbox tail-drops at capacity (pushTimeOut 0, AbstractBoundedNodeQueue.java:92-113);
    *  a positive push timeout would block the sender, which a superstep cannot do. */
-  private val capacity: Int = if (config.hasPath("mailbox-capacity")) config.getInt("mailbox-capacity") else 0
+  protected val capacity: Int = if (config.hasPath("mailbox-capacity")) config.getInt("mailbox-capacity") else 0
   if (capacity < 0) throw new IllegalArgumentException("The capacity for GpuMailboxType can not be negative")
   if (capacity > 0 && config.hasPath("mailbox-push-timeout-time") &&
       config.getDuration("mailbox-push-timeout-time").toNanos != 0L)
@@ -54,19 +62,33 @@ class GpuMailboxType(settings: ActorSystem.Settings, config: Config)
       case Some(ref) => engine.register(ref, kind, Array.fill(engine.stateWords)(0L), capacity)
       case None      => Agx.NoSender // the dummy queue of a top-level actor under construction
     }
-    val q = new GpuMessageQueue(id, engine, system)
+    val q: GpuQueue =
+      if (capacity > 0) new GpuBoundedMessageQueue(id, engine, system, capacity)
+      else new GpuMessageQueue(id, engine, system)
     if (id != Agx.NoSender) engine.queues.put(id, q)
     q
   }
+}
+
+/** mailbox-type = "akka.dispatch.gpu.GpuMailboxType": unbounded semantics (UnboundedMailbox). */
+class GpuMailboxType(settings: ActorSystem.Settings, config: Config)
+    extends GpuMailboxTypeBase(settings, config)
+    with ProducesMessageQueue[GpuMessageQueue]
+
+/** mailbox-type = "akka.dispatch.gpu.GpuBoundedMailboxType": BoundedMailbox(mailbox-capacity, 0)
+ *  semantics (Mailbox.scala:699-720), tail-drop to dead letters at the capacity. */
+class GpuBoundedMailboxType(settings: ActorSystem.Settings, config: Config)
+    extends GpuMailboxTypeBase(settings, config)
+    with ProducesMessageQueue[GpuBoundedMessageQueue] {
+  if (capacity <= 0)
+    throw new IllegalArgumentException("The capacity for GpuBoundedMailboxType must be positive (mailbox-capacity)")
 }
 
 /** The device-side mailbox of one actor.  enqueue stages the tell for the engine; nothing is
  *  ever dequeued on the JVM (MessageQueue contract, Mailbox.scala:359-390).  numberOfMessages
  *  counts this actor's tells staged on the JVM and not yet handed to the engine; the messages on
  *  the device are in the engine's in-flight count (GpuEngine.stats()(6)). */
-final class GpuMessageQueue(val id: Int, engine: GpuEngine, system: Option[ActorSystem])
-    extends MessageQueue
-    with UnboundedMessageQueueSemantics {
+sealed abstract class GpuQueue(val id: Int, engine: GpuEngine, system: Option[ActorSystem]) extends MessageQueue {
 
   private val staged = new AtomicInteger(0)
 
@@ -90,4 +112,17 @@ final class GpuMessageQueue(val id: Int, engine: GpuEngine, system: Option[Actor
   def numberOfMessages: Int = staged.get
   def hasMessages: Boolean = staged.get > 0
   def cleanUp(owner: ActorRef, deadLetters: MessageQueue): Unit = () // the engine dead-letters them
+}
+
+/** A GPU actor's unbounded mailbox. */
+final class GpuMessageQueue(id: Int, engine: GpuEngine, system: Option[ActorSystem])
+    extends GpuQueue(id, engine, system)
+    with UnboundedMessageQueueSemantics
+
+/** A GPU actor's bounded mailbox: admission `p < capacity` on the device, the rest dead letters;
+ *  never blocks a sender (pushTimeOut 0, AbstractBoundedNodeQueue.java:92-113). */
+final class GpuBoundedMessageQueue(id: Int, engine: GpuEngine, system: Option[ActorSystem], val capacity: Int)
+    extends GpuQueue(id, engine, system)
+    with BoundedMessageQueueSemantics {
+  def pushTimeOut: Duration = Duration.Zero
 }

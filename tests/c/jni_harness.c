@@ -43,6 +43,7 @@ void Java_akka_dispatch_gpu_AgxJni_stageTellsArrays(JNIEnv*, jclass, jlong, jint
 void Java_akka_dispatch_gpu_AgxJni_run(JNIEnv*, jclass, jlong, jint, jlongArray);
 void Java_akka_dispatch_gpu_AgxJni_getStats(JNIEnv*, jclass, jlong, jlongArray);
 void Java_akka_dispatch_gpu_AgxJni_readState(JNIEnv*, jclass, jlong, jlong, jlong, jlongArray, jbyteArray);
+void Java_akka_dispatch_gpu_AgxJni_setGraph(JNIEnv*, jclass, jlong, jlongArray, jintArray);
 void Java_akka_dispatch_gpu_AgxJni_setOutbound(JNIEnv*, jclass, jlong, jint, jint, jlong);
 jint Java_akka_dispatch_gpu_AgxJni_takeOutbound(JNIEnv*, jclass, jlong, jintArray, jintArray, jintArray, jint);
 jint Java_akka_dispatch_gpu_AgxJni_shardId(JNIEnv*, jclass, jint, jint);
@@ -244,8 +245,25 @@ int main(void) {
   CHECK(L(st)[0] == 200 * 50 + 10 + 20, "delivered %lld", (long long)L(st)[0]);
   CHECK(L(st)[1] == 10, "dead letters %lld (bounded-capacity:10 drops 10 of 20)", (long long)L(st)[1]);
   CHECK(L(st)[6] == 0, "in flight");
-  jlongArray w = longs(3 * 2);
+  jlongArray w = longs(2); /* count 1 x n_words 2 */
   jbyteArray al = bytes(3);
+  /* arrays that do not match count x n_words: rejected before any native write */
+  jlongArray wshort = longs(1), wlong = longs(3);
+  RAISES("akka/ConfigurationException", Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 3, 1, wshort, al));
+  RAISES("akka/ConfigurationException", Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 3, 1, wlong, al));
+  RAISES("akka/ConfigurationException", Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 0, 2, w, al));
+  /* a CSR whose rowPtr is shorter than n_actors + 1 (or col shorter than rowPtr[n]): rejected */
+  jlongArray rp_short = longs(3);
+  jintArray col1 = ints(1);
+  RAISES("akka/ConfigurationException", Java_akka_dispatch_gpu_AgxJni_setGraph(env, K, eng, rp_short, col1));
+  jlongArray rp = longs(N + 1);
+  for (jint i = 0; i <= N; ++i) L(rp)[i] = i < 8 ? i : 8; /* actors 0..7 have one edge each */
+  RAISES("akka/ConfigurationException", Java_akka_dispatch_gpu_AgxJni_setGraph(env, K, eng, rp, col1));
+  free_obj(wshort);
+  free_obj(wlong);
+  free_obj(rp_short);
+  free_obj(rp);
+  free_obj(col1);
   NOEXC(Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 3, 1, w, al));
   CHECK(L(w)[0] == 200 * 50 && B(al)[0] == 1, "msgsProcessed == msgsReceived (%lld)", (long long)L(w)[0]);
   NOEXC(Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 101, 1, w, al));
@@ -303,6 +321,17 @@ int main(void) {
   }
   NOEXC(n = Java_akka_dispatch_gpu_AgxJni_takeOutbound(env, K, eng, od, os, op, 64));
   CHECK(n == 0, "outbox drained");
+
+  /* an outbox overflow is reported once by takeOutbound (IllegalStateException) and the engine
+     stays usable: the kept replies come out of the next take, later runs work */
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_setOutbound(env, K, eng, HOST, NHOST, 4));
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_stageTellsArrays(env, K, eng, md, ms, mp, 40));
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_run(env, K, eng, 1 << 30, st));
+  RAISES("java/lang/IllegalStateException", Java_akka_dispatch_gpu_AgxJni_takeOutbound(env, K, eng, od, os, op, 64));
+  NOEXC(n = Java_akka_dispatch_gpu_AgxJni_takeOutbound(env, K, eng, od, os, op, 64));
+  CHECK(n == 4, "the 4 kept replies (%d)", n);
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_stageTellsArrays(env, K, eng, td, ts, tp, 1));
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_run(env, K, eng, 1 << 30, st));
 
   NOEXC(Java_akka_dispatch_gpu_AgxJni_destroy(env, K, eng));
   free_obj(d);
