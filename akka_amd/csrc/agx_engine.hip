@@ -87,10 +87,10 @@ struct DevMsgs {
 };
 
 enum KClass { K_CROWSCAN, K_CDOWN, K_UPSWEEP, K_ROWSCAN, K_DOWNSWEEP, K_APPLY, K_EXCHANGE, K_MCOMPACT, K_SKEW, K_TICK,
-              K_BOUNDS, K_NCLASS };
+              K_BOUNDS, K_SKEWPRE, K_NCLASS };
 const char* kClassNames[K_NCLASS] = {"chunk_rowscan", "chunk_downsweep", "sort_upsweep", "sort_rowscan",
                                      "sort_downsweep", "bucket_apply", "exchange", "mcompact", "bucket_apply_skew",
-                                     "fused_tick", "bucket_bounds"};
+                                     "fused_tick", "bucket_bounds", "skew_prepass"};
 
 constexpr uint32_t kGraphSizes[5] = {1, 2, 4, 8, 16};  // superstep replays (agx_engine::gx)
 constexpr uint32_t kRowAlign = 32;  // CRDT row pitch (u32) of rows wider than one 128-B line
@@ -692,8 +692,11 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
       HIP_TRY(agx_launch_apply(vid, mode, false, g, e->stream, bf));
     }
     if (!(mode == M_FUSED && e->strict_cap)) {
+      if (!kVariants[vid].wide && mode == M_BYPASS) {
+        Scope s(e, K_SKEWPRE);  // (k_skew_plan / count / scan / scatter: their own profiling class)
+        skew_prepass(e, ba, ska);
+      }
       Scope s(e, K_SKEW);
-      if (!kVariants[vid].wide && mode == M_BYPASS) skew_prepass(e, ba, ska);
       HIP_TRY(agx_launch_apply(vid, mode, true, gs, e->stream, ba));
     }
     if (orm) {

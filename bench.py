@@ -193,18 +193,25 @@ def timed_ring(n_total: int, hops: int, warmup: int, steps: int, world: int, ran
     return eng, t1 - t0, s1.delivered - s0.delivered, s1.supersteps - s0.supersteps
 
 
-def timed_workload(w, warmup: int, steps: int, prof_steps: int = 8, msg_capacity: int = 0) -> dict:
+def timed_workload(w, warmup: int, steps: int, msg_capacity: int = 0) -> dict:
     """One BASELINE config on one GPU: install the workload, `warmup` untimed supersteps,
-    then exactly `steps` timed supersteps (inputs resident in HBM), then a short profiled
-    window (eager launches, HIP events per kernel)."""
+    then exactly `steps` timed supersteps (inputs resident in HBM, replayed from hipGraphs).
+    The per-kernel breakdown comes from a second engine on the same workload driven through
+    the SAME superstep window (warmup, then `steps` eager supersteps with HIP events around
+    every kernel class): a workload's mail changes from superstep to superstep (C5's tokens die
+    after 15 hops), so a window after the timed one would describe different supersteps."""
     import torch
     from akka_amd.engine import EngineConfig, GpuEngine
 
+    def make():
+        cfg = EngineConfig(**w.gpu_kwargs())
+        cfg.msg_capacity = msg_capacity
+        eng = GpuEngine(cfg)
+        w.apply_to(eng)
+        return eng
+
     t0 = time.perf_counter()
-    cfg = EngineConfig(**w.gpu_kwargs())
-    cfg.msg_capacity = msg_capacity
-    eng = GpuEngine(cfg)
-    w.apply_to(eng)
+    eng = make()
     setup = time.perf_counter() - t0
     s0 = eng.run(warmup)
     torch.cuda.synchronize()
@@ -213,21 +220,25 @@ def timed_workload(w, warmup: int, steps: int, prof_steps: int = 8, msg_capacity
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     s1 = eng.stats()
+    rings = eng.ring_buckets()
+    eng.close()
+    eng = make()  # the profiled replay of the same window
+    eng.run(warmup)
     eng.profile(True)
     eng.profile_reset()
-    eng.run(prof_steps)
+    sp = eng.run(steps)
     prof = eng.profile_read()
-    rings = eng.ring_buckets()
     eng.close()
     d = s1.delivered - s0.delivered
     ss = s1.supersteps - s0.supersteps
     bytes_alg = s1.bytes_alg - s0.bytes_alg
+    kms = {k: round(v["total_ms"] / max(ss, 1), 4) for k, v in prof.items() if v["launches"]}
     return {"value": d / el, "unit": "msg/s", "delivered": d, "dead_letters": s1.dead_letters - s0.dead_letters,
             "supersteps_timed": ss, "ms_per_step": el / max(ss, 1) * 1e3, "setup_s": round(setup, 2),
             "alg_bytes_per_msg": bytes_alg / max(d, 1), "ring_buckets": rings,
             "superstep_frac": bytes_alg / el / 1e9 / PEAK_HBM_GBS,
-            "kernel_ms_per_step": {k: round(v["total_ms"] / max(v["launches"], 1), 4) for k, v in prof.items()
-                                   if v["launches"]}}
+            "profiled_window_same": sp.delivered == s1.delivered and sp.supersteps == s1.supersteps,
+            "kernel_ms_per_step": kms, "kernel_ms_per_step_sum": round(sum(kms.values()), 4)}
 
 
 def other_configs(quick: bool, only: str = "") -> dict:

@@ -3,7 +3,7 @@
  * dispatcher.  Only tests/, __graft_entry__.smoke() and bench.py's
  * cpu_baseline leg may load this; the product path (akka_amd/) never does.
  *
- * A single-threaded, deterministic restatement of the reference's
+ * A deterministic restatement of the reference's
  * Dispatcher/Mailbox drain loop as bulk-synchronous supersteps
  * (SURVEY.md §7 "Execution model").  Each step follows these reference
  * functions (paths relative to /root/reference):
@@ -40,6 +40,7 @@
  * (sender id, emission index).  It preserves per-sender FIFO, the only order
  * Akka guarantees (akka-docs/.../general/message-delivery-reliability.md:110-131).
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -145,6 +146,7 @@ typedef struct bsp_sim {
   uint8_t* alive;
   uint64_t* state; /* actor-major: state[a*W + w] */
   uint32_t* order; /* apply order: by (owner, id) */
+  uint32_t* pos;   /* its inverse (built at the first superstep) */
   /* params */
   ref_params P;
   uint32_t* zipf_cdf;
@@ -155,7 +157,12 @@ typedef struct bsp_sim {
   agx_act* bact;
   uint32_t* bfirst;
   /* mail */
-  envvec backlog, emitted, staged;
+  /* mail in flight: runs of backlog then runs of emitted tells (one run per apply thread of the last
+   * superstep, in canonical order: concatenated without a copy), then the host-staged tells */
+  envvec* seg;
+  uint32_t nseg, nbl; /* runs; the first nbl are backlog */
+  uint32_t rw;        /* inline snapshot words per envelope (CRDT state gossips) */
+  envvec staged;
   agx_stats st;
   /* per-actor mailboxes (Mailboxes.lookupConfigurator, Mailboxes.scala:204-260): class per actor,
    * capacity per class (class 0 = the dispatcher default), Tr = throughput before the bound clamp */
@@ -214,12 +221,28 @@ bsp_sim* bsp_create(uint64_t n_actors, uint32_t throughput, uint32_t capacity, u
 
 void bsp_destroy(bsp_sim* s) {
   if (!s) return;
-  free(s->kind); free(s->alive); free(s->state); free(s->order); free(s->mcls); free(s->outbox);
+  free(s->kind); free(s->alive); free(s->state); free(s->order); free(s->pos); free(s->mcls); free(s->outbox);
   free(s->zipf_cdf); free(s->zipf_perm); free(s->row_ptr); free(s->col);
   free(s->bcase); free(s->bact); free(s->bfirst);
-  free(s->backlog.v); free(s->emitted.v); free(s->staged.v);
-  free(s->backlog.rows); free(s->emitted.rows); free(s->staged.rows);
+  for (uint32_t i = 0; i < s->nseg; ++i) { free(s->seg[i].v); free(s->seg[i].rows); }
+  free(s->seg);
+  free(s->staged.v); free(s->staged.rows);
   free(s);
+}
+
+static uint64_t bsp_in_flight(const bsp_sim* s) {
+  uint64_t n = s->staged.n;
+  for (uint32_t i = 0; i < s->nseg; ++i) n += s->seg[i].n;
+  return n;
+}
+
+/* inline snapshot rows of `rw` u64 per envelope (only before any mail exists) */
+static int bsp_set_rw(bsp_sim* s, uint32_t rw) {
+  if (rw <= s->rw) return 0;
+  if (bsp_in_flight(s)) return -1;
+  if (ev_set_rw(&s->staged, rw)) return -1;
+  s->rw = rw;
+  return 0;
 }
 
 int bsp_register_range(bsp_sim* s, uint64_t first, uint64_t count, uint32_t kind, const uint64_t* init,
@@ -230,7 +253,7 @@ int bsp_register_range(bsp_sim* s, uint64_t first, uint64_t count, uint32_t kind
   uint32_t rw = ref_crdt_words(kind);
   if (rw) {
     if (s->W < rw) return 1;
-    if (ev_set_rw(&s->backlog, rw) || ev_set_rw(&s->emitted, rw) || ev_set_rw(&s->staged, rw)) return 1;
+    if (bsp_set_rw(s, rw)) return 1;
   }
   for (uint64_t i = 0; i < count; ++i) {
     uint64_t a = first + i;
@@ -312,7 +335,7 @@ int bsp_set_delta_crdt(bsp_sim* s, uint32_t max_delta_size) {
     const uint32_t r = ref_row_words(k, max_delta_size);
     if (r > rw) rw = r;
   }
-  if (ev_set_rw(&s->backlog, rw) || ev_set_rw(&s->emitted, rw) || ev_set_rw(&s->staged, rw)) return 1;
+  if (bsp_set_rw(s, rw)) return 1;
   return 0;
 }
 
@@ -344,6 +367,57 @@ int bsp_set_graph(bsp_sim* s, const uint64_t* row_ptr, const uint32_t* col) {
   return 0;
 }
 
+/* Workload setup (not the dispatcher): the R-MAT destinations agx_set_graph_rmat generates on the
+ * device, restated from its formula in include/akka_gpu.h -- edge e's destination takes `bits`
+ * quadrant draws q = splitmix64(e*64 + bit + seed) & 0xFFFF, bit = (ta <= q < tb) | (q >= tc), MSB
+ * first, reduced mod n (workloads.rmat_cols is the numpy form; tests/test_oracle_golden.py checks
+ * they agree).  Split over `threads` host threads so a 10^8-actor graph (~3.6e8 edges) takes
+ * seconds, not minutes, in the full-size parity tests. */
+typedef struct {
+  uint32_t* col;
+  uint64_t lo, hi, seed, n;
+  uint32_t bits, ta, tb, tc;
+} rmat_job;
+
+static void* rmat_worker(void* arg) {
+  const rmat_job* j = (const rmat_job*)arg;
+  for (uint64_t e = j->lo; e < j->hi; ++e) {
+    uint64_t c = 0;
+    for (uint32_t bit = 0; bit < j->bits; ++bit) {
+      const uint32_t q = (uint32_t)(ref_splitmix64(e * 64ull + bit + j->seed) & 0xFFFFull);
+      c |= (uint64_t)(((q >= j->ta && q < j->tb) || q >= j->tc) ? 1u : 0u) << (j->bits - 1 - bit);
+    }
+    j->col[e] = (uint32_t)(c % j->n);
+  }
+  return 0;
+}
+
+int bsp_set_graph_rmat(bsp_sim* s, const uint64_t* row_ptr, uint32_t bits, uint32_t ta, uint32_t tb, uint32_t tc,
+                       uint64_t seed, uint32_t threads) {
+  free(s->row_ptr); free(s->col);
+  s->row_ptr = (uint64_t*)malloc((s->n + 1) * 8);
+  const uint64_t m = row_ptr[s->n];
+  s->col = (uint32_t*)malloc((m ? m : 1) * 4);
+  if (!s->row_ptr || !s->col) return 2;
+  memcpy(s->row_ptr, row_ptr, (s->n + 1) * 8);
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  rmat_job jobs[64];
+  pthread_t th[64];
+  int live[64] = {0};
+  for (uint32_t t = 0; t < threads; ++t) {
+    jobs[t] = (rmat_job){s->col, m * t / threads, m * (t + 1) / threads, seed, s->n, bits, ta, tb, tc};
+    /* the last slice (and any whose thread could not start) runs on this thread */
+    live[t] = t + 1 < threads && pthread_create(&th[t], 0, rmat_worker, &jobs[t]) == 0;
+    if (!live[t]) rmat_worker(&jobs[t]);
+  }
+  for (uint32_t t = 0; t < threads; ++t)
+    if (live[t]) pthread_join(th[t], 0);
+  s->P.row_ptr = s->row_ptr;
+  s->P.col = s->col;
+  return 0;
+}
+
 int bsp_stage(bsp_sim* s, const uint32_t* dst, const uint32_t* src, const uint32_t* payload, uint64_t n) {
   for (uint64_t i = 0; i < n; ++i) {
     s->st.staged++;
@@ -355,84 +429,259 @@ int bsp_stage(bsp_sim* s, const uint32_t* dst, const uint32_t* src, const uint32
   return 0;
 }
 
+/* ---------------------------------------------------------------- one superstep
+ * Inbox formation is a stable sort of the message list [backlog ++ emitted ++ staged] by the
+ * destination's position in the canonical apply order (the counting sort of the restatement; a
+ * radix sort of the message indices when the mail is sparse against the population, so a
+ * superstep costs O(mail), not O(actors)).  The actors with mail are then applied in canonical
+ * order, split over host threads into contiguous runs: each run collects its own emitted tells,
+ * backlog, outbox and counters, and the runs are concatenated in order afterwards -- exactly the
+ * sequence one thread produces (every behaviour touches only its own actor's state).
+ * BSP_THREADS=1 restores a single thread; the tests compare 1 and N threads. */
+
+typedef struct {
+  bsp_sim* s;
+  ref_params P;  /* per-thread copy: ref_apply may set P.error */
+  envvec emitted, backlog;
+  uint32_t* outbox;
+  uint64_t outbox_n;
+  agx_stats st;
+  int error;
+} bsp_part;
+
 /* emit: tell(dst, payload) from `self`; unknown dst -> deadLetters now. */
 static void emit_cb(void* ctx, uint32_t dst, uint32_t self, uint32_t payload, const uint64_t* row, uint32_t rw) {
-  bsp_sim* s = (bsp_sim*)ctx;
+  bsp_part* t = (bsp_part*)ctx;
+  bsp_sim* s = t->s;
   if (dst >= s->n && dst - s->host_lo < s->host_n) { /* a host-side actor: the outbox (not emitted here) */
-    if (s->outbox_n >= s->outbox_cap) { s->P.error = 1; return; }
-    uint32_t* o = (uint32_t*)realloc(s->outbox, (size_t)(s->outbox_n + 1) * 12);
-    if (!o) { s->P.error = 1; return; }
-    s->outbox = o;
-    o[3 * s->outbox_n] = dst;
-    o[3 * s->outbox_n + 1] = self;
-    o[3 * s->outbox_n + 2] = payload;
-    s->outbox_n++;
+    uint32_t* o = (uint32_t*)realloc(t->outbox, (size_t)(t->outbox_n + 1) * 12);
+    if (!o) { t->error = 1; return; }
+    t->outbox = o;
+    o[3 * t->outbox_n] = dst;
+    o[3 * t->outbox_n + 1] = self;
+    o[3 * t->outbox_n + 2] = payload;
+    t->outbox_n++;
     return;
   }
-  s->st.emitted++;
-  if (dst >= s->n) { s->st.dead_letters++; return; }
-  ev_push(&s->emitted, dst, row ? (self | AGX_WIDE_BIT) : self, payload, row, rw);
+  t->st.emitted++;
+  if (dst >= s->n) { t->st.dead_letters++; return; }
+  if (ev_push(&t->emitted, dst, row ? (self | AGX_WIDE_BIT) : self, payload, row, rw)) t->error = 1;
 }
 
-/* One BSP superstep.  Returns 1 if any message was in flight. */
-static int bsp_step(bsp_sim* s) {
-  uint64_t total = s->backlog.n + s->emitted.n + s->staged.n;
-  if (total == 0) return 0;
-  /* inbox formation: stable counting sort of [backlog ++ emitted ++ staged] by dst */
-  const uint32_t rw = s->backlog.rw;
-  env_t* in = (env_t*)malloc(total * sizeof(env_t));
-  uint64_t* inrows = rw ? (uint64_t*)malloc(total * rw * 8) : (uint64_t*)0;
-  uint64_t* off = (uint64_t*)calloc(s->n + 1, 8);
-  envvec* srcs[3] = {&s->backlog, &s->emitted, &s->staged};
-  for (int k = 0; k < 3; ++k)
-    for (uint64_t i = 0; i < srcs[k]->n; ++i) off[srcs[k]->v[i].dst + 1]++;
-  for (uint64_t a = 0; a < s->n; ++a) off[a + 1] += off[a];
-  uint64_t* cur = (uint64_t*)malloc((s->n) * 8);
-  memcpy(cur, off, s->n * 8);
-  for (int k = 0; k < 3; ++k)
-    for (uint64_t i = 0; i < srcs[k]->n; ++i) {
-      uint64_t q = cur[srcs[k]->v[i].dst]++;
-      in[q] = srcs[k]->v[i];
-      if (rw) memcpy(inrows + q * rw, srcs[k]->rows + i * rw, (size_t)rw * 8);
-    }
-  free(cur);
-  s->backlog.n = 0;
-  s->emitted.n = 0;
-  s->staged.n = 0;
+/* a message of the run list [backlog runs ++ emitted runs ++ staged], named (run << 40) | index */
+#define MSG_RUN_SHIFT 40
+typedef struct {
+  const envvec** v;
+} msgview;
+static inline const env_t* mv_env(const msgview* m, uint64_t q, const uint64_t** row) {
+  const envvec* e = m->v[q >> MSG_RUN_SHIFT];
+  const uint64_t i = q & ((1ull << MSG_RUN_SHIFT) - 1);
+  *row = e->rw ? e->rows + i * e->rw : (const uint64_t*)0;
+  return &e->v[i];
+}
+/* every message id of the run list, in order */
+#define FOR_EACH_MSG(mv, nruns, q)                                               \
+  for (uint64_t _r = 0; _r < (nruns); ++_r)                                     \
+    for (uint64_t _i = 0, q = (_r << MSG_RUN_SHIFT); _i < (mv).v[_r]->n; ++_i, ++q)
 
-  /* drain + apply, actors in canonical (owner, id) order so that emission
-   * order is (owner(src), src, idx) */
-  for (uint64_t oi = 0; oi < s->n; ++oi) {
-    uint32_t a = s->order[oi];
-    uint64_t b = off[a], L = off[a + 1] - b;
-    if (!L) continue;
-    if (!s->alive[a]) { s->st.dead_letters += L; continue; }
+typedef struct {
+  bsp_sim* s;
+  bsp_part* part;
+  const msgview* mv;
+  const uint64_t* perm;   /* message indices in inbox order */
+  const uint64_t* abeg;   /* per active actor: first inbox position (abeg[k+1] = end) */
+  const uint32_t* aact;   /* per active actor: its id */
+  uint64_t k0, k1;        /* this run's active actors */
+} bsp_job;
+
+static void* bsp_apply_run(void* arg) {
+  const bsp_job* j = (const bsp_job*)arg;
+  bsp_sim* s = j->s;
+  bsp_part* t = j->part;
+  const uint32_t rw = s->rw;
+  for (uint64_t k = j->k0; k < j->k1; ++k) {
+    const uint32_t a = j->aact[k];
+    const uint64_t b = j->abeg[k], L = j->abeg[k + 1] - b;
+    if (!s->alive[a]) { t->st.dead_letters += L; continue; }
     /* this actor's mailbox: capacity C (0 = unbounded), drain <= min(throughput, C) */
     const uint32_t C = s->mcap[s->mcls[a]];
     const uint32_t T = C && s->Tr > C ? C : s->Tr;
-    uint64_t nd = L < T ? L : T;
+    const uint64_t nd = L < T ? L : T;
     uint32_t kcur = s->kind[a];
     for (uint64_t p = 0; p < nd; ++p) {
-      uint32_t r = ref_apply(&s->P, &kcur, a, &s->state[(uint64_t)a * s->W], in[b + p].src, in[b + p].payload,
-                             rw ? inrows + (b + p) * rw : (const uint64_t*)0, emit_cb, s);
+      const uint64_t* row;
+      const env_t* m = mv_env(j->mv, j->perm[b + p], &row);
+      const uint32_t r = ref_apply(&t->P, &kcur, a, &s->state[(uint64_t)a * s->W], m->src, m->payload, row, emit_cb, t);
       s->kind[a] = (uint8_t)kcur;
-      s->st.delivered++;
-      if (r == AGX_RES_UNHANDLED) s->st.unhandled++;
+      t->st.delivered++;
+      if (r == AGX_RES_UNHANDLED) t->st.unhandled++;
       if (r == AGX_RES_STOPPED) {
         s->alive[a] = 0;
-        s->st.dead_letters += nd - p - 1;
+        t->st.dead_letters += nd - p - 1;
         break;
       }
     }
     for (uint64_t p = nd; p < L; ++p) {
-      if (C == 0 || p < C)
-        ev_push(&s->backlog, in[b + p].dst, in[b + p].src, in[b + p].payload, rw ? inrows + (b + p) * rw : 0, rw);
-      else s->st.dead_letters++;
+      if (C == 0 || p < C) {
+        const uint64_t* row;
+        const env_t* m = mv_env(j->mv, j->perm[b + p], &row);
+        if (ev_push(&t->backlog, m->dst, m->src, m->payload, row, rw)) t->error = 1;
+      } else {
+        t->st.dead_letters++;
+      }
     }
   }
-  free(in);
-  free(inrows);
-  free(off);
+  return 0;
+}
+
+static uint32_t bsp_threads(void) {
+  const char* e = getenv("BSP_THREADS");
+  int t = e ? atoi(e) : 16;
+  return t < 1 ? 1u : t > 64 ? 64u : (uint32_t)t;
+}
+
+/* One BSP superstep.  Returns 1 if any message was in flight. */
+static int bsp_step(bsp_sim* s) {
+  const uint64_t total = bsp_in_flight(s);
+  if (total == 0) return 0;
+  const uint32_t nruns = s->nseg + 1;
+  const envvec** runs = (const envvec**)malloc(nruns * sizeof(envvec*));
+  if (!runs) return s->P.error = 1, 1;
+  for (uint32_t i = 0; i < s->nseg; ++i) runs[i] = &s->seg[i];
+  runs[s->nseg] = &s->staged;
+  msgview mv = {runs};
+  if (!s->pos) { /* position of each actor in the canonical apply order */
+    s->pos = (uint32_t*)malloc(s->n * 4);
+    if (!s->pos) { free(runs); return s->P.error = 1, 1; }
+    for (uint64_t i = 0; i < s->n; ++i) s->pos[s->order[i]] = (uint32_t)i;
+  }
+  uint64_t* perm = (uint64_t*)malloc(total * 8);
+  uint64_t* abeg = (uint64_t*)malloc((total + 1) * 8);
+  uint32_t* aact = (uint32_t*)malloc(total * 4);
+  if (!perm || !abeg || !aact) { free(perm); free(abeg); free(aact); free(runs); s->P.error = 1; return 1; }
+  uint64_t nact = 0;
+  if (total * 4 >= s->n) { /* dense: counting sort over the positions */
+    uint64_t* off = (uint64_t*)calloc(s->n + 1, 8);
+    if (!off) { free(perm); free(abeg); free(aact); free(runs); s->P.error = 1; return 1; }
+    FOR_EACH_MSG(mv, nruns, q) {
+      const uint64_t* row;
+      off[s->pos[mv_env(&mv, q, &row)->dst] + 1]++;
+    }
+    for (uint64_t i = 0; i < s->n; ++i) {
+      if (off[i + 1]) {
+        aact[nact] = s->order[i];
+        abeg[nact++] = off[i];
+      }
+      off[i + 1] += off[i];
+    }
+    abeg[nact] = total;
+    FOR_EACH_MSG(mv, nruns, q) {
+      const uint64_t* row;
+      perm[off[s->pos[mv_env(&mv, q, &row)->dst]]++] = q;
+    }
+    free(off);
+  } else { /* sparse: stable LSD radix sort of (position, message id) in 11-bit digits */
+    uint32_t* key = (uint32_t*)malloc(total * 4);
+    uint32_t* key2 = (uint32_t*)malloc(total * 4);
+    uint64_t* perm2 = (uint64_t*)malloc(total * 8);
+    if (!key || !key2 || !perm2) {
+      free(key); free(key2); free(perm2); free(perm); free(abeg); free(aact); free(runs);
+      s->P.error = 1;
+      return 1;
+    }
+    uint64_t o = 0;
+    FOR_EACH_MSG(mv, nruns, q) {
+      const uint64_t* row;
+      key[o] = s->pos[mv_env(&mv, q, &row)->dst];
+      perm[o++] = q;
+    }
+    uint32_t bits = 1;
+    while (bits < 32 && (1ull << bits) < s->n) ++bits;
+    for (uint32_t sh = 0; sh < bits; sh += 11) {
+      uint64_t cnt[2049];
+      memset(cnt, 0, sizeof cnt);
+      for (uint64_t q = 0; q < total; ++q) cnt[((key[q] >> sh) & 2047u) + 1]++;
+      for (int d = 0; d < 2048; ++d) cnt[d + 1] += cnt[d];
+      for (uint64_t q = 0; q < total; ++q) {
+        const uint64_t x = cnt[(key[q] >> sh) & 2047u]++;
+        key2[x] = key[q];
+        perm2[x] = perm[q];
+      }
+      uint32_t* tk = key; key = key2; key2 = tk;
+      uint64_t* tp = perm; perm = perm2; perm2 = tp;
+    }
+    for (uint64_t q = 0; q < total; ++q)
+      if (q == 0 || key[q] != key[q - 1]) {
+        aact[nact] = s->order[key[q]];
+        abeg[nact++] = q;
+      }
+    abeg[nact] = total;
+    free(key); free(key2); free(perm2);
+  }
+
+  /* runs of active actors, balanced by messages */
+  uint32_t nt = bsp_threads();
+  if ((uint64_t)nt > nact) nt = (uint32_t)(nact ? nact : 1);
+  if (total < 4096) nt = 1;
+  bsp_part* parts = (bsp_part*)calloc(nt, sizeof(bsp_part));
+  bsp_job* jobs = (bsp_job*)calloc(nt, sizeof(bsp_job));
+  pthread_t* th = (pthread_t*)calloc(nt, sizeof(pthread_t));
+  int* live = (int*)calloc(nt, sizeof(int));
+  envvec* seg = (envvec*)calloc(2 * nt, sizeof(envvec));
+  if (!parts || !jobs || !th || !live || !seg) {
+    free(parts); free(jobs); free(th); free(live); free(seg); free(perm); free(abeg); free(aact); free(runs);
+    s->P.error = 1;
+    return 1;
+  }
+  uint64_t k = 0;
+  for (uint32_t t = 0; t < nt; ++t) {
+    parts[t].s = s;
+    parts[t].P = s->P;
+    ev_set_rw(&parts[t].emitted, s->rw);
+    ev_set_rw(&parts[t].backlog, s->rw);
+    const uint64_t goal = total * (t + 1) / nt;
+    uint64_t k1 = k;
+    if (t + 1 == nt) k1 = nact;
+    else while (k1 < nact && abeg[k1] < goal) ++k1;
+    jobs[t] = (bsp_job){s, &parts[t], &mv, perm, abeg, aact, k, k1};
+    k = k1;
+  }
+  for (uint32_t t = 0; t < nt; ++t) {
+    live[t] = t + 1 < nt && pthread_create(&th[t], 0, bsp_apply_run, &jobs[t]) == 0;
+    if (!live[t]) bsp_apply_run(&jobs[t]);
+  }
+  for (uint32_t t = 0; t < nt; ++t)
+    if (live[t]) pthread_join(th[t], 0);
+  free(th); free(live); free(jobs);
+  free(perm); free(abeg); free(aact); free(runs);
+
+  /* the runs become the mail in flight, in canonical order (backlog runs, then emitted runs) */
+  for (uint32_t i = 0; i < s->nseg; ++i) { free(s->seg[i].v); free(s->seg[i].rows); }
+  free(s->seg);
+  s->staged.n = 0;
+  for (uint32_t t = 0; t < nt; ++t) {
+    bsp_part* x = &parts[t];
+    if (x->error || x->P.error) s->P.error = 1;
+    seg[t] = x->backlog;
+    seg[nt + t] = x->emitted;
+    s->st.delivered += x->st.delivered;
+    s->st.dead_letters += x->st.dead_letters;
+    s->st.unhandled += x->st.unhandled;
+    s->st.emitted += x->st.emitted;
+    for (uint64_t i = 0; i < x->outbox_n; ++i) {
+      if (s->outbox_n >= s->outbox_cap) { s->P.error = 1; break; }
+      uint32_t* o = (uint32_t*)realloc(s->outbox, (size_t)(s->outbox_n + 1) * 12);
+      if (!o) { s->P.error = 1; break; }
+      s->outbox = o;
+      memcpy(o + 3 * s->outbox_n, x->outbox + 3 * i, 12);
+      s->outbox_n++;
+    }
+    free(x->outbox);
+  }
+  s->seg = seg;
+  s->nseg = 2 * nt;
+  s->nbl = nt;
+  free(parts);
   s->st.supersteps++;
   return 1;
 }
@@ -440,7 +689,7 @@ static int bsp_step(bsp_sim* s) {
 int bsp_run(bsp_sim* s, uint32_t max_steps, agx_stats* out) {
   for (uint32_t i = 0; i < max_steps && !s->P.error; ++i)
     if (!bsp_step(s)) break;
-  s->st.in_flight = s->backlog.n + s->emitted.n + s->staged.n;
+  s->st.in_flight = bsp_in_flight(s);
   if (out) *out = s->st;
   return s->P.error ? AGX_ECAPACITY : 0;
 }

@@ -82,6 +82,7 @@ def _load_bsp():
             "bsp_vv_compare": (u32, [P32, P32]),
             "bsp_set_fanout": (ctypes.c_int, [vp, u32, u64, P32, P32, u64]),
             "bsp_set_graph": (ctypes.c_int, [vp, P64, P32]),
+            "bsp_set_graph_rmat": (ctypes.c_int, [vp, P64, u32, u32, u32, u32, u64, u32]),
             "bsp_stage": (ctypes.c_int, [vp, P32, P32, P32, u64]),
             "bsp_run": (ctypes.c_int, [vp, u32, ctypes.POINTER(Stats)]),
             "bsp_read_state": (None, [vp, u64, u64, P64, P8]),
@@ -207,6 +208,14 @@ class BspOracle(_Base):
         rp = np.ascontiguousarray(np.asarray(row_ptr, dtype=np.uint64))
         cl = _u32(col) if len(col) else np.zeros(1, np.uint32)
         self.lib.bsp_set_graph(self.h, _p(rp, ctypes.c_uint64), _p(cl, ctypes.c_uint32))
+
+    def set_graph_rmat(self, row_ptr, bits, ta, tb, tc, seed):
+        """agx_set_graph_rmat's destinations generated on the host (bsp_ref.c bsp_set_graph_rmat; the
+        same formula as workloads.rmat_cols, threaded for 10^8-actor graphs)."""
+        rp = np.ascontiguousarray(np.asarray(row_ptr, dtype=np.uint64))
+        threads = min(len(os.sched_getaffinity(0)), 16)
+        if self.lib.bsp_set_graph_rmat(self.h, _p(rp, ctypes.c_uint64), bits, ta, tb, tc, seed, threads):
+            raise MemoryError("bsp_set_graph_rmat: allocation failed")
 
     def tell(self, dst, payload, src=None):
         dst = _u32(dst)

@@ -419,3 +419,50 @@ def test_delta_crdt_placeholders_and_log_capacity():
     w.apply_to(o)
     with pytest.raises(OverflowError):
         o.run()
+
+
+# ------------------------------------------------------------------ the oracle's own execution
+@pytest.mark.parametrize("case", ["mixed", "zipf", "plaw", "orset", "orset_delta", "mbox", "sharded"])
+def test_oracle_threads_identical(monkeypatch, case):
+    """bsp_ref.c applies the actors with mail on host threads, in contiguous runs of the canonical
+    order whose outputs are concatenated in order: every count, state word, alive flag and outbox
+    envelope is the same for 1 thread and for 7 (and the dense / sparse inbox sorts agree)."""
+    w = {
+        "mixed": lambda: wl.mixed(20000, seed=3, throughput=2, capacity=3),
+        "zipf": lambda: wl.zipf_fanout(100_000, k=4, ttl=3, root_every=16, capacity=50),
+        "plaw": lambda: wl.power_law_forward(100_000, ttl=8, capacity=64, device_graph=True),
+        "orset": lambda: wl.crdt_gossip(3_000, Kind.ORSET, rounds=4),
+        "orset_delta": lambda: wl.crdt_delta(8 * 300, Kind.ORSET, rounds=6, write=True, gossip_rounds=2),
+        "mbox": lambda: wl.mailbox_mix(8192, seed=2, throughput=3, capacity=4),
+        "sharded": lambda: wl.zipf_fanout(50_000, k=2, ttl=3, root_every=8, capacity=20),
+    }[case]
+    ranks = 5 if case == "sharded" else 1
+    res = []
+    for threads in ("1", "7"):
+        monkeypatch.setenv("BSP_THREADS", threads)
+        x = w()
+        o = BspOracle(n_ranks=ranks, **x.engine_kwargs())
+        x.apply_to(o)
+        sts = [o.run(2), o.run(3), o.run()]
+        ws, al = o.read_state()
+        ob = o.take_outbound() if x.outbound else ()
+        o.close()
+        res.append((sts, ws, al, ob))
+    (s1, w1, a1, o1), (s7, w7, a7, o7) = res
+    assert s1 == s7 and np.array_equal(w1, w7) and np.array_equal(a1, a7)
+    assert all(np.array_equal(p, q) for p, q in zip(o1, o7))
+    assert s1[-1]["delivered"] > 0
+
+
+def test_oracle_rmat_generator_matches_workloads():
+    """bsp_set_graph_rmat (the device generator's formula, restated in C and threaded) gives the
+    same graph as workloads.rmat_cols: the power-law run is identical either way."""
+    runs = []
+    for dev in (True, False):
+        x = wl.power_law_forward(60_000, ttl=6, capacity=16, device_graph=dev)
+        o = BspOracle(**x.engine_kwargs())
+        x.apply_to(o)
+        st = o.run()
+        runs.append((st, o.read_state()[0]))
+        o.close()
+    assert runs[0][0] == runs[1][0] and np.array_equal(runs[0][1], runs[1][1])
