@@ -109,7 +109,8 @@ struct agx_engine {
   agx_cfg cfg{};
   hipStream_t stream = nullptr;
   uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0;
-  uint32_t max_supers = 1, dstride = 4, dsuper = kSuper;  // dense passes: super-tiles, table row stride, tile size
+  uint32_t max_supers = 1, dstride = 4, dsub = kSub;  // dense passes: super-tiles (at most), table row stride, max tiles
+                                                      // per super-tile (the size itself is chosen per pass: pass_super)
   uint32_t T = 1, C = 0, W = 1, kmax = 1, R = 1, rank = 0, num_shards = 1000, key_bits = 1;
   uint32_t Traw = 1;  // dispatcher throughput (>= 1); T = min(Traw, C) for the default mailbox class
   // mailbox classes (agx_set_mailbox_class): capacity per class, class 0 = cfg.capacity
@@ -432,7 +433,7 @@ agx_status launch_dense_pass(agx_engine* e, const DevMsgs& in, const DevMsgs& ou
   sa.tot = e->d_tot;
   sa.bstart = e->d_bstart;
   sa.stride = e->dstride;
-  sa.super = e->dsuper;
+  sa.maxsub = e->dsub;
   sa.shift = shift;
   sa.bits = bits;
   // (multi-rank: the device-resident replays' stop word -- [0] != 0 makes the pass return, like identity)
@@ -1614,12 +1615,13 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   if (e->cap >= (1ull << 32) - kTile) { delete e; return set_err(AGX_EINVAL, "msg_capacity too large"); }
   e->cap_emit = e->cap * e->kmax;  // bucket b's tells live at [lo*kmax, (lo+cnt)*kmax)
   if (e->cap_emit >= (1ull << 32)) { delete e; return set_err(AGX_EINVAL, "msg_capacity * max_emit must be < 2^32"); }
-  {  // super-tile size of the dense sort passes: about 1024+ workgroups when the buffers allow it
+  {  // largest super-tile of the dense sort passes: about 1024+ workgroups at full capacity; each pass
+     // picks its own size from its input (pass_super), down to one tile, so the histogram table is
+     // sized for one-tile super-tiles
     const uint64_t mx = std::max(e->cap, e->cap_emit);
-    const uint64_t sub = std::min<uint64_t>(kSub, std::max<uint64_t>(1, mx / ((uint64_t)kTile * 1024)));
-    e->dsuper = (uint32_t)(kTile * sub);
+    e->dsub = (uint32_t)std::min<uint64_t>(kSub, std::max<uint64_t>(1, mx / ((uint64_t)kTile * 1024)));
   }
-  e->max_supers = (uint32_t)((std::max(e->cap, e->cap_emit) + e->dsuper - 1) / e->dsuper + 1);
+  e->max_supers = (uint32_t)((std::max(e->cap, e->cap_emit) + kTile - 1) / kTile + 1);
   e->dstride = (e->max_supers + 3) & ~3u;
   // buckets of 2^bb actors; LSD passes over key bits [bb, key_bits), <= kRadixBits each
   e->nb = (uint32_t)((nl + (1ull << e->bb) - 1) >> e->bb);

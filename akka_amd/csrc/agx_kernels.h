@@ -298,29 +298,45 @@ __device__ __forceinline__ uint32_t digit_bases(const uint32_t* tot, uint32_t nd
 }
 
 // Exclusive prefix, in place, of one digit row of a histogram table (len entries,
-// row 16-byte aligned): 4 consecutive entries per thread.  Returns the row total.
+// row 16-byte aligned): 16 consecutive entries per thread per round, their four uint4 loads in
+// flight together before the block scan (a row of up to 4096 entries -- the first pass's units at
+// 10^7 actors -- is one round trip, not four).  Returns the row total.
 __device__ __forceinline__ uint32_t scan_row(uint32_t* row, uint32_t len, uint32_t* scratch) {
+  constexpr uint32_t kPer = 16;
   const int tid = threadIdx.x;
   uint32_t run = 0;
-  for (uint32_t base = 0; base < len; base += 4 * kThreads) {
-    const uint32_t i0 = base + 4 * tid;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (i0 + 3 < len) {
-      v = reinterpret_cast<const uint4*>(row)[i0 / 4];
-    } else if (i0 < len) {
-      v.x = row[i0];
-      if (i0 + 1 < len) v.y = row[i0 + 1];
-      if (i0 + 2 < len) v.z = row[i0 + 2];
+  for (uint32_t base = 0; base < len; base += kPer * kThreads) {
+    const uint32_t i0 = base + kPer * tid;
+    uint4 v[kPer / 4];
+#pragma unroll
+    for (uint32_t q = 0; q < kPer / 4; ++q) {
+      const uint32_t j = i0 + 4 * q;
+      v[q] = make_uint4(0, 0, 0, 0);
+      if (j + 3 < len) {
+        v[q] = reinterpret_cast<const uint4*>(row)[j / 4];
+      } else if (j < len) {
+        v[q].x = row[j];
+        if (j + 1 < len) v[q].y = row[j + 1];
+        if (j + 2 < len) v[q].z = row[j + 2];
+      }
     }
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kPer / 4; ++q) sum += v[q].x + v[q].y + v[q].z + v[q].w;
     uint32_t t;
-    const uint32_t ex = run + block_excl_sum<kThreads>(v.x + v.y + v.z + v.w, scratch, &t);
-    const uint4 o = make_uint4(ex, ex + v.x, ex + v.x + v.y, ex + v.x + v.y + v.z);
-    if (i0 + 3 < len) {
-      reinterpret_cast<uint4*>(row)[i0 / 4] = o;
-    } else if (i0 < len) {
-      row[i0] = o.x;
-      if (i0 + 1 < len) row[i0 + 1] = o.y;
-      if (i0 + 2 < len) row[i0 + 2] = o.z;
+    uint32_t ex = run + block_excl_sum<kThreads>(sum, scratch, &t);
+#pragma unroll
+    for (uint32_t q = 0; q < kPer / 4; ++q) {
+      const uint32_t j = i0 + 4 * q;
+      const uint4 o = make_uint4(ex, ex + v[q].x, ex + v[q].x + v[q].y, ex + v[q].x + v[q].y + v[q].z);
+      ex += v[q].x + v[q].y + v[q].z + v[q].w;
+      if (j + 3 < len) {
+        reinterpret_cast<uint4*>(row)[j / 4] = o;
+      } else if (j < len) {
+        row[j] = o.x;
+        if (j + 1 < len) row[j + 1] = o.y;
+        if (j + 2 < len) row[j + 2] = o.z;
+      }
     }
     run += t;
   }
@@ -712,9 +728,18 @@ struct SortArgs {
   uint32_t* bstart;  // out (block 0 of the downsweep): exclusive scan of digit totals
   uint32_t stride;
   uint32_t shift, bits;
-  uint32_t super;  // envelopes per super-tile (kTile * 1..kSub): small inputs get more workgroups
+  uint32_t maxsub;  // largest super-tile, in tiles (1..kSub): sized from the message capacity
   const uint32_t* ident;  // single-rank multi-pass: [0] != 0 = identity grouping this superstep (no pass runs)
 };
+
+// Envelopes per super-tile of THIS pass, from its input size n (on the device, so a graph-captured
+// pass adapts to each superstep's mail): about 1024 super-tiles, 1..maxsub tiles each.  A sparse
+// superstep (C3: ~4e5 messages against a capacity of 4e7) gets one-tile super-tiles on ~200
+// workgroups instead of ~25 workgroups walking 8 tiles each.
+__device__ __forceinline__ uint32_t pass_super(const SortArgs& a, uint32_t n) {
+  const uint32_t sub = n / ((uint32_t)kTile * 1024u);
+  return (uint32_t)kTile * (sub < 1u ? 1u : sub > a.maxsub ? a.maxsub : sub);
+}
 
 // Digit counts of four keys into a wave's LDS histogram.  Sorted-by-lower-bits input
 // (the ring after the first pass) gives whole waves of one digit: those cost one LDS
@@ -740,13 +765,13 @@ __device__ __forceinline__ void count4(uint32_t* h, const uint4& v, uint32_t shi
 static __global__ void __launch_bounds__(kThreads) k_sort_upsweep(SortArgs a) {
   if (a.ident && a.ident[0]) return;  // identity grouping: the mail is already in key order
   __shared__ uint32_t h[kWaves][kRadix];
-  const uint32_t n = *a.d_n, nt = div_up(n, a.super);
+  const uint32_t n = *a.d_n, super = pass_super(a, n), nt = div_up(n, super);
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t mask = (1u << a.bits) - 1u, nd = 1u << a.bits;
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     for (int i = tid; i < kWaves * kRadix; i += kThreads) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t b0 = t * a.super, b1 = min(n, b0 + a.super);
+    const uint32_t b0 = t * super, b1 = min(n, b0 + super);
     const uint32_t nfull = (b1 - b0) / (4 * kThreads);  // full rounds of one uint4 per thread
     const uint4* k4 = reinterpret_cast<const uint4*>(a.in.key + b0);
     uint32_t j = 0;
@@ -777,7 +802,8 @@ static __global__ void __launch_bounds__(kThreads) k_sort_rowscan(SortArgs a) {
   __shared__ uint32_t scratch[kWaves + 1];
   const uint32_t d = blockIdx.x;
   if (d >= (1u << a.bits)) return;
-  const uint32_t t = scan_row(a.hist + (size_t)d * a.stride, div_up(*a.d_n, a.super), scratch);
+  const uint32_t n = *a.d_n;
+  const uint32_t t = scan_row(a.hist + (size_t)d * a.stride, div_up(n, pass_super(a, n)), scratch);
   if (threadIdx.x == 0) a.tot[d] = t;
 }
 
@@ -789,7 +815,8 @@ static __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) 
   __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
   const SplitLds S{&whist[0][0], s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
   const int tid = threadIdx.x;
-  const uint32_t n = *a.d_n, nt = div_up(n, a.super);
+  const uint32_t n = *a.d_n, super = pass_super(a, n), nt = div_up(n, super);
+  if (blockIdx.x >= nt && blockIdx.x != 0) return;  // (no super-tile: the grid is sized for the capacity)
   const uint32_t nd = 1u << a.bits;
   const uint32_t total = digit_bases(a.tot, nd, s_dbase, scratch);
   if (blockIdx.x == 0) {
@@ -799,7 +826,7 @@ static __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) 
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     for (uint32_t d = tid; d < nd; d += kThreads) s_base[d] = s_dbase[d] + a.hist[(size_t)d * a.stride + t];
     __syncthreads();
-    const uint32_t b0 = t * a.super, b1 = min(n, b0 + a.super);
+    const uint32_t b0 = t * super, b1 = min(n, b0 + super);
     for (uint32_t base = b0; base < b1; base += kTile)
       split_tile<kThreads>(a.in, base, min((uint32_t)kTile, b1 - base), a.out, a.shift, a.bits, S);
   }

@@ -125,21 +125,31 @@ def cpu_baseline(hops: int) -> dict:
     sb = b.run()
     bsp_s = time.perf_counter() - t0
     b.close()
+    # C1 as the JMH config, C2 / C3 / C4 at the GPU run's full populations (C4 ORSet with
+    # fewer gossip rounds: each full-state merge moves 2 KB rows, ~1 us per merge on a host core), C5 at
+    # 10M actors (host RAM / run time; the GPU config is 100M)
     samples = {
         "C1_ping_pong": ("ForkJoinActorBenchmark.pingPong: 1000 pairs, throughput 50, 100 in flight per pair, "
                          "1,000,000 messages per pair (the JMH run uses 2,000,000)",
                          lambda: wl.ping_pong(1000, messages_per_pair=1_000_000, throughput=50)),
-        "C3_zipf_tree": ("1M actors, Zipf(1.1) FANOUT k=4 ttl=3, 1/64 roots, throughput 5, to quiescence",
-                         lambda: wl.zipf_fanout(1_000_000, k=4, ttl=3, root_every=64, throughput=5)),
-        "C4_gcounter_gossip": ("200k GCounter replicas, 8 rounds of full-state gossip to 2 peers",
-                               lambda: wl.crdt_gossip(200_000, Kind.GCOUNTER, rounds=8)),
-        "C4_orset_gossip": ("50k ORSet replicas, 4 rounds of full-state gossip to 2 peers",
-                            lambda: wl.crdt_gossip(50_000, Kind.ORSET, rounds=4)),
-        "C4_orset_delta_gossip": ("200k delta-CRDT ORSet replicas (keys of 8), 8 DeltaPropagationTicks with a "
-                                  "writer update each",
-                                  lambda: wl.crdt_delta(200_000, Kind.ORSET, rounds=8, write=True)),
-        "C5_power_law_bounded": ("4M actors, power-law R-MAT graph, FORWARD_RR ttl 15, BoundedMailbox(64)",
-                                 lambda: wl.power_law_forward(4_000_000, ttl=15, capacity=64, throughput=5)),
+        "C3_zipf_fanout": ("10M actors (full size), Zipf(1.1) FANOUT k=1, every actor one message with ttl 15, "
+                           "BoundedMailbox(1000), throughput 5, to quiescence",
+                           lambda: wl.zipf_fanout(10_000_000, k=1, ttl=15, root_every=1, capacity=1000)),
+        "C3_zipf_tree": ("10M actors (full size), Zipf(1.1) FANOUT k=4 ttl=3, 1/64 roots, BoundedMailbox(1000), "
+                         "throughput 5, to quiescence",
+                         lambda: wl.zipf_fanout(10_000_000, k=4, ttl=3, root_every=64, capacity=1000)),
+        "C4_gcounter_gossip": ("1M GCounter replicas (full size), 40 rounds of full-state gossip to 2 peers "
+                               "(the GPU config)",
+                               lambda: wl.crdt_gossip(1_000_000, Kind.GCOUNTER, rounds=40)),
+        "C4_orset_gossip": ("1M ORSet replicas (full size), 4 rounds of full-state gossip to 2 peers (the GPU "
+                            "config runs 20)",
+                            lambda: wl.crdt_gossip(1_000_000, Kind.ORSET, rounds=4)),
+        "C4_orset_delta_gossip": ("1M delta-CRDT ORSet replicas (full size, keys of 8), 8 DeltaPropagationTicks "
+                                  "with a writer update each (the GPU config runs 40)",
+                                  lambda: wl.crdt_delta(1_000_000, Kind.ORSET, rounds=8, write=True)),
+        "C5_power_law_bounded": ("10M actors (the GPU config: 100M), power-law R-MAT graph, FORWARD_RR ttl 15, "
+                                 "BoundedMailbox(64), to quiescence",
+                                 lambda: wl.power_law_forward(10_000_000, ttl=15, capacity=64, throughput=5)),
     }
     configs = {}
     for name, (desc, make) in samples.items():

@@ -1,0 +1,40 @@
+#!/bin/bash
+# Round-4 GPU check: the full-size parity tests, the rest of the -m gpu suite, the driver's bench
+# command.  Each GPU step has its own time limit; the first failure ends the script.
+#   STEPS="full gpu ab bench" (default: full gpu bench); ab: CFGS (bench configs) for every library in
+#   LIBS (default: akka_amd/lib/var/base.so and the tree's build), AB_REPS times; prof: rocprofv3
+#   kernel trace + stats of PROF_CFGS
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r04}
+STEPS=${STEPS:-"full gpu bench"}
+for s in $STEPS; do
+  case $s in
+    full)
+      timeout -k 10 1000 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 900 --timeout-method thread \
+        > gpurun_out/${TAG}_full.log 2>&1 || { echo "fullsize failed"; tail -60 gpurun_out/${TAG}_full.log; exit 1; }
+      tail -3 gpurun_out/${TAG}_full.log ;;
+    gpu)
+      timeout -k 10 900 python -u -m pytest tests -x -q -m "gpu and not fullsize" --timeout 280 --timeout-method thread \
+        > gpurun_out/${TAG}_gpu.log 2>&1 || { echo "gpu suite failed"; tail -60 gpurun_out/${TAG}_gpu.log; exit 1; }
+      tail -3 gpurun_out/${TAG}_gpu.log ;;
+    ab)
+      for c in ${CFGS:-C3_zipf_fanout C3_zipf_tree C5_power_law_bounded}; do
+        AB_REPS=${AB_REPS:-2} bash tools/ab_cfg.sh $c ${LIBS:-akka_amd/lib/var/base.so akka_amd/lib/libakka_gpu.so} \
+          >> gpurun_out/${TAG}_ab.log 2>&1 || { echo "ab failed"; tail -30 gpurun_out/${TAG}_ab.log; exit 1; }
+      done
+      cat gpurun_out/${TAG}_ab.log ;;
+    prof)  # rocprofv3 kernel trace + stats of single bench configs (PROF_CFGS), the tree's build
+      for c in ${PROF_CFGS:-C5_power_law_bounded C3_zipf_fanout C3_zipf_tree}; do
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_$c -o run \
+          -- python3 tools/cfg_one.py $c > gpurun_out/${TAG}_prof_$c.log 2>&1 || { echo "prof $c failed"; tail -30 gpurun_out/${TAG}_prof_$c.log; exit 1; }
+        echo "prof $c ok"
+      done ;;
+    bench)
+      timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_bench.json \
+        2> gpurun_out/${TAG}_bench.err || { echo "bench failed"; tail -40 gpurun_out/${TAG}_bench.err; exit 1; }
+      python -c "import json; d=json.loads(open('gpurun_out/${TAG}_bench.json').read().strip().splitlines()[-1]); print(json.dumps(d['summary']))" ;;
+  esac
+done
+exit 0
