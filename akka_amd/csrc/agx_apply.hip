@@ -23,6 +23,14 @@ hipError_t agx_launch_apply_g4(uint32_t, uint32_t, bool, dim3, hipStream_t, cons
 hipError_t agx_launch_apply_g5(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_apply_g6(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_apply_g7(uint32_t, uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_tiny_g0(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_tiny_g1(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_tiny_g2(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_tiny_g3(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_tiny_g4(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_tiny_g5(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_tiny_g6(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_tiny_g7(uint32_t, dim3, hipStream_t, const BucketArgs&);
 static_assert(kVGroups == 8, "one declaration per group");
 
 namespace {
@@ -56,7 +64,26 @@ hipError_t group_dispatch(uint32_t vid, uint32_t mode, bool skew, dim3 g, hipStr
   }
 }
 
+// k_tiny_apply of the plain / compiled variants of this group
+template <uint32_t V>
+hipError_t tiny_dispatch(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  if constexpr (V >= V_N) {
+    return hipErrorInvalidValue;
+  } else {
+    if constexpr (kVariantGroup[V] == AGX_VGROUP && !kVariants[V].wide)
+      if (vid == V) {
+        hipLaunchKernelGGL((k_tiny_apply<kVariants[V].km>), g, dim3(kTinyThreads), 0, s, ba);
+        return hipGetLastError();
+      }
+    return tiny_dispatch<V + 1>(vid, g, s, ba);
+  }
+}
+
 }  // namespace
+
+hipError_t AGX_CAT(agx_launch_tiny_g, AGX_VGROUP)(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  return tiny_dispatch<0>(vid, g, s, ba);
+}
 
 hipError_t AGX_GROUP_FN(uint32_t vid, uint32_t mode, bool skew, dim3 g, hipStream_t s, const BucketArgs& ba) {
   return group_dispatch<0>(vid, mode, skew, g, s, ba);
@@ -74,6 +101,19 @@ hipError_t agx_launch_apply(uint32_t vid, uint32_t mode, bool skew, dim3 g, hipS
     case 5: return agx_launch_apply_g5(vid, mode, skew, g, s, ba);
     case 6: return agx_launch_apply_g6(vid, mode, skew, g, s, ba);
     default: return agx_launch_apply_g7(vid, mode, skew, g, s, ba);
+  }
+}
+hipError_t agx_launch_tiny(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  if (vid >= V_N || kVariants[vid].wide) return hipErrorInvalidValue;
+  switch (kVariantGroup[vid]) {
+    case 0: return agx_launch_tiny_g0(vid, g, s, ba);
+    case 1: return agx_launch_tiny_g1(vid, g, s, ba);
+    case 2: return agx_launch_tiny_g2(vid, g, s, ba);
+    case 3: return agx_launch_tiny_g3(vid, g, s, ba);
+    case 4: return agx_launch_tiny_g4(vid, g, s, ba);
+    case 5: return agx_launch_tiny_g5(vid, g, s, ba);
+    case 6: return agx_launch_tiny_g6(vid, g, s, ba);
+    default: return agx_launch_tiny_g7(vid, g, s, ba);
   }
 }
 #endif

@@ -87,10 +87,10 @@ struct DevMsgs {
 };
 
 enum KClass { K_CROWSCAN, K_CDOWN, K_UPSWEEP, K_ROWSCAN, K_DOWNSWEEP, K_APPLY, K_EXCHANGE, K_MCOMPACT, K_SKEW, K_TICK,
-              K_BOUNDS, K_SKEWPRE, K_NCLASS };
+              K_BOUNDS, K_SKEWPRE, K_TINY, K_NCLASS };
 const char* kClassNames[K_NCLASS] = {"chunk_rowscan", "chunk_downsweep", "sort_upsweep", "sort_rowscan",
                                      "sort_downsweep", "bucket_apply", "exchange", "mcompact", "bucket_apply_skew",
-                                     "fused_tick", "bucket_bounds", "skew_prepass"};
+                                     "fused_tick", "bucket_bounds", "skew_prepass", "bucket_apply_tiny"};
 
 constexpr uint32_t kGraphSizes[5] = {1, 2, 4, 8, 16};  // superstep replays (agx_engine::gx)
 constexpr uint32_t kRowAlign = 32;  // CRDT row pitch (u32) of rows wider than one 128-B line
@@ -203,7 +203,12 @@ struct agx_engine {
   uint32_t cur_slot = 0;       // superstep index within the replay being captured / launched
   uint64_t host_steps = 0;     // fused: supersteps with mail, counted on the host from h_cntb
   uint32_t par = 0;  // fused: parity of the next superstep (host-tracked; graphs are captured per parity)
-  uint32_t *d_skew_list = nullptr, *d_skew_n = nullptr;  // buckets for the general-path launch
+  uint32_t *d_skew_list = nullptr, *d_skew_n = nullptr;  // buckets for the general-path launch ([2]: block-list count)
+  // single-rank multi-pass, plain behaviours: k_tiny_apply drains the buckets of <= tiny_max messages
+  // one wave each and lists the others here for the block launch (AGX_TINY_LAUNCH=0: the fast launch's
+  // own wave check instead)
+  uint32_t* d_blist = nullptr;
+  bool tiny_launch = true;
   // multi-pass, plain behaviours: skewed buckets split over workgroups (k_skew_*, agx_kernels.h)
   uint32_t *d_sk_rec = nullptr, *d_sk_act = nullptr, *d_sk_pc = nullptr, *d_sk_meta = nullptr;
   uint32_t sk_budget = 0, sk_rows = 0;
@@ -684,6 +689,14 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     }
     const uint32_t mode = e->fused ? M_FUSED : e->R > 1 ? M_OWNER : M_BYPASS;
     const dim3 g(grid_for(e->nb, e->apply_grid));
+    const bool tl = mode == M_BYPASS && !kVariants[vid].wide && e->tiny_launch && e->tiny_max && !e->skew_only;
+    if (tl) {  // wave-per-bucket launch first; the block launch then walks the buckets it listed
+      ba.blist = e->d_blist;
+      ba.blist_n = e->d_skew_n + 2;
+      Scope s(e, K_TINY);
+      const uint32_t gt = grid_for((e->nb + kTinyWaves - 1) / kTinyWaves, kMaxApplyGrid);
+      HIP_TRY(agx_launch_tiny(vid, dim3(gt), e->stream, ba));
+    }
     // skew list (grid-stride); ring buckets take the skew launch every superstep: a wider grid then
     const dim3 gs(grid_for(e->nb, std::min(e->apply_grid, e->ring_live ? std::max(e->skew_grid, 2048u) : e->skew_grid)));
     if (!e->skew_only) {
@@ -1582,6 +1595,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->num_shards = cfg->num_shards ? cfg->num_shards : 1000;
   e->bb = cfg->bucket_actors ? ceil_log2(cfg->bucket_actors) : (uint32_t)kBucketBits;
   if (const char* s = getenv("AGX_TINY")) e->tiny_max = std::min<uint32_t>(kTinyMax, (uint32_t)std::max(0, atoi(s)));
+  if (const char* s = getenv("AGX_TINY_LAUNCH")) e->tiny_launch = atoi(s) != 0;
   if (const char* s = getenv("AGX_BUCKET_ACTORS")) {  // diagnostic: override the bucket width (power of two)
     const uint32_t ba = (uint32_t)atoi(s);
     if (ba >= (1u << kMinBucketBits) && ba <= (uint32_t)kBucket && !(ba & (ba - 1))) e->bb = ceil_log2(ba);
@@ -1796,8 +1810,9 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
                    ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
   }
   CREATE_TRY(dalloc(&e->d_skew_list, e->nb));
-  CREATE_TRY(dalloc(&e->d_skew_n, 2));
-  CREATE_TRY(hipMemset(e->d_skew_n, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  CREATE_TRY(dalloc(&e->d_skew_n, 4));
+  CREATE_TRY(hipMemset(e->d_skew_n, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+  if (!e->fused && e->R == 1) CREATE_TRY(dalloc(&e->d_blist, e->nb));
   CREATE_TRY(dalloc(&e->d_chunk_off, e->nchunks));
   CREATE_TRY(dalloc(&e->d_chunk_cnt, e->nchunks));
   CREATE_TRY(hipMemset(e->d_chunk_off, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
@@ -1865,7 +1880,7 @@ agx_status agx_destroy(agx_engine* e) {
   if (e->h_cntb) hipHostFree(e->h_cntb); hipFree(e->d_parv);
   hipFree(e->d_abort); hipFree(e->d_rctr);
   if (e->h_abort) hipHostFree(e->h_abort);
-  hipFree(e->d_skew_list); hipFree(e->d_skew_n);
+  hipFree(e->d_skew_list); hipFree(e->d_skew_n); hipFree(e->d_blist);
   hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);
   hipFree(e->d_ring_of); hipFree(e->d_ring_state); hipFree(e->d_ring_src); hipFree(e->d_ring_pay);
   hipFree(e->d_ring_next); hipFree(e->d_ring_free); hipFree(e->d_ring_total);

@@ -575,7 +575,10 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs
   if (blockIdx.x == 0) {
     begin_step(a.step, a.heap_top);
     commit_stops(a.alive, a.stopq, a.nstop);
-    if (threadIdx.x == 0) *a.skew_n = 0u;
+    if (threadIdx.x == 0) {
+      a.skew_n[0] = 0u;
+      if (a.bypass) a.skew_n[2] = 0u;  // (the block list of k_tiny_apply, BucketArgs::blist_n)
+    }
   }
   const uint32_t d = blockIdx.x;
   const uint32_t nsl = (a.ch.nb + kBlSlice - 1) / kBlSlice;
@@ -1024,6 +1027,10 @@ struct BucketArgs {
   // passes the mark on, and the host runs the deferred skew launch and resumes (run_single)
   uint32_t* abort;
   uint32_t tiny_max;       // bypass: inboxes of at most this many messages take the wave path (0 = off)
+  // bypass, plain behaviours: the buckets k_tiny_apply left to the block path (non-null: the fast
+  // launch walks this list instead of every bucket, with no wave check of its own)
+  uint32_t* blist;
+  uint32_t* blist_n;
   // bypass, plain behaviours: skewed buckets pre-partitioned by k_skew_* (see there); [i] = skew index
   const uint32_t* sk_rec;  // [i][kSkRec] bucket, bounds, parts, drained and queued totals
   const uint32_t* sk_act;  // [i][3][kBucket] per actor: admitted, drained-segment start, backlog start
@@ -2284,6 +2291,46 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
   }
 }
 
+// Wave-per-bucket launch (single-rank multi-pass, plain and compiled behaviours): every bucket whose
+// inbox -- backlog in place plus sorted new mail -- holds at most tiny_max messages is drained by one
+// wave (tiny_bucket); the others are listed for the block launch that follows (k_bucket_apply over
+// a.blist).  A separate kernel so that its residency is set by the wave path's own registers and
+// 10 KB of LDS, not by the block path's 80 KB: all of a sparse superstep's buckets (C3: 4883, most
+// with a few dozen messages) are in flight at once instead of one or two waves of each of 512
+// resident 8-wave blocks (the rest of such a block idled while its wave drained).
+constexpr int kTinyThreads = 256;
+constexpr int kTinyWaves = kTinyThreads / kWave;
+template <uint32_t KM>
+static __global__ void __launch_bounds__(kTinyThreads) k_tiny_apply(BucketArgs a) {
+  __shared__ TinyLds T[kTinyWaves];
+  const uint32_t w = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t wpar = *a.pstep & 1u, rpar = wpar ^ 1u;
+  const InView iv = in_view(a);
+  const uint32_t nw = gridDim.x * kTinyWaves;
+  for (uint32_t bw = blockIdx.x * kTinyWaves + w; bw < a.nb; bw += nw) {
+    uint32_t bs = 0, lo_w = 0, hi_w = 0, blc = 0, blo = 0;
+    if (lane == 0) {  // (k_bucket_apply's bypass bounds)
+      bs = a.bstart[bw];
+      const uint32_t be = a.bstart[bw + 1], bp = a.blpre[bw] + a.bl_sbase[bw / kBlSlice];
+      blc = a.chunk_cnt[bw];
+      blo = a.chunk_off[bw];
+      lo_w = bs + bp;
+      hi_w = lo_w + blc + (be - bs);
+    }
+    bs = (uint32_t)__builtin_amdgcn_readlane((int)bs, 0);
+    lo_w = (uint32_t)__builtin_amdgcn_readlane((int)lo_w, 0);
+    hi_w = (uint32_t)__builtin_amdgcn_readlane((int)hi_w, 0);
+    blc = (uint32_t)__builtin_amdgcn_readlane((int)blc, 0);
+    blo = (uint32_t)__builtin_amdgcn_readlane((int)blo, 0);
+    const bool tiny = hi_w - lo_w <= a.tiny_max && (uint64_t)hi_w <= a.cap &&  // (over capacity: the block path reports it)
+                      !(a.ring_of && a.ring_of[bw]);                         // (a ring bucket: skew path)
+    if (tiny)
+      tiny_bucket<KM>(a, iv, T[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
+    else if (lane == 0)
+      a.blist[atomicAdd(a.blist_n, 1u)] = bw;
+  }
+}
+
 // kSkew = false: every bucket whose inbox fits one LDS tile (<= kBucket messages); larger
 // inboxes are appended to the skew list.  kSkew = true (launched right after): the listed
 // buckets, general path — separate instantiation, so its register pressure never reaches
@@ -2822,7 +2869,10 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
 
   // single-rank multi-pass, plain behaviours: groups of kBWaves buckets; each wave first drains its
   // bucket if it is tiny (wave path), then the block drains the group's other buckets
-  constexpr bool kTiny = kBypass && !kSkew && !kWide;
+  constexpr bool kTinyV = kBypass && !kSkew && !kWide;
+  // (k_tiny_apply ran first and listed the other buckets: no wave check here)
+  const bool listed = kTinyV && a.blist != nullptr;
+  const bool kTiny = kTinyV && !listed;
   __shared__ uint32_t s_tiny[kBWaves];
   // (kTiny) the bounds the wave check read for bucket w: [bs, lo, hi, blc, blo, valid] -- the block
   // path takes them from here instead of a second round trip to global memory
@@ -2830,11 +2880,11 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
   // (a group is kBWaves consecutive iterations of the block's grid-stride sequence, so the
   // bucket -> block assignment, and with it the load balance, is the block path's own)
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};  // this thread's counters over the block's buckets
-  const uint32_t nwork = kSkew ? *skew_n : a.nb;
+  const uint32_t nwork = kSkew ? *skew_n : listed ? *a.blist_n : a.nb;
   const uint32_t istride = kTiny ? kBWaves * gridDim.x : gridDim.x;
   for (uint32_t it = blockIdx.x; it < nwork; it += istride) {
-    uint32_t bfirst = kSkew ? a.skew_list[it] : it, nblk = 1, todo = 1u, bstep = 0;
-    if constexpr (kTiny) {
+    uint32_t bfirst = kSkew ? a.skew_list[it] : listed ? a.blist[it] : it, nblk = 1, todo = 1u, bstep = 0;
+    if (kTiny) {
       nblk = kBWaves;
       bstep = gridDim.x;
       const uint32_t bw = bfirst + w * bstep;
@@ -2863,8 +2913,9 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
           s_tb[w][3] = blc;
           s_tb[w][4] = blo;
         }
-        if (tiny)
-          tiny_bucket<KM>(a, iv, reinterpret_cast<TinyLds*>(U)[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
+        if constexpr (kTinyV)
+          if (tiny)
+            tiny_bucket<KM>(a, iv, reinterpret_cast<TinyLds*>(U)[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
       }
       if (lane == 0) {
         s_tiny[w] = tiny || bw >= a.nb;
@@ -3105,7 +3156,6 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
       __syncthreads();  // (fused) the segment list in s_pay is read before the items overwrite it
       // in-order copy + sortedness check: local topologies (rings, stencils) arrive already in
       // actor order, and then the wave multisplit ranking is unnecessary (same result)
-      for (uint32_t i = tid; i < kBucket + 4; i += kBThreads) s_seg[i] = 0;
 #pragma unroll
       for (int r = 0; r < kBIpt; ++r) {
         const uint32_t q = wbase + r * kWave + lane;
@@ -3125,14 +3175,22 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
       const bool presorted = __syncthreads_and(ok) != 0;
       uint32_t tl[kBAct];
       if (presorted) {
+        // segment starts straight from the sorted keys in LDS: actor la's run starts at the number
+        // of items with a smaller actor index (a branchless lower bound, the four actors of a
+        // thread stepping together) -- no per-item LDS atomics, no block scan, one barrier
+        uint32_t lb[kBAct] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int r = 0; r < kBIpt; ++r) {
-          const uint32_t q = wbase + r * kWave + lane;
-          if (q < cnt) atomicAdd(&s_seg[k[r] & amask], 1u);
+        for (uint32_t step = (uint32_t)kBucket; step; step >>= 1) {
+#pragma unroll
+          for (int j = 0; j < kBAct; ++j) {
+            const uint32_t p = lb[j] + step, la = tid * kBAct + j;
+            if (p <= cnt && (s_key[p - 1] & amask) < la) lb[j] = p;
+          }
         }
-        __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kBAct; ++j) tl[j] = s_seg[tid * kBAct + j];
+        for (int j = 0; j < kBAct; ++j) s_seg[tid * kBAct + j] = lb[j];
+        if (tid == 0) s_seg[kBucket] = cnt;
+        __syncthreads();
       } else {
         for (uint32_t i = tid; i < kBWaves * kBucket / 2; i += kBThreads) reinterpret_cast<uint32_t*>(whist)[i] = 0;
         __syncthreads();
@@ -3156,7 +3214,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
           tl[j] = run;
         }
       }
-      {  // segment starts: exclusive scan of per-actor counts (blocked)
+      if (!presorted) {  // segment starts: exclusive scan of per-actor counts (blocked)
         uint32_t run = 0;
 #pragma unroll
         for (int j = 0; j < kBAct; ++j) run += tl[j];
@@ -3168,8 +3226,8 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
           ex += tl[j];
         }
         if (tid == 0) s_seg[kBucket] = t;
+        __syncthreads();
       }
-      __syncthreads();
       if (!presorted) {  // stable scatter into actor order (items come from registers)
 #pragma unroll
         for (int r = 0; r < kBIpt; ++r) {
@@ -3334,7 +3392,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
       bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, cnt2, a0, na, wpar, ndead0, acc);
     }
     }  // buckets of the group (one without kTiny)
-    if constexpr (kTiny) __syncthreads();  // s_tiny and the waves' LDS are rewritten by the next group
+    if (kTiny) __syncthreads();  // s_tiny and the waves' LDS are rewritten by the next group (uniform)
   }
   if (!kOwner && !(kGather && kSkew) && blockIdx.x < nwork) flush_stats(a, acc);  // (block-uniform)
 }

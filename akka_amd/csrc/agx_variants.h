@@ -47,5 +47,7 @@ constexpr uint32_t kVariantGroup[V_N] = {0, 1, 2, 3, 4, 5, 6, 7, 0, 1, 2, 3, 4, 
 // launch k_bucket_apply<variant vid, mode, skew> with `grid` x kBThreads threads on `s`
 // (defined in agx_apply.hip; returns hipErrorInvalidValue for an unknown combination)
 hipError_t agx_launch_apply(uint32_t vid, uint32_t mode, bool skew, dim3 grid, hipStream_t s, const BucketArgs& ba);
+// launch k_tiny_apply<variant vid's kinds> (plain / compiled variants only: hipErrorInvalidValue otherwise)
+hipError_t agx_launch_tiny(uint32_t vid, dim3 grid, hipStream_t s, const BucketArgs& ba);
 
 }  // namespace agx

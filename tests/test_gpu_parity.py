@@ -397,23 +397,29 @@ def test_bucket_width_rejects_bad_values(built):
             GpuEngine(EngineConfig(n_actors=100, bucket_actors=ba))
 
 
+@pytest.mark.parametrize("launch", ["1", "0"])
 @pytest.mark.parametrize("tiny", [0, 16, 128])
 @pytest.mark.parametrize("ba", [32, 2048])
 @pytest.mark.parametrize("case", sorted(set(MULTIPASS_CASES) - {"crdt"}))
-def test_tiny_wave_path(built, monkeypatch, tiny, ba, case):
+def test_tiny_wave_path(built, monkeypatch, launch, tiny, ba, case):
     """Multi-pass supersteps: inboxes of <= AGX_TINY messages are drained by one wave (no block
-    barrier), the others by the block path -- both bit-exact against the oracle (0 = block only)."""
+    barrier), the others by the block path -- both bit-exact against the oracle (0 = block only).
+    launch 1: the wave path is its own launch (k_tiny_apply) that lists the other buckets for the
+    block launch; 0: the block launch's own wave check (AGX_TINY_LAUNCH=0)."""
     monkeypatch.setenv("AGX_RADIX_BITS", "3")
     monkeypatch.setenv("AGX_TINY", str(tiny))
+    monkeypatch.setenv("AGX_TINY_LAUNCH", launch)
     w = MULTIPASS_CASES[case]()
     sg, so, a, b = run_both(w, bucket_actors=ba)
     assert_same(sg, so, a, b, f"tiny={tiny} ba={ba} {case}")
 
 
+@pytest.mark.parametrize("launch", ["1", "0"])
 @pytest.mark.parametrize("tiny", [0, 128])
-def test_tiny_wave_path_compiled(built, monkeypatch, tiny):
+def test_tiny_wave_path_compiled(built, monkeypatch, launch, tiny):
     monkeypatch.setenv("AGX_RADIX_BITS", "3")
     monkeypatch.setenv("AGX_TINY", str(tiny))
+    monkeypatch.setenv("AGX_TINY_LAUNCH", launch)
     w = wl.compiled(20_000, seed=5, throughput=2, capacity=4, builtin=True)
     sg, so, a, b = run_both(w, bucket_actors=64)
     assert_same(sg, so, a, b, f"compiled tiny={tiny}")
