@@ -25,6 +25,11 @@ for s in $STEPS; do
           >> gpurun_out/${TAG}_ab.log 2>&1 || { echo "ab failed"; tail -30 gpurun_out/${TAG}_ab.log; exit 1; }
       done
       cat gpurun_out/${TAG}_ab.log ;;
+    abring)  # the ring at 1M / 100M actors (tools/ab.sh, PERF_NS) for every library in LIBS
+      PERF_NS="${PERF_NS:-1000000 100000000}" AB_REPS=${AB_REPS:-2} bash tools/ab.sh ${TAG}ring \
+        ${LIBS:-akka_amd/lib/var/base.so akka_amd/lib/libakka_gpu.so} > /dev/null 2>&1 \
+        || { echo "abring failed"; tail -30 gpurun_out/${TAG}ring_ab.err; exit 1; }
+      cat gpurun_out/${TAG}ring_ab.txt ;;
     prof)  # rocprofv3 kernel trace + stats of single bench configs (PROF_CFGS), the tree's build
       for c in ${PROF_CFGS:-C5_power_law_bounded C3_zipf_fanout C3_zipf_tree}; do
         timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_$c -o run \
