@@ -182,25 +182,37 @@ struct SplitLds {
   uint32_t *key, *src, *pay;  // [kTile]
 };
 
-// `ld(q, k, sv, pv)` loads item q < cnt of the tile.
-template <int NT, class Load>
-__device__ __forceinline__ void split_tile_ld(const Load& ld, uint32_t cnt, const Msgs& out, uint32_t shift,
-                                              uint32_t bits, const SplitLds& S) {
+// `loc(q)` is the index in `src` of item q < cnt of the tile.  Every item is located first (LDS /
+// arithmetic only), then all 3 x IPT loads are issued back to back with no branch around them (items
+// past cnt read index 0 and are masked) -- a per-item locate-then-load left the compiler waiting for
+// each item's loads before the next item's search.
+template <int NT, class Loc>
+__device__ __forceinline__ void split_tile_ld(const CMsgs& src, const Loc& loc, uint32_t cnt, const Msgs& out,
+                                              uint32_t shift, uint32_t bits, const SplitLds& S) {
   constexpr int NW = NT / kWave, IPT = kTile / NT, DPT = kRadix / NT;
   const int tid = threadIdx.x, w = tid / kWave;
   const uint32_t lane = lane_id();
   const uint32_t mask = (1u << bits) - 1u, nd = 1u << bits;
   const uint64_t ltm = lanemask_lt();
   for (int i = tid; i < NW * kRadix; i += NT) S.whist[i] = 0;
-  __syncthreads();
   const uint32_t wbase = w * (IPT * kWave);
-  uint32_t k[IPT], sv[IPT], pv[IPT], rk[IPT];
+  uint32_t k[IPT], sv[IPT], pv[IPT], rk[IPT], ix[IPT];
 #pragma unroll
   for (int r = 0; r < IPT; ++r) {
     const uint32_t q = wbase + r * kWave + lane;
-    if (q < cnt) ld(q, k[r], sv[r], pv[r]);
-    else k[r] = 0xFFFFFFFFu;
+    ix[r] = q < cnt ? loc(q) : 0u;
   }
+  const uint32_t *Kp = sgpr_ptr(src.key), *Sp = sgpr_ptr(src.src), *Pp = sgpr_ptr(src.pay);
+#pragma unroll
+  for (int r = 0; r < IPT; ++r) {
+    k[r] = ldg(Kp, ix[r]);
+    sv[r] = ldg(Sp, ix[r]);
+    pv[r] = ldg(Pp, ix[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < IPT; ++r)
+    if (wbase + r * kWave + lane >= cnt) k[r] = 0xFFFFFFFFu;
+  __syncthreads();  // (the histogram clear above is visible before the ranks' LDS updates)
 #pragma unroll
   for (int r = 0; r < IPT; ++r) {
     const uint32_t q = wbase + r * kWave + lane;
@@ -273,13 +285,7 @@ __device__ __forceinline__ void split_tile_ld(const Load& ld, uint32_t cnt, cons
 template <int NT>
 __device__ __forceinline__ void split_tile(const CMsgs& in, uint32_t base, uint32_t cnt, const Msgs& out,
                                            uint32_t shift, uint32_t bits, const SplitLds& S) {
-  split_tile_ld<NT>(
-      [&](uint32_t q, uint32_t& k, uint32_t& sv, uint32_t& pv) {
-        k = in.key[base + q];
-        sv = in.src[base + q];
-        pv = in.pay[base + q];
-      },
-      cnt, out, shift, bits, S);
+  split_tile_ld<NT>(in, [&](uint32_t q) -> uint32_t { return base + q; }, cnt, out, shift, bits, S);
 }
 
 // digit bases: s_dbase[d] = exclusive scan of tot[d] over digits; returns the total
@@ -698,19 +704,16 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortAr
       continue;
     }
     for (uint32_t t0 = 0; t0 < ntot; t0 += kTile) {
-      const auto ld = [&](uint32_t q, uint32_t& k, uint32_t& sv, uint32_t& pv) {
+      const auto loc = [&](uint32_t q) -> uint32_t {
         const uint32_t i = t0 + q;
         uint32_t lo = 0, hi = nc - 1;  // last chunk whose start <= i
         while (lo < hi) {
           const uint32_t mid = (lo + hi + 1) >> 1;
           if (s_cpre[mid] <= i) lo = mid; else hi = mid - 1;
         }
-        const uint32_t x = s_coff[lo] + (i - s_cpre[lo]);
-        k = src.key[x];
-        sv = src.src[x];
-        pv = src.pay[x];
+        return s_coff[lo] + (i - s_cpre[lo]);
       };
-      split_tile_ld<kThreads>(ld, min((uint32_t)kTile, ntot - t0), a.out, a.shift, a.bits, S);
+      split_tile_ld<kThreads>(src, loc, min((uint32_t)kTile, ntot - t0), a.out, a.shift, a.bits, S);
     }
   }
 }
@@ -2731,15 +2734,26 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
     };
     if (q1 <= blc) {  // a part of the previous backlog: grouped by actor, every item admitted unless
                       // its actor stopped; rank = earlier parts' count + distance to the run start
+      // (every load of a sub-tile -- keys, the previous keys, senders, payloads -- is issued before the
+      // run-start barrier: one round trip per sub-tile instead of two)
+      const uint32_t *Bk = sgpr_ptr(a.g.bl[rpar].key), *Bs = sgpr_ptr(a.g.bl[rpar].src),
+                     *Bp = sgpr_ptr(a.g.bl[rpar].pay);
       for (uint32_t sub = q0; sub < q1; sub += kBucket) {
         const uint32_t wbase = sub + w * (kBIpt * kWave);
-        uint32_t kk[kBIpt];
+        uint32_t kk[kBIpt], kp[kBIpt], sv[kBIpt], pv[kBIpt];
 #pragma unroll
         for (int u = 0; u < kBIpt; ++u) {
           const uint32_t q = wbase + u * kWave + lane;
-          kk[u] = q < q1 ? a.g.bl[rpar].key[blo + q] : 0u;
-          const uint32_t kp = q < q1 && q > q0 ? a.g.bl[rpar].key[blo + q - 1] : ~0u;
-          if (q < q1 && (q == q0 || (kp & amask) != (kk[u] & amask))) s_first[kk[u] & amask] = q;
+          const uint32_t i = q < q1 ? blo + q : blo, ip = q < q1 && q > q0 ? blo + q - 1 : blo;
+          kk[u] = ldg(Bk, i);
+          kp[u] = ldg(Bk, ip);
+          sv[u] = ldg(Bs, i);
+          pv[u] = ldg(Bp, i);
+        }
+#pragma unroll
+        for (int u = 0; u < kBIpt; ++u) {
+          const uint32_t q = wbase + u * kWave + lane;
+          if (q < q1 && (q == q0 || (kp[u] & amask) != (kk[u] & amask))) s_first[kk[u] & amask] = q;
         }
         __syncthreads();  // (a run start written in a later sub-tile belongs to another actor)
 #pragma unroll
@@ -2748,7 +2762,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
           if (q >= q1) continue;
           const uint32_t rank = s_run[la] + (q - s_first[la]);
           if (rank >= s_keep[la]) continue;
-          place(la, rank, kk[u], a.g.bl[rpar].src[blo + q], a.g.bl[rpar].pay[blo + q]);
+          place(la, rank, kk[u], sv[u], pv[u]);
         }
       }
       __syncthreads();

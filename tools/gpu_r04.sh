@@ -30,6 +30,22 @@ for s in $STEPS; do
         ${LIBS:-akka_amd/lib/var/base.so akka_amd/lib/libakka_gpu.so} > /dev/null 2>&1 \
         || { echo "abring failed"; tail -30 gpurun_out/${TAG}ring_ab.err; exit 1; }
       cat gpurun_out/${TAG}ring_ab.txt ;;
+    stamps)  # per-phase cycle stamps of the block apply (AGX_STAMPS, eager) on STAMP_WL (tools/diag_c5.py)
+      for wlname in ${STAMP_WL:-c5 c3}; do
+        AGX_STAMPS=1 timeout -k 10 300 python tools/diag_c5.py --workload $wlname --steps 3 \
+          > gpurun_out/${TAG}_stamps_$wlname.log 2>&1 || { echo "stamps $wlname failed"; tail -20 gpurun_out/${TAG}_stamps_$wlname.log; exit 1; }
+        grep -a "agx stamps\|^step" gpurun_out/${TAG}_stamps_$wlname.log | tail -8
+      done ;;
+    pmc)  # FETCH_SIZE / WRITE_SIZE passes (separate runs) of PMC_CFGS "name:warmup", per-superstep window sums
+      for cw in ${PMC_CFGS:-C5_power_law_bounded:2 C3_zipf_fanout:2}; do
+        c=${cw%%:*}; wu=${cw##*:}
+        for grp in FETCH_SIZE WRITE_SIZE; do
+          timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${TAG}_pmc_${c}_$grp -o run \
+            -- python3 tools/cfg_one.py $c > gpurun_out/${TAG}_pmc_${c}_$grp.log 2>&1 || { echo "pmc $c $grp failed"; tail -20 gpurun_out/${TAG}_pmc_${c}_$grp.log; exit 1; }
+        done
+        python3 tools/pmc_window.py $c gpurun_out/${TAG}_pmc_${c}_FETCH_SIZE gpurun_out/${TAG}_pmc_${c}_WRITE_SIZE \
+          gpurun_out/${TAG}_pmc_${c}_FETCH_SIZE.log --warmup $wu | tee gpurun_out/${TAG}_pmc_${c}.json
+      done ;;
     prof)  # rocprofv3 kernel trace + stats of single bench configs (PROF_CFGS), the tree's build
       for c in ${PROF_CFGS:-C5_power_law_bounded C3_zipf_fanout C3_zipf_tree}; do
         timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_$c -o run \
