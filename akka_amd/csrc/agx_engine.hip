@@ -87,10 +87,11 @@ struct DevMsgs {
 };
 
 enum KClass { K_CROWSCAN, K_CDOWN, K_UPSWEEP, K_ROWSCAN, K_DOWNSWEEP, K_APPLY, K_EXCHANGE, K_MCOMPACT, K_SKEW, K_TICK,
-              K_BOUNDS, K_SKEWPRE, K_TINY, K_NCLASS };
+              K_BOUNDS, K_SKEWPRE, K_TINY, K_RINGAPPLY, K_NCLASS };
 const char* kClassNames[K_NCLASS] = {"chunk_rowscan", "chunk_downsweep", "sort_upsweep", "sort_rowscan",
                                      "sort_downsweep", "bucket_apply", "exchange", "mcompact", "bucket_apply_skew",
-                                     "fused_tick", "bucket_bounds", "skew_prepass", "bucket_apply_tiny"};
+                                     "fused_tick", "bucket_bounds", "skew_prepass", "bucket_apply_tiny",
+                                     "ring_apply"};
 
 constexpr uint32_t kGraphSizes[5] = {1, 2, 4, 8, 16};  // superstep replays (agx_engine::gx)
 constexpr uint32_t kRowAlign = 32;  // CRDT row pitch (u32) of rows wider than one 128-B line
@@ -203,12 +204,20 @@ struct agx_engine {
   uint32_t cur_slot = 0;       // superstep index within the replay being captured / launched
   uint64_t host_steps = 0;     // fused: supersteps with mail, counted on the host from h_cntb
   uint32_t par = 0;  // fused: parity of the next superstep (host-tracked; graphs are captured per parity)
-  uint32_t *d_skew_list = nullptr, *d_skew_n = nullptr;  // buckets for the general-path launch ([2]: block-list count)
+  uint32_t *d_skew_list = nullptr, *d_skew_n = nullptr;  // buckets for the general-path launch
   // single-rank multi-pass, plain behaviours: k_tiny_apply drains the buckets of <= tiny_max messages
-  // one wave each and lists the others here for the block launch (AGX_TINY_LAUNCH=0: the fast launch's
-  // own wave check instead)
+  // one wave each and marks the others here ([nb]) for the block launch (AGX_TINY_LAUNCH=0: no wave
+  // path, the block launch takes every bucket)
   uint32_t* d_blist = nullptr;
   bool tiny_launch = true;
+  // ring apply (agx_ring.h): bounded mailboxes whose queued messages stay in per-actor rings; decided
+  // at the first run (setup_ring_apply), then one k_ring_apply per superstep replaces the tiny / block /
+  // skew launches.  AGX_RING_APPLY=0 keeps the backlog arena.
+  bool rg_on = false;
+  uint32_t rg_c = 0, rg_dstride = 0;
+  uint32_t *d_rg_state = nullptr, *d_rg_src = nullptr, *d_rg_pay = nullptr;
+  uint32_t *d_rg_dk = nullptr, *d_rg_ds = nullptr, *d_rg_dp = nullptr;
+  uint64_t em_cap = 0;  // entries of the tell arenas em / em2
   // multi-pass, plain behaviours: skewed buckets split over workgroups (k_skew_*, agx_kernels.h)
   uint32_t *d_sk_rec = nullptr, *d_sk_act = nullptr, *d_sk_pc = nullptr, *d_sk_meta = nullptr;
   uint32_t sk_budget = 0, sk_rows = 0;
@@ -484,7 +493,7 @@ agx_status launch_bucket_sort(agx_engine* e, bool first_from_chunks, DevMsgs** r
     ca.bl_stot = e->d_blpre + e->nb;
     ca.bl_sbase = e->d_blpre + e->nb + kMaxBlSlices;
     ca.d_ninbox = e->d_ninbox;
-    ca.ring_total = e->ring_live ? e->d_ring_total : nullptr;
+    ca.ring_total = e->ring_live || e->rg_on ? e->d_ring_total : nullptr;
     ca.bypass = 1;
     ca.heap_top = e->d_heap_top;
     ca.skew_n = e->d_skew_n;
@@ -677,6 +686,17 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     ba.ring_lo0 = (uint32_t)e->acap;
   }
   SkewArgs ska{e->d_sk_rec, e->d_sk_act, e->d_sk_pc, e->d_sk_meta, e->sk_budget, e->sk_rows};
+  if (e->rg_on) {  // ring apply: one launch does admission, drains and ring appends (agx_ring.h)
+    RingArgs ra{e->d_rg_state, e->d_rg_src, e->d_rg_pay, e->d_rg_dk, e->d_rg_ds, e->d_rg_dp, e->d_ring_total,
+                e->rg_c, e->rg_dstride};
+    {
+      Scope s(e, K_RINGAPPLY);
+      HIP_TRY(agx_launch_ring(apply_variant(e), dim3(grid_for(e->nb, e->apply_grid)), e->stream, ba, ra));
+    }
+    e->par ^= 1u;
+    HIP_TRY(hipGetLastError());
+    return AGX_OK;
+  }
   {
     const uint32_t vid = apply_variant(e);
     const bool orm = vid == V_OR;  // ORSet-only full state: state effects in k_orset_merge
@@ -690,9 +710,8 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     const uint32_t mode = e->fused ? M_FUSED : e->R > 1 ? M_OWNER : M_BYPASS;
     const dim3 g(grid_for(e->nb, e->apply_grid));
     const bool tl = mode == M_BYPASS && !kVariants[vid].wide && e->tiny_launch && e->tiny_max && !e->skew_only;
-    if (tl) {  // wave-per-bucket launch first; the block launch then walks the buckets it listed
+    if (tl) {  // wave-per-bucket launch first; the block launch then takes the buckets it marked
       ba.blist = e->d_blist;
-      ba.blist_n = e->d_skew_n + 2;
       Scope s(e, K_TINY);
       const uint32_t gt = grid_for((e->nb + kTinyWaves - 1) / kTinyWaves, kMaxApplyGrid);
       HIP_TRY(agx_launch_tiny(vid, dim3(gt), e->stream, ba));
@@ -770,6 +789,59 @@ agx_status setup_rings(agx_engine* e) {
   e->ring_c = cmax;
   e->ring_live = true;
   drop_graphs(e);  // the ring arrays are kernel arguments of the captured supersteps
+  return AGX_OK;
+}
+
+// Ring apply (agx_ring.h), decided once before the first superstep: a single-rank multi-pass engine
+// with plain behaviours, one tell per message (max_emit 1) and every mailbox class bounded keeps its
+// queued messages in per-actor rings of the largest capacity when they fit the HBM budget (at most
+// half of the free memory: n_local x capacity x 8 B, C5's 10^8 actors x 64 = 51 GB of a 288 GB
+// MI355X), so a queued message is written once and read once instead of being copied forward by every
+// superstep it waits.  Each bucket's tells get a fixed slice of kBucket x throughput slots of the tell
+// arenas (a bucket may drain more messages than it receives: its rings' heads).
+agx_status setup_ring_apply(agx_engine* e) {
+  if (e->started || e->rg_on || e->ring_live || e->ring_res) return AGX_OK;
+  if (e->fused || e->R != 1 || e->pw || e->kmax != 1 || e->n_local == 0) return AGX_OK;
+  if (const char* s = getenv("AGX_RING_APPLY"))
+    if (atoi(s) == 0) return AGX_OK;
+  if (kVariants[apply_variant(e)].wide) return AGX_OK;
+  uint32_t cmax = 0;
+  for (uint32_t c = 0; c < AGX_MAX_MAILBOX_CLASSES; ++c) {
+    if (!((e->mclass_set >> c) & 1u)) continue;
+    if (e->mcap[c] == 0 || e->mcap[c] > kRingApplyMaxC) return AGX_OK;  // an unbounded (or huge) mailbox class
+    cmax = std::max(cmax, e->mcap[c]);
+  }
+  const uint64_t dstr = e->Traw, slice = (uint64_t)kBucket * dstr;  // (drained per actor <= min(T, C) <= Traw)
+  const uint64_t em_need = (uint64_t)e->nb * slice;
+  if (em_need >= (1ull << 32)) return AGX_OK;
+  const uint64_t ring_bytes = e->n_local * (uint64_t)cmax * 8 + e->n_local * 4;
+  const uint64_t scratch_bytes = em_need * 12;
+  const uint64_t em_bytes = em_need > e->em_cap ? 2 * em_need * 12 : 0;  // (bigger tell arenas, both parities)
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return AGX_OK;
+  if (ring_bytes + scratch_bytes + em_bytes > fr / 2) return AGX_OK;  // the backlog arena, as before
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (em_need > e->em_cap) {
+    free_msgs(e->em);
+    free_msgs(e->em2);
+    AGX_TRY(alloc_msgs(e->em, em_need));
+    AGX_TRY(alloc_msgs(e->em2, em_need));
+    e->em_cap = em_need;
+  }
+  AGX_TRY(dalloc(&e->d_rg_state, e->n_local));
+  AGX_TRY(dalloc(&e->d_rg_src, e->n_local * (uint64_t)cmax));
+  AGX_TRY(dalloc(&e->d_rg_pay, e->n_local * (uint64_t)cmax));
+  AGX_TRY(dalloc(&e->d_rg_dk, em_need));
+  AGX_TRY(dalloc(&e->d_rg_ds, em_need));
+  AGX_TRY(dalloc(&e->d_rg_dp, em_need));
+  if (!e->d_ring_total) AGX_TRY(dalloc(&e->d_ring_total, 2));
+  HIP_TRY(hipMemsetAsync(e->d_rg_state, 0, e->n_local * 4, e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_ring_total, 0, 16, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->rg_c = cmax;
+  e->rg_dstride = (uint32_t)dstr;
+  e->rg_on = true;
+  drop_graphs(e);  // the arenas are kernel arguments of the captured supersteps
   return AGX_OK;
 }
 
@@ -1017,7 +1089,7 @@ agx_status read_counters(agx_engine* e, uint64_t* s) {
                        e->d_emc[0], e->d_emc[1], e->d_stg_cnt, e->par ^ 1u, e->nb, (unsigned long long*)e->d_inflight);
   else
     hipLaunchKernelGGL(k_inflight, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_chunk_cnt, e->nchunks,
-                       (unsigned long long*)e->d_inflight, e->ring_live ? e->d_ring_total : nullptr);
+                       (unsigned long long*)e->d_inflight, e->ring_live || e->rg_on ? e->d_ring_total : nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(e->h_stat, e->d_stats, kStatBlk * 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1733,7 +1805,8 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(alloc_msgs(e->B, e->fused ? 1 : e->cap));
   CREATE_TRY(alloc_msgs(e->scr, e->acap + ring_extra));
   CREATE_TRY(alloc_msgs(e->bl, e->acap));
-  CREATE_TRY(alloc_msgs(e->em, (e->acap + ring_extra) * e->kmax));
+  e->em_cap = (e->acap + ring_extra) * e->kmax;
+  CREATE_TRY(alloc_msgs(e->em, e->em_cap));
   if (e->R > 1) {  // tells grouped by owner per bucket (eg0 + [R][tstride] tables), send buffer s2
     const uint64_t tsz = (uint64_t)e->R * e->tstride;
     CREATE_TRY(alloc_msgs(e->eg0, e->cap_emit));
@@ -1751,7 +1824,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   }
   if (!e->fused && e->R == 1) {  // multi-pass: backlog and tell arenas by superstep parity
     CREATE_TRY(alloc_msgs(e->bl2, e->acap));
-    CREATE_TRY(alloc_msgs(e->em2, (e->acap + ring_extra) * e->kmax));
+    CREATE_TRY(alloc_msgs(e->em2, e->em_cap));
     if (e->ident_on) {
       CREATE_TRY(dalloc(&e->d_emmeta, e->nb));
       CREATE_TRY(dalloc(&e->d_slsum, (uint64_t)(kMaxBlSlices + 1) * kSlSum));
@@ -1883,6 +1956,8 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_skew_list); hipFree(e->d_skew_n); hipFree(e->d_blist);
   hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);
   hipFree(e->d_ring_of); hipFree(e->d_ring_state); hipFree(e->d_ring_src); hipFree(e->d_ring_pay);
+  hipFree(e->d_rg_state); hipFree(e->d_rg_src); hipFree(e->d_rg_pay); hipFree(e->d_rg_dk); hipFree(e->d_rg_ds);
+  hipFree(e->d_rg_dp);
   hipFree(e->d_ring_next); hipFree(e->d_ring_free); hipFree(e->d_ring_total);
   hipFree(e->d_orw); hipFree(e->d_orm); hipFree(e->d_orw_n);
   hipFree(e->d_chunk_off); hipFree(e->d_chunk_cnt); hipFree(e->d_hist_c); hipFree(e->d_hist_d); hipFree(e->d_tot); hipFree(e->d_bstart); hipFree(e->d_dbg);
@@ -1951,6 +2026,10 @@ agx_status agx_set_mailbox_class(agx_engine* e, uint32_t cls, uint32_t capacity)
     return set_err(AGX_EINVAL,
                    "mailbox class %u capacity %u: this engine keeps queued messages in rings of %u (set every "
                    "mailbox class before the first run, or AGX_RING_SLOTS=0)", cls, capacity, e->ring_c);
+  if (e->rg_on && (capacity == 0 || capacity > e->rg_c))
+    return set_err(AGX_EINVAL,
+                   "mailbox class %u capacity %u: this engine keeps queued messages in per-actor rings of %u (set "
+                   "every mailbox class before the first run, or AGX_RING_APPLY=0)", cls, capacity, e->rg_c);
   e->mcap[cls] = capacity;
   e->mclass_set |= 1u << cls;
   e->mclasses = true;
@@ -2239,6 +2318,7 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
   if (e->R > 1 && !e->comm) return set_err(AGX_ESTATE, "n_ranks > 1 needs agx_comm_init (or agx_group_run)");
   AGX_TRY(prepare_run(e));
   AGX_TRY(setup_rings(e));
+  AGX_TRY(setup_ring_apply(e));
   AGX_TRY(setup_orset(e));
   e->started = true;
   if (e->R > 1) {

@@ -583,7 +583,6 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs
     commit_stops(a.alive, a.stopq, a.nstop);
     if (threadIdx.x == 0) {
       a.skew_n[0] = 0u;
-      if (a.bypass) a.skew_n[2] = 0u;  // (the block list of k_tiny_apply, BucketArgs::blist_n)
     }
   }
   const uint32_t d = blockIdx.x;
@@ -1030,10 +1029,9 @@ struct BucketArgs {
   // passes the mark on, and the host runs the deferred skew launch and resumes (run_single)
   uint32_t* abort;
   uint32_t tiny_max;       // bypass: inboxes of at most this many messages take the wave path (0 = off)
-  // bypass, plain behaviours: the buckets k_tiny_apply left to the block path (non-null: the fast
-  // launch walks this list instead of every bucket, with no wave check of its own)
+  // bypass, plain behaviours: [nb] marks of the buckets k_tiny_apply left to the block launch
+  // (non-null: the block launch skips the unmarked ones)
   uint32_t* blist;
-  uint32_t* blist_n;
   // bypass, plain behaviours: skewed buckets pre-partitioned by k_skew_* (see there); [i] = skew index
   const uint32_t* sk_rec;  // [i][kSkRec] bucket, bounds, parts, drained and queued totals
   const uint32_t* sk_act;  // [i][3][kBucket] per actor: admitted, drained-segment start, backlog start
@@ -2296,8 +2294,8 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
 
 // Wave-per-bucket launch (single-rank multi-pass, plain and compiled behaviours): every bucket whose
 // inbox -- backlog in place plus sorted new mail -- holds at most tiny_max messages is drained by one
-// wave (tiny_bucket); the others are listed for the block launch that follows (k_bucket_apply over
-// a.blist).  A separate kernel so that its residency is set by the wave path's own registers and
+// wave (tiny_bucket); the others are marked for the block launch that follows (k_bucket_apply over
+// the a.blist marks).  A separate kernel so that its residency is set by the wave path's own registers and
 // 10 KB of LDS, not by the block path's 80 KB: all of a sparse superstep's buckets (C3: 4883, most
 // with a few dozen messages) are in flight at once instead of one or two waves of each of 512
 // resident 8-wave blocks (the rest of such a block idled while its wave drained).
@@ -2329,8 +2327,7 @@ static __global__ void __launch_bounds__(kTinyThreads) k_tiny_apply(BucketArgs a
                       !(a.ring_of && a.ring_of[bw]);                         // (a ring bucket: skew path)
     if (tiny)
       tiny_bucket<KM>(a, iv, T[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
-    else if (lane == 0)
-      a.blist[atomicAdd(a.blist_n, 1u)] = bw;
+    if (lane == 0) a.blist[bw] = tiny ? 0u : 1u;  // (the block launch's work marks)
   }
 }
 
@@ -2364,10 +2361,10 @@ static __global__ void __launch_bounds__(kTinyThreads) k_tiny_apply(BucketArgs a
 #define AGX_EARLY_STATE 1
 #endif
 constexpr bool kEarlyState = AGX_EARLY_STATE != 0;  // fused fast path: state loads at bucket start (A/B build knob)
-#ifndef AGX_TINY_BOUNDS
-#define AGX_TINY_BOUNDS 1
+#ifndef AGX_DENSE_SEG
+#define AGX_DENSE_SEG 1
 #endif
-constexpr bool kTinyBounds = AGX_TINY_BOUNDS != 0;
+constexpr bool kDenseSeg = AGX_DENSE_SEG != 0;  // presorted dense buckets: segment starts from run starts (A/B knob)
 #ifndef AGX_LATE_ALIVE
 #define AGX_LATE_ALIVE 1
 #endif
@@ -2881,64 +2878,29 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
     for (uint32_t i = tid; i < kStagedChunks; i += kBThreads) a.chunk_cnt[2 * a.nb + i] = 0;  // staged consumed
   }
 
-  // single-rank multi-pass, plain behaviours: groups of kBWaves buckets; each wave first drains its
-  // bucket if it is tiny (wave path), then the block drains the group's other buckets
-  constexpr bool kTinyV = kBypass && !kSkew && !kWide;
-  // (k_tiny_apply ran first and listed the other buckets: no wave check here)
-  const bool listed = kTinyV && a.blist != nullptr;
-  const bool kTiny = kTinyV && !listed;
-  __shared__ uint32_t s_tiny[kBWaves];
-  // (kTiny) the bounds the wave check read for bucket w: [bs, lo, hi, blc, blo, valid] -- the block
-  // path takes them from here instead of a second round trip to global memory
-  __shared__ uint32_t s_tb[kBWaves][6];
-  // (a group is kBWaves consecutive iterations of the block's grid-stride sequence, so the
-  // bucket -> block assignment, and with it the load balance, is the block path's own)
+  // single-rank multi-pass, plain behaviours, after k_tiny_apply: a.blist[b] != 0 marks the buckets
+  // the wave launch left to this one.  A block takes kListBatch of its grid-stride buckets at a time:
+  // wave 0 reads their marks in one round trip, the ballot is the batch's work mask (no list, no
+  // atomics; the bucket -> block assignment stays the grid-stride one)
+  constexpr uint32_t kListBatch = 32;
+  const bool listed = kBypass && !kSkew && !kWide && a.blist != nullptr;
+  __shared__ uint32_t s_todo;
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};  // this thread's counters over the block's buckets
-  const uint32_t nwork = kSkew ? *skew_n : listed ? *a.blist_n : a.nb;
-  const uint32_t istride = kTiny ? kBWaves * gridDim.x : gridDim.x;
+  const uint32_t nwork = kSkew ? *skew_n : a.nb;
+  const uint32_t istride = listed ? kListBatch * gridDim.x : gridDim.x;
   for (uint32_t it = blockIdx.x; it < nwork; it += istride) {
-    uint32_t bfirst = kSkew ? a.skew_list[it] : listed ? a.blist[it] : it, nblk = 1, todo = 1u, bstep = 0;
-    if (kTiny) {
-      nblk = kBWaves;
+    uint32_t bfirst = kSkew ? a.skew_list[it] : it, nblk = 1, todo = 1u, bstep = 0;
+    if (listed) {
+      nblk = kListBatch;
       bstep = gridDim.x;
-      const uint32_t bw = bfirst + w * bstep;
-      bool tiny = false;
-      if (bw < a.nb && a.tiny_max) {
-        uint32_t bs = 0, lo_w = 0, hi_w = 0, blc = 0, blo = 0;
-        if (lane == 0) {  // (the block path's bypass bounds, below)
-          bs = a.bstart[bw];
-          const uint32_t be = a.bstart[bw + 1], bp = a.blpre[bw] + a.bl_sbase[bw / kBlSlice];
-          blc = a.chunk_cnt[bw];
-          blo = a.chunk_off[bw];
-          lo_w = bs + bp;
-          hi_w = lo_w + blc + (be - bs);
-        }
-        bs = (uint32_t)__builtin_amdgcn_readlane((int)bs, 0);
-        lo_w = (uint32_t)__builtin_amdgcn_readlane((int)lo_w, 0);
-        hi_w = (uint32_t)__builtin_amdgcn_readlane((int)hi_w, 0);
-        blc = (uint32_t)__builtin_amdgcn_readlane((int)blc, 0);
-        blo = (uint32_t)__builtin_amdgcn_readlane((int)blo, 0);
-        tiny = hi_w - lo_w <= a.tiny_max && (uint64_t)hi_w <= a.cap &&  // (over capacity: the block path reports it)
-               !(a.ring_of && a.ring_of[bw]);                         // (a ring bucket: skew path)
-        if (lane == 0 && kTinyBounds) {
-          s_tb[w][0] = bs;
-          s_tb[w][1] = lo_w;
-          s_tb[w][2] = hi_w;
-          s_tb[w][3] = blc;
-          s_tb[w][4] = blo;
-        }
-        if constexpr (kTinyV)
-          if (tiny)
-            tiny_bucket<KM>(a, iv, reinterpret_cast<TinyLds*>(U)[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
-      }
-      if (lane == 0) {
-        s_tiny[w] = tiny || bw >= a.nb;
-        s_tb[w][5] = bw < a.nb && a.tiny_max;  // (bounds above valid)
+      if (w == 0) {
+        const uint32_t bw = it + lane * bstep;
+        const uint64_t m = __ballot(lane < kListBatch && bw < a.nb && a.blist[bw] != 0u);
+        if (lane == 0) s_todo = (uint32_t)m;
       }
       __syncthreads();
-      todo = 0;
-#pragma unroll
-      for (uint32_t j = 0; j < kBWaves; ++j) todo |= s_tiny[j] ? 0u : 1u << j;
+      todo = s_todo;
+      __syncthreads();  // (s_todo is rewritten by the next batch)
     }
     for (uint32_t j = 0; j < nblk; ++j) {
     if (!((todo >> j) & 1u)) continue;
@@ -2965,13 +2927,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
     if (!kGather) {
       if (tid == 0) {
         if constexpr (kBypass) {  // inbox = [previous backlog, in place][sorted new mail]
-          if (kTiny && kTinyBounds && s_tb[j][5]) {  // (read by the wave check of this group)
-            s_g[0] = s_tb[j][3];
-            s_g[1] = s_tb[j][4];
-            s_g[3] = s_tb[j][0];
-            s_lo = s_tb[j][1];
-            s_hi = s_tb[j][2];
-          } else {
+          {
             const uint32_t bs = a.bstart[b], be = a.bstart[b + 1], bp = a.blpre[b] + a.bl_sbase[b / kBlSlice];
             const uint32_t blc = a.chunk_cnt[b], blo = a.chunk_off[b];
             s_g[0] = blc;
@@ -3180,30 +3136,45 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
         }
       }
       __syncthreads();
-      int ok = 1;
+      // (dense: every actor of the bucket has mail -- rings, stencils -- so each run start is an actor's
+      // segment start)
+      int ok = 1, dense = cnt > 0;
 #pragma unroll
       for (int r = 0; r < kBIpt; ++r) {
-        const uint32_t q = wbase + r * kWave + lane;
-        if (q < cnt && q > 0) ok &= (s_key[q - 1] & amask) <= (k[r] & amask);
+        const uint32_t q = wbase + r * kWave + lane, la = k[r] & amask;
+        const uint32_t lp = q > 0 && q < cnt ? s_key[q - 1] & amask : 0xFFFFFFFFu;
+        if (q < cnt) {
+          if (q > 0) ok &= lp <= la;
+          dense &= la - lp <= 1u && (q + 1 < cnt || la == (uint32_t)kBucket - 1u);
+        }
       }
       const bool presorted = __syncthreads_and(ok) != 0;
       uint32_t tl[kBAct];
       if (presorted) {
-        // segment starts straight from the sorted keys in LDS: actor la's run starts at the number
-        // of items with a smaller actor index (a branchless lower bound, the four actors of a
-        // thread stepping together) -- no per-item LDS atomics, no block scan, one barrier
-        uint32_t lb[kBAct] = {0u, 0u, 0u, 0u};
+        // segment starts straight from the sorted keys in LDS, no per-item LDS atomics, no block scan:
+        // a dense bucket's run starts; otherwise actor la's run starts at the number of items with a
+        // smaller actor index (a branchless lower bound, the four actors of a thread stepping together)
+        if (kDenseSeg && __syncthreads_and(dense)) {
 #pragma unroll
-        for (uint32_t step = (uint32_t)kBucket; step; step >>= 1) {
-#pragma unroll
-          for (int j = 0; j < kBAct; ++j) {
-            const uint32_t p = lb[j] + step, la = tid * kBAct + j;
-            if (p <= cnt && (s_key[p - 1] & amask) < la) lb[j] = p;
+          for (int r = 0; r < kBIpt; ++r) {
+            const uint32_t q = wbase + r * kWave + lane, la = k[r] & amask;
+            if (q < cnt && (q == 0 || (s_key[q - 1] & amask) != la)) s_seg[la] = q;
           }
-        }
+          if (tid == 0) s_seg[kBucket] = cnt;
+        } else {
+          uint32_t lb[kBAct] = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int j = 0; j < kBAct; ++j) s_seg[tid * kBAct + j] = lb[j];
-        if (tid == 0) s_seg[kBucket] = cnt;
+          for (uint32_t step = (uint32_t)kBucket; step; step >>= 1) {
+#pragma unroll
+            for (int j = 0; j < kBAct; ++j) {
+              const uint32_t p = lb[j] + step, la = tid * kBAct + j;
+              if (p <= cnt && (s_key[p - 1] & amask) < la) lb[j] = p;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < kBAct; ++j) s_seg[tid * kBAct + j] = lb[j];
+          if (tid == 0) s_seg[kBucket] = cnt;
+        }
         __syncthreads();
       } else {
         for (uint32_t i = tid; i < kBWaves * kBucket / 2; i += kBThreads) reinterpret_cast<uint32_t*>(whist)[i] = 0;
@@ -3405,8 +3376,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs
       __threadfence_block();
       bucket_finish<false, kWide, KM, kGather, kOwner>(a, L, b, lo, cnt2, a0, na, wpar, ndead0, acc);
     }
-    }  // buckets of the group (one without kTiny)
-    if (kTiny) __syncthreads();  // s_tiny and the waves' LDS are rewritten by the next group (uniform)
+    }  // buckets of the batch (one unless listed)
   }
   if (!kOwner && !(kGather && kSkew) && blockIdx.x < nwork) flush_stats(a, acc);  // (block-uniform)
 }
@@ -3832,3 +3802,5 @@ static __global__ void __launch_bounds__(kThreads) k_fix_rx(Msgs a, uint32_t lo,
 }
 
 }  // namespace agx
+
+#include "agx_ring.h"

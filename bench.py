@@ -53,6 +53,7 @@ def kernel_bytes_per_msg(W: int) -> dict:
     """Algorithmic HBM bytes per message for each kernel class."""
     return {
         "bucket_apply": 12 + 12 + (16 * W + 2),  # read inbox envelope, write emitted tell, state r/w + kind/alive
+        "ring_apply": 12 + 12 + (16 * W + 2),    # the same per delivered message (bounded mailboxes, agx_ring.h)
         "chunk_downsweep": 24,                  # read + write one 12 B envelope (first radix pass)
         "sort_downsweep": 24,                   # read + write one 12 B envelope (later passes)
         "sort_upsweep": 4,                      # read key

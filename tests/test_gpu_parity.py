@@ -263,12 +263,15 @@ MULTIPASS_CASES = {
 }
 
 
+@pytest.mark.parametrize("ring", ["1", "0"])
 @pytest.mark.parametrize("bits,G", [(2, 1), (3, 5), (9, 3)])
 @pytest.mark.parametrize("case", sorted(MULTIPASS_CASES))
-def test_multipass_grouping(built, monkeypatch, bits, G, case):
-    """AGX_UNIT_G groups G buckets per first-pass histogram column (as at 100M actors)."""
+def test_multipass_grouping(built, monkeypatch, bits, G, case, ring):
+    """AGX_UNIT_G groups G buckets per first-pass histogram column (as at 100M actors); bounded
+    cases with ring apply (default) and with the backlog arena (AGX_RING_APPLY=0)."""
     monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
     monkeypatch.setenv("AGX_UNIT_G", str(G))
+    monkeypatch.setenv("AGX_RING_APPLY", ring)
     w = MULTIPASS_CASES[case]()
     sg, so, a, b = run_both(w)
     assert_same(sg, so, a, b, f"multipass {case} bits={bits}")
@@ -404,11 +407,12 @@ def test_bucket_width_rejects_bad_values(built):
 def test_tiny_wave_path(built, monkeypatch, launch, tiny, ba, case):
     """Multi-pass supersteps: inboxes of <= AGX_TINY messages are drained by one wave (no block
     barrier), the others by the block path -- both bit-exact against the oracle (0 = block only).
-    launch 1: the wave path is its own launch (k_tiny_apply) that lists the other buckets for the
-    block launch; 0: the block launch's own wave check (AGX_TINY_LAUNCH=0)."""
+    launch 1: the wave path is its own launch (k_tiny_apply) that marks the other buckets for the
+    block launch; 0: no wave path, the block launch takes every bucket (AGX_TINY_LAUNCH=0)."""
     monkeypatch.setenv("AGX_RADIX_BITS", "3")
     monkeypatch.setenv("AGX_TINY", str(tiny))
     monkeypatch.setenv("AGX_TINY_LAUNCH", launch)
+    monkeypatch.setenv("AGX_RING_APPLY", "0")  # (bounded cases: the backlog arena's wave / block paths)
     w = MULTIPASS_CASES[case]()
     sg, so, a, b = run_both(w, bucket_actors=ba)
     assert_same(sg, so, a, b, f"tiny={tiny} ba={ba} {case}")
@@ -420,6 +424,7 @@ def test_tiny_wave_path_compiled(built, monkeypatch, launch, tiny):
     monkeypatch.setenv("AGX_RADIX_BITS", "3")
     monkeypatch.setenv("AGX_TINY", str(tiny))
     monkeypatch.setenv("AGX_TINY_LAUNCH", launch)
+    monkeypatch.setenv("AGX_RING_APPLY", "0")
     w = wl.compiled(20_000, seed=5, throughput=2, capacity=4, builtin=True)
     sg, so, a, b = run_both(w, bucket_actors=64)
     assert_same(sg, so, a, b, f"compiled tiny={tiny}")
@@ -489,3 +494,111 @@ def test_identity_grouping(built, monkeypatch, bits, ba):
             assert_same(s2, o2, st, st_o, f"{w.name} ident={ident}")
         assert res[False][3] == 0
         assert res[True][3] > 0, f"{w.name}: identity grouping never engaged"
+
+
+# ------------------------------------------------------------------ ring apply (bounded mailboxes, agx_ring.h)
+def _compiled_classes_host(n=16_000, seed=9):
+    """typed + built-in behaviours (one tell per message) under three bounded mailbox classes and
+    the dispatcher default, with host-side senders that PINGPONG actors answer through the outbox"""
+    w = wl.compiled(n, seed=seed, throughput=3, capacity=6, builtin=True)
+    q = n // 4
+    w.name = "compiled_classes_host"
+    w.mailbox_classes = {1: 2, 2: 9, 3: 17}
+    w.mailboxes = [(0, q, 1), (q, q, 2), (2 * q, q, 3)]
+    w.outbound = (n, 32)
+    rng = np.random.default_rng(seed + 101)
+    m = n // 4
+    dst, src, pay = w.tells
+    w.tells = (np.concatenate([dst, rng.integers(0, n, m).astype(np.uint32)]),
+               np.concatenate([src, rng.integers(n, n + 32, m).astype(np.uint32)]),
+               np.concatenate([pay, rng.integers(0, 12, m).astype(np.uint32)]))
+    return w
+
+
+def _bounded_ring(n=50_000, hops=7, tokens=3, C=2, T=2):
+    w = wl.token_ring(n, hops, throughput=T, tokens_per_actor=tokens)
+    w.name, w.capacity = "bounded_ring", C
+    return w
+
+
+RING_APPLY_CASES = {
+    "power_law_c8": lambda: wl.power_law_forward(50_000, ttl=5, capacity=8, throughput=5),
+    # (C5's shape: hub buckets take more than one tile of arrivals and drain more than kBucket)
+    "power_law_c64": lambda: wl.power_law_forward(60_000, ttl=14, capacity=64, throughput=5),
+    "power_law_t1": lambda: wl.power_law_forward(30_000, ttl=8, capacity=3, throughput=1),
+    "compiled": lambda: wl.compiled(20_000, seed=5, throughput=2, capacity=4, builtin=True),
+    "classes_host": _compiled_classes_host,
+    "bounded_ring": _bounded_ring,
+}
+
+
+def _run_profiled(w, ba, max_steps=1 << 30):
+    eng = GpuEngine(EngineConfig(**dict(w.gpu_kwargs(), bucket_actors=ba or w.bucket_actors)))
+    w.apply_to(eng)
+    eng.profile(True)
+    sg = eng.run(max_steps)
+    launches = eng.profile_read().get("ring_apply", {"launches": 0})["launches"]
+    st = eng.read_state()
+    return eng, sg, st, launches
+
+
+@pytest.mark.parametrize("mode", ["bits3", "single_pass"])
+@pytest.mark.parametrize("ba", [0, 64])
+@pytest.mark.parametrize("case", sorted(RING_APPLY_CASES))
+def test_ring_apply(built, monkeypatch, mode, ba, case):
+    """Bounded mailboxes whose queued messages stay in per-actor rings (one k_ring_apply per
+    superstep): bit-exact against the oracle and against the backlog arena (AGX_RING_APPLY=0), at
+    multi-pass grouping (3-bit digits) and at one unfused pass; 64-actor buckets put several
+    tiles of arrivals and drains larger than kBucket into one bucket."""
+    from oracle import BspOracle
+    if mode == "bits3":
+        monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    else:
+        monkeypatch.setenv("AGX_NO_FUSED", "1")
+    w = RING_APPLY_CASES[case]()
+    ref = BspOracle(**w.engine_kwargs())
+    w.apply_to(ref)
+    so = ref.run()
+    sto = ref.read_state()
+    ref.close()
+    for ring in ("1", "0"):
+        monkeypatch.setenv("AGX_RING_APPLY", ring)
+        eng, sg, st, launches = _run_profiled(w, ba)
+        eng.close()
+        assert (launches > 0) == (ring == "1"), f"{case}: ring_apply launches {launches} with AGX_RING_APPLY={ring}"
+        assert_same(sg, so, st, sto, f"{case} ring={ring}")
+
+
+@pytest.mark.parametrize("case", ["power_law_c64", "classes_host"])
+def test_ring_apply_resume_and_shrink(built, monkeypatch, case):
+    """Runs split into budgets (the rings persist across agx_run calls), a host burst staged
+    mid-run, then a mailbox class shrunk below what its rings hold (keep = min(len, C): the
+    excess queued messages become dead letters) -- counts after every leg and the final state
+    bit-exact against the oracle."""
+    from oracle import BspOracle
+    monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    w = RING_APPLY_CASES[case]()
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+    ref = BspOracle(**w.engine_kwargs())
+    for t in (eng, ref):
+        w.apply_to(t)
+    eng.profile(True)
+    burst = np.arange(0, w.n_actors, 5, dtype=np.uint32)
+    for leg, steps in enumerate((2, 3, 1, 4, 1 << 30)):
+        if leg == 2:
+            eng.tell(burst, 3)
+            ref.tell(burst, 3)
+        if leg == 3:
+            for t in (eng, ref):
+                if w.mailbox_classes:
+                    t.set_mailbox_class(3, 5)  # (17 -> 5)
+                else:
+                    t.set_mailbox_class(1, 4)  # (the default 64 -> 4 for half the population)
+                    t.set_mailbox(0, w.n_actors // 2, 1)
+        sg, so = eng.run(steps), ref.run(steps)
+        for k in COUNT_KEYS:
+            assert getattr(sg, k) == so[k], f"{case} leg {leg}: {k} gpu={getattr(sg, k)} oracle={so[k]}"
+    assert eng.profile_read()["ring_apply"]["launches"] > 0
+    assert_same(sg, so, eng.read_state(), ref.read_state(), case)
+    eng.close()
+    ref.close()
