@@ -497,7 +497,7 @@ def test_identity_grouping(built, monkeypatch, bits, ba):
 
 
 # ------------------------------------------------------------------ ring apply (bounded mailboxes, agx_ring.h)
-def _compiled_classes_host(n=16_000, seed=9):
+def _compiled_classes_host(n=40_000, seed=9):  # (> 8 buckets: 3-bit digits take two passes, not fused)
     """typed + built-in behaviours (one tell per message) under three bounded mailbox classes and
     the dispatcher default, with host-side senders that PINGPONG actors answer through the outbox"""
     w = wl.compiled(n, seed=seed, throughput=3, capacity=6, builtin=True)
