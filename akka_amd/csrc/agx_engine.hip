@@ -169,6 +169,7 @@ struct agx_engine {
   uint32_t *d_sslab = nullptr, *d_rslab = nullptr, *d_halt = nullptr, *h_halt = nullptr;
   uint32_t slab = 0;
   uint64_t mr_exact = 0;  // supersteps whose exchange the host redid exactly (a count over the slab)
+  uint64_t mr_replays = 0;  // multi-rank replays launched as a captured graph
 
   DevMsgs A, B, scr, bl, em, stg, s2;
   // single-rank multi-pass: the tell arena by superstep parity (em = even, em2 = odd superstep
@@ -263,6 +264,12 @@ struct agx_engine {
   // of K supersteps replays its binary decomposition (20 = 8 + 8 + 4), never a run of singles.
   static constexpr uint32_t kNSizes = 5;
   hipGraphExec_t gx[2][2][kNSizes] = {};
+  // multi-rank device-resident replays (run_multi_rccl): kMrReplay supersteps -- phase 1, the count
+  // all-gather, k_mr_pack, the slab sends / receives, unpack, bucket passes, apply -- captured once as
+  // one graph (RCCL collectives are captured with the kernels); mr_graph_ok cleared when a capture
+  // fails (the replays then stay eager).  AGX_MR_GRAPH=0: eager.
+  hipGraphExec_t mr_gx = nullptr;
+  bool mr_graph_ok = true;
   // fused "strict" replays: graphs without the (usually empty) skew-list launches.  A superstep that
   // defers a skewed bucket marks d_abort; the rest of the replay is void and run_single runs the
   // deferred skew launch, then continues with the full graphs (strict_ok cleared for this engine).
@@ -1436,6 +1443,40 @@ agx_status mr_slabs(agx_engine* e, uint64_t want) {
   AGX_TRY(dalloc(&e->d_sslab, (uint64_t)e->R * n * 3));
   AGX_TRY(dalloc(&e->d_rslab, (uint64_t)e->R * n * 3));
   e->slab = n;
+  drop_graphs(e);  // (the slabs are kernel and collective arguments of a captured replay)
+  return AGX_OK;
+}
+
+agx_status mr_step_dev(agx_engine* e, uint32_t idx);
+
+// kMrReplay device-resident supersteps as one graph.  A failed capture (a collective that cannot be
+// captured) ends the capture, clears mr_graph_ok and returns AGX_OK: the caller replays eagerly.
+agx_status capture_mr(agx_engine* e, uint32_t steps) {
+  hipGraph_t g = nullptr;
+  if (hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    (void)hipGetLastError();
+    e->mr_graph_ok = false;
+    return AGX_OK;
+  }
+  agx_status st = AGX_OK;
+  for (uint32_t i = 0; i < steps && st == AGX_OK; ++i) st = mr_step_dev(e, i);
+  hipError_t ce = hipStreamEndCapture(e->stream, &g);
+  hipGraphExec_t x = nullptr;
+  if (st == AGX_OK && ce == hipSuccess && g && hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess &&
+      hipGraphUpload(x, e->stream) == hipSuccess) {
+    hipGraphDestroy(g);
+    e->mr_gx = x;
+    if (getenv("AGX_MR_DEBUG")) fprintf(stderr, "[agx rank %u] multi-rank replay captured (%u supersteps)\n", e->rank, steps);
+    return AGX_OK;
+  }
+  if (getenv("AGX_MR_DEBUG"))
+    fprintf(stderr, "[agx rank %u] multi-rank replay capture failed (status %d, %s): eager replays\n", e->rank, (int)st,
+            hipGetErrorString(ce));
+  if (x) hipGraphExecDestroy(x);
+  if (g) hipGraphDestroy(g);
+  (void)hipGetLastError();
+  e->mr_graph_ok = false;
+  set_err(AGX_OK, "");  // (the eager replays report their own errors)
   return AGX_OK;
 }
 
@@ -1535,9 +1576,17 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
   if (dev) {
     if (!e->slab) AGX_TRY(mr_slabs(e, mr_initial_slab(e)));
     constexpr uint32_t kMrReplay = 8;  // supersteps enqueued before the host reads the stop word
+    const bool graphs = !e->prof && e->graphs_enabled && e->mr_graph_ok && !(getenv("AGX_MR_GRAPH") &&
+                                                                            atoi(getenv("AGX_MR_GRAPH")) == 0);
     while (left && !quiet) {
       const uint32_t k = std::min(left, kMrReplay);
-      for (uint32_t i = 0; i < k; ++i) AGX_TRY(mr_step_dev(e, i));
+      if (graphs && k == kMrReplay && !e->mr_gx) AGX_TRY(capture_mr(e, kMrReplay));
+      if (graphs && k == kMrReplay && e->mr_gx) {
+        HIP_TRY(hipGraphLaunch(e->mr_gx, e->stream));
+        ++e->mr_replays;
+      } else {
+        for (uint32_t i = 0; i < k; ++i) AGX_TRY(mr_step_dev(e, i));
+      }
       HIP_TRY(hipMemcpyAsync(e->h_halt, e->d_halt, 8, hipMemcpyDeviceToHost, e->stream));
       HIP_TRY(hipStreamSynchronize(e->stream));
       const uint32_t code = e->h_halt[0], at = e->h_halt[1];
@@ -1576,6 +1625,8 @@ void drop_graphs(agx_engine* e) {
         if (g) hipGraphExecDestroy(g);
         g = nullptr;
       }
+  if (e->mr_gx) hipGraphExecDestroy(e->mr_gx);
+  e->mr_gx = nullptr;
 }
 
 // First CRDT kind (or a wider one): size the snapshot heap for `kind`'s rows (full state, plus

@@ -244,17 +244,80 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
       for (int j = 0; j < kBAct; ++j) S.cnt[la0 + j] += tt[j];
       __syncthreads();
     }
-    // ---- state of the actors that drain (issued here, used by the drain)
+    // ---- state of the actors that drain (issued here, used by the drain).  FORWARD_RR (C5): each
+    // actor's out-edge row and the destination of its next round-robin edge, all four actors' loads
+    // together (bucket_finish's hint: no dependent row_ptr -> col loads inside the serial drain)
     uint64_t w0[kBAct], w1[kBAct];
     uint32_t kd[kBAct], drn[kBAct];
     constexpr bool kKindNeeded = (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0;
+    constexpr bool kFwd = KM == kb(AGX_KIND_FORWARD_RR);
+    constexpr bool kFan = KM == kb(AGX_KIND_FANOUT);
+    constexpr uint32_t kNoHint = 0xFFFFFFFFu;
+    uint64_t frb[kBAct], fre[kBAct];
+#pragma unroll
+    for (int j = 0; j < kBAct; ++j) drn[j] = S.dpos[la0 + j] - ds[j] + (S.dadm[la0 + j] & 0xFFFFu);
+    // (before the state loads: their registers are not live across the lookups)
+    // FANOUT with one tell per message (C3 steady): every drained message's Zipf destination, the
+    // four actors' q-th messages in lockstep (index range, each binary-search step's loads together,
+    // then the permutation), written over the message's sender (FANOUT does not read it)
+    const bool fan_pre = kFan && P.fan_k == 1;
+    if (kFan && fan_pre) {
+      uint32_t dmax = 0;
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) dmax = max(dmax, drn[j]);
+      for (uint32_t q = 0; q < dmax; ++q) {
+        uint32_t lo[kBAct], hi[kBAct], uu[kBAct];
+        bool need[kBAct];
+#pragma unroll
+        for (int j = 0; j < kBAct; ++j) {
+          const uint32_t pv = q < drn[j] ? bpay[ds[j] + q] : 0u;
+          need[j] = (pv >> 24) > 0;
+          uu[j] = need[j] ? (uint32_t)(fanout_rand(P.fan_seed, a0 + la0 + j, pv & 0x00FFFFFFu, 0) >> 32) : 0u;
+          const uint32_t t = uu[j] >> (32 - kZipfBits);
+          lo[j] = need[j] ? P.zipf_idx[t] : 0u;
+          hi[j] = need[j] ? P.zipf_idx[t + 1] : 0u;
+        }
+        for (;;) {
+          bool more = false;
+          uint32_t c[kBAct];
+#pragma unroll
+          for (int j = 0; j < kBAct; ++j) c[j] = lo[j] < hi[j] ? P.zipf_cdf[(lo[j] + hi[j]) >> 1] : 0u;
+#pragma unroll
+          for (int j = 0; j < kBAct; ++j)
+            if (lo[j] < hi[j]) {
+              const uint32_t mid = (lo[j] + hi[j]) >> 1;
+              if (c[j] >= uu[j]) hi[j] = mid; else lo[j] = mid + 1;
+              more |= lo[j] < hi[j];
+            }
+          if (!more) break;
+        }
+#pragma unroll
+        for (int j = 0; j < kBAct; ++j)
+          if (need[j]) bsrc[ds[j] + q] = P.zipf_perm[lo[j]];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
-      drn[j] = S.dpos[la0 + j] - ds[j] + (S.dadm[la0 + j] & 0xFFFFu);
       const uint32_t l = drn[j] ? a0 + la0 + j : a0;  // (no drain: a harmless cached load, masked below)
       w0[j] = ldg64(P.state, sidx(P, l, 0));
       w1[j] = P.W > 1 ? ldg64(P.state, sidx(P, l, 1)) : 0ull;
       kd[j] = kKindNeeded ? P.kind[l] : 0u;
+      if constexpr (kFwd) {
+        frb[j] = P.row_ptr[l];
+        fre[j] = P.row_ptr[l + 1];
+      }
+    }
+    if constexpr (kFwd) {  // the hint (degree, first destination) -> LDS (S.cnt / S.dpos are free now)
+      uint32_t fdst[kBAct];
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        const uint64_t deg = fre[j] - frb[j];
+        const bool ok = drn[j] && deg < kNoHint && w1[j] <= 0xFFFFFFFFull;
+        S.cnt[la0 + j] = ok ? (uint32_t)deg : kNoHint;
+        fdst[j] = ok && deg ? P.col[frb[j] + (uint32_t)w1[j] % (uint32_t)deg] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) S.dpos[la0 + j] = fdst[j];
     }
     // ---- drain + apply, actor after actor; tell e of an actor is staged at its drain slot e (already
     // consumed: tell e comes from a message at slot >= e)
@@ -271,9 +334,37 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
       uint64_t wv[2] = {w0[j], w1[j]};
       uint32_t kcur = kd[j];
       ++acc[4];
+      uint32_t hdeg = kNoHint, hdst = 0;
+      bool fresh = true;  // no forward yet: the next edge is hdst
+      if constexpr (kFwd) {
+        hdeg = S.cnt[la];
+        hdst = S.dpos[la];
+      }
       for (uint32_t q = 0; q < drn[j]; ++q) {
         const uint32_t s = bsrc[ds[j] + q], p = bpay[ds[j] + q];
-        const uint32_t r = apply_msg<KM>(P, kcur, self, l, wv, s, p, em);
+        uint32_t r;
+        if (kFan && fan_pre) {  // apply_msg's FANOUT with the destination looked up above (in s)
+          wv[0] += 1;
+          wv[1] += p;
+          const uint32_t ttl = p >> 24;
+          if (ttl > 0) {
+            const uint64_t rr = fanout_rand(P.fan_seed, self, p & 0x00FFFFFFu, 0);
+            em(s, ((ttl - 1) << 24) | ((uint32_t)rr & 0x00FFFFFFu));
+          }
+          r = AGX_RES_SAME;
+        } else if (kFwd && hdeg != kNoHint && wv[1] <= 0xFFFFFFFFull) {
+          // apply_msg's FORWARD_RR with the prefetched row (same cursor arithmetic)
+          wv[0] += 1;
+          if (p > 0 && hdeg) {
+            const uint32_t d = fresh ? hdst : P.col[P.row_ptr[l] + (uint32_t)wv[1] % hdeg];
+            fresh = false;
+            wv[1] += 1;
+            em(d, p - 1);
+          }
+          r = AGX_RES_SAME;
+        } else {
+          r = apply_msg<KM>(P, kcur, self, l, wv, s, p, em);
+        }
         ++acc[0];
         if (r == AGX_RES_UNHANDLED) ++acc[2];
         if (r == AGX_RES_STOPPED) {
