@@ -19,6 +19,10 @@ for s in $STEPS; do
       timeout -k 10 900 python -u -m pytest tests -x -q -m "gpu and not fullsize" --timeout 280 --timeout-method thread \
         > gpurun_out/${TAG}_gpu.log 2>&1 || { echo "gpu suite failed"; tail -60 gpurun_out/${TAG}_gpu.log; exit 1; }
       tail -3 gpurun_out/${TAG}_gpu.log ;;
+    sub)  # a subset of the GPU suite: SUB_FILES (default tests), SUB_K (pytest -k expression)
+      timeout -k 10 900 python -u -m pytest ${SUB_FILES:-tests} -x -q -m "gpu and not fullsize" -k "${SUB_K:-.}" \
+        --timeout 280 --timeout-method thread > gpurun_out/${TAG}_sub.log 2>&1 || { echo "gpu subset failed"; tail -60 gpurun_out/${TAG}_sub.log; exit 1; }
+      tail -3 gpurun_out/${TAG}_sub.log ;;
     ab)
       for c in ${CFGS:-C3_zipf_fanout C3_zipf_tree C5_power_law_bounded}; do
         AB_REPS=${AB_REPS:-2} bash tools/ab_cfg.sh $c ${LIBS:-akka_amd/lib/var/base.so akka_amd/lib/libakka_gpu.so} \
