@@ -267,7 +267,7 @@ struct agx_engine {
   // multi-rank device-resident replays (run_multi_rccl): kMrReplay supersteps -- phase 1, the count
   // all-gather, k_mr_pack, the slab sends / receives, unpack, bucket passes, apply -- captured once as
   // one graph (RCCL collectives are captured with the kernels); mr_graph_ok cleared when a capture
-  // fails (the replays then stay eager).  AGX_MR_GRAPH=0: eager.
+  // fails (the replays then stay eager).  Opt-in: AGX_MR_GRAPH=1 (see run_multi_rccl).
   hipGraphExec_t mr_gx = nullptr;
   bool mr_graph_ok = true;
   // fused "strict" replays: graphs without the (usually empty) skew-list launches.  A superstep that
@@ -1576,8 +1576,11 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
   if (dev) {
     if (!e->slab) AGX_TRY(mr_slabs(e, mr_initial_slab(e)));
     constexpr uint32_t kMrReplay = 8;  // supersteps enqueued before the host reads the stop word
-    const bool graphs = !e->prof && e->graphs_enabled && e->mr_graph_ok && !(getenv("AGX_MR_GRAPH") &&
-                                                                            atoi(getenv("AGX_MR_GRAPH")) == 0);
+    // (opt-in, AGX_MR_GRAPH=1: a captured replay of ncclAllGather + grouped send/recv hung in its
+    // first launch with RCCL's socket transport -- two ranks sharing the one-GPU test box -- so the
+    // eager replay stays the default until the capture is proven over xGMI)
+    const bool graphs = !e->prof && e->graphs_enabled && e->mr_graph_ok && getenv("AGX_MR_GRAPH") &&
+                        atoi(getenv("AGX_MR_GRAPH")) != 0;
     while (left && !quiet) {
       const uint32_t k = std::min(left, kMrReplay);
       if (graphs && k == kMrReplay && !e->mr_gx) AGX_TRY(capture_mr(e, kMrReplay));

@@ -31,8 +31,6 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
     ("zipf", 2, 30_000, 3, {}),
     ("zipf", 4, 40_000, 3, {}),     # C3 sharded over 4 ranks
     ("orset", 4, 4_000, 5, {}),     # C4 ORSet rows over 4 ranks
-    ("ring", 2, 20_000, 20, {"AGX_MR_GRAPH": "0"}),  # eager device-resident replays (no graph capture)
-    ("power", 3, 60_000, 17, {"AGX_MR_DEBUG": "1", "EXPECT": "multi-rank replay captured"}),
     # (world <= 4 on ONE device: a round-3 run of 8 ranks on the 1-GPU box stalled after communicator
     # setup and was killed at its time limit; its log was scratch output and was not kept -- see
     # DESIGN.md §7.  The 8-rank exchange is covered by agx_group_run's loopback of the same kernels,
