@@ -268,7 +268,7 @@ MULTIPASS_CASES = {
 @pytest.mark.parametrize("case", sorted(MULTIPASS_CASES))
 def test_multipass_grouping(built, monkeypatch, bits, G, case, ring):
     """AGX_UNIT_G groups G buckets per first-pass histogram column (as at 100M actors); bounded
-    cases with ring apply (default) and with the backlog arena (AGX_RING_APPLY=0)."""
+    cases with ring apply (AGX_RING_APPLY=1) and with the backlog arena (the default)."""
     monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
     monkeypatch.setenv("AGX_UNIT_G", str(G))
     monkeypatch.setenv("AGX_RING_APPLY", ring)
@@ -577,6 +577,7 @@ def test_ring_apply_resume_and_shrink(built, monkeypatch, case):
     bit-exact against the oracle."""
     from oracle import BspOracle
     monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    monkeypatch.setenv("AGX_RING_APPLY", "1")
     w = RING_APPLY_CASES[case]()
     eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
     ref = BspOracle(**w.engine_kwargs())
