@@ -2413,7 +2413,8 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
     fprintf(stderr, "[agx stamps%s] mean cycles per phase over %llu blocks:", e->stamps_skew ? " (skew launch)" : "",
             (unsigned long long)nst);
     const char* nm[8] = {"range+alive", "sort", "->finish", "classify+backlog", "prefetch+phaseA", "scan", "phaseB", "hist+stats"};
-    for (int k = 0; k < 8; ++k) fprintf(stderr, " %s=%.0f", nm[k], nst ? acc[k] / nst : 0.0);
+    const char* nr[8] = {"count", "admission", "ring_heads", "placement", "prefetch", "drain", "tells", "words+hist"};
+    for (int k = 0; k < 8; ++k) fprintf(stderr, " %s=%.0f", (e->rg_on ? nr : nm)[k], nst ? acc[k] / nst : 0.0);
     fprintf(stderr, " | kernel span=%llu cycles\n", t8max - t0min);
     std::vector<std::pair<unsigned long long, uint64_t>> slow;
     for (uint64_t b = 0; b < nbk; ++b) slow.push_back({h[b * 16 + 10], b});

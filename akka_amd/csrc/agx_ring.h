@@ -75,6 +75,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
   for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x) {
     const uint32_t a0 = b << a.bb;
     const uint32_t na = min(1u << a.bb, P.n_local - a0);
+    AGX_STAMP(a, 0);
     const uint32_t bs = a.bstart[b], n = a.bstart[b + 1] - bs;
     // ---- this thread's four actors (blocked: la = 4 tid + j): flags, limits, ring words
     const uint32_t la0 = tid * kBAct;
@@ -108,6 +109,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
         if (t0 + wbase + r * kWave + lane < n) lds_hist_inc(S.cnt, k[r] & amask);
     }
     __syncthreads();
+    AGX_STAMP(a, 1);
     // ---- per actor: admission, drain and ring bookkeeping (kept in LDS: rr = dpos - ds, da | adm)
     uint32_t ds[kBAct];
     uint32_t dsum = 0, ndead = 0;
@@ -145,6 +147,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
       dseg += rr + (dd & 0xFFFFu);
       rmax = max(rmax, rr);
     }
+    AGX_STAMP(a, 2);
     // ring heads -> the front of each actor's drain segment (a thread's loads of one position together)
     for (uint32_t q = 0; q < rmax; ++q) {
       uint32_t hs[kBAct], hp[kBAct], rr[kBAct];
@@ -165,6 +168,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
         }
     }
     __syncthreads();
+    AGX_STAMP(a, 3);
     // ---- placement: stable rank of every admitted arrival among its actor's arrivals; ranks < da to
     // the drain buffer, the rest of the admitted ones appended to the ring
     for (uint32_t t0 = 0; t0 < n; t0 += kBucket) {
@@ -244,6 +248,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
       for (int j = 0; j < kBAct; ++j) S.cnt[la0 + j] += tt[j];
       __syncthreads();
     }
+    AGX_STAMP(a, 4);
     // ---- state of the actors that drain (issued here, used by the drain).  FORWARD_RR (C5): each
     // actor's out-edge row and the destination of its next round-robin edge, all four actors' loads
     // together (bucket_finish's hint: no dependent row_ptr -> col loads inside the serial drain)
@@ -319,6 +324,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
 #pragma unroll
       for (int j = 0; j < kBAct; ++j) S.dpos[la0 + j] = fdst[j];
     }
+    AGX_STAMP(a, 5);
     // ---- drain + apply, actor after actor; tell e of an actor is staged at its drain slot e (already
     // consumed: tell e comes from a message at slot >= e)
     uint32_t* const skey = lds_drain ? S.whist32 : g.dk + sbase;
@@ -382,6 +388,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
       ecl[j] = em.n_valid;
       esum += em.n_valid;
     }
+    AGX_STAMP(a, 6);
     // ---- tells in sender order into the bucket's slice of the tell arena
     uint32_t emtot;
     uint32_t eo = block_excl_sum<kBThreads>(esum, S.scratch, &emtot);  // (syncs: staging complete)
@@ -395,6 +402,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
       }
       eo += ecl[j];
     }
+    AGX_STAMP(a, 7);
     // ---- ring words, chunk entries, next first-pass histogram column
     {
       uint32_t nv[kBAct];
@@ -432,6 +440,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
     for (uint32_t d = tid; d < (1u << a.nx_bits); d += kBThreads)
       if (S.nh[d]) atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + a.ng + b / a.G], S.nh[d]);
     __syncthreads();  // (LDS reused by the next bucket)
+    AGX_STAMP(a, 8);
   }
   if (blockIdx.x < a.nb) flush_stats(a, acc);
   // messages held in rings: the block's change, two's complement into the u64 total

@@ -7,7 +7,8 @@ runs the config as bench.py does: engine 1 = warmup + the timed supersteps, engi
 again with per-kernel HIP events.  Every dispatch is attributed to a superstep of its engine:
   * an engine starts at its host-staged tells (k_chunk_hist), the first superstep's first kernel;
   * a later superstep starts at its first-pass rowscan (k_chunk_rowscan; with identity grouping the
-    split launch's first part, the one followed by k_ident_combine).
+    split launch's first part, the one followed by k_ident_combine);
+  * engine setup (k_gen_rmat: the next engine's graph) closes the previous engine's last superstep.
 The window is engine 1's supersteps [warmup, warmup + timed).  HBM bytes per dispatch = 2 x FETCH_SIZE
 + WRITE_SIZE (KiB; MI355X_MICROARCH.md HBM section: gfx950 FETCH_SIZE counts half of a wide streaming
 read, WRITE_SIZE is exact).  Algorithmic bytes = the config's alg_bytes_per_msg x delivered (SURVEY.md
@@ -31,10 +32,17 @@ def dispatches(d):
     return rows
 
 
+SETUP_KERNELS = ("k_gen_rmat",)  # engine setup (the device R-MAT graph): not part of any superstep
+
+
 def supersteps(rows):
-    """[(engine, superstep) per dispatch] by the kernel-sequence rules above."""
+    """[(engine, superstep) per dispatch] by the kernel-sequence rules above; dispatches from an
+    engine-setup kernel up to the next engine's first superstep get superstep -1 (outside every window)."""
     out, eng, step, started = [], -1, -1, False
     for i, (_, k, _) in enumerate(rows):
+        if k in SETUP_KERNELS:
+            started = False
+            step = -1
         if k == "k_chunk_hist":
             if not (out and out[-1][1] == step and rows[i - 1][1] == "k_chunk_hist"):
                 eng += 1
