@@ -18,7 +18,7 @@
 // A CRDT engine keeps the state actor-major (wide_state: a replica's words are one contiguous
 // row of P.pitch u64, 128-B aligned), so a replica's 2 KB of ORSet dots are whole cache lines
 // however its lanes diverge; plain engines keep the word-major SoA.  A state gossip carries a handle to
-// an immutable snapshot row (row-major, 16-B vector loads per lane).  Rows are
+// an immutable snapshot row (counters: the state words; ORSet: sparse, kOrRow* below).  Rows are
 // allocated per superstep in heap[step & 1] and read in the next superstep
 // from heap[(step - 1) & 1]; a gossip that stays queued beyond the
 // throughput cap has its row copied forward (see bucket_finish).
@@ -97,6 +97,18 @@ struct St32 {
 
 // Envelope / selector area and delta log (include/akka_gpu.h "delta-CRDT replication"), u32 indices
 __device__ __forceinline__ uint32_t dl_env(uint32_t kind) { return 2u * crdt_words(kind); }
+
+// ORSet snapshot rows (the payload of a full-state gossip) are sparse: a converged set holds a few
+// non-zero dots per element (one per writer node that added it), so the row carries only those --
+// the receiver rebuilds the zeros.  u32 layout: [0, 8) version vector, [8, 16) deltaVersions
+// (delta-CRDT mode), [16, 32) node masks (64 x u8, element e's byte: bit n = dot (e, n) non-zero),
+// [32, ...) the non-zero dots in (element, node) order -- 32 + 512 u32 at most, within the
+// 544-u32 row pitch.  Same merge results as the dense row; C4 rows shrink from 2080 B to
+// 128 B + 4 B per live dot.
+constexpr uint32_t kOrRowVV = 0, kOrRowDV = 8, kOrRowMask = 16, kOrRowDots = 32;
+static_assert(kOrRowDots + AGX_ORSET_ELEMS * AGX_CRDT_NODES <= 544u, "sparse ORSet row within the row pitch");
+// where a full-state gossip row keeps the sender's deltaVersions (delta-CRDT mode)
+__device__ __forceinline__ uint32_t row_dv(uint32_t kind) { return kind == AGX_KIND_ORSET ? kOrRowDV : dl_env(kind); }
 __device__ __forceinline__ uint32_t dl_entry(uint32_t kind, uint32_t seq) {
   return dl_env(kind) + 2u * AGX_DELTA_ENV_WORDS + AGX_DELTA_LOG_U32(kind == AGX_KIND_ORSET) * (seq % AGX_DELTA_LOG);
 }
@@ -443,11 +455,11 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       dl_receive(s32, kind, row);
       return AGX_RES_SAME;
     }
-    if (dm) {  // DataEnvelope.merge: the deltaVersions after the data words
-      const uint32_t e0 = dl_env(kind);
+    if (dm) {  // DataEnvelope.merge: the sender's deltaVersions (row_dv) into ours (after the data words)
+      const uint32_t e0 = dl_env(kind), r0 = row_dv(kind);
 #pragma unroll
       for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
-        const uint32_t c = s32.ld(e0 + n), r = row[e0 + n];
+        const uint32_t c = s32.ld(e0 + n), r = row[r0 + n];
         if (r > c) s32.put(e0 + n, r);
       }
     }
@@ -477,26 +489,28 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       const uint64_t s = st[(vw + k) * nl];
       lvv[2 * k] = (uint32_t)s;
       lvv[2 * k + 1] = (uint32_t)(s >> 32);
-      rvv[2 * k] = row[2 * (vw + k)];
-      rvv[2 * k + 1] = row[2 * (vw + k) + 1];
+      rvv[2 * k] = row[kOrRowVV + 2 * k];
+      rvv[2 * k + 1] = row[kOrRowVV + 2 * k + 1];
     }
 #ifndef AGX_ORSET_BATCH
 #define AGX_ORSET_BATCH 2
 #endif
-    constexpr uint32_t kE = AGX_ORSET_BATCH;  // elements per batch (8 row words + 4 state words each)
+    constexpr uint32_t kE = AGX_ORSET_BATCH;  // elements per batch (their live dots + 4 state words each)
+    uint32_t ro = kOrRowDots;                 // next live dot of the (sparse) row
     for (uint32_t e0 = 0; e0 < AGX_ORSET_ELEMS; e0 += kE) {
-      uint4 ra[kE], rb[kE];
+      uint32_t rm[kE];
       uint64_t s[kE][4];
 #pragma unroll
       for (uint32_t u = 0; u < kE; ++u) {
-        ra[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u));
-        rb[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u) + 4);
+        rm[u] = reinterpret_cast<const uint8_t*>(row + kOrRowMask)[e0 + u];
 #pragma unroll
         for (int k = 0; k < 4; ++k) s[u][k] = st[(size_t)(4 * (e0 + u) + k) * nl];
       }
 #pragma unroll
       for (uint32_t u = 0; u < kE; ++u) {
-        const uint32_t r[8] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w, rb[u].x, rb[u].y, rb[u].z, rb[u].w};
+        uint32_t r[8];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) r[n] = (rm[u] >> n) & 1u ? row[ro++] : 0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const uint64_t sv = s[u][k];
@@ -572,7 +586,39 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       const uint32_t f = P.n_global > 1 && (!dm || key_size(self, P.n_global) > 1) ? P.gossip_f : 0u;
       if (f) {
         const uint32_t h = row_cursor++;
-        if (h < H.rows) {  // snapshot of the current state (+ deltaVersions), shared by the f gossips
+        if (h < H.rows && kind == AGX_KIND_ORSET) {  // sparse snapshot (kOrRow*), shared by the f gossips
+          uint32_t* row = H.wrow(h);
+          const uint32_t vw = AGX_ORSET_ELEMS * AGX_CRDT_NODES / 2;
+          uint32_t o = kOrRowDots;
+          for (uint32_t e0 = 0; e0 < AGX_ORSET_ELEMS; e0 += 4) {  // four elements' dots (one mask word) per batch
+            uint64_t d[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int k = 0; k < 4; ++k) d[u][k] = st[(size_t)(4 * (e0 + u) + k) * nl];
+            uint32_t mw = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int n = 0; n < 8; ++n) {
+                const uint32_t x = (uint32_t)(d[u][n >> 1] >> (32 * (n & 1)));
+                if (x) {
+                  row[o++] = x;
+                  mw |= 1u << (8 * u + n);
+                }
+              }
+            row[kOrRowMask + e0 / 4] = mw;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint64_t v = st[(vw + k) * nl];
+            row[kOrRowVV + 2 * k] = (uint32_t)v;
+            row[kOrRowVV + 2 * k + 1] = (uint32_t)(v >> 32);
+          }
+          if (dm)
+#pragma unroll
+            for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) row[kOrRowDV + n] = s32.ld(dl_env(kind) + n);
+        } else if (h < H.rows) {  // snapshot of the current state (+ deltaVersions), shared by the f gossips
           uint32_t* row = H.wrow(h);
           const uint32_t nw = crdt_words(kind) + (dm ? AGX_CRDT_NODES / 2u : 0u);  // batches of 4 (loads first)
           for (uint32_t i0 = 0; i0 < nw; i0 += 4) {
@@ -674,9 +720,14 @@ __device__ __forceinline__ void orset_merge_wave(const DevParams& P, const CrdtH
     const uint32_t arg = pv & 0xFFFFFFu;
     if (c == kOrMerge) {  // ORSet.merge: dots per (element, node) against both vvectors, then vvector max
       const uint32_t* row = H.row(pv & kHandleMask);
-      const uint4 ra = *reinterpret_cast<const uint4*>(row + 8 * e), rb = *reinterpret_cast<const uint4*>(row + 8 * e + 4);
-      const uint4 va = *reinterpret_cast<const uint4*>(row + 2 * vw), vb = *reinterpret_cast<const uint4*>(row + 2 * vw + 4);
-      const uint32_t r[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+      // sparse row: element e's live dots start after the earlier elements' (a wave prefix count)
+      const uint32_t rm = reinterpret_cast<const uint8_t*>(row + kOrRowMask)[e];
+      const uint32_t rc = __popc(rm);
+      uint32_t ro = kOrRowDots + wave_incl_sum(rc) - rc;
+      const uint4 va = *reinterpret_cast<const uint4*>(row + kOrRowVV), vb = *reinterpret_cast<const uint4*>(row + kOrRowVV + 4);
+      uint32_t r[8];
+#pragma unroll
+      for (int n = 0; n < 8; ++n) r[n] = (rm >> n) & 1u ? row[ro++] : 0u;
       const uint32_t rvv[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
@@ -700,13 +751,20 @@ __device__ __forceinline__ void orset_merge_wave(const DevParams& P, const CrdtH
       }
     } else if (c == kOrSnap && f) {  // snapshot row: element e per lane, the vvector from lane 0
       const uint32_t hr = h++;
-      if (hr < H.rows) {
+      if (hr < H.rows) {  // sparse row (kOrRow*): lane e's node mask byte and its live dots
         uint32_t* row = H.wrow(hr);
-        *reinterpret_cast<uint4*>(row + 8 * e) = make_uint4(d[0], d[1], d[2], d[3]);
-        *reinterpret_cast<uint4*>(row + 8 * e + 4) = make_uint4(d[4], d[5], d[6], d[7]);
+        uint32_t m = 0;
+#pragma unroll
+        for (int n = 0; n < 8; ++n) m |= d[n] ? 1u << n : 0u;
+        const uint32_t cnt = __popc(m);
+        uint32_t o = kOrRowDots + wave_incl_sum(cnt) - cnt;
+        reinterpret_cast<uint8_t*>(row + kOrRowMask)[e] = (uint8_t)m;
+#pragma unroll
+        for (int n = 0; n < 8; ++n)
+          if (d[n]) row[o++] = d[n];
         if (e == 0) {
-          *reinterpret_cast<uint4*>(row + 2 * vw) = make_uint4(cur[0], cur[1], cur[2], cur[3]);
-          *reinterpret_cast<uint4*>(row + 2 * vw + 4) = make_uint4(cur[4], cur[5], cur[6], cur[7]);
+          *reinterpret_cast<uint4*>(row + kOrRowVV) = make_uint4(cur[0], cur[1], cur[2], cur[3]);
+          *reinterpret_cast<uint4*>(row + kOrRowVV + 4) = make_uint4(cur[4], cur[5], cur[6], cur[7]);
         }
       }
     }

@@ -12,7 +12,7 @@ STEPS=${STEPS:-"full gpu bench"}
 for s in $STEPS; do
   case $s in
     full)
-      timeout -k 10 1000 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 900 --timeout-method thread \
+      timeout -k 10 1000 python -u -m pytest tests/test_gpu_fullsize.py -x -v -k "${FULL_K:-.}" --timeout 900 --timeout-method thread \
         > gpurun_out/${TAG}_full.log 2>&1 || { echo "fullsize failed"; tail -60 gpurun_out/${TAG}_full.log; exit 1; }
       tail -3 gpurun_out/${TAG}_full.log ;;
     gpu)

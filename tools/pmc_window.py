@@ -54,6 +54,13 @@ def supersteps(rows):
             if first_of_step:
                 step += 1
         out.append((eng, step))
+    # the memsets / copies right before an engine's first superstep are that engine's setup
+    for i, (_, k, _) in enumerate(rows):
+        if (k in SETUP_KERNELS or k == "k_chunk_hist") and i and rows[i - 1][1] != "k_chunk_hist":
+            j = i - 1
+            while j >= 0 and rows[j][1].startswith("__amd_rocclr"):
+                out[j] = (out[j][0], -1)
+                j -= 1
     return out
 
 
