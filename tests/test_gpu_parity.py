@@ -260,6 +260,8 @@ MULTIPASS_CASES = {
     "zipf": lambda: wl.zipf_fanout(40_000, k=4, ttl=3, root_every=32, throughput=1000),
     "power_law": lambda: wl.power_law_forward(50_000, ttl=5, capacity=8, throughput=5),
     "crdt": lambda: wl.crdt_mixed(20_000, rounds=4, throughput=2, capacity=5),
+    # (ORSet-only full state: the wave path, orset_protocol + k_orset_merge, with sparse snapshot rows)
+    "orset": lambda: wl.crdt_gossip(20_000, Kind.ORSET, rounds=6),
 }
 
 
@@ -403,7 +405,7 @@ def test_bucket_width_rejects_bad_values(built):
 @pytest.mark.parametrize("launch", ["1", "0"])
 @pytest.mark.parametrize("tiny", [0, 16, 128])
 @pytest.mark.parametrize("ba", [32, 2048])
-@pytest.mark.parametrize("case", sorted(set(MULTIPASS_CASES) - {"crdt"}))
+@pytest.mark.parametrize("case", sorted(set(MULTIPASS_CASES) - {"crdt", "orset"}))
 def test_tiny_wave_path(built, monkeypatch, launch, tiny, ba, case):
     """Multi-pass supersteps: inboxes of <= AGX_TINY messages are drained by one wave (no block
     barrier), the others by the block path -- both bit-exact against the oracle (0 = block only).
