@@ -1512,44 +1512,6 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     uint32_t* const stk = kLds ? L.key : a.scr.key + lo;
     uint32_t* const sts = kLds ? L.src : a.scr.src + lo;
     uint32_t* const stp = kLds ? L.pay : a.scr.pay + lo;
-    // FORWARD_RR: every drained message's destination up front.  The c-th forward of an actor goes
-    // to out-edge (cursor + c) mod deg, so the four actors' q-th messages look theirs up together
-    // (one round trip per message index instead of one dependent col load per message inside the
-    // serial drain), written over the message's sender, which FORWARD_RR does not read
-    if constexpr (kFwd) {
-      // (per round, each actor's segment, drain count and cursor come back from LDS: only the four
-      // forward counters stay in registers across the rounds)
-      auto fwd_nd = [&](int j, uint32_t& s0) -> uint32_t {
-        const uint32_t la = j * kBThreads + tid;
-        s0 = L.seg[la];
-        const uint32_t len = L.seg[la + 1] - s0, ab = L.alive[la];
-        uint32_t Ca, Ta;
-        mbox_limits(P, ab, Ca, Ta);
-        return la < na && len && (ab & 1u) && fdeg[j] != kNoHint && fdeg[j] > 0u ? min(len, Ta) : 0u;
-      };
-      uint32_t c4[kBAct] = {0u, 0u, 0u, 0u}, dmax = 0;
-#pragma unroll
-      for (int j = 0; j < kBAct; ++j) {
-        uint32_t s0;
-        dmax = max(dmax, fwd_nd(j, s0));
-      }
-      for (uint32_t q = 0; q < dmax; ++q) {
-        uint32_t dv[kBAct], so[kBAct];
-        bool wr[kBAct];
-#pragma unroll
-        for (int j = 0; j < kBAct; ++j) {
-          const uint32_t nd = fwd_nd(j, so[j]);
-          const uint32_t pv = q < nd ? stp[so[j] + q] : 0u;
-          const uint32_t cur = (uint32_t)w1s[j * kBThreads + tid];  // (a hint exists only for cursors < 2^32)
-          wr[j] = pv > 0 && (uint64_t)cur + c4[j] <= 0xFFFFFFFFull;
-          dv[j] = wr[j] ? (c4[j] == 0 ? fdst[j] : P.col[frb[j] + (cur + c4[j]) % fdeg[j]]) : 0u;
-          c4[j] += wr[j] ? 1u : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < kBAct; ++j)
-          if (wr[j]) sts[so[j] + q] = dv[j];
-      }
-    }
     uint32_t ecl[kBAct];
     auto sp_actor = [&](int j) {
       const uint32_t la = j * kBThreads + tid;
@@ -1565,8 +1527,14 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       const uint32_t nd = min(len, Ta);
       uint32_t kcur = L.kind[la];  // (a compiled behaviour's become changes it)
       ++nact;
-      uint32_t hdeg = kNoHint;
-      if constexpr (kFwd) hdeg = j == 0 ? fdeg[0] : j == 1 ? fdeg[1] : j == 2 ? fdeg[2] : fdeg[3];  // (j wave-uniform)
+      uint64_t hb = 0;
+      uint32_t hdeg = kNoHint, hdst = 0;
+      bool fresh = true;  // no forward yet: the next edge is fdst
+      if constexpr (kFwd) {  // (j is wave-uniform)
+        hb = j == 0 ? frb[0] : j == 1 ? frb[1] : j == 2 ? frb[2] : frb[3];
+        hdeg = j == 0 ? fdeg[0] : j == 1 ? fdeg[1] : j == 2 ? fdeg[2] : fdeg[3];
+        hdst = j == 0 ? fdst[0] : j == 1 ? fdst[1] : j == 2 ? fdst[2] : fdst[3];
+      }
       for (uint32_t q = 0; q < nd; ++q) {
         const uint32_t sv = sts[s0 + q], pv = stp[s0 + q];
         uint32_t r;
@@ -1582,9 +1550,11 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         } else if (kFwd && hdeg != kNoHint && wv[1] <= 0xFFFFFFFFull) {
           // apply_msg's FORWARD_RR with the prefetched row (same cursor arithmetic)
           wv[0] += 1;
-          if (pv > 0 && hdeg) {  // (the destination was looked up above, in the sender's slot)
+          if (pv > 0 && hdeg) {
+            const uint32_t d = fresh ? hdst : P.col[hb + (uint32_t)wv[1] % hdeg];
+            fresh = false;
             wv[1] += 1;
-            em(sv, pv - 1);
+            em(d, pv - 1);
           }
           r = AGX_RES_SAME;
         } else {
