@@ -56,6 +56,24 @@ for s in $STEPS; do
           -- python3 tools/cfg_one.py $c > gpurun_out/${TAG}_prof_$c.log 2>&1 || { echo "prof $c failed"; tail -30 gpurun_out/${TAG}_prof_$c.log; exit 1; }
         echo "prof $c ok"
       done ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.log 2>&1 \
+        || { echo "smoke failed"; tail -30 gpurun_out/${TAG}_smoke.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_smoke.log ;;
+    benchprof)  # rocprofv3 kernel trace + stats of the driver's bench command itself
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_benchprof -o run \
+        -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_benchprof.json 2> gpurun_out/${TAG}_benchprof.err \
+        || { echo "benchprof failed"; tail -30 gpurun_out/${TAG}_benchprof.err; exit 1; }
+      echo "benchprof ok" ;;
+    pmcring)  # counter passes of the ring operating points (1M fused + 100M multi-pass), one run each
+      i=0
+      for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES"; do
+        i=$((i+1))
+        timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${TAG}_ring_p$i -o run \
+          -- python3 bench.py --steps 20 --warmup 4 --no-cpu-baseline --no-configs --large-steps 8 > gpurun_out/${TAG}_ring_p$i.log 2>&1 \
+          || { echo "ring pmc pass $i failed"; tail -20 gpurun_out/${TAG}_ring_p$i.log; exit 1; }
+        echo "ring pmc pass $i ok"
+      done ;;
     bench)
       timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_bench.json \
         2> gpurun_out/${TAG}_bench.err || { echo "bench failed"; tail -40 gpurun_out/${TAG}_bench.err; exit 1; }
