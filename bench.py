@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--cpu-hops", type=int, default=96, help="hop budget of the bounded CPU sample")
     ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (N=1 only)")
     ap.add_argument("--quick-configs", action="store_true", help="C5 at 10M instead of 100M actors")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_r03.json"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_r04.json"),
                     help="PMC traffic summary written by profiles/collect_pmc.py")
     return ap.parse_args()
 
