@@ -2674,9 +2674,12 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scan(BucketArgs a, Sk
 }
 
 static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a, SkewArgs k) {
+  // (80 KB of LDS or less: two workgroups per CU -- with a per-actor totals array beside these it
+  // was 82 KB, one workgroup per CU)
   __shared__ __attribute__((aligned(16))) uint16_t whist[kBWaves * kBucket];  // 32 KB
-  __shared__ uint32_t s_run[kBucket], s_keep[kBucket], s_ds[kBucket + 1], s_bs[kBucket], s_tmp[kBucket], s_T[kBucket];
-  uint32_t* const s_first = s_tmp;  // backlog parts: first position of each actor's run in the part
+  __shared__ uint32_t s_run[kBucket], s_keep[kBucket], s_ds[kBucket + 1], s_bs[kBucket], s_T[kBucket];
+  // backlog parts (no ranking): first position of each actor's run in the part, over whist
+  uint32_t* const s_first = reinterpret_cast<uint32_t*>(whist);
   __shared__ uint32_t s_q[3];
   const DevParams& P = a.P;
   const uint32_t tid = threadIdx.x, w = tid / kWave, lane = lane_id(), nparts = k.meta[0];
@@ -2797,7 +2800,10 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
 #pragma unroll
       for (int u = 0; u < kBIpt; ++u) rk[u] = wave_rank(live[u], kk[u] & amask, a.bb, whist + w * kBucket, ltm);
       __syncthreads();
-      for (uint32_t la = tid; la < kBucket; la += kBThreads) {
+      uint32_t tot[kBucket / kBThreads];  // this thread's actors' arrivals in the sub-tile
+#pragma unroll
+      for (uint32_t i = 0; i < kBucket / kBThreads; ++i) {
+        const uint32_t la = i * kBThreads + tid;
         uint32_t run = 0;
 #pragma unroll
         for (int x = 0; x < kBWaves; ++x) {
@@ -2805,7 +2811,7 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
           whist[x * kBucket + la] = (uint16_t)run;
           run += c2;
         }
-        s_tmp[la] = run;
+        tot[i] = run;
       }
       __syncthreads();
 #pragma unroll
@@ -2816,7 +2822,8 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
         if (rank < s_keep[la]) place(la, rank, kk[u], sv[u], pv[u]);
       }
       __syncthreads();
-      for (uint32_t la = tid; la < kBucket; la += kBThreads) s_run[la] += s_tmp[la];
+#pragma unroll
+      for (uint32_t i = 0; i < kBucket / kBThreads; ++i) s_run[i * kBThreads + tid] += tot[i];
       __syncthreads();
     }
   }
