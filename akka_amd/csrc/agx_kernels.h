@@ -396,7 +396,8 @@ __device__ __forceinline__ uint64_t block_scan_table(const uint32_t* in, uint32_
   return t;
 }
 
-constexpr uint32_t kMaxUnitChunks = kThreads;  // chunks per histogram unit (G) — one per thread
+constexpr uint32_t kMaxUnitChunks = kThreads - 4;  // chunks per histogram unit (G) — one per thread (252: the
+                                                   // chunk downsweep's LDS stays within 40 KB, 4 workgroups/CU)
 constexpr uint32_t kBlSlice = kThreads * 8;     // backlog-prefix slice (buckets per rowscan block)
 constexpr uint32_t kMaxBlSlices = kWave;        // nb <= 2^17 (n_local < 2^28): one wave sums the slices
 
@@ -616,11 +617,15 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_rowscan(ChunkSortArgs
 }
 
 static __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortArgs a) {
+  // 40 KB of LDS or less (four workgroups per CU, not three): the digit bases stay in registers
+  // (thread t owns digits t and t + kThreads), the block scans' scratch lives in s_gadj's first
+  // words (as in k_sort_downsweep), the chunk prefix keeps its total at index nc
+  static_assert(kRadix == 2 * kThreads, "two digit bases per thread");
   __shared__ uint32_t whist[kWaves][kRadix];
-  __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
-  __shared__ uint32_t scratch[kWaves + 1];
+  __shared__ uint32_t s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
   __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
-  __shared__ uint32_t s_cpre[kMaxUnitChunks + 2], s_coff[kMaxUnitChunks];
+  __shared__ uint32_t s_cpre[kMaxUnitChunks + 1], s_coff[kMaxUnitChunks];
+  uint32_t* const scratch = s_gadj;
   const SplitLds S{&whist[0][0], s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
   const int tid = threadIdx.x;
   const uint32_t nd = 1u << a.bits;
@@ -628,11 +633,14 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortAr
   // (split launch: the digit rows were not scanned -- the total is the identity stream's, and
   // k_bucket_bounds writes the bucket starts)
   const bool idsk = idn && a.part == 2;
-  const uint32_t total = idsk ? a.ident[2] : digit_bases(a.tot, nd, s_dbase, scratch);
+  const uint32_t total = idsk ? a.ident[2] : digit_bases(a.tot, nd, s_base, scratch);
+  const uint32_t db0 = idsk ? 0u : s_base[tid], db1 = idsk ? 0u : s_base[tid + kThreads];  // digit bases
   const bool over = total > a.cap;  // the sorted mail must fit A (the apply checks mail + backlog)
   if (blockIdx.x == 0) {
-    if (!idsk)
-      for (uint32_t d = tid; d < nd; d += kThreads) a.bstart[d] = s_dbase[d];
+    if (!idsk) {
+      if ((uint32_t)tid < nd) a.bstart[tid] = db0;
+      if ((uint32_t)tid + kThreads < nd) a.bstart[tid + kThreads] = db1;
+    }
     if (tid == 0) {
       a.bstart[nd] = total;
       *a.d_n = over ? 0u : total;
@@ -672,10 +680,15 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortAr
     }
     // this unit's per-digit prefix (from the rowscan); the column is then zeroed so
     // that the next k_bucket_apply can accumulate fresh counts without a memset
-    for (uint32_t d = tid; d < nd; d += kThreads) {
-      uint32_t* hp = a.hist + (size_t)d * a.stride + u;
-      s_base[d] = s_dbase[d] + *hp;
-      *hp = 0u;
+    __syncthreads();  // (the previous unit's tiles are done with s_base; digit_bases' reads of it too)
+#pragma unroll
+    for (uint32_t j = 0; j < 2; ++j) {
+      const uint32_t d = tid + j * kThreads;
+      if (d < nd) {
+        uint32_t* hp = a.hist + (size_t)d * a.stride + u;
+        s_base[d] = (j ? db1 : db0) + *hp;
+        *hp = 0u;
+      }
     }
     if (idn) continue;
     // the unit's chunks as one stream (tiles cross chunk boundaries: small chunks — skewed
@@ -688,15 +701,15 @@ static __global__ void __launch_bounds__(kThreads) k_chunk_downsweep(ChunkSortAr
       if (j < nc) s_coff[j] = a.ch.off[c0 + j];
       uint32_t t;
       const uint32_t ex = block_excl_sum<kThreads>(v, scratch, &t);
-      if (j <= nc) s_cpre[j] = ex;
-      if (j == 0) s_cpre[kMaxUnitChunks + 1] = t;
+      if (j <= nc) s_cpre[j] = ex;  // (s_cpre[nc] = the unit's total)
+      if (j == 0) s_cpre[nc] = t;
     }
     __syncthreads();
-    const uint32_t ntot = s_cpre[kMaxUnitChunks + 1];
+    const uint32_t ntot = s_cpre[nc];
     const CMsgs& src = a.ch.arena(c0);  // one arena per unit
     if (ntot >= nc * (uint32_t)(kTile / 2)) {  // large chunks: tile by tile, direct addressing
       for (uint32_t j = 0; j < nc; ++j) {
-        const uint32_t cnt = s_cpre[j + 1 <= nc - 1 ? j + 1 : kMaxUnitChunks + 1] - s_cpre[j];
+        const uint32_t cnt = s_cpre[j + 1] - s_cpre[j];
         for (uint32_t sub = 0; sub < cnt; sub += kTile)
           split_tile<kThreads>(src, s_coff[j] + sub, min((uint32_t)kTile, cnt - sub), a.out, a.shift, a.bits, S);
       }
@@ -816,8 +829,11 @@ static __global__ void __launch_bounds__(kThreads) k_sort_downsweep(SortArgs a) 
   if (a.ident && a.ident[0]) return;
   __shared__ uint32_t whist[kWaves][kRadix];
   __shared__ uint32_t s_dbase[kRadix], s_base[kRadix], s_ldig[kRadix], s_gadj[kRadix];
-  __shared__ uint32_t scratch[kWaves + 1];
   __shared__ uint32_t s_key[kTile], s_src[kTile], s_pay[kTile];
+  // the block scans' scratch lives in s_gadj's first kWaves + 1 words: digit_bases runs before any
+  // tile, and a tile scans its digit starts before it writes s_gadj (and after the previous tile's
+  // scatter, which read it, has passed its barrier) -- 40 KB of LDS exactly: four workgroups per CU
+  uint32_t* const scratch = s_gadj;
   const SplitLds S{&whist[0][0], s_base, s_ldig, s_gadj, scratch, s_key, s_src, s_pay};
   const int tid = threadIdx.x;
   const uint32_t n = *a.d_n, super = pass_super(a, n), nt = div_up(n, super);
