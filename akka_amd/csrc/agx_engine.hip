@@ -163,6 +163,8 @@ struct agx_engine {
   uint64_t gossip_seed = 0;
   uint32_t *d_heap = nullptr, *d_heap_top = nullptr, *d_step = nullptr;
   uint32_t *d_rx = nullptr, *d_s2rows = nullptr;  // multi-rank: received rows / rows packed for sending
+  uint64_t rx_rows = 0;                            // rows of d_rx (>= cap; >= R x slab on the device path)
+  uint32_t* d_srows = nullptr;                     // device-resident exchange: [R][slab][pw] row send slabs
   uint32_t *d_s2p = nullptr, *d_rcvp = nullptr;    // multi-rank: tells as (key, src, payload) triples, sent / received
   // device-resident multi-rank replays (run_multi_rccl, plain behaviours): fixed per-peer slabs of
   // `slab` envelopes, the replay's stop word halt[2] (k_mr_pack); h_halt = its pinned copy
@@ -1445,6 +1447,20 @@ agx_status mr_slabs(agx_engine* e, uint64_t want) {
   e->slab = 0;
   AGX_TRY(dalloc(&e->d_sslab, (uint64_t)e->R * n * 3));
   AGX_TRY(dalloc(&e->d_rslab, (uint64_t)e->R * n * 3));
+  if (e->pw) {  // CRDT rows: row send slabs, and rx large enough to receive R slabs of rows
+    const uint64_t rr = (uint64_t)e->R * n;
+    if (e->heap_rows + std::max<uint64_t>(rr, e->rx_rows) >= kHandleMask)
+      return set_err(AGX_ECAPACITY, "multi-rank CRDT row slabs of %u exceed the row handle space", n);
+    hipFree(e->d_srows);
+    e->d_srows = nullptr;
+    AGX_TRY(dalloc(&e->d_srows, rr * e->pw));
+    if (rr > e->rx_rows) {
+      hipFree(e->d_rx);
+      e->d_rx = nullptr;
+      AGX_TRY(dalloc(&e->d_rx, rr * e->pw));
+      e->rx_rows = rr;
+    }
+  }
   e->slab = n;
   drop_graphs(e);  // (the slabs are kernel and collective arguments of a captured replay)
   return AGX_OK;
@@ -1502,6 +1518,10 @@ agx_status mr_step_dev(agx_engine* e, uint32_t idx) {
   a.rank = e->rank;
   a.slab = e->slab;
   a.step = idx;
+  a.s2rows = e->d_s2rows;
+  a.srows = e->d_srows;
+  a.pw = e->pw;
+  a.heap_rows = (uint32_t)e->heap_rows;
   const dim3 g(grid_for((uint64_t)e->R * e->slab / kThreads + 1, 2048));
   {
     Scope sc(e, K_EXCHANGE);
@@ -1512,6 +1532,12 @@ agx_status mr_step_dev(agx_engine* e, uint32_t idx) {
       if (q == e->rank) continue;
       NCCL_TRY(ncclSend(e->d_sslab + (size_t)q * e->slab * 3, 3ull * e->slab, ncclUint32, (int)q, e->comm, e->stream));
       NCCL_TRY(ncclRecv(e->d_rslab + (size_t)q * e->slab * 3, 3ull * e->slab, ncclUint32, (int)q, e->comm, e->stream));
+      if (e->pw) {  // the state gossips' rows, slab-sized as well
+        NCCL_TRY(ncclSend(e->d_srows + (size_t)q * e->slab * e->pw, (size_t)e->slab * e->pw, ncclUint32, (int)q, e->comm,
+                          e->stream));
+        NCCL_TRY(ncclRecv(e->d_rx + (size_t)q * e->slab * e->pw, (size_t)e->slab * e->pw, ncclUint32, (int)q, e->comm,
+                          e->stream));
+      }
     }
     NCCL_TRY(ncclGroupEnd());
     hipLaunchKernelGGL(k_mr_unpack, g, dim3(kThreads), 0, e->stream, a);
@@ -1569,9 +1595,9 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
   };
   uint32_t left = max_steps;
   bool quiet = false;
-  // device-resident replays (plain behaviours: CRDT rows keep the host-planned exchange); a staged
+  // device-resident replays (CRDT rows travel in row slabs beside the envelope slabs); a staged
   // burst enters through one host-planned superstep (its staged count is a host number)
-  const bool dev = e->pw == 0 && !getenv("AGX_MR_HOST");
+  const bool dev = !getenv("AGX_MR_HOST");
   if (dev && e->n_staged_dev && left) {
     AGX_TRY(host_step(&quiet));
     --left;
@@ -1663,6 +1689,10 @@ agx_status enable_crdt(agx_engine* e, uint32_t kind) {
   if (e->R > 1) {
     AGX_TRY(dalloc(&e->d_rx, e->cap * pw));
     AGX_TRY(dalloc(&e->d_s2rows, e->cap_emit * pw));
+    e->rx_rows = e->cap;
+    hipFree(e->d_srows);
+    e->d_srows = nullptr;
+    e->slab = 0;  // (the row slabs are sized with the envelope slabs, for this pitch)
   }
   e->pw = pw;
   drop_graphs(e);
@@ -2023,7 +2053,7 @@ agx_status agx_destroy(agx_engine* e) {
   if (e->h_stat) hipHostFree(e->h_stat);
   for (auto ev : e->lag_ev)
     if (ev) hipEventDestroy(ev);
-  hipFree(e->d_heap); hipFree(e->d_heap_top); hipFree(e->d_step); hipFree(e->d_rx); hipFree(e->d_s2rows);
+  hipFree(e->d_heap); hipFree(e->d_heap_top); hipFree(e->d_step); hipFree(e->d_rx); hipFree(e->d_s2rows); hipFree(e->d_srows);
   hipFree(e->d_bcase); hipFree(e->d_bact); hipFree(e->d_bfirst);
   if (e->h_pin) hipHostFree(e->h_pin);
   if (e->h_pin64) hipHostFree(e->h_pin64);

@@ -3559,6 +3559,11 @@ struct MrArgs {
   uint64_t* stats;
   uint64_t cap;
   uint32_t R, rank, slab, step;
+  // CRDT rows (pw > 0): row i of s2rows belongs to tell i of s2 (k_pack_rows); a state gossip to
+  // peer q travels as row i of srows[q] beside its envelope, and lands in rx[sender][i]
+  const uint32_t* s2rows;
+  uint32_t* srows;        // [R][slab][pw]
+  uint32_t pw, heap_rows;
 };
 
 // the plan every block derives from cmat: own send offsets, receive offsets, counts, the decision
@@ -3623,6 +3628,22 @@ static __global__ void __launch_bounds__(kThreads) k_mr_pack(MrArgs a) {
       d[3 * i + 2] = a.s2.pay[o + i];
     }
   }
+  if (!a.pw) return;
+  // state gossips' rows -> the row slabs (a wave copies its lanes' rows one after the other)
+  const uint32_t lane = lane_id();
+  for (uint32_t q = 0; q < a.R; ++q) {
+    if (q == a.rank) continue;
+    const uint32_t o = p.soff[q], n = p.scnt[q];
+    for (uint32_t ib = blockIdx.x * kThreads + threadIdx.x - lane; ib < n; ib += gridDim.x * kThreads) {
+      const uint32_t i = ib + lane;
+      for (uint64_t mm = __ballot(i < n && is_wide(a.s2.src[o + i])); mm; mm &= mm - 1) {
+        const uint32_t j = ib + (uint32_t)__builtin_ctzll(mm);
+        const uint4* sr = reinterpret_cast<const uint4*>(a.s2rows + (size_t)(o + j) * a.pw);
+        uint4* dr = reinterpret_cast<uint4*>(a.srows + ((size_t)q * a.slab + j) * a.pw);
+        for (uint32_t k2 = lane; k2 < a.pw / 4; k2 += kWave) dr[k2] = sr[k2];
+      }
+    }
+  }
 }
 
 // received slabs (and the own run) -> A after the backlog, sender-rank order
@@ -3645,7 +3666,8 @@ static __global__ void __launch_bounds__(kThreads) k_mr_unpack(MrArgs a) {
       const uint32_t* s = a.rslab + ((size_t)r * a.slab + j) * 3;
       a.A.key[o] = s[0];
       a.A.src[o] = s[1];
-      a.A.pay[o] = s[2];
+      // a state gossip's row arrived in rx[r][j]: its handle points there
+      a.A.pay[o] = a.pw && is_wide(s[1]) ? (s[2] & ~kHandleMask) | (a.heap_rows + r * a.slab + j) : s[2];
     }
   }
 }

@@ -1,8 +1,9 @@
 """The real multi-process RCCL path on one GPU: N ranks (processes) with one engine each,
 agx_comm_init + run_multi_rccl (ncclAllGather of the count vectors, grouped
 ncclSend/ncclRecv of envelopes and CRDT rows), bit-exact against the BSP oracle in the
-sharded canonical order.  Plain behaviours run the device-resident replays (fixed per-peer
-slabs, k_mr_pack / k_mr_unpack, no host round trip per superstep); `env` forces the
+sharded canonical order.  Every behaviour runs the device-resident replays (fixed per-peer
+slabs, k_mr_pack / k_mr_unpack, no host round trip per superstep; CRDT state rows travel in row
+slabs beside the envelope slabs); `env` forces the
 host-planned exchange (AGX_MR_HOST) or tiny slabs (AGX_MR_SLAB: the first superstep's counts
 overflow them -> the host redoes that exchange exactly, grows the slabs and the replays resume).  tools/rccl_two_rank.py gives every rank its own NCCL_HOSTID so
 RCCL accepts several ranks on one device (socket transport on loopback)."""
@@ -26,7 +27,11 @@ ROOT = pathlib.Path(__file__).resolve().parents[1]
     ("zipf", 2, 30_000, 3, {"AGX_MR_SLAB": "2000"}),   # fan-out grows 4x: the slab overflows mid-replay
     ("ring", 2, 20_000, 12, {"RESTAGE": "5"}),         # a staged burst between device-resident replays
     ("mixed", 3, 20_000, 8, {}),
-    ("orset", 2, 6_000, 6, {}),  # (CRDT rows: the host-planned exchange)
+    ("orset", 2, 6_000, 6, {}),  # CRDT rows in row slabs beside the envelope slabs
+    ("orset", 2, 6_000, 6, {"AGX_MR_SLAB": "64"}),     # row slabs overflow -> exact exchange, regrown
+    ("orset", 3, 6_000, 6, {"AGX_MR_HOST": "1"}),      # CRDT rows over the host-planned exchange
+    ("orset_delta", 2, 4_096, 4, {}),
+    ("crdt_mixed", 3, 5_000, 5, {}),
     ("power", 4, 60_000, 8, {}),
     ("zipf", 2, 30_000, 3, {}),
     ("zipf", 4, 40_000, 3, {}),     # C3 sharded over 4 ranks

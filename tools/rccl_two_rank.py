@@ -37,6 +37,10 @@ def _make(a):
         return wl.token_ring(a.n, a.hops)
     if a.workload == "orset":  # CRDT snapshot rows travel beside the envelopes
         return wl.crdt_gossip(a.n, Kind.ORSET, rounds=a.hops, throughput=2)
+    if a.workload == "orset_delta":  # delta rows (DeltaPropagation) and full-state gossips
+        return wl.crdt_delta(a.n, Kind.ORSET, rounds=a.hops, ops_per_replica=2, gossip_rounds=2, throughput=2)
+    if a.workload == "crdt_mixed":  # GCounter / PNCounter / ORSet rows of three pitches' kinds
+        return wl.crdt_mixed(a.n, rounds=a.hops, throughput=2)
     if a.workload == "power":  # C5 shape: bounded(64) forwarding over the R-MAT graph
         return wl.power_law_forward(a.n, ttl=a.hops, capacity=64, throughput=5, device_graph=True)
     if a.workload == "zipf":
