@@ -31,14 +31,14 @@ hipError_t agx_launch_tiny_g4(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_tiny_g5(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_tiny_g6(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_tiny_g7(uint32_t, dim3, hipStream_t, const BucketArgs&);
-hipError_t agx_launch_ring_g0(uint32_t, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
-hipError_t agx_launch_ring_g1(uint32_t, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
-hipError_t agx_launch_ring_g2(uint32_t, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
-hipError_t agx_launch_ring_g3(uint32_t, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
-hipError_t agx_launch_ring_g4(uint32_t, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
-hipError_t agx_launch_ring_g5(uint32_t, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
-hipError_t agx_launch_ring_g6(uint32_t, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
-hipError_t agx_launch_ring_g7(uint32_t, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
+hipError_t agx_launch_ring_g0(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
+hipError_t agx_launch_ring_g1(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
+hipError_t agx_launch_ring_g2(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
+hipError_t agx_launch_ring_g3(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
+hipError_t agx_launch_ring_g4(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
+hipError_t agx_launch_ring_g5(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
+hipError_t agx_launch_ring_g6(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
+hipError_t agx_launch_ring_g7(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
 static_assert(kVGroups == 8, "one declaration per group");
 
 namespace {
@@ -87,26 +87,29 @@ hipError_t tiny_dispatch(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& 
   }
 }
 
-// k_ring_apply of the plain / compiled variants of this group
+// k_ring_apply (tiny: k_ring_tiny) of the plain / compiled variants of this group
 template <uint32_t V>
-hipError_t ring_dispatch(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba, const RingArgs& ra) {
+hipError_t ring_dispatch(uint32_t vid, bool tiny, dim3 g, hipStream_t s, const BucketArgs& ba, const RingArgs& ra) {
   if constexpr (V >= V_N) {
     return hipErrorInvalidValue;
   } else {
     if constexpr (kVariantGroup[V] == AGX_VGROUP && !kVariants[V].wide)
       if (vid == V) {
-        hipLaunchKernelGGL((k_ring_apply<kVariants[V].km>), g, dim3(kBThreads), 0, s, ba, ra);
+        if (tiny)
+          hipLaunchKernelGGL((k_ring_tiny<kVariants[V].km>), g, dim3(kTinyThreads), 0, s, ba, ra);
+        else
+          hipLaunchKernelGGL((k_ring_apply<kVariants[V].km>), g, dim3(kBThreads), 0, s, ba, ra);
         return hipGetLastError();
       }
-    return ring_dispatch<V + 1>(vid, g, s, ba, ra);
+    return ring_dispatch<V + 1>(vid, tiny, g, s, ba, ra);
   }
 }
 
 }  // namespace
 
-hipError_t AGX_CAT(agx_launch_ring_g, AGX_VGROUP)(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba,
+hipError_t AGX_CAT(agx_launch_ring_g, AGX_VGROUP)(uint32_t vid, bool tiny, dim3 g, hipStream_t s, const BucketArgs& ba,
                                                   const RingArgs& ra) {
-  return ring_dispatch<0>(vid, g, s, ba, ra);
+  return ring_dispatch<0>(vid, tiny, g, s, ba, ra);
 }
 
 hipError_t AGX_CAT(agx_launch_tiny_g, AGX_VGROUP)(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba) {
@@ -131,17 +134,17 @@ hipError_t agx_launch_apply(uint32_t vid, uint32_t mode, bool skew, dim3 g, hipS
     default: return agx_launch_apply_g7(vid, mode, skew, g, s, ba);
   }
 }
-hipError_t agx_launch_ring(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba, const RingArgs& ra) {
+hipError_t agx_launch_ring(uint32_t vid, bool tiny, dim3 g, hipStream_t s, const BucketArgs& ba, const RingArgs& ra) {
   if (vid >= V_N || kVariants[vid].wide) return hipErrorInvalidValue;
   switch (kVariantGroup[vid]) {
-    case 0: return agx_launch_ring_g0(vid, g, s, ba, ra);
-    case 1: return agx_launch_ring_g1(vid, g, s, ba, ra);
-    case 2: return agx_launch_ring_g2(vid, g, s, ba, ra);
-    case 3: return agx_launch_ring_g3(vid, g, s, ba, ra);
-    case 4: return agx_launch_ring_g4(vid, g, s, ba, ra);
-    case 5: return agx_launch_ring_g5(vid, g, s, ba, ra);
-    case 6: return agx_launch_ring_g6(vid, g, s, ba, ra);
-    default: return agx_launch_ring_g7(vid, g, s, ba, ra);
+    case 0: return agx_launch_ring_g0(vid, tiny, g, s, ba, ra);
+    case 1: return agx_launch_ring_g1(vid, tiny, g, s, ba, ra);
+    case 2: return agx_launch_ring_g2(vid, tiny, g, s, ba, ra);
+    case 3: return agx_launch_ring_g3(vid, tiny, g, s, ba, ra);
+    case 4: return agx_launch_ring_g4(vid, tiny, g, s, ba, ra);
+    case 5: return agx_launch_ring_g5(vid, tiny, g, s, ba, ra);
+    case 6: return agx_launch_ring_g6(vid, tiny, g, s, ba, ra);
+    default: return agx_launch_ring_g7(vid, tiny, g, s, ba, ra);
   }
 }
 

@@ -698,9 +698,16 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   if (e->rg_on) {  // ring apply: one launch does admission, drains and ring appends (agx_ring.h)
     RingArgs ra{e->d_rg_state, e->d_rg_src, e->d_rg_pay, e->d_rg_dk, e->d_rg_ds, e->d_rg_dp, e->d_ring_total,
                 e->rg_c, e->rg_dstride};
+    const uint32_t vid = apply_variant(e);
+    if (e->tiny_launch && e->tiny_max && !e->skew_only) {  // sparse buckets a wave each, then the marked ones
+      ba.blist = e->d_blist;
+      Scope s(e, K_TINY);
+      HIP_TRY(agx_launch_ring(vid, true, dim3(grid_for((e->nb + kTinyWaves - 1) / kTinyWaves, kMaxApplyGrid)), e->stream,
+                              ba, ra));
+    }
     {
       Scope s(e, K_RINGAPPLY);
-      HIP_TRY(agx_launch_ring(apply_variant(e), dim3(grid_for(e->nb, e->apply_grid)), e->stream, ba, ra));
+      HIP_TRY(agx_launch_ring(vid, false, dim3(grid_for(e->nb, e->apply_grid)), e->stream, ba, ra));
     }
     e->par ^= 1u;
     HIP_TRY(hipGetLastError());

@@ -31,6 +31,7 @@
 namespace agx {
 
 constexpr uint32_t kRingApplyMaxC = 0xFFFFu;  // head / length are 16-bit fields
+constexpr uint32_t kRingListBatch = 32;      // marked buckets found per ballot (after k_ring_tiny)
 
 struct RingArgs {
   uint32_t* state;   // [n_local] head | len << 16
@@ -72,7 +73,24 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
   const uint32_t *Mk = sgpr_ptr(iv.m.key), *Ms = sgpr_ptr(iv.m.src), *Mp = sgpr_ptr(iv.m.pay);
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};  // delivered, dead letters, unhandled, tells, active actors
   long long dring = 0;                           // this thread's change of the messages held in rings
-  for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x) {
+  // after k_ring_tiny (a.blist set): only the buckets it marked, found kListBatch at a time by one
+  // ballot (k_bucket_apply's listed mode)
+  const bool listed = a.blist != nullptr;
+  __shared__ uint32_t s_todo;
+  for (uint32_t it = blockIdx.x; it < a.nb; it += (listed ? kRingListBatch : 1u) * gridDim.x) {
+  uint32_t todo = 1u;
+  if (listed) {
+    if (w == 0) {
+      const uint32_t bw = it + lane * gridDim.x;
+      const uint64_t mk = __ballot(lane < kRingListBatch && bw < a.nb && a.blist[bw] != 0u);
+      if (lane == 0) s_todo = (uint32_t)mk;
+    }
+    __syncthreads();
+    todo = s_todo;
+    __syncthreads();
+  }
+  for (; todo; todo &= todo - 1u) {
+    const uint32_t b = it + (uint32_t)__builtin_ctz(todo) * gridDim.x;
     const uint32_t a0 = b << a.bb;
     const uint32_t na = min(1u << a.bb, P.n_local - a0);
     AGX_STAMP(a, 0);
@@ -442,10 +460,319 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
     __syncthreads();  // (LDS reused by the next bucket)
     AGX_STAMP(a, 8);
   }
+  }
   if (blockIdx.x < a.nb) flush_stats(a, acc);
   // messages held in rings: the block's change, two's complement into the u64 total
   const uint32_t gp = wave_incl_sum(dring > 0 ? (uint32_t)dring : 0u), gn = wave_incl_sum(dring < 0 ? (uint32_t)-dring : 0u);
   if (lane == kWave - 1 && gp != gn) atomicAdd(g.total, (unsigned long long)((long long)gp - (long long)gn));
+}
+
+
+// ---- Wave-per-bucket ring apply.  A sparse superstep (C3: 4883 buckets of a few dozen arrivals
+// and a handful of actors with queued mail each) is dominated by the block kernel's per-bucket
+// chain of phases, so -- as k_tiny_apply does for the backlog arena -- every bucket whose arrivals
+// fit kTinyMax, whose actors with work (arrivals or a non-empty ring) fit kTinyMax and whose drains
+// fit kRingTinyD is done by one wave; k_ring_apply then takes only the buckets marked in a.blist.
+// Same per-actor rule as k_ring_apply (admission, ring heads first, appends, dead letters), same
+// tell order (actor order), same ring words.
+constexpr uint32_t kRingTinyD = 256;  // drained messages of a wave-path bucket
+static_assert(kBucket == 32 * kWave, "lane l owns the ring words of actors [32 l, 32 l + 32)");
+
+struct RingTinyLds {                              // one per wave (5.6 KB)
+  uint32_t src[kTinyMax], pay[kTinyMax];          // arrivals by (actor, inbox position)
+  uint32_t dk[kRingTinyD], ds[kRingTinyD], dp[kRingTinyD];  // drained messages, then the staged tells
+  uint32_t am[kWave], mw[kWave], pw[kWave];       // arrival bits, active bits, active prefix per 32 actors
+  uint16_t act[kTinyMax], ast[kTinyMax], alen[kTinyMax];  // active actors in order; their arrival runs
+};
+
+struct RingStageEmitter {  // max_emit 1: tell e of a message staged at its drain slot's run (e <= slot)
+  const DevParams* P;
+  uint32_t *key, *src, *pay;
+  uint32_t slot, self;
+  uint32_t n_valid, n_all;
+  __device__ __forceinline__ void operator()(uint32_t dst, uint32_t p) {
+    if (dst >= P->n_global) {  // the reply path (outbox) or an unknown ref -> deadLetters
+      if (!outbound_tell(*P, dst, self, p, true)) ++n_all;
+      return;
+    }
+    ++n_all;
+    ++n_valid;
+    key[slot] = dst;
+    src[slot] = self;
+    pay[slot] = p;
+    ++slot;
+  }
+  __device__ __forceinline__ void wide(uint32_t, uint32_t) {}
+};
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// returns false (nothing written) when the bucket exceeds the wave path's bounds
+template <uint32_t KM>
+__device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const RingArgs& g, const InView& iv,
+                                                 RingTinyLds& T, uint32_t b, uint32_t bs, uint32_t n) {
+  const DevParams& P = a.P;
+  const uint32_t lane = lane_id(), rc = g.rc;
+  const uint32_t amask = (1u << a.bb) - 1u, a0 = b << a.bb;
+  const uint32_t na = min(1u << a.bb, P.n_local - a0);
+  // ---- actors with queued mail: lane l's 32 ring words -> one bit each
+  uint32_t rm = 0;
+  {
+    const uint32_t o0 = lane * 32u;
+    if (o0 + 32u <= na && ((a0 + o0) & 3u) == 0u) {
+      const uint4* q4 = reinterpret_cast<const uint4*>(g.state + a0 + o0);
+      uint4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = q4[i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        rm |= (uint32_t)(v[i].x > 0xFFFFu) << (4 * i) | (uint32_t)(v[i].y > 0xFFFFu) << (4 * i + 1) |
+              (uint32_t)(v[i].z > 0xFFFFu) << (4 * i + 2) | (uint32_t)(v[i].w > 0xFFFFu) << (4 * i + 3);
+    } else {
+      for (uint32_t i = 0; i < 32u; ++i)
+        if (o0 + i < na && g.state[a0 + o0 + i] > 0xFFFFu) rm |= 1u << i;
+    }
+  }
+  // ---- arrivals: stable rank by (actor, position), run starts / lengths (tiny_bucket's rank loop)
+  uint32_t k[kTinyIpl], sv[kTinyIpl], pv[kTinyIpl], la[kTinyIpl];
+#pragma unroll
+  for (uint32_t r = 0; r < kTinyIpl; ++r) {
+    const uint32_t q = r * kWave + lane;
+    const uint32_t i = q < n ? iv.at(bs + q) : 0u;
+    k[r] = q < n ? ldg(iv.m.key, i) : 0u;
+    sv[r] = q < n ? ldg(iv.m.src, i) : 0u;
+    pv[r] = q < n ? ldg(iv.m.pay, i) : 0u;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kTinyIpl; ++r) la[r] = r * kWave + lane < n ? k[r] & amask : 0xFFFFFFFFu;
+  T.am[lane] = 0u;
+  wave_sync_lds();
+  uint32_t rank[kTinyIpl] = {}, st[kTinyIpl] = {}, len[kTinyIpl] = {};
+#pragma unroll
+  for (uint32_t r2 = 0; r2 < kTinyIpl; ++r2) {
+    const uint32_t jn = n > r2 * kWave ? min(n - r2 * kWave, (uint32_t)kWave) : 0u;
+    for (uint32_t jj = 0; jj < jn; ++jj) {
+      const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)la[r2], (int)jj), j = r2 * kWave + jj;
+#pragma unroll
+      for (uint32_t r = 0; r < kTinyIpl; ++r) {
+        const bool lt = lj < la[r], eq = lj == la[r];
+        st[r] += lt;
+        len[r] += eq;
+        rank[r] += lt || (eq && j < r * kWave + lane);
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kTinyIpl; ++r)
+    if (r * kWave + lane < n) {
+      T.src[rank[r]] = sv[r];
+      T.pay[rank[r]] = pv[r];
+      if (rank[r] == st[r]) atomicOr(&T.am[la[r] >> 5], 1u << (la[r] & 31u));
+    }
+  wave_sync_lds();
+  // ---- the active actors (arrivals or queued mail) in actor order
+  const uint32_t m = rm | T.am[lane], c = __builtin_popcount(m);
+  const uint32_t cinc = wave_incl_sum(c), A = (uint32_t)__builtin_amdgcn_readlane((int)cinc, kWave - 1);
+  if (A > kTinyMax) return false;
+  uint32_t pe = cinc - c;
+  T.mw[lane] = m;
+  T.pw[lane] = pe;
+  for (uint32_t mm = m; mm; mm &= mm - 1u, ++pe) {
+    T.act[pe] = (uint16_t)(lane * 32u + (uint32_t)__builtin_ctz(mm));
+    T.alen[pe] = 0;
+  }
+  wave_sync_lds();
+#pragma unroll
+  for (uint32_t r = 0; r < kTinyIpl; ++r)
+    if (r * kWave + lane < n && rank[r] == st[r]) {  // run head: its actor's active index
+      const uint32_t wd = la[r] >> 5, idx = T.pw[wd] + __builtin_popcount(T.mw[wd] & ((1u << (la[r] & 31u)) - 1u));
+      T.ast[idx] = (uint16_t)st[r];
+      T.alen[idx] = (uint16_t)len[r];
+    }
+  wave_sync_lds();
+  // ---- per active actor (lane j: active actors kTinyIpl j + i, so lane order is actor order)
+  uint32_t hl[kTinyIpl], sw[kTinyIpl], ab[kTinyIpl], hk[kTinyIpl], rr[kTinyIpl], da[kTinyIpl], adm[kTinyIpl],
+      Lk[kTinyIpl], arr[kTinyIpl], as0[kTinyIpl];
+  uint64_t w0[kTinyIpl], w1[kTinyIpl];
+  bool on[kTinyIpl];
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) {
+    const uint32_t x = lane * kTinyIpl + i;
+    on[i] = x < A;
+    hl[i] = on[i] ? a0 + T.act[x] : a0;
+    arr[i] = on[i] ? T.alen[x] : 0u;
+    as0[i] = on[i] ? T.ast[x] : 0u;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) {  // (all loads in flight together)
+    sw[i] = on[i] ? g.state[hl[i]] : 0u;
+    ab[i] = on[i] ? P.alive[hl[i]] : 0u;
+    hk[i] = on[i] ? P.kind[hl[i]] : 0u;
+    w0[i] = on[i] ? ldg64(P.state, sidx(P, hl[i], 0)) : 0ull;
+    w1[i] = on[i] && P.W > 1 ? ldg64(P.state, sidx(P, hl[i], 1)) : 0ull;
+  }
+  uint32_t ndead = 0, dl = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) {
+    uint32_t C, Tt;
+    mbox_limits(P, ab[i], C, Tt);
+    const uint32_t L = sw[i] >> 16;
+    const bool al = on[i] && (ab[i] & 1u) != 0;
+    Lk[i] = al ? min(L, C) : 0u;
+    rr[i] = min(Lk[i], Tt);
+    adm[i] = al ? min(arr[i], C - Lk[i]) : 0u;
+    da[i] = min(adm[i], Tt - rr[i]);
+    ndead += arr[i] - adm[i] + (L - Lk[i]);
+    dl += rr[i] + da[i];
+  }
+  const uint32_t dinc = wave_incl_sum(dl), D = (uint32_t)__builtin_amdgcn_readlane((int)dinc, kWave - 1);
+  if (D > kRingTinyD) return false;
+  // ---- drain buffer: ring heads, then the drained arrivals; admitted arrivals beyond them -> ring
+  uint32_t d0[kTinyIpl];
+  {
+    uint32_t o = dinc - dl;
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i) {
+      d0[i] = o;
+      o += rr[i] + da[i];
+    }
+  }
+  uint32_t rmax = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) rmax = max(rmax, rr[i]);
+  for (uint32_t q = 0; q < rmax; ++q) {
+    uint32_t hs[kTinyIpl], hp[kTinyIpl];
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i) {
+      uint32_t x = (sw[i] & 0xFFFFu) + q;
+      x = x < rc ? x : x - rc;
+      const size_t o = (size_t)hl[i] * rc + (q < rr[i] ? x : 0u);
+      hs[i] = g.src[o];
+      hp[i] = g.pay[o];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kTinyIpl; ++i)
+      if (q < rr[i]) {
+        T.ds[d0[i] + q] = hs[i];
+        T.dp[d0[i] + q] = hp[i];
+      }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) {
+    for (uint32_t q = 0; q < da[i]; ++q) {
+      T.ds[d0[i] + rr[i] + q] = T.src[as0[i] + q];
+      T.dp[d0[i] + rr[i] + q] = T.pay[as0[i] + q];
+    }
+    const uint32_t t0 = (sw[i] & 0xFFFFu) + Lk[i];
+    for (uint32_t q = da[i]; q < adm[i]; ++q) {  // appended: ring slot head + Lk + (rank - da)
+      uint32_t x = t0 + (q - da[i]);
+      x = x < rc ? x : (x < 2u * rc ? x - rc : x - 2u * rc);
+      const size_t o = (size_t)hl[i] * rc + x;
+      g.src[o] = T.src[as0[i] + q];
+      g.pay[o] = T.pay[as0[i] + q];
+    }
+  }
+  wave_sync_lds();
+  // ---- drain + apply, actor after actor (tell e staged at drain slot d0 + e)
+  uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0, ncount = 0;
+  uint32_t ecl[kTinyIpl];
+  long long dring = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i) {
+    ecl[i] = 0;
+    const uint32_t drn = rr[i] + da[i], l = hl[i];
+    if (drn) {
+      ++nact;
+      RingStageEmitter em{&P, T.dk + d0[i], T.ds + d0[i], T.dp + d0[i], 0, l, 0, 0};
+      uint64_t wv[2] = {w0[i], w1[i]};
+      uint32_t kcur = hk[i];
+      for (uint32_t q = 0; q < drn; ++q) {
+        const uint32_t s = T.ds[d0[i] + q], p = T.dp[d0[i] + q];
+        const uint32_t r = apply_msg<KM>(P, kcur, l, l, wv, s, p, em);
+        ++ndel;
+        if (r == AGX_RES_UNHANDLED) ++nunh;
+        if (r == AGX_RES_STOPPED) {
+          P.stopq[atomicAdd(P.nstop, 1u)] = l;
+          ndead += drn - q - 1;  // drained-but-unprocessed after the stop
+          break;
+        }
+      }
+      P.state[sidx(P, l, 0)] = wv[0];
+      if (P.W > 1) P.state[sidx(P, l, 1)] = wv[1];
+      if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
+        if (kcur != hk[i]) P.kind[l] = (uint8_t)kcur;
+      nall += em.n_all;
+      ndead += em.n_all - em.n_valid;
+      ecl[i] = em.n_valid;
+      ncount += em.n_valid;
+    }
+    if (on[i]) {  // the ring word: head past the drained ring messages, length after drains / appends
+      const uint32_t L = sw[i] >> 16, nl = Lk[i] - rr[i] + (adm[i] - da[i]);
+      uint32_t h = (sw[i] & 0xFFFFu) + rr[i];
+      h = h < rc ? h : h - rc;
+      const uint32_t nv = nl ? (h | nl << 16) : 0u;
+      if (nv != sw[i]) g.state[l] = nv;
+      dring += (long long)nl - (long long)L;
+    }
+  }
+  // ---- tells in actor order into the bucket's slice of the tell arena
+  const uint32_t tinc = wave_incl_sum(ncount), emtot = (uint32_t)__builtin_amdgcn_readlane((int)tinc, kWave - 1);
+  const uint64_t embase = (uint64_t)b * kBucket * g.dstride;
+  const uint32_t col = a.ng + b / a.G, nhmask = (1u << a.nx_bits) - 1u;
+  uint32_t toff = tinc - ncount;
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i)
+    for (uint32_t e = 0; e < ecl[i]; ++e, ++toff) {
+      const uint32_t d = T.dk[d0[i] + e];
+      a.em.key[embase + toff] = d;
+      a.em.src[embase + toff] = T.ds[d0[i] + e];
+      a.em.pay[embase + toff] = T.dp[d0[i] + e];
+      atomicAdd(&a.nhist[(size_t)((d >> a.nx_shift) & nhmask) * a.nhist_stride + col], 1u);
+    }
+  if (lane == 0) {
+    a.chunk_off[b] = bs;
+    a.chunk_cnt[b] = 0u;  // (no backlog: queued messages are in the rings)
+    a.chunk_off[a.nb + b] = (uint32_t)embase;
+    a.chunk_cnt[a.nb + b] = emtot;
+    if (a.emmeta) a.emmeta[b] = make_uint4(0u, 0u, 2u, 0u);
+  }
+  const uint32_t v0 = wave_incl_sum(ndel), v1 = wave_incl_sum(ndead), v2 = wave_incl_sum(nunh),
+                 v3 = wave_incl_sum(nall), v4 = wave_incl_sum(nact);
+  const uint32_t gp = wave_incl_sum(dring > 0 ? (uint32_t)dring : 0u),
+                 gn = wave_incl_sum(dring < 0 ? (uint32_t)-dring : 0u);
+  if (lane == kWave - 1) {
+    unsigned long long* bst = a.bstats + (size_t)blockIdx.x * kBStats;
+    if (v0) atomicAdd(&bst[0], (unsigned long long)v0);
+    if (v1) atomicAdd(&bst[1], (unsigned long long)v1);
+    if (v2) atomicAdd(&bst[2], (unsigned long long)v2);
+    if (v3) atomicAdd(&bst[3], (unsigned long long)v3);
+    if (v4) atomicAdd(&bst[4], (unsigned long long)v4);
+    if (gp != gn) atomicAdd(g.total, (unsigned long long)((long long)gp - (long long)gn));
+  }
+  return true;
+}
+
+template <uint32_t KM>
+static __global__ void __launch_bounds__(kTinyThreads, 4) k_ring_tiny(BucketArgs a, RingArgs g) {
+  __shared__ RingTinyLds T[kTinyWaves];
+  const uint32_t w = threadIdx.x / kWave, lane = lane_id();
+  const InView iv = in_view(a);
+  const uint32_t nw = gridDim.x * kTinyWaves;
+  for (uint32_t bw = blockIdx.x * kTinyWaves + w; bw < a.nb; bw += nw) {
+    uint32_t bs = 0, be = 0;
+    if (lane == 0) {
+      bs = a.bstart[bw];
+      be = a.bstart[bw + 1];
+    }
+    bs = (uint32_t)__builtin_amdgcn_readlane((int)bs, 0);
+    be = (uint32_t)__builtin_amdgcn_readlane((int)be, 0);
+    const bool tiny = be - bs <= a.tiny_max && ring_tiny_bucket<KM>(a, g, iv, T[w], bw, bs, be - bs);
+    if (lane == 0) a.blist[bw] = tiny ? 0u : 1u;  // (the block launch's work marks)
+  }
 }
 
 }  // namespace agx

@@ -539,8 +539,10 @@ def _run_profiled(w, ba, max_steps=1 << 30):
     w.apply_to(eng)
     eng.profile(True)
     sg = eng.run(max_steps)
-    launches = eng.profile_read().get("ring_apply", {"launches": 0})["launches"]
+    prof = eng.profile_read()
+    launches = prof.get("ring_apply", {"launches": 0})["launches"]
     st = eng.read_state()
+    eng.tiny_launches = prof.get("bucket_apply_tiny", {"launches": 0})["launches"]
     return eng, sg, st, launches
 
 
@@ -569,6 +571,28 @@ def test_ring_apply(built, monkeypatch, mode, ba, case):
         eng.close()
         assert (launches > 0) == (ring == "1"), f"{case}: ring_apply launches {launches} with AGX_RING_APPLY={ring}"
         assert_same(sg, so, st, sto, f"{case} ring={ring}")
+
+
+@pytest.mark.parametrize("case", ["power_law_c64", "compiled", "classes_host", "bounded_ring"])
+def test_ring_apply_wave_and_block(built, monkeypatch, case):
+    """The wave-per-bucket ring launch (k_ring_tiny: sparse buckets a wave each, the rest marked for
+    k_ring_apply) and the block kernel alone (AGX_TINY_LAUNCH=0), both bit-exact against the oracle."""
+    from oracle import BspOracle
+    monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    monkeypatch.setenv("AGX_RING_APPLY", "1")
+    w = RING_APPLY_CASES[case]()
+    ref = BspOracle(**w.engine_kwargs())
+    w.apply_to(ref)
+    so = ref.run()
+    sto = ref.read_state()
+    ref.close()
+    for tl in ("1", "0"):
+        monkeypatch.setenv("AGX_TINY_LAUNCH", tl)
+        eng, sg, st, launches = _run_profiled(w, 0)
+        tiny = eng.tiny_launches
+        eng.close()
+        assert launches > 0 and (tiny > 0) == (tl == "1"), f"{case}: ring {launches} / wave {tiny} launches, TINY_LAUNCH={tl}"
+        assert_same(sg, so, st, sto, f"{case} tiny_launch={tl}")
 
 
 @pytest.mark.parametrize("case", ["power_law_c64", "classes_host"])
