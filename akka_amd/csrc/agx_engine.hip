@@ -214,8 +214,9 @@ struct agx_engine {
   uint32_t* d_blist = nullptr;
   bool tiny_launch = true;
   // ring apply (agx_ring.h): bounded mailboxes whose queued messages stay in per-actor rings; decided
-  // at the first run (setup_ring_apply), then one k_ring_apply per superstep replaces the tiny / block /
-  // skew launches.  Opt-in: AGX_RING_APPLY=1 (the backlog arena is the default).
+  // at the first run (setup_ring_apply), then k_ring_tiny + k_ring_apply per superstep replace the tiny /
+  // block / skew launches.  On by default for deep bounded mailboxes (capacity >= kRingAutoC);
+  // AGX_RING_APPLY=1 / 0 forces it.
   bool rg_on = false;
   uint32_t rg_c = 0, rg_dstride = 0;
   uint32_t *d_rg_state = nullptr, *d_rg_src = nullptr, *d_rg_pay = nullptr;
@@ -815,14 +816,18 @@ agx_status setup_rings(agx_engine* e) {
 // MI355X), so a queued message is written once and read once instead of being copied forward by every
 // superstep it waits.  Each bucket's tells get a fixed slice of kBucket x throughput slots of the tell
 // arenas (a bucket may drain more messages than it receives: its rings' heads).
+constexpr uint32_t kRingAutoC = 256;  // ring apply by default from this mailbox capacity up (setup_ring_apply)
 agx_status setup_ring_apply(agx_engine* e) {
   if (e->started || e->rg_on || e->ring_live || e->ring_res) return AGX_OK;
   if (e->fused || e->R != 1 || e->pw || e->kmax != 1 || e->n_local == 0) return AGX_OK;
-  // opt-in (AGX_RING_APPLY=1): same-box A/B, C5 100M 1.73e9 msg/s with rings vs 2.73e9 with the
-  // backlog arena (a bucket's ring phases are one serial latency chain per block, while the backlog
-  // path drains its sparse buckets a wave each); C3 steady within 3 %
+  // AGX_RING_APPLY=1 / 0 forces rings on / off; unset: on when the largest bounded capacity is at
+  // least kRingAutoC.  Deep queues are where re-copying the backlog every superstep costs most (C3,
+  // BoundedMailbox(1000): 4.67e8 -> 6.7e8 msg/s with rings, the sparse buckets a wave each); at
+  // C5's BoundedMailbox(64) the hub buckets' serial ring chain in one block still loses (2.9e9 with
+  // the backlog arena vs 1.8e9).
   const char* rs = getenv("AGX_RING_APPLY");
-  if (!rs || atoi(rs) == 0) return AGX_OK;
+  const int force = rs ? atoi(rs) : -1;
+  if (force == 0) return AGX_OK;
   if (kVariants[apply_variant(e)].wide) return AGX_OK;
   uint32_t cmax = 0;
   for (uint32_t c = 0; c < AGX_MAX_MAILBOX_CLASSES; ++c) {
@@ -830,6 +835,7 @@ agx_status setup_ring_apply(agx_engine* e) {
     if (e->mcap[c] == 0 || e->mcap[c] > kRingApplyMaxC) return AGX_OK;  // an unbounded (or huge) mailbox class
     cmax = std::max(cmax, e->mcap[c]);
   }
+  if (force < 0 && cmax < kRingAutoC) return AGX_OK;
   const uint64_t dstr = e->Traw, slice = (uint64_t)kBucket * dstr;  // (drained per actor <= min(T, C) <= Traw)
   const uint64_t em_need = (uint64_t)e->nb * slice;
   if (em_need >= (1ull << 32)) return AGX_OK;

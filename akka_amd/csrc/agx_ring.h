@@ -113,18 +113,18 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
     // ---- arrivals per actor (keys only: an arrival to a full mailbox costs this one read)
     const uint32_t wbase = w * (kBIpt * kWave);
     uint32_t k[kBIpt];
-    for (uint32_t t0 = 0; t0 < n; t0 += kBucket) {
-      uint32_t ix[kBIpt];
+    for (uint32_t t0 = 0; t0 < n; t0 += 2 * kBucket) {  // (two tiles' key loads in flight: hub buckets)
+      uint32_t ix[2 * kBIpt], k2[2 * kBIpt];
 #pragma unroll
-      for (int r = 0; r < kBIpt; ++r) {
-        const uint32_t q = t0 + wbase + r * kWave + lane;
+      for (int r = 0; r < 2 * kBIpt; ++r) {
+        const uint32_t q = t0 + (r / kBIpt) * kBucket + wbase + (r % kBIpt) * kWave + lane;
         ix[r] = q < n ? iv.at(bs + q) : 0u;
       }
 #pragma unroll
-      for (int r = 0; r < kBIpt; ++r) k[r] = ldg(Mk, ix[r]);
+      for (int r = 0; r < 2 * kBIpt; ++r) k2[r] = ldg(Mk, ix[r]);
 #pragma unroll
-      for (int r = 0; r < kBIpt; ++r)  // (a hot actor's wave of arrivals: one aggregated LDS atomic)
-        if (t0 + wbase + r * kWave + lane < n) lds_hist_inc(S.cnt, k[r] & amask);
+      for (int r = 0; r < 2 * kBIpt; ++r)  // (a hot actor's wave of arrivals: one aggregated LDS atomic)
+        if (t0 + (r / kBIpt) * kBucket + wbase + (r % kBIpt) * kWave + lane < n) lds_hist_inc(S.cnt, k2[r] & amask);
     }
     __syncthreads();
     AGX_STAMP(a, 1);
@@ -641,42 +641,90 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
       o += rr[i] + da[i];
     }
   }
-  uint32_t rmax = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < kTinyIpl; ++i) rmax = max(rmax, rr[i]);
-  for (uint32_t q = 0; q < rmax; ++q) {
-    uint32_t hs[kTinyIpl], hp[kTinyIpl];
-#pragma unroll
-    for (uint32_t i = 0; i < kTinyIpl; ++i) {
-      uint32_t x = (sw[i] & 0xFFFFu) + q;
-      x = x < rc ? x : x - rc;
-      const size_t o = (size_t)hl[i] * rc + (q < rr[i] ? x : 0u);
-      hs[i] = g.src[o];
-      hp[i] = g.pay[o];
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < kTinyIpl; ++i)
-      if (q < rr[i]) {
-        T.ds[d0[i] + q] = hs[i];
-        T.dp[d0[i] + q] = hp[i];
-      }
-  }
+  // slot metadata: the actor (bit 31: a ring head, whose ring slot is in ds) or the arrival itself
 #pragma unroll
   for (uint32_t i = 0; i < kTinyIpl; ++i) {
+    const uint32_t h0 = sw[i] & 0xFFFFu;
+    for (uint32_t q = 0; q < rr[i]; ++q) {
+      const uint32_t x = h0 + q;
+      T.dk[d0[i] + q] = hl[i] | 0x80000000u;
+      T.ds[d0[i] + q] = x < rc ? x : x - rc;
+    }
     for (uint32_t q = 0; q < da[i]; ++q) {
+      T.dk[d0[i] + rr[i] + q] = hl[i];
       T.ds[d0[i] + rr[i] + q] = T.src[as0[i] + q];
       T.dp[d0[i] + rr[i] + q] = T.pay[as0[i] + q];
     }
-    const uint32_t t0 = (sw[i] & 0xFFFFu) + Lk[i];
-    for (uint32_t q = da[i]; q < adm[i]; ++q) {  // appended: ring slot head + Lk + (rank - da)
-      uint32_t x = t0 + (q - da[i]);
-      x = x < rc ? x : (x < 2u * rc ? x - rc : x - 2u * rc);
-      const size_t o = (size_t)hl[i] * rc + x;
+    const uint32_t t0 = h0 + Lk[i];
+    for (uint32_t q = da[i]; q < adm[i]; ++q) {  // appended: ring slot head + Lk + (rank - da)  (< 2 rc)
+      const uint32_t x = t0 + (q - da[i]);
+      const size_t o = (size_t)hl[i] * rc + (x < rc ? x : x - rc);
       g.src[o] = T.src[as0[i] + q];
       g.pay[o] = T.pay[as0[i] + q];
     }
   }
   wave_sync_lds();
+  // ring heads: every drained ring message of the bucket, kRingTinyD / kWave slots per lane in lockstep
+  constexpr uint32_t kF = kRingTinyD / kWave;
+  {
+    uint32_t hs[kF], hp[kF];
+    bool rg[kF];
+#pragma unroll
+    for (uint32_t f = 0; f < kF; ++f) {
+      const uint32_t j = f * kWave + lane;
+      const uint32_t dk = j < D ? T.dk[j] : 0u;
+      rg[f] = (dk >> 31) != 0u;
+      const size_t o = rg[f] ? (size_t)(dk & 0x7FFFFFFFu) * rc + T.ds[j] : 0u;
+      hs[f] = rg[f] ? g.src[o] : 0u;
+      hp[f] = rg[f] ? g.pay[o] : 0u;
+    }
+#pragma unroll
+    for (uint32_t f = 0; f < kF; ++f)
+      if (rg[f]) {
+        T.ds[f * kWave + lane] = hs[f];
+        T.dp[f * kWave + lane] = hp[f];
+      }
+  }
+  wave_sync_lds();
+  // FANOUT with one tell per message (C3 steady): every drained message's Zipf destination, the
+  // wave's slots in lockstep (index range, each binary-search step's loads together, then the
+  // permutation), written over the message's sender (FANOUT does not read it)
+  constexpr bool kFan = KM == kb(AGX_KIND_FANOUT);
+  const bool fan_pre = kFan && P.fan_k == 1;
+  if (kFan && fan_pre) {
+    uint32_t uu[kF], lo2[kF], hi2[kF];
+    bool need[kF];
+#pragma unroll
+    for (uint32_t f = 0; f < kF; ++f) {
+      const uint32_t j = f * kWave + lane, pv = j < D ? T.dp[j] : 0u;
+      need[f] = (pv >> 24) > 0;
+      uu[f] = need[f] ? (uint32_t)(fanout_rand(P.fan_seed, T.dk[j] & 0x7FFFFFFFu, pv & 0x00FFFFFFu, 0) >> 32) : 0u;
+      const uint32_t t = uu[f] >> (32 - kZipfBits);
+      lo2[f] = need[f] ? P.zipf_idx[t] : 0u;
+      hi2[f] = need[f] ? P.zipf_idx[t + 1] : 0u;
+    }
+    for (;;) {
+      bool more = false;
+      uint32_t cv[kF];
+#pragma unroll
+      for (uint32_t f = 0; f < kF; ++f) cv[f] = lo2[f] < hi2[f] ? P.zipf_cdf[(lo2[f] + hi2[f]) >> 1] : 0u;
+#pragma unroll
+      for (uint32_t f = 0; f < kF; ++f)
+        if (lo2[f] < hi2[f]) {
+          const uint32_t mid = (lo2[f] + hi2[f]) >> 1;
+          if (cv[f] >= uu[f]) hi2[f] = mid; else lo2[f] = mid + 1;
+          more |= lo2[f] < hi2[f];
+        }
+      if (!more) break;
+    }
+    uint32_t dd[kF];
+#pragma unroll
+    for (uint32_t f = 0; f < kF; ++f) dd[f] = need[f] ? P.zipf_perm[lo2[f]] : 0u;
+#pragma unroll
+    for (uint32_t f = 0; f < kF; ++f)
+      if (need[f]) T.ds[f * kWave + lane] = dd[f];
+    wave_sync_lds();
+  }
   // ---- drain + apply, actor after actor (tell e staged at drain slot d0 + e)
   uint32_t ndel = 0, nunh = 0, nall = 0, nact = 0, ncount = 0;
   uint32_t ecl[kTinyIpl];
@@ -692,7 +740,16 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
       uint32_t kcur = hk[i];
       for (uint32_t q = 0; q < drn; ++q) {
         const uint32_t s = T.ds[d0[i] + q], p = T.dp[d0[i] + q];
-        const uint32_t r = apply_msg<KM>(P, kcur, l, l, wv, s, p, em);
+        uint32_t r;
+        if (kFan && fan_pre) {  // apply_msg's FANOUT with the destination looked up above (in s)
+          wv[0] += 1;
+          wv[1] += p;
+          const uint32_t ttl = p >> 24;
+          if (ttl > 0) em(s, ((ttl - 1) << 24) | ((uint32_t)fanout_rand(P.fan_seed, l, p & 0x00FFFFFFu, 0) & 0x00FFFFFFu));
+          r = AGX_RES_SAME;
+        } else {
+          r = apply_msg<KM>(P, kcur, l, l, wv, s, p, em);
+        }
         ++ndel;
         if (r == AGX_RES_UNHANDLED) ++nunh;
         if (r == AGX_RES_STOPPED) {
