@@ -471,15 +471,24 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
 // ---- Wave-per-bucket ring apply.  A sparse superstep (C3: 4883 buckets of a few dozen arrivals
 // and a handful of actors with queued mail each) is dominated by the block kernel's per-bucket
 // chain of phases, so -- as k_tiny_apply does for the backlog arena -- every bucket whose arrivals
-// fit kTinyMax, whose actors with work (arrivals or a non-empty ring) fit kTinyMax and whose drains
+// fit kRingTinyN, whose actors with work (arrivals or a non-empty ring) fit kTinyMax and whose drains
 // fit kRingTinyD is done by one wave; k_ring_apply then takes only the buckets marked in a.blist.
 // Same per-actor rule as k_ring_apply (admission, ring heads first, appends, dead letters), same
 // tell order (actor order), same ring words.
-constexpr uint32_t kRingTinyD = 256;  // drained messages of a wave-path bucket
+#ifndef AGX_RING_IPL
+#define AGX_RING_IPL 2  // arrivals per lane of the wave path (A/B build knob)
+#endif
+#ifndef AGX_RING_DPL
+#define AGX_RING_DPL 4  // drained messages per lane of the wave path (A/B build knob)
+#endif
+constexpr uint32_t kRingIpl = AGX_RING_IPL;
+constexpr uint32_t kRingTinyN = kRingIpl * kWave;         // arrivals of a wave-path bucket
+constexpr uint32_t kRingTinyD = AGX_RING_DPL * kWave;     // drained messages of a wave-path bucket
+static_assert(AGX_RING_DPL % 4 == 0, "lockstep passes of four drain slots per lane");
 static_assert(kBucket == 32 * kWave, "lane l owns the ring words of actors [32 l, 32 l + 32)");
 
-struct RingTinyLds {                              // one per wave (5.6 KB)
-  uint32_t src[kTinyMax], pay[kTinyMax];          // arrivals by (actor, inbox position)
+struct RingTinyLds {                              // one per wave (5.6 KB at 2 arrivals / 4 drains per lane)
+  uint32_t src[kRingTinyN], pay[kRingTinyN];      // arrivals by (actor, inbox position)
   uint32_t dk[kRingTinyD], ds[kRingTinyD], dp[kRingTinyD];  // drained messages, then the staged tells
   uint32_t am[kWave], mw[kWave], pw[kWave];       // arrival bits, active bits, active prefix per 32 actors
   uint16_t act[kTinyMax], ast[kTinyMax], alen[kTinyMax];  // active actors in order; their arrival runs
@@ -538,9 +547,9 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
     }
   }
   // ---- arrivals: stable rank by (actor, position), run starts / lengths (tiny_bucket's rank loop)
-  uint32_t k[kTinyIpl], sv[kTinyIpl], pv[kTinyIpl], la[kTinyIpl];
+  uint32_t k[kRingIpl], sv[kRingIpl], pv[kRingIpl], la[kRingIpl];
 #pragma unroll
-  for (uint32_t r = 0; r < kTinyIpl; ++r) {
+  for (uint32_t r = 0; r < kRingIpl; ++r) {
     const uint32_t q = r * kWave + lane;
     const uint32_t i = q < n ? iv.at(bs + q) : 0u;
     k[r] = q < n ? ldg(iv.m.key, i) : 0u;
@@ -548,17 +557,17 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
     pv[r] = q < n ? ldg(iv.m.pay, i) : 0u;
   }
 #pragma unroll
-  for (uint32_t r = 0; r < kTinyIpl; ++r) la[r] = r * kWave + lane < n ? k[r] & amask : 0xFFFFFFFFu;
+  for (uint32_t r = 0; r < kRingIpl; ++r) la[r] = r * kWave + lane < n ? k[r] & amask : 0xFFFFFFFFu;
   T.am[lane] = 0u;
   wave_sync_lds();
-  uint32_t rank[kTinyIpl] = {}, st[kTinyIpl] = {}, len[kTinyIpl] = {};
+  uint32_t rank[kRingIpl] = {}, st[kRingIpl] = {}, len[kRingIpl] = {};
 #pragma unroll
-  for (uint32_t r2 = 0; r2 < kTinyIpl; ++r2) {
+  for (uint32_t r2 = 0; r2 < kRingIpl; ++r2) {
     const uint32_t jn = n > r2 * kWave ? min(n - r2 * kWave, (uint32_t)kWave) : 0u;
     for (uint32_t jj = 0; jj < jn; ++jj) {
       const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)la[r2], (int)jj), j = r2 * kWave + jj;
 #pragma unroll
-      for (uint32_t r = 0; r < kTinyIpl; ++r) {
+      for (uint32_t r = 0; r < kRingIpl; ++r) {
         const bool lt = lj < la[r], eq = lj == la[r];
         st[r] += lt;
         len[r] += eq;
@@ -567,7 +576,7 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
     }
   }
 #pragma unroll
-  for (uint32_t r = 0; r < kTinyIpl; ++r)
+  for (uint32_t r = 0; r < kRingIpl; ++r)
     if (r * kWave + lane < n) {
       T.src[rank[r]] = sv[r];
       T.pay[rank[r]] = pv[r];
@@ -587,7 +596,7 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
   }
   wave_sync_lds();
 #pragma unroll
-  for (uint32_t r = 0; r < kTinyIpl; ++r)
+  for (uint32_t r = 0; r < kRingIpl; ++r)
     if (r * kWave + lane < n && rank[r] == st[r]) {  // run head: its actor's active index
       const uint32_t wd = la[r] >> 5, idx = T.pw[wd] + __builtin_popcount(T.mw[wd] & ((1u << (la[r] & 31u)) - 1u));
       T.ast[idx] = (uint16_t)st[r];
@@ -664,14 +673,15 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
     }
   }
   wave_sync_lds();
-  // ring heads: every drained ring message of the bucket, kRingTinyD / kWave slots per lane in lockstep
-  constexpr uint32_t kF = kRingTinyD / kWave;
-  {
+  // ring heads: every drained ring message of the bucket, four slots per lane in lockstep per pass
+  constexpr uint32_t kF = 4;
+#pragma unroll 1
+  for (uint32_t f0 = 0; f0 < kRingTinyD / kWave; f0 += kF) {
     uint32_t hs[kF], hp[kF];
     bool rg[kF];
 #pragma unroll
     for (uint32_t f = 0; f < kF; ++f) {
-      const uint32_t j = f * kWave + lane;
+      const uint32_t j = (f0 + f) * kWave + lane;
       const uint32_t dk = j < D ? T.dk[j] : 0u;
       rg[f] = (dk >> 31) != 0u;
       const size_t o = rg[f] ? (size_t)(dk & 0x7FFFFFFFu) * rc + T.ds[j] : 0u;
@@ -681,8 +691,8 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
 #pragma unroll
     for (uint32_t f = 0; f < kF; ++f)
       if (rg[f]) {
-        T.ds[f * kWave + lane] = hs[f];
-        T.dp[f * kWave + lane] = hp[f];
+        T.ds[(f0 + f) * kWave + lane] = hs[f];
+        T.dp[(f0 + f) * kWave + lane] = hp[f];
       }
   }
   wave_sync_lds();
@@ -692,37 +702,40 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
   constexpr bool kFan = KM == kb(AGX_KIND_FANOUT);
   const bool fan_pre = kFan && P.fan_k == 1;
   if (kFan && fan_pre) {
-    uint32_t uu[kF], lo2[kF], hi2[kF];
-    bool need[kF];
+#pragma unroll 1
+    for (uint32_t f0 = 0; f0 < kRingTinyD / kWave; f0 += kF) {
+      uint32_t uu[kF], lo2[kF], hi2[kF];
+      bool need[kF];
 #pragma unroll
-    for (uint32_t f = 0; f < kF; ++f) {
-      const uint32_t j = f * kWave + lane, pv = j < D ? T.dp[j] : 0u;
-      need[f] = (pv >> 24) > 0;
-      uu[f] = need[f] ? (uint32_t)(fanout_rand(P.fan_seed, T.dk[j] & 0x7FFFFFFFu, pv & 0x00FFFFFFu, 0) >> 32) : 0u;
-      const uint32_t t = uu[f] >> (32 - kZipfBits);
-      lo2[f] = need[f] ? P.zipf_idx[t] : 0u;
-      hi2[f] = need[f] ? P.zipf_idx[t + 1] : 0u;
-    }
-    for (;;) {
-      bool more = false;
-      uint32_t cv[kF];
+      for (uint32_t f = 0; f < kF; ++f) {
+        const uint32_t j = (f0 + f) * kWave + lane, pv = j < D ? T.dp[j] : 0u;
+        need[f] = j < D && (pv >> 24) > 0;
+        uu[f] = need[f] ? (uint32_t)(fanout_rand(P.fan_seed, T.dk[j] & 0x7FFFFFFFu, pv & 0x00FFFFFFu, 0) >> 32) : 0u;
+        const uint32_t t = uu[f] >> (32 - kZipfBits);
+        lo2[f] = need[f] ? P.zipf_idx[t] : 0u;
+        hi2[f] = need[f] ? P.zipf_idx[t + 1] : 0u;
+      }
+      for (;;) {
+        bool more = false;
+        uint32_t cv[kF];
 #pragma unroll
-      for (uint32_t f = 0; f < kF; ++f) cv[f] = lo2[f] < hi2[f] ? P.zipf_cdf[(lo2[f] + hi2[f]) >> 1] : 0u;
+        for (uint32_t f = 0; f < kF; ++f) cv[f] = lo2[f] < hi2[f] ? P.zipf_cdf[(lo2[f] + hi2[f]) >> 1] : 0u;
+#pragma unroll
+        for (uint32_t f = 0; f < kF; ++f)
+          if (lo2[f] < hi2[f]) {
+            const uint32_t mid = (lo2[f] + hi2[f]) >> 1;
+            if (cv[f] >= uu[f]) hi2[f] = mid; else lo2[f] = mid + 1;
+            more |= lo2[f] < hi2[f];
+          }
+        if (!more) break;
+      }
+      uint32_t dd[kF];
+#pragma unroll
+      for (uint32_t f = 0; f < kF; ++f) dd[f] = need[f] ? P.zipf_perm[lo2[f]] : 0u;
 #pragma unroll
       for (uint32_t f = 0; f < kF; ++f)
-        if (lo2[f] < hi2[f]) {
-          const uint32_t mid = (lo2[f] + hi2[f]) >> 1;
-          if (cv[f] >= uu[f]) hi2[f] = mid; else lo2[f] = mid + 1;
-          more |= lo2[f] < hi2[f];
-        }
-      if (!more) break;
+        if (need[f]) T.ds[(f0 + f) * kWave + lane] = dd[f];
     }
-    uint32_t dd[kF];
-#pragma unroll
-    for (uint32_t f = 0; f < kF; ++f) dd[f] = need[f] ? P.zipf_perm[lo2[f]] : 0u;
-#pragma unroll
-    for (uint32_t f = 0; f < kF; ++f)
-      if (need[f]) T.ds[f * kWave + lane] = dd[f];
     wave_sync_lds();
   }
   // ---- drain + apply, actor after actor (tell e staged at drain slot d0 + e)
@@ -827,7 +840,7 @@ static __global__ void __launch_bounds__(kTinyThreads, 4) k_ring_tiny(BucketArgs
     }
     bs = (uint32_t)__builtin_amdgcn_readlane((int)bs, 0);
     be = (uint32_t)__builtin_amdgcn_readlane((int)be, 0);
-    const bool tiny = be - bs <= a.tiny_max && ring_tiny_bucket<KM>(a, g, iv, T[w], bw, bs, be - bs);
+    const bool tiny = be - bs <= kRingTinyN && ring_tiny_bucket<KM>(a, g, iv, T[w], bw, bs, be - bs);
     if (lane == 0) a.blist[bw] = tiny ? 0u : 1u;  // (the block launch's work marks)
   }
 }
