@@ -280,44 +280,48 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) drn[j] = S.dpos[la0 + j] - ds[j] + (S.dadm[la0 + j] & 0xFFFFu);
     // (before the state loads: their registers are not live across the lookups)
-    // FANOUT with one tell per message (C3 steady): every drained message's Zipf destination, the
-    // four actors' q-th messages in lockstep (index range, each binary-search step's loads together,
-    // then the permutation), written over the message's sender (FANOUT does not read it)
+    // FANOUT with one tell per message (C3 steady): every drained message's Zipf destination (index
+    // range, binary search, permutation), written over the message's sender (FANOUT does not read it)
     const bool fan_pre = kFan && P.fan_k == 1;
+    uint32_t* const skey = lds_drain ? S.whist32 : g.dk + sbase;  // (tell staging; free until the drain)
     if (kFan && fan_pre) {
-      uint32_t dmax = 0;
+      // every drain slot's actor into the staging area, then the whole block looks up the slots'
+      // Zipf destinations, four per thread in lockstep (independent chains, not one per actor)
 #pragma unroll
-      for (int j = 0; j < kBAct; ++j) dmax = max(dmax, drn[j]);
-      for (uint32_t q = 0; q < dmax; ++q) {
-        uint32_t lo[kBAct], hi[kBAct], uu[kBAct];
-        bool need[kBAct];
+      for (int j = 0; j < kBAct; ++j)
+        for (uint32_t q = 0; q < drn[j]; ++q) skey[ds[j] + q] = a0 + la0 + j;
+      __syncthreads();
+      for (uint32_t j0 = tid; j0 < D; j0 += 4 * kBThreads) {
+        uint32_t uu[4], lo[4], hi[4];
+        bool need[4];
 #pragma unroll
-        for (int j = 0; j < kBAct; ++j) {
-          const uint32_t pv = q < drn[j] ? bpay[ds[j] + q] : 0u;
-          need[j] = (pv >> 24) > 0;
-          uu[j] = need[j] ? (uint32_t)(fanout_rand(P.fan_seed, a0 + la0 + j, pv & 0x00FFFFFFu, 0) >> 32) : 0u;
-          const uint32_t t = uu[j] >> (32 - kZipfBits);
-          lo[j] = need[j] ? P.zipf_idx[t] : 0u;
-          hi[j] = need[j] ? P.zipf_idx[t + 1] : 0u;
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t j = j0 + c * kBThreads, pv = j < D ? bpay[j] : 0u;
+          need[c] = j < D && (pv >> 24) > 0;
+          uu[c] = need[c] ? (uint32_t)(fanout_rand(P.fan_seed, skey[j], pv & 0x00FFFFFFu, 0) >> 32) : 0u;
+          const uint32_t t = uu[c] >> (32 - kZipfBits);
+          lo[c] = need[c] ? P.zipf_idx[t] : 0u;
+          hi[c] = need[c] ? P.zipf_idx[t + 1] : 0u;
         }
         for (;;) {
           bool more = false;
-          uint32_t c[kBAct];
+          uint32_t cv[4];
 #pragma unroll
-          for (int j = 0; j < kBAct; ++j) c[j] = lo[j] < hi[j] ? P.zipf_cdf[(lo[j] + hi[j]) >> 1] : 0u;
+          for (int c = 0; c < 4; ++c) cv[c] = lo[c] < hi[c] ? P.zipf_cdf[(lo[c] + hi[c]) >> 1] : 0u;
 #pragma unroll
-          for (int j = 0; j < kBAct; ++j)
-            if (lo[j] < hi[j]) {
-              const uint32_t mid = (lo[j] + hi[j]) >> 1;
-              if (c[j] >= uu[j]) hi[j] = mid; else lo[j] = mid + 1;
-              more |= lo[j] < hi[j];
+          for (int c = 0; c < 4; ++c)
+            if (lo[c] < hi[c]) {
+              const uint32_t mid = (lo[c] + hi[c]) >> 1;
+              if (cv[c] >= uu[c]) hi[c] = mid; else lo[c] = mid + 1;
+              more |= lo[c] < hi[c];
             }
           if (!more) break;
         }
 #pragma unroll
-        for (int j = 0; j < kBAct; ++j)
-          if (need[j]) bsrc[ds[j] + q] = P.zipf_perm[lo[j]];
+        for (int c = 0; c < 4; ++c)
+          if (need[c]) bsrc[j0 + c * kBThreads] = P.zipf_perm[lo[c]];
       }
+      __syncthreads();
     }
 #pragma unroll
     for (int j = 0; j < kBAct; ++j) {
@@ -345,7 +349,6 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
     AGX_STAMP(a, 5);
     // ---- drain + apply, actor after actor; tell e of an actor is staged at its drain slot e (already
     // consumed: tell e comes from a message at slot >= e)
-    uint32_t* const skey = lds_drain ? S.whist32 : g.dk + sbase;
     uint32_t ecl[kBAct];
     uint32_t esum = 0;
 #pragma unroll 1
@@ -411,14 +414,36 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
     uint32_t emtot;
     uint32_t eo = block_excl_sum<kBThreads>(esum, S.scratch, &emtot);  // (syncs: staging complete)
     const uint64_t embase = (uint64_t)b * kBucket * g.dstride;
+    if (lds_drain) {
 #pragma unroll 1
-    for (int j = 0; j < kBAct; ++j) {
-      for (uint32_t e = 0; e < ecl[j]; ++e) {
-        a.em.key[embase + eo + e] = skey[ds[j] + e];
-        a.em.src[embase + eo + e] = bsrc[ds[j] + e];
-        a.em.pay[embase + eo + e] = bpay[ds[j] + e];
+      for (int j = 0; j < kBAct; ++j) {
+        for (uint32_t e = 0; e < ecl[j]; ++e) {
+          a.em.key[embase + eo + e] = skey[ds[j] + e];
+          a.em.src[embase + eo + e] = bsrc[ds[j] + e];
+          a.em.pay[embase + eo + e] = bpay[ds[j] + e];
+        }
+        eo += ecl[j];
       }
-      eo += ecl[j];
+    } else {  // staged in the bucket's global slice (hub buckets draining > kBucket): one LDS index of
+              // source slots (S.whist32 is free here), then a block-wide copy with independent loads
+      constexpr uint32_t kMap = kBWaves * kBucket / 2;
+      for (uint32_t base = 0; base < emtot; base += kMap) {
+        uint32_t o = eo;
+#pragma unroll 1
+        for (int j = 0; j < kBAct; ++j)
+          for (uint32_t e = 0; e < ecl[j]; ++e, ++o)
+            if (o >= base && o < base + kMap) S.whist32[o - base] = ds[j] + e;
+        __syncthreads();
+        const uint32_t m = min(kMap, emtot - base);
+#pragma unroll 4
+        for (uint32_t i = tid; i < m; i += kBThreads) {
+          const uint32_t x = S.whist32[i];
+          a.em.key[embase + base + i] = skey[x];
+          a.em.src[embase + base + i] = bsrc[x];
+          a.em.pay[embase + base + i] = bpay[x];
+        }
+        __syncthreads();
+      }
     }
     AGX_STAMP(a, 7);
     // ---- ring words, chunk entries, next first-pass histogram column
