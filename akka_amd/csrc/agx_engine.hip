@@ -1832,6 +1832,25 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
       e->plan.bits[p] = b;
       sh += b;
     }
+    // AGX_PASS0_BITS (A/B knob): the first (chunk-list) pass's digit width, the rest spread over the
+    // dense passes -- fewer first-pass digits make longer per-digit runs out of its small tiles
+    if (const char* s = getenv("AGX_PASS0_BITS"); s && e->plan.npass > 1) {
+      const uint32_t b0 = std::min<uint32_t>(rb, std::max(1, atoi(s)));
+      if (b0 < hi - lo) {
+        const uint32_t rest = hi - lo - b0, np = (rest + rb - 1) / rb;
+        if (1 + np <= 4) {
+          e->plan.npass = 1 + np;
+          e->plan.shift[0] = lo;
+          e->plan.bits[0] = b0;
+          for (uint32_t p = 1, sh = lo + b0; p < e->plan.npass; ++p) {
+            const uint32_t b = (hi - sh + (e->plan.npass - p) - 1) / (e->plan.npass - p);
+            e->plan.shift[p] = sh;
+            e->plan.bits[p] = b;
+            sh += b;
+          }
+        }
+      }
+    }
   }
 
   // fused superstep when one radix digit covers every bucket of a single rank
