@@ -221,6 +221,7 @@ struct agx_engine {
   uint32_t rg_c = 0, rg_dstride = 0;
   uint32_t *d_rg_state = nullptr, *d_rg_src = nullptr, *d_rg_pay = nullptr;
   uint32_t *d_rg_dk = nullptr, *d_rg_ds = nullptr, *d_rg_dp = nullptr;
+  uint32_t* d_rg_nz = nullptr;  // [nb][64] non-empty-ring bits
   uint64_t em_cap = 0;  // entries of the tell arenas em / em2
   // multi-pass, plain behaviours: skewed buckets split over workgroups (k_skew_*, agx_kernels.h)
   uint32_t *d_sk_rec = nullptr, *d_sk_act = nullptr, *d_sk_pc = nullptr, *d_sk_meta = nullptr;
@@ -698,7 +699,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   SkewArgs ska{e->d_sk_rec, e->d_sk_act, e->d_sk_pc, e->d_sk_meta, e->sk_budget, e->sk_rows};
   if (e->rg_on) {  // ring apply: one launch does admission, drains and ring appends (agx_ring.h)
     RingArgs ra{e->d_rg_state, e->d_rg_src, e->d_rg_pay, e->d_rg_dk, e->d_rg_ds, e->d_rg_dp, e->d_ring_total,
-                e->rg_c, e->rg_dstride};
+                e->d_rg_nz, e->rg_c, e->rg_dstride};
     const uint32_t vid = apply_variant(e);
     if (e->tiny_launch && e->tiny_max && !e->skew_only) {  // sparse buckets a wave each, then the marked ones
       ba.blist = e->d_blist;
@@ -854,6 +855,7 @@ agx_status setup_ring_apply(agx_engine* e) {
     e->em_cap = em_need;
   }
   AGX_TRY(dalloc(&e->d_rg_state, e->n_local));
+  AGX_TRY(dalloc(&e->d_rg_nz, (uint64_t)e->nb * (kBucket / 32)));
   AGX_TRY(dalloc(&e->d_rg_src, e->n_local * (uint64_t)cmax));
   AGX_TRY(dalloc(&e->d_rg_pay, e->n_local * (uint64_t)cmax));
   AGX_TRY(dalloc(&e->d_rg_dk, em_need));
@@ -861,6 +863,7 @@ agx_status setup_ring_apply(agx_engine* e) {
   AGX_TRY(dalloc(&e->d_rg_dp, em_need));
   if (!e->d_ring_total) AGX_TRY(dalloc(&e->d_ring_total, 2));
   HIP_TRY(hipMemsetAsync(e->d_rg_state, 0, e->n_local * 4, e->stream));
+  HIP_TRY(hipMemsetAsync(e->d_rg_nz, 0, (size_t)e->nb * (kBucket / 32) * 4, e->stream));
   HIP_TRY(hipMemsetAsync(e->d_ring_total, 0, 16, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->rg_c = cmax;
@@ -2075,7 +2078,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_skew_list); hipFree(e->d_skew_n); hipFree(e->d_blist);
   hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);
   hipFree(e->d_ring_of); hipFree(e->d_ring_state); hipFree(e->d_ring_src); hipFree(e->d_ring_pay);
-  hipFree(e->d_rg_state); hipFree(e->d_rg_src); hipFree(e->d_rg_pay); hipFree(e->d_rg_dk); hipFree(e->d_rg_ds);
+  hipFree(e->d_rg_state); hipFree(e->d_rg_nz); hipFree(e->d_rg_src); hipFree(e->d_rg_pay); hipFree(e->d_rg_dk); hipFree(e->d_rg_ds);
   hipFree(e->d_rg_dp);
   hipFree(e->d_ring_next); hipFree(e->d_ring_free); hipFree(e->d_ring_total);
   hipFree(e->d_orw); hipFree(e->d_orm); hipFree(e->d_orw_n);

@@ -41,6 +41,7 @@ struct RingArgs {
   uint32_t* ds;
   uint32_t* dp;
   unsigned long long* total;  // messages held in rings (in flight)
+  uint32_t* nz;      // [nb][kBucket / 32] one bit per actor: its ring holds mail (the wave path's scan)
   uint32_t rc;       // ring slots per actor (>= every mailbox class's capacity)
   uint32_t dstride;  // drain slots per actor of a bucket's slice (the largest throughput)
 };
@@ -470,6 +471,16 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
         for (int j = 0; j < kBAct; ++j)
           if (la0 + j < na) g.state[a0 + la0 + j] = nv[j];
       }
+      // the bucket's non-empty-ring bits (S.cnt is free here): thread t's four actors are bits
+      // 4 t .. 4 t + 3 of the bucket
+      uint32_t nib = 0;
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) nib |= (nv[j] != 0u ? 1u : 0u) << j;
+      if (tid < kBucket / 32) S.cnt[tid] = 0u;
+      __syncthreads();
+      if (nib) atomicOr(&S.cnt[la0 >> 5], nib << (la0 & 31u));
+      __syncthreads();
+      if (tid < kBucket / 32) g.nz[(size_t)b * (kBucket / 32) + tid] = S.cnt[tid];
     }
     acc[1] += ndead;
     if (tid == 0) {
@@ -553,24 +564,8 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
   const uint32_t lane = lane_id(), rc = g.rc;
   const uint32_t amask = (1u << a.bb) - 1u, a0 = b << a.bb;
   const uint32_t na = min(1u << a.bb, P.n_local - a0);
-  // ---- actors with queued mail: lane l's 32 ring words -> one bit each
-  uint32_t rm = 0;
-  {
-    const uint32_t o0 = lane * 32u;
-    if (o0 + 32u <= na && ((a0 + o0) & 3u) == 0u) {
-      const uint4* q4 = reinterpret_cast<const uint4*>(g.state + a0 + o0);
-      uint4 v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = q4[i];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        rm |= (uint32_t)(v[i].x > 0xFFFFu) << (4 * i) | (uint32_t)(v[i].y > 0xFFFFu) << (4 * i + 1) |
-              (uint32_t)(v[i].z > 0xFFFFu) << (4 * i + 2) | (uint32_t)(v[i].w > 0xFFFFu) << (4 * i + 3);
-    } else {
-      for (uint32_t i = 0; i < 32u; ++i)
-        if (o0 + i < na && g.state[a0 + o0 + i] > 0xFFFFu) rm |= 1u << i;
-    }
-  }
+  // ---- actors with queued mail: one bit each, lane l holding actors [32 l, 32 l + 32)
+  const uint32_t rm = g.nz[(size_t)b * kWave + lane];
   // ---- arrivals: stable rank by (actor, position), run starts / lengths (tiny_bucket's rank loop)
   uint32_t k[kRingIpl], sv[kRingIpl], pv[kRingIpl], la[kRingIpl];
 #pragma unroll
@@ -814,6 +809,17 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
       dring += (long long)nl - (long long)L;
     }
   }
+  // ---- the bucket's non-empty-ring bits after this superstep (T.am is free again)
+  T.am[lane] = 0u;
+  wave_sync_lds();
+#pragma unroll
+  for (uint32_t i = 0; i < kTinyIpl; ++i)
+    if (on[i] && Lk[i] - rr[i] + (adm[i] - da[i]) != 0u) {
+      const uint32_t x = hl[i] - a0;
+      atomicOr(&T.am[x >> 5], 1u << (x & 31u));
+    }
+  wave_sync_lds();
+  g.nz[(size_t)b * kWave + lane] = T.am[lane];
   // ---- tells in actor order into the bucket's slice of the tell arena
   const uint32_t tinc = wave_incl_sum(ncount), emtot = (uint32_t)__builtin_amdgcn_readlane((int)tinc, kWave - 1);
   const uint64_t embase = (uint64_t)b * kBucket * g.dstride;
