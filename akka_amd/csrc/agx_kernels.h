@@ -2845,8 +2845,11 @@ static __global__ void __launch_bounds__(kBThreads) k_skew_scatter(BucketArgs a,
   }
 }
 
+#ifndef AGX_WIDE_WPE
+#define AGX_WIDE_WPE 4  // CRDT (wide) variants: minimum waves per SIMD (4: 128 VGPRs; 2: 256, one block per CU)
+#endif
 template <bool kWide, uint32_t KM, bool kGather, bool kSkew, bool kOwner = false>
-static __global__ void __launch_bounds__(kBThreads, 4) k_bucket_apply(BucketArgs a) {
+static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_bucket_apply(BucketArgs a) {
   constexpr bool kDefer = !kSkew;  // large inboxes are appended to the skew list
   if (kOwner && a.halt && a.halt[0]) return;  // (device-resident multi-rank replay stopped)
   // key/src/pay carved from one array: group_tells reuses key+src as a 16 KB histogram
