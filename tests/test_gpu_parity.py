@@ -270,7 +270,8 @@ MULTIPASS_CASES = {
 @pytest.mark.parametrize("case", sorted(MULTIPASS_CASES))
 def test_multipass_grouping(built, monkeypatch, bits, G, case, ring):
     """AGX_UNIT_G groups G buckets per first-pass histogram column (as at 100M actors); bounded
-    cases with ring apply (AGX_RING_APPLY=1) and with the backlog arena (the default)."""
+    cases with ring apply (AGX_RING_APPLY=1) and with the backlog arena (AGX_RING_APPLY=0; the
+    default below a bounded capacity of 256)."""
     monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
     monkeypatch.setenv("AGX_UNIT_G", str(G))
     monkeypatch.setenv("AGX_RING_APPLY", ring)
