@@ -3621,8 +3621,17 @@ static __global__ void __launch_bounds__(kThreads) k_mr_pack(MrArgs a) {
     }
   }
   if (p.code) return;
+  {  // own run: straight from the send buffer to its place after the backlog (no slab, no wait
+     // for the exchange)
+    const uint32_t x0 = p.soff[a.rank], o0 = p.nbl + p.roff[a.rank];
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < p.scnt[a.rank]; i += gridDim.x * kThreads) {
+      a.A.key[o0 + i] = a.s2.key[x0 + i];
+      a.A.src[o0 + i] = a.s2.src[x0 + i];
+      a.A.pay[o0 + i] = a.s2.pay[x0 + i];
+    }
+  }
   for (uint32_t q = 0; q < a.R; ++q) {
-    if (q == a.rank) continue;  // (own run: unpacked from s2 directly)
+    if (q == a.rank) continue;
     uint32_t* d = a.sslab + (size_t)q * a.slab * 3;
     const uint32_t o = p.soff[q];
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < p.scnt[q]; i += gridDim.x * kThreads) {
@@ -3659,19 +3668,13 @@ static __global__ void __launch_bounds__(kThreads) k_mr_unpack(MrArgs a) {
   for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
     uint32_t r = 0;
     while (i >= p.roff[r + 1]) ++r;
+    if (r == a.rank) continue;  // (own run: placed by k_mr_pack)
     const uint32_t j = i - p.roff[r], o = p.nbl + i;
-    if (r == a.rank) {
-      const uint32_t x = p.soff[a.rank] + j;
-      a.A.key[o] = a.s2.key[x];
-      a.A.src[o] = a.s2.src[x];
-      a.A.pay[o] = a.s2.pay[x];
-    } else {
-      const uint32_t* s = a.rslab + ((size_t)r * a.slab + j) * 3;
-      a.A.key[o] = s[0];
-      a.A.src[o] = s[1];
-      // a state gossip's row arrived in rx[r][j]: its handle points there
-      a.A.pay[o] = a.pw && is_wide(s[1]) ? (s[2] & ~kHandleMask) | (a.heap_rows + r * a.slab + j) : s[2];
-    }
+    const uint32_t* s = a.rslab + ((size_t)r * a.slab + j) * 3;
+    a.A.key[o] = s[0];
+    a.A.src[o] = s[1];
+    // a state gossip's row arrived in rx[r][j]: its handle points there
+    a.A.pay[o] = a.pw && is_wide(s[1]) ? (s[2] & ~kHandleMask) | (a.heap_rows + r * a.slab + j) : s[2];
   }
 }
 
