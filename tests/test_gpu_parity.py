@@ -574,6 +574,26 @@ def test_ring_apply(built, monkeypatch, mode, ba, case):
         assert_same(sg, so, st, sto, f"{case} ring={ring}")
 
 
+@pytest.mark.parametrize("capacity,rings", [(64, False), (255, False), (256, True), (1000, True)])
+def test_ring_apply_default(built, monkeypatch, capacity, rings):
+    """Without AGX_RING_APPLY the ring apply is on exactly when the largest bounded capacity is
+    >= 256 (deep queues: C3's BoundedMailbox(1000)), and either way bit-exact against the oracle
+    (C3's FANOUT shape at 3-bit digits, hot actors' queues filling up)."""
+    from oracle import BspOracle
+    monkeypatch.delenv("AGX_RING_APPLY", raising=False)
+    monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    w = wl.zipf_fanout(60_000, k=1, ttl=12, root_every=1, capacity=capacity)
+    ref = BspOracle(**w.engine_kwargs())
+    w.apply_to(ref)
+    so = ref.run()
+    sto = ref.read_state()
+    ref.close()
+    eng, sg, st, launches = _run_profiled(w, 0)
+    eng.close()
+    assert (launches > 0) == rings, f"capacity {capacity}: ring_apply launches {launches}"
+    assert_same(sg, so, st, sto, f"zipf capacity={capacity}")
+
+
 @pytest.mark.parametrize("case", ["power_law_c64", "compiled", "classes_host", "bounded_ring"])
 def test_ring_apply_wave_and_block(built, monkeypatch, case):
     """The wave-per-bucket ring launch (k_ring_tiny: sparse buckets a wave each, the rest marked for
