@@ -108,8 +108,18 @@ __device__ __forceinline__ uint32_t dl_env(uint32_t kind) { return 2u * crdt_wor
 // CRDT kinds or run delta-CRDT replication go through crdt_apply and keep dense rows: the sparse form
 // there failed the multi-pass mixed-CRDT parity test -- a wrong emitted counter, cause not found --
 // so it was taken out again.  The two row forms never meet in one engine.)
-constexpr uint32_t kOrRowVV = 0, kOrRowMask = 16, kOrRowDots = 32;
+constexpr uint32_t kOrRowVV = 0, kOrRowDV = 8, kOrRowMask = 16, kOrRowDots = 32;
 static_assert(kOrRowDots + AGX_ORSET_ELEMS * AGX_CRDT_NODES <= 544u, "sparse ORSet row within the row pitch");
+#ifdef AGX_SPARSE_SERIAL
+// (diagnostic build knob: the round-4 serial sparse form in crdt_apply, for every ORSet population)
+constexpr bool kSparseSerial = true;
+#else
+constexpr bool kSparseSerial = false;
+#endif
+// where a full-state gossip row keeps the sender's deltaVersions (delta-CRDT mode)
+__device__ __forceinline__ uint32_t row_dv(uint32_t kind) {
+  return kSparseSerial && kind == AGX_KIND_ORSET ? kOrRowDV : 2u * crdt_words(kind);
+}
 __device__ __forceinline__ uint32_t dl_entry(uint32_t kind, uint32_t seq) {
   return dl_env(kind) + 2u * AGX_DELTA_ENV_WORDS + AGX_DELTA_LOG_U32(kind == AGX_KIND_ORSET) * (seq % AGX_DELTA_LOG);
 }
@@ -457,10 +467,10 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       return AGX_RES_SAME;
     }
     if (dm) {  // DataEnvelope.merge: the deltaVersions after the data words
-      const uint32_t e0 = dl_env(kind);
+      const uint32_t e0 = dl_env(kind), r0 = row_dv(kind);
 #pragma unroll
       for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
-        const uint32_t c = s32.ld(e0 + n), r = row[e0 + n];
+        const uint32_t c = s32.ld(e0 + n), r = row[r0 + n];
         if (r > c) s32.put(e0 + n, r);
       }
     }
@@ -490,26 +500,39 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       const uint64_t s = st[(vw + k) * nl];
       lvv[2 * k] = (uint32_t)s;
       lvv[2 * k + 1] = (uint32_t)(s >> 32);
-      rvv[2 * k] = row[2 * (vw + k)];
-      rvv[2 * k + 1] = row[2 * (vw + k) + 1];
+      rvv[2 * k] = row[kSparseSerial ? kOrRowVV + 2 * k : 2 * (vw + k)];
+      rvv[2 * k + 1] = row[kSparseSerial ? kOrRowVV + 2 * k + 1 : 2 * (vw + k) + 1];
     }
 #ifndef AGX_ORSET_BATCH
 #define AGX_ORSET_BATCH 2
 #endif
     constexpr uint32_t kE = AGX_ORSET_BATCH;  // elements per batch (8 row words + 4 state words each)
+    uint32_t ro = kOrRowDots;                 // (kSparseSerial) next live dot of the sparse row
     for (uint32_t e0 = 0; e0 < AGX_ORSET_ELEMS; e0 += kE) {
       uint4 ra[kE], rb[kE];
+      uint32_t rm[kE];
       uint64_t s[kE][4];
 #pragma unroll
       for (uint32_t u = 0; u < kE; ++u) {
-        ra[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u));
-        rb[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u) + 4);
+        if (kSparseSerial) {
+          rm[u] = reinterpret_cast<const uint8_t*>(row + kOrRowMask)[e0 + u];
+        } else {
+          ra[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u));
+          rb[u] = *reinterpret_cast<const uint4*>(row + 8 * (e0 + u) + 4);
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) s[u][k] = st[(size_t)(4 * (e0 + u) + k) * nl];
       }
 #pragma unroll
       for (uint32_t u = 0; u < kE; ++u) {
-        const uint32_t r[8] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w, rb[u].x, rb[u].y, rb[u].z, rb[u].w};
+        uint32_t r[8];
+        if (kSparseSerial) {
+#pragma unroll
+          for (int n = 0; n < 8; ++n) r[n] = (rm[u] >> n) & 1u ? row[ro++] : 0u;
+        } else {
+          r[0] = ra[u].x, r[1] = ra[u].y, r[2] = ra[u].z, r[3] = ra[u].w;
+          r[4] = rb[u].x, r[5] = rb[u].y, r[6] = rb[u].z, r[7] = rb[u].w;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const uint64_t sv = s[u][k];
@@ -585,7 +608,39 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       const uint32_t f = P.n_global > 1 && (!dm || key_size(self, P.n_global) > 1) ? P.gossip_f : 0u;
       if (f) {
         const uint32_t h = row_cursor++;
-        if (h < H.rows) {  // snapshot of the current state (+ deltaVersions), shared by the f gossips
+        if (kSparseSerial && h < H.rows && kind == AGX_KIND_ORSET) {  // sparse snapshot (kOrRow*)
+          uint32_t* row = H.wrow(h);
+          const uint32_t vw = AGX_ORSET_ELEMS * AGX_CRDT_NODES / 2;
+          uint32_t o = kOrRowDots;
+          for (uint32_t e0 = 0; e0 < AGX_ORSET_ELEMS; e0 += 4) {  // four elements' dots (one mask word) per batch
+            uint64_t d[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int k = 0; k < 4; ++k) d[u][k] = st[(size_t)(4 * (e0 + u) + k) * nl];
+            uint32_t mw = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int n = 0; n < 8; ++n) {
+                const uint32_t x = (uint32_t)(d[u][n >> 1] >> (32 * (n & 1)));
+                if (x) {
+                  row[o++] = x;
+                  mw |= 1u << (8 * u + n);
+                }
+              }
+            row[kOrRowMask + e0 / 4] = mw;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint64_t v = st[(vw + k) * nl];
+            row[kOrRowVV + 2 * k] = (uint32_t)v;
+            row[kOrRowVV + 2 * k + 1] = (uint32_t)(v >> 32);
+          }
+          if (dm)
+#pragma unroll
+            for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) row[kOrRowDV + n] = s32.ld(dl_env(kind) + n);
+        } else if (h < H.rows) {  // snapshot of the current state (+ deltaVersions), shared by the f gossips
           uint32_t* row = H.wrow(h);
           const uint32_t nw = crdt_words(kind) + (dm ? AGX_CRDT_NODES / 2u : 0u);  // batches of 4 (loads first)
           for (uint32_t i0 = 0; i0 < nw; i0 += 4) {

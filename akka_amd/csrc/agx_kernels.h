@@ -1223,6 +1223,11 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
 
 // the block's counters -> its own slot of the per-block stats (summed by k_stats_reduce)
 __device__ __forceinline__ void flush_stats(const BucketArgs& a, const uint32_t (&acc)[kBStats]) {
+#ifdef AGX_DEBUG_EMIT
+  if (acc[3] > (1u << 22) || acc[0] > (1u << 22) || acc[1] > (1u << 22))
+    printf("[agx dbg flush] block %u tid %u acc %u %u %u %u %u\n", blockIdx.x, threadIdx.x, acc[0], acc[1], acc[2], acc[3],
+           acc[4]);
+#endif
   uint32_t v[kBStats];
 #pragma unroll
   for (int i = 0; i < kBStats; ++i) v[i] = wave_incl_sum(acc[i]);
@@ -1846,6 +1851,11 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       nall += em.n_all;
       ndead += em.n_all - em.n_valid;
       nvoid += em.n_void;
+#ifdef AGX_DEBUG_EMIT
+      if (em.n_all > 4096u || nall > (1u << 22))
+        printf("[agx dbg actor] b %u la %u kind %u nd %u n_all %u n_valid %u nall %u pos %llu base %llu\n", b, la, kd, nd,
+               em.n_all, em.n_valid, nall, (unsigned long long)em.pos, (unsigned long long)(embase + L.ecnt[la]));
+#endif
     }
     if constexpr (kOrWave) {  // the runs with state work -> k_orset_merge's list (wave-aggregated slots)
       const uint32_t lane = lane_id();

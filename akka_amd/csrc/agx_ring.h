@@ -175,7 +175,9 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
         rr[j] = S.dpos[la0 + j] - ds[j];
         uint32_t x = (rsv[j] & 0xFFFFu) + q;
         x = x < rc ? x : x - rc;
-        const size_t o = (size_t)(a0 + la0 + j) * rc + (q < rr[j] ? x : 0u);
+        // (an actor with no ring head to drain -- past n_local in the last bucket too -- reads slot 0
+        // of the bucket's first actor: the rings are allocated for exactly n_local actors)
+        const size_t o = q < rr[j] ? (size_t)(a0 + la0 + j) * rc + x : (size_t)a0 * rc;
         hs[j] = g.src[o];
         hp[j] = g.pay[o];
       }

@@ -174,6 +174,10 @@ typedef struct bsp_sim {
   uint32_t host_lo, host_n;
   uint32_t* outbox;
   uint64_t outbox_n, outbox_cap;
+  /* the engine's overflow rule (agx_take_outbound, include/akka_gpu.h): at most outbox_cap appends
+   * between two takes are kept, later ones are dropped and counted; the next take reports the drop
+   * once (AGX_ECAPACITY) and clears it -- the run itself goes on */
+  uint64_t outbox_since, outbox_lost;
 } bsp_sim;
 
 bsp_sim* bsp_create(uint64_t n_actors, uint32_t throughput, uint32_t capacity, uint32_t n_words,
@@ -283,10 +287,18 @@ int bsp_set_outbound(bsp_sim* s, uint32_t first, uint32_t n, uint64_t cap) {
   if (n && first < s->n) return 1;
   s->host_lo = first;
   s->host_n = n;
-  s->outbox_cap = cap;
+  if (n && cap != s->outbox_cap) s->outbox_since = 0; /* the engine drains its device outbox here */
+  if (n) s->outbox_cap = cap;
   return 0;
 }
-uint64_t bsp_take_outbound(bsp_sim* s, uint32_t* dst, uint32_t* src, uint32_t* pay, uint64_t cap) {
+/* returns 0, or 5 (AGX_ECAPACITY: tells were dropped since the last take; nothing is taken then) */
+int bsp_take_outbound(bsp_sim* s, uint32_t* dst, uint32_t* src, uint32_t* pay, uint64_t cap, uint64_t* n) {
+  *n = 0;
+  s->outbox_since = 0;
+  if (s->outbox_lost) {
+    s->outbox_lost = 0;
+    return 5;
+  }
   const uint64_t k = s->outbox_n < cap ? s->outbox_n : cap;
   for (uint64_t i = 0; i < k; ++i) {
     dst[i] = s->outbox[3 * i];
@@ -295,7 +307,8 @@ uint64_t bsp_take_outbound(bsp_sim* s, uint32_t* dst, uint32_t* src, uint32_t* p
   }
   memmove(s->outbox, s->outbox + 3 * k, (size_t)(s->outbox_n - k) * 12);
   s->outbox_n -= k;
-  return k;
+  *n = k;
+  return 0;
 }
 
 void bsp_set_gossip(bsp_sim* s, uint32_t fanout, uint64_t seed) {
@@ -669,7 +682,10 @@ static int bsp_step(bsp_sim* s) {
     s->st.unhandled += x->st.unhandled;
     s->st.emitted += x->st.emitted;
     for (uint64_t i = 0; i < x->outbox_n; ++i) {
-      if (s->outbox_n >= s->outbox_cap) { s->P.error = 1; break; }
+      if (s->outbox_since++ >= s->outbox_cap) { /* past the capacity: dropped, reported by the next take */
+        s->outbox_lost++;
+        continue;
+      }
       uint32_t* o = (uint32_t*)realloc(s->outbox, (size_t)(s->outbox_n + 1) * 12);
       if (!o) { s->P.error = 1; break; }
       s->outbox = o;

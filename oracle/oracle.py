@@ -41,6 +41,10 @@ def build(force: bool = False) -> None:
             subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
 
 
+class OutboxOverflow(RuntimeError):
+    """bsp_take_outbound's AGX_ECAPACITY: outbound tells were dropped at a full outbox."""
+
+
 def _u32(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.uint32))
 
@@ -64,7 +68,7 @@ def _load_bsp():
             "bsp_set_mailbox_class": (ctypes.c_int, [vp, u32, u32]),
             "bsp_set_mailbox": (ctypes.c_int, [vp, u64, u64, u32]),
             "bsp_set_outbound": (ctypes.c_int, [vp, u32, u32, u64]),
-            "bsp_take_outbound": (u64, [vp, P32, P32, P32, u64]),
+            "bsp_take_outbound": (ctypes.c_int, [vp, P32, P32, P32, u64, P64]),
             "bsp_set_gossip": (None, [vp, u32, u64]),
             "bsp_set_delta_crdt": (ctypes.c_int, [vp, u32]),
             "bsp_set_behaviors": (ctypes.c_int, [vp, vp, u32, vp, u32, P32, u32]),
@@ -180,11 +184,17 @@ class BspOracle(_Base):
             raise ValueError("bsp_set_outbound failed")
 
     def take_outbound(self, cap=1 << 24):
-        """(dst, src, payload) arrays of the outbox, canonical emission order."""
+        """(dst, src, payload) arrays of the outbox, canonical emission order.  Raises OutboxOverflow
+        once when more than the outbox capacity was appended since the last take (the engine's
+        AGX_ECAPACITY from agx_take_outbound); the kept tells come out of the next take."""
         d, s, p = (np.zeros(cap, np.uint32) for _ in range(3))
-        n = self.lib.bsp_take_outbound(self.h, _p(d, ctypes.c_uint32), _p(s, ctypes.c_uint32),
-                                       _p(p, ctypes.c_uint32), cap)
-        return d[:n], s[:n], p[:n]
+        n = ctypes.c_uint64()
+        rc = self.lib.bsp_take_outbound(self.h, _p(d, ctypes.c_uint32), _p(s, ctypes.c_uint32),
+                                        _p(p, ctypes.c_uint32), cap, ctypes.byref(n))
+        if rc:
+            raise OutboxOverflow("outbound tells dropped: more than the outbox capacity between two takes")
+        k = int(n.value)
+        return d[:k], s[:k], p[:k]
 
     def set_gossip(self, fanout, seed):
         self.lib.bsp_set_gossip(self.h, fanout, seed)

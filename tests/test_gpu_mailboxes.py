@@ -137,6 +137,35 @@ def test_outbox_capacity_is_loud(built):
     eng.close()
 
 
+def test_outbox_overflow_parity(built):
+    """Outbox overflow, engine against the oracle (the oracle used to halt its run): both
+    keep running, both report the drop at the same take, the counters and final states agree, and
+    the take after the report hands out the capacity's worth of kept tells on both.  (Which tells are
+    kept differs: the device keeps the first appends to land, the oracle the first in canonical order.)"""
+    from akka_amd._lib import AgxError
+    from oracle import BspOracle
+    from oracle.oracle import OutboxOverflow
+    w = wl.mailbox_mix(4096, seed=1, throughput=5)
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+    ref = BspOracle(**w.engine_kwargs())
+    for t in (eng, ref):
+        w.apply_to(t)
+        t.set_outbound(w.n_actors, 32, capacity=4)
+    sg, so = eng.run(3), ref.run(3)
+    for k in COUNT_KEYS:
+        assert getattr(sg, k) == so[k], (k, getattr(sg, k), so[k])
+    with pytest.raises(AgxError, match="outbound tells dropped"):
+        eng.take_outbound()
+    with pytest.raises(OutboxOverflow):
+        ref.take_outbound()
+    assert eng.take_outbound()[0].size == ref.take_outbound()[0].size == 4
+    sg, so = eng.run(), ref.run()
+    for k in COUNT_KEYS:
+        assert getattr(sg, k) == so[k], (k, getattr(sg, k), so[k])
+    assert np.array_equal(eng.read_state()[0], ref.read_state()[0])
+    eng.close()
+
+
 def test_outbox_capacity_change_keeps_pending(built):
     """agx_set_outbound with a new capacity while tells wait in the device outbox: they move to the
     host queue first and come out of the next take, in order (they were lost)."""

@@ -574,15 +574,18 @@ def test_ring_apply(built, monkeypatch, mode, ba, case):
         assert_same(sg, so, st, sto, f"{case} ring={ring}")
 
 
-@pytest.mark.parametrize("capacity,rings", [(64, False), (255, False), (256, True), (1000, True)])
-def test_ring_apply_default(built, monkeypatch, capacity, rings):
+@pytest.mark.parametrize("capacity,rings,n", [(64, False, 60_000), (255, False, 60_000), (256, True, 60_000),
+                                              (1000, True, 60_000), (1000, True, 60_001), (300, True, 4_099)])
+def test_ring_apply_default(built, monkeypatch, capacity, rings, n):
     """Without AGX_RING_APPLY the ring apply is on exactly when the largest bounded capacity is
     >= 256 (deep queues: C3's BoundedMailbox(1000)), and either way bit-exact against the oracle
-    (C3's FANOUT shape at 3-bit digits, hot actors' queues filling up)."""
+    (C3's FANOUT shape at 3-bit digits, hot actors' queues filling up).  Populations that are not a
+    multiple of 4 (or of the bucket width) put actors past n_local into the last bucket's threads:
+    their ring-head loads must stay inside the n_local rings."""
     from oracle import BspOracle
     monkeypatch.delenv("AGX_RING_APPLY", raising=False)
     monkeypatch.setenv("AGX_RADIX_BITS", "3")
-    w = wl.zipf_fanout(60_000, k=1, ttl=12, root_every=1, capacity=capacity)
+    w = wl.zipf_fanout(n, k=1, ttl=12, root_every=1, capacity=capacity)
     ref = BspOracle(**w.engine_kwargs())
     w.apply_to(ref)
     so = ref.run()

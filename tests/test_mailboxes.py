@@ -9,6 +9,7 @@ reference's mailbox specs.  The GPU parity of the same workloads is in tests/tes
   actor answering a host-side sender leaves its replies in the outbox, not in dead letters.
 """
 import numpy as np
+import pytest
 
 from akka_amd import workloads as wl
 from akka_amd.engine import Kind, NO_SENDER
@@ -71,3 +72,29 @@ def test_mailbox_mix_conservation():
     d, s, p = o.take_outbound()
     assert d.size > 0 and (d >= w.n_actors).all()
     assert st["staged"] + st["emitted"] == st["delivered"] + st["dead_letters"] + st["in_flight"]
+
+
+def test_outbox_overflow_oracle_matches_engine_rule():
+    """The oracle's outbox overflow follows the engine (agx_take_outbound): the run goes
+    on, the next take reports the drop once (OutboxOverflow = AGX_ECAPACITY), the kept tells (the
+    capacity's worth) come out of the take after it, and the counters are unaffected."""
+    from oracle.oracle import OutboxOverflow
+    w = wl.mailbox_mix(4096, seed=1, throughput=5)
+    big = BspOracle(**w.engine_kwargs())
+    w.apply_to(big)
+    big.set_outbound(w.n_actors, 32, capacity=1 << 20)
+    sb = big.run(3)
+    total = big.take_outbound()[0].size
+    assert total > 4
+    o = BspOracle(**w.engine_kwargs())
+    w.apply_to(o)
+    o.set_outbound(w.n_actors, 32, capacity=4)
+    st = o.run(3)
+    assert st == sb  # (outbound tells leave the engine: no counter depends on the outbox)
+    with pytest.raises(OutboxOverflow):
+        o.take_outbound()
+    d, s, p = o.take_outbound()
+    assert d.size == 4 and (d >= w.n_actors).all()
+    o.take_outbound()  # nothing lost since: no report
+    st2, sb2 = o.run(), big.run()
+    assert st2 == sb2
