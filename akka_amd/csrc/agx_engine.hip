@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "agx_kernels.h"
+#include "agx_tellq.h"
 #include "agx_variants.h"
 
 using namespace agx;
@@ -108,6 +109,7 @@ struct SortPlan {  // LSD passes over key bits [bb, key_bits)
 
 struct agx_engine {
   agx_cfg cfg{};
+  TellQueue tq;  // agx_tell: the lock-free tell path (agx_tellq.h), taken by agx_run
   hipStream_t stream = nullptr;
   uint64_t n_global = 0, n_local = 0, cap = 0, cap_emit = 0;
   uint32_t max_supers = 1, dstride = 4, dsub = kSub;  // dense passes: super-tiles (at most), table row stride, max tiles
@@ -1484,6 +1486,30 @@ agx_status mr_slabs(agx_engine* e, uint64_t want) {
 
 agx_status mr_step_dev(agx_engine* e, uint32_t idx);
 
+// All-or-nothing capture: every rank all-gathers its capture result before the first replay, and a
+// rank keeps its graph only if every rank captured -- otherwise all of them replay eagerly.  (A rank
+// replaying its captured collectives while a peer issues the same collectives eagerly is legal for
+// RCCL, but one rank's failed capture must not leave the ranks on different paths whose first
+// launches then wait on each other.)
+agx_status mr_agree_capture(agx_engine* e) {
+  e->h_pin64[0] = e->mr_gx ? 1u : 0u;
+  HIP_TRY(hipMemcpyAsync(e->d_cvec, e->h_pin64, 8, hipMemcpyHostToDevice, e->stream));
+  NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, 1, ncclUint64, e->comm, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_cmat, (size_t)e->R * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  uint32_t ok = 0;
+  for (uint32_t r = 0; r < e->R; ++r) ok += e->h_pin64[r] ? 1u : 0u;
+  if (getenv("AGX_MR_DEBUG"))
+    fprintf(stderr, "[agx rank %u] multi-rank replay capture: %u of %u ranks captured%s\n", e->rank, ok, e->R,
+            ok == e->R ? "" : " -> eager replays on every rank");
+  if (ok != e->R) {
+    if (e->mr_gx) hipGraphExecDestroy(e->mr_gx);
+    e->mr_gx = nullptr;
+    e->mr_graph_ok = false;
+  }
+  return AGX_OK;
+}
+
 // kMrReplay device-resident supersteps as one graph.  A failed capture (a collective that cannot be
 // captured) ends the capture, clears mr_graph_ok and returns AGX_OK: the caller replays eagerly.
 agx_status capture_mr(agx_engine* e, uint32_t steps) {
@@ -1628,7 +1654,10 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
                         atoi(getenv("AGX_MR_GRAPH")) != 0;
     while (left && !quiet) {
       const uint32_t k = std::min(left, kMrReplay);
-      if (graphs && k == kMrReplay && !e->mr_gx) AGX_TRY(capture_mr(e, kMrReplay));
+      if (graphs && k == kMrReplay && !e->mr_gx) {
+        AGX_TRY(capture_mr(e, kMrReplay));
+        AGX_TRY(mr_agree_capture(e));
+      }
       if (graphs && k == kMrReplay && e->mr_gx) {
         HIP_TRY(hipGraphLaunch(e->mr_gx, e->stream));
         ++e->mr_replays;
@@ -2351,6 +2380,11 @@ agx_status agx_set_fanout(agx_engine* e, uint32_t k, uint64_t seed, const uint32
 
 agx_status agx_set_graph(agx_engine* e, const uint64_t* row_ptr, const uint32_t* col) {
   if (!e || !row_ptr) return set_err(AGX_EINVAL, "bad graph args");
+  // the whole row_ptr is checked before col is read: then col[0, row_ptr[n_actors]) is every index
+  // read below, the length a binding checks its array against (agx_jni.c setGraph)
+  for (uint64_t id = 0; id < e->n_global; ++id)
+    if (row_ptr[id + 1] < row_ptr[id]) return set_err(AGX_EINVAL, "row_ptr not monotone at %llu", (unsigned long long)id);
+  if (row_ptr[e->n_global] > row_ptr[0] && !col) return set_err(AGX_EINVAL, "bad graph args: null col");
   AGX_TRY(ensure_dev(e));
   // keep only the rows of local actors (rows indexed by local id)
   std::vector<uint64_t> row(e->n_local + 1, 0);
@@ -2358,7 +2392,6 @@ agx_status agx_set_graph(agx_engine* e, const uint64_t* row_ptr, const uint32_t*
   for (uint64_t l = 0; l < e->n_local; ++l) {
     uint64_t id = e->R > 1 ? e->h_gid[l] : l;
     uint64_t b = row_ptr[id], en = row_ptr[id + 1];
-    if (en < b) return set_err(AGX_EINVAL, "row_ptr not monotone at %llu", (unsigned long long)id);
     for (uint64_t j = b; j < en; ++j) c.push_back(col[j]);
     row[l + 1] = c.size();
   }
@@ -2434,9 +2467,37 @@ agx_status agx_stage_tells(agx_engine* e, const uint32_t* dst, const uint32_t* s
   return AGX_OK;
 }
 
+// the lock-free tell path: take every tell published so far (producer by producer, each in its
+// order) into the host staging, exactly as agx_stage_tells would have staged them
+agx_status take_tells(agx_engine* e) {
+  agx_status st = AGX_OK;
+  e->tq.take([&](uint32_t d, uint32_t s, uint32_t p) {
+    const agx_status r = agx_stage_tells(e, &d, &s, &p, 1);
+    if (r != AGX_OK && st == AGX_OK) st = r;
+  });
+  return st;
+}
+
+agx_status agx_tell(agx_engine* e, uint32_t dst, uint32_t src, uint32_t payload, int32_t* schedule) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  if ((src & AGX_WIDE_BIT) && src != AGX_NO_SENDER)
+    return set_err(AGX_EINVAL, "tell: sender %u is not an actor id (bit 31 tags CRDT state gossips)", src);
+  const bool sched = e->tq.tell(dst, src, payload);
+  if (schedule) *schedule = sched ? 1 : 0;
+  return AGX_OK;
+}
+
+agx_status agx_pump_idle(agx_engine* e, int32_t* reschedule) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  const bool again = e->tq.pump_idle();
+  if (reschedule) *reschedule = again ? 1 : 0;
+  return AGX_OK;
+}
+
 agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
   if (!e) return set_err(AGX_EINVAL, "null engine");
   AGX_TRY(ensure_dev(e));
+  AGX_TRY(take_tells(e));
   if (e->R > 1 && !e->comm) return set_err(AGX_ESTATE, "n_ranks > 1 needs agx_comm_init (or agx_group_run)");
   AGX_TRY(prepare_run(e));
   AGX_TRY(setup_rings(e));

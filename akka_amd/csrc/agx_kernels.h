@@ -959,6 +959,15 @@ constexpr bool kMonoShortcut = false;
 #ifndef AGX_PF
 #define AGX_PF 4
 #endif
+#ifndef AGX_COMPACT_DRAIN
+#define AGX_COMPACT_DRAIN 1
+#endif
+// single-pass drains of the actors with mail, one actor per thread (bucket_finish kCompact; A/B build knob)
+constexpr bool kCompactDrain = AGX_COMPACT_DRAIN != 0;
+#ifndef AGX_FWD_PRE
+#define AGX_FWD_PRE 4
+#endif
+constexpr uint32_t kFwdPre = AGX_FWD_PRE;  // FORWARD_RR destinations loaded before a compacted drain
 constexpr int kPF = AGX_PF;                     // apply prefetch window (messages in global scratch)
 
 // Tell staging in LDS (single-pass path): tells overwrite consumed inbox slots of the same actor.
@@ -1437,6 +1446,11 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   // loads (row_ptr, then col) per message inside the serial drain (fdeg = kNoHint: no hint).
   constexpr bool kFwd = !kWide && KM == kb(AGX_KIND_FORWARD_RR);
   constexpr bool kUnrollActors = KM == kb(AGX_KIND_RING);  // single pass: see sp_actor below
+  // single pass, behaviours other than the ring: the actors with mail are drained one per thread
+  // (a compacted list) instead of four fixed actors per thread one after the other -- a sparse
+  // bucket (C5: ~150 of 2048 actors with mail) then costs one actor's drain, not up to four
+  constexpr bool kCompact = !kWide && !kUnrollActors && kCompactDrain;
+  constexpr bool kFwdHint = kFwd && !kCompact;  // (the compacted drain loads its hints itself)
   constexpr uint32_t kNoHint = 0xFFFFFFFFu;
   uint64_t frb[kBAct];
   uint32_t fdeg[kBAct], fdst[kBAct];
@@ -1458,7 +1472,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           x0[j] = has ? ldg64(P.state, sidx(P, l, 0)) : 0ull;  // (32-bit offsets: one VGPR per address)
           x1[j] = has && P.W > 1 ? ldg64(P.state, sidx(P, l, 1)) : 0ull;
         }
-        if constexpr (kFwd) {
+        if constexpr (kFwdHint) {
           frb[j] = has ? P.row_ptr[l] : 0ull;
           fre[j] = has ? P.row_ptr[l + 1] : ~0ull;  // (no mail: deg out of range -> no hint)
         }
@@ -1489,7 +1503,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
         x0[j] = ldg64(P.state, li[j] * P.sa);  // (32-bit offsets: one VGPR per address)
         x1[j] = ldg64(P.state, li[j] * P.sa + w1off);
       }
-      if constexpr (kFwd) {
+      if constexpr (kFwdHint) {
         frb[j] = P.row_ptr[li[j]];
         fre[j] = P.row_ptr[li[j] + 1];
       }
@@ -1500,13 +1514,13 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       kd[j] = has ? kd[j] : 0u;
       x0[j] = has ? x0[j] : 0ull;
       x1[j] = has && P.W > 1 ? x1[j] : 0ull;
-      if constexpr (kFwd) {
+      if constexpr (kFwdHint) {
         frb[j] = has ? frb[j] : 0ull;
         fre[j] = has ? fre[j] : ~0ull;  // (no mail: deg out of range -> no hint)
       }
     }
     }  // fused
-    if constexpr (kFwd) {
+    if constexpr (kFwdHint) {
 #pragma unroll
       for (int j = 0; j < kBAct; ++j) {
         const uint64_t deg = fre[j] - frb[j];
@@ -1534,10 +1548,37 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     uint32_t* const sts = kLds ? L.src : a.scr.src + lo;
     uint32_t* const stp = kLds ? L.pay : a.scr.pay + lo;
     uint32_t ecl[kBAct];
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    uint32_t alist[kBAct];  // kCompact: this thread's actors with mail (active index x * kBThreads + tid)
+    if constexpr (kCompact) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        const uint32_t la = j * kBThreads + tid;
+        c += la < na && L.seg[la + 1] != L.seg[la] && (L.alive[la] & 1u) ? 1u : 0u;
+      }
+      uint32_t nactive;
+      uint32_t pos = block_excl_sum<kBThreads>(c, L.scratch, &nactive);  // (syncs: LDS state stores done)
+      uint32_t* const actl = L.key;  // (the inbox keys are not read any more: the drains read src / pay)
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        const uint32_t la = j * kBThreads + tid;
+        if (la < na && L.seg[la + 1] != L.seg[la] && (L.alive[la] & 1u)) actl[pos++] = la;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int x = 0; x < kBAct; ++x) {
+        const uint32_t i = x * kBThreads + tid;
+        alist[x] = i < nactive ? actl[i] : kNone;
+      }
+      __syncthreads();  // (every entry read before the drains stage tells over L.key)
+    }
+    auto act_of = [&](int j) -> uint32_t { return kCompact ? alist[j] : (uint32_t)(j * kBThreads + tid); };
     auto sp_actor = [&](int j) {
-      const uint32_t la = j * kBThreads + tid;
-      const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
+      const uint32_t la = act_of(j);
       ecl[j] = 0;
+      if (kCompact && la == kNone) return;
+      const uint32_t s0 = L.seg[la], len = L.seg[la + 1] - s0;
       if (la >= na || !len || !(L.alive[la] & 1u)) return;
       const uint32_t l = a0 + la;
       const uint32_t self = P.R > 1 ? P.gid[l] : l;
@@ -1551,10 +1592,27 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       uint64_t hb = 0;
       uint32_t hdeg = kNoHint, hdst = 0;
       bool fresh = true;  // no forward yet: the next edge is fdst
-      if constexpr (kFwd) {  // (j is wave-uniform)
+      uint32_t fpre[kFwdPre], nfw = 0;  // (kCompact) the first kFwdPre forwards' destinations, forwards so far
+      if constexpr (kFwdHint) {  // (j is wave-uniform)
         hb = j == 0 ? frb[0] : j == 1 ? frb[1] : j == 2 ? frb[2] : frb[3];
         hdeg = j == 0 ? fdeg[0] : j == 1 ? fdeg[1] : j == 2 ? fdeg[2] : fdeg[3];
         hdst = j == 0 ? fdst[0] : j == 1 ? fdst[1] : j == 2 ? fdst[2] : fdst[3];
+      }
+      if constexpr (kFwd && kCompact) {
+        // this actor's out-edge row, then the destinations of its next kFwdPre round-robin edges in
+        // one round trip (forward m of the drain takes edge (cursor + m) mod deg: apply_msg's
+        // arithmetic), so a drain of up to kFwdPre forwards has no dependent global load
+        const uint64_t rb = P.row_ptr[l], deg = P.row_ptr[l + 1] - rb;
+        if (deg < kNoHint && wv[1] + kFwdPre <= 0xFFFFFFFFull) {
+          hb = rb;
+          hdeg = (uint32_t)deg;
+          uint32_t e = deg ? (uint32_t)wv[1] % (uint32_t)deg : 0u;
+#pragma unroll
+          for (uint32_t m = 0; m < kFwdPre; ++m) {
+            fpre[m] = deg && m < nd ? P.col[rb + e] : 0u;
+            e = e + 1u == (uint32_t)deg ? 0u : e + 1u;
+          }
+        }
       }
       for (uint32_t q = 0; q < nd; ++q) {
         const uint32_t sv = sts[s0 + q], pv = stp[s0 + q];
@@ -1572,8 +1630,17 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           // apply_msg's FORWARD_RR with the prefetched row (same cursor arithmetic)
           wv[0] += 1;
           if (pv > 0 && hdeg) {
-            const uint32_t d = fresh ? hdst : P.col[hb + (uint32_t)wv[1] % hdeg];
-            fresh = false;
+            uint32_t d;
+            if constexpr (kCompact) {
+              d = 0u;
+#pragma unroll
+              for (uint32_t m = 0; m < kFwdPre; ++m) d = nfw == m ? fpre[m] : d;
+              if (nfw >= kFwdPre) d = P.col[hb + (uint32_t)wv[1] % hdeg];
+              ++nfw;
+            } else {
+              d = fresh ? hdst : P.col[hb + (uint32_t)wv[1] % hdeg];
+              fresh = false;
+            }
             wv[1] += 1;
             em(d, pv - 1);
           }
@@ -1631,7 +1698,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       // group them by destination straight into this superstep's tell arena
       uint32_t* ukey = reinterpret_cast<uint32_t*>(L.U);
       auto compact = [&](int j) {
-        const uint32_t la = j * kBThreads + tid;
+        if (!ecl[j]) return;
+        const uint32_t la = act_of(j);
         const uint32_t s0 = L.seg[la], o = L.ecnt[la];
         for (uint32_t e = 0; e < ecl[j]; ++e) {
           ukey[o + e] = L.key[s0 + e];
@@ -1652,7 +1720,8 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       constexpr bool kMeta = !kGather && !kOwner && kLds;  // bypass fast path: the chunk's key summary
       uint32_t* const ck = reinterpret_cast<uint32_t*>(L.U);  // (free: the state was written back)
       auto compact = [&](int j) {
-        const uint32_t la = j * kBThreads + tid;
+        if (!ecl[j]) return;
+        const uint32_t la = act_of(j);
         const uint32_t s0 = L.seg[la], o = L.ecnt[la];
         for (uint32_t e = 0; e < ecl[j]; ++e) {
           a.em.key[embase + o + e] = stk[s0 + e];
@@ -1934,6 +2003,216 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     acc[4] += nact;
   }
   __syncthreads();  // (L.nh and the other per-bucket LDS arrays are reset by the next bucket)
+  AGX_STAMP(a, 8);
+  if (a.dbg && tid == 0) {  // diagnostic: slowest bucket of this block (cycles, bucket, inbox size)
+    const unsigned long long dur = a.dbg[blockIdx.x * 16 + 8] - a.dbg[blockIdx.x * 16 + 0];
+    if (dur > a.dbg[blockIdx.x * 16 + 10]) {
+      a.dbg[blockIdx.x * 16 + 10] = dur;
+      a.dbg[blockIdx.x * 16 + 11] = b;
+      a.dbg[blockIdx.x * 16 + 12] = cnt;
+    }
+  }
+}
+
+// ---- Dense buckets: at most one message per actor.
+// When a bucket's inbox keys are strictly increasing in inbox order (a token ring, a stencil, any
+// one-to-one topology), every actor holds at most one message, and bucket_finish's rule for len = 1
+// is: admitted (C = 0 or C >= 1), drained (T >= 1), nothing queued (AD/Mailbox.scala:261,551-565).
+// Each message is then applied by the thread that holds it, straight from registers, and its tell
+// (max_emit 1) goes to its rank among the bucket's tells -- sender order = inbox order = actor
+// order, exactly where bucket_finish's per-actor scan would put it.  What this skips: the in-bucket
+// counting sort (segment counts and scan), the classification and backlog scans, the LDS round of
+// the state words and the per-actor drain loop -- about half of the barriers of a bucket.
+struct RegEmitter {  // at most one tell per message (max_emit 1), kept in registers
+  const DevParams* P;
+  uint32_t self, key, pay, n_valid, n_all;
+  __device__ __forceinline__ void operator()(uint32_t dst, uint32_t p) {
+    if (dst >= P->n_global) {  // a host-side actor (the reply path: outbox) or an unknown ref -> deadLetters
+      if (!outbound_tell(*P, dst, self, p, true)) ++n_all;
+      return;
+    }
+    ++n_all;
+    ++n_valid;
+    key = (P->R > 1) ? P->route[dst] : dst;
+    pay = p;
+  }
+  __device__ __forceinline__ void wide(uint32_t, uint32_t) {}
+};
+
+// Items: the bucket's inbox in LDS (L.key / L.src / L.pay, inbox order); item q is handled by thread
+// q % kBThreads as its r = q / kBThreads -- the actor mapping of the fused early state loads
+// (pre0 / pre1: actor r * kBThreads + tid), so a full bucket (item q = actor q) uses them directly.
+template <uint32_t KM, bool kGather, bool kOwner>
+__device__ __forceinline__ void dense_finish(const BucketArgs& a, const BucketLds& L, uint32_t b, uint32_t lo,
+                                             uint32_t cnt, uint32_t a0, uint32_t w, uint32_t (&acc)[kBStats],
+                                             const uint64_t* pre0, const uint64_t* pre1) {
+  const DevParams& P = a.P;
+  const int tid = threadIdx.x;
+  const uint32_t lane = lane_id(), wv = (uint32_t)tid / kWave;
+  const uint64_t ltm = lanemask_lt();
+  const uint32_t amask = (1u << a.bb) - 1u, nhmask = (1u << a.nx_bits) - 1u;
+  constexpr bool kKindNeeded = (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0;
+  constexpr bool kBypass = !kGather && !kOwner;
+  AGX_STAMP(a, 3);
+  // ---- items, their actors' flags and state words (all loads issued together)
+  uint32_t sv[kBIpt], pv[kBIpt], l[kBIpt], ab[kBIpt], kd[kBIpt];
+  uint64_t x0[kBIpt], x1[kBIpt];
+  bool on[kBIpt];
+#pragma unroll
+  for (int r = 0; r < kBIpt; ++r) {
+    const uint32_t q = r * kBThreads + tid;
+    on[r] = q < cnt;
+    const uint32_t la = on[r] ? L.key[q] & amask : 0u;
+    sv[r] = on[r] ? L.src[q] : 0u;
+    pv[r] = on[r] ? L.pay[q] : 0u;
+    ab[r] = on[r] ? L.alive[la] : 0u;
+    l[r] = a0 + la;
+  }
+  const uint32_t w1off = P.W > 1 ? P.sw : 0u;
+#pragma unroll
+  for (int r = 0; r < kBIpt; ++r) {
+    kd[r] = kKindNeeded ? P.kind[l[r]] : 0u;
+    const bool early = pre0 && l[r] == a0 + r * kBThreads + tid;  // (fused: loaded at the bucket's start)
+    x0[r] = early ? pre0[r] : ldg64(P.state, l[r] * P.sa);
+    x1[r] = early ? pre1[r] : ldg64(P.state, l[r] * P.sa + w1off);
+  }
+  // ---- apply (one message per actor: admitted and drained, bucket_finish with len = 1)
+  uint32_t ndel = 0, ndead = 0, nunh = 0, nall = 0, nact = 0;
+  uint32_t tk[kBIpt], ts[kBIpt], tp[kBIpt];
+  bool tv[kBIpt];
+#pragma unroll
+  for (int r = 0; r < kBIpt; ++r) {
+    tv[r] = false;
+    tk[r] = ts[r] = tp[r] = 0u;
+    if (!on[r]) continue;
+    if (!(ab[r] & 1u)) {  // to a stopped actor: a dead letter
+      ++ndead;
+      continue;
+    }
+    const uint32_t self = P.R > 1 ? P.gid[l[r]] : l[r];
+    RegEmitter em{&P, self, 0u, 0u, 0u, 0u};
+    uint64_t wv2[2] = {x0[r], x1[r]};
+    uint32_t kc = kd[r];
+    ++nact;
+    ++ndel;
+    const uint32_t res = apply_msg<KM>(P, kc, self, l[r], wv2, sv[r], pv[r], em);
+    if (res == AGX_RES_UNHANDLED) ++nunh;
+    if (res == AGX_RES_STOPPED) {
+      if constexpr (kGather) P.alive[l[r]] = (uint8_t)(ab[r] & 0xFEu);  // fused: only this block reads the bucket's flags
+      else P.stopq[atomicAdd(P.nstop, 1u)] = l[r];
+    }
+    stg64(P.state, l[r] * P.sa, wv2[0]);
+    if (P.W > 1) stg64(P.state, l[r] * P.sa + w1off, wv2[1]);
+    if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
+      if (kc != kd[r]) P.kind[l[r]] = (uint8_t)kc;
+    nall += em.n_all;
+    ndead += em.n_all - em.n_valid;
+    tv[r] = em.n_valid != 0u;
+    tk[r] = em.key;
+    ts[r] = self;
+    tp[r] = em.pay;
+  }
+#pragma unroll
+  for (int r = 0; r < kBIpt; ++r)
+    if (tv[r]) lds_hist_inc(L.nh, (tk[r] >> a.nx_shift) & nhmask);
+  AGX_STAMP(a, 5);
+  // ---- each tell's rank in item order: per (row r, wave) counts, one block-wide exclusive scan
+  uint32_t rk[kBIpt];
+#pragma unroll
+  for (int r = 0; r < kBIpt; ++r) {
+    const uint64_t m = __ballot(tv[r]);
+    rk[r] = (uint32_t)__popcll(m & ltm);
+    if (lane == 0) L.seg[r * kBWaves + wv] = (uint32_t)__popcll(m);  // (L.seg: no segments on this path)
+  }
+  __syncthreads();
+  uint32_t emtot = 0;
+  {
+    uint32_t run = 0;
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r)
+#pragma unroll
+      for (int x = 0; x < kBWaves; ++x) {
+        const uint32_t c = L.seg[r * kBWaves + x];
+        if (x == (int)wv) rk[r] += run;
+        run += c;
+      }
+    emtot = run;
+  }
+  const uint64_t embase = (uint64_t)lo * a.kmax;  // this bucket's slice of the tell arena
+  if (tid == 0) {  // nothing queued: the bucket's backlog is empty
+    if constexpr (kGather) {
+      a.g.blo[w][b] = lo;
+      a.g.blc[w][b] = 0u;
+    } else {
+      a.chunk_off[b] = lo;
+      a.chunk_cnt[b] = 0u;
+    }
+  }
+  if constexpr (kGather || kOwner) {
+    // compacted in sender order into U, then grouped by destination (bucket / owner rank)
+    uint32_t* ukey = reinterpret_cast<uint32_t*>(L.U);
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r)
+      if (tv[r]) {
+        ukey[rk[r]] = tk[r];
+        ukey[kBucket + rk[r]] = ts[r];
+        ukey[2 * kBucket + rk[r]] = tp[r];
+      }
+    __syncthreads();
+    group_tells<true>(a, L, b, w, embase, emtot, a.em);
+  } else {
+    uint32_t* const ck = reinterpret_cast<uint32_t*>(L.U);
+#pragma unroll
+    for (int r = 0; r < kBIpt; ++r)
+      if (tv[r]) {
+        a.em.key[embase + rk[r]] = tk[r];
+        a.em.src[embase + rk[r]] = ts[r];
+        a.em.pay[embase + rk[r]] = tp[r];
+        ck[rk[r]] = tk[r];
+      }
+    if (a.emmeta) {  // identity grouping (k_ident_combine): first / last key and descents, sender order
+      __syncthreads();
+      uint32_t nd = 0, dp = 0;
+#pragma unroll
+      for (uint32_t i = 4 * tid; i < 4 * tid + 4; ++i)
+        if (i > 0 && i < emtot && ck[i] < ck[i - 1]) {
+          ++nd;
+          dp = i;
+        }
+      uint32_t tnd, tdp;
+      block_excl_sum2<kBThreads>(nd, nd ? dp : 0u, L.scratch, &tnd, &tdp);
+      if (tid == 0) a.emmeta[b] = make_uint4(emtot ? ck[0] : 0u, emtot ? ck[emtot - 1] : 0u, tnd, tdp);
+    }
+  }
+  if (!kGather && tid == 0) {  // the bucket's tell chunk (multi-pass and multi-rank: in-flight accounting)
+    a.chunk_off[a.nb + b] = (uint32_t)embase;
+    a.chunk_cnt[a.nb + b] = emtot;
+  }
+  __syncthreads();
+  AGX_STAMP(a, 7);
+  if constexpr (kBypass)  // next first-pass histogram column of this bucket's tell chunk
+    for (uint32_t d = tid; d < (1u << a.nx_bits); d += kBThreads)
+      if (L.nh[d]) atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + a.ng + b / a.G], L.nh[d]);
+  if constexpr (kOwner) {  // multi-rank: per bucket through LDS (as bucket_finish)
+    const uint32_t v0 = wave_incl_sum(ndel), v1 = wave_incl_sum(ndead), v2 = wave_incl_sum(nunh),
+                   v3 = wave_incl_sum(nall), v4 = wave_incl_sum(nact);
+    if (lane == kWave - 1) {
+      atomicAdd(&L.stat[0], (unsigned long long)v0);
+      atomicAdd(&L.stat[1], (unsigned long long)v1);
+      atomicAdd(&L.stat[2], (unsigned long long)v2);
+      atomicAdd(&L.stat[3], (unsigned long long)v3);
+      atomicAdd(&L.stat[4], (unsigned long long)v4);
+    }
+    __syncthreads();
+    if (tid < kBStats && L.stat[tid]) atomicAdd(&a.bstats[(size_t)blockIdx.x * kBStats + tid], L.stat[tid]);
+  } else {
+    acc[0] += ndel;
+    acc[1] += ndead;
+    acc[2] += nunh;
+    acc[3] += nall;
+    acc[4] += nact;
+  }
+  __syncthreads();  // (the per-bucket LDS arrays are reset by the next bucket)
   AGX_STAMP(a, 8);
   if (a.dbg && tid == 0) {  // diagnostic: slowest bucket of this block (cycles, bucket, inbox size)
     const unsigned long long dur = a.dbg[blockIdx.x * 16 + 8] - a.dbg[blockIdx.x * 16 + 0];
@@ -2386,6 +2665,10 @@ static __global__ void __launch_bounds__(kTinyThreads) k_tiny_apply(BucketArgs a
 #ifndef AGX_EARLY_STATE
 #define AGX_EARLY_STATE 1
 #endif
+#ifndef AGX_DENSE
+#define AGX_DENSE 1
+#endif
+constexpr bool kDenseBuckets = AGX_DENSE != 0;  // dense buckets (one message per actor) skip the sort (A/B build knob)
 constexpr bool kEarlyState = AGX_EARLY_STATE != 0;  // fused fast path: state loads at bucket start (A/B build knob)
 #ifndef AGX_LATE_ALIVE
 #define AGX_LATE_ALIVE 1
@@ -2874,7 +3157,7 @@ static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_
   __shared__ uint8_t s_kind[kBucket];
   __shared__ uint32_t s_nh[kRadix];
   __shared__ uint32_t scratch[2 * (kBWaves + 1)];
-  __shared__ uint32_t s_lo, s_hi, s_g[6], s_rowtop;
+  __shared__ uint32_t s_lo, s_hi, s_g[6], s_rowtop, s_flags;
   __shared__ unsigned long long s_stat[5];
   const BucketLds L{s_key, s_src, s_pay, U, s_seg, s_ecnt, s_alive, s_kind, s_nh, scratch, s_stat, &s_rowtop};
   uint16_t* whist = reinterpret_cast<uint16_t*>(U);  // [kBWaves][kBucket]
@@ -2942,12 +3225,14 @@ static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_
     const uint32_t na = min(1u << a.bb, P.n_local - a0);
     if (tid < 5) s_stat[tid] = 0;
     if (tid == 0) s_rowtop = 0;
+    if (tid == 0) s_flags = 0;
     for (uint32_t d = tid; d < kRadix; d += kBThreads) s_nh[d] = 0;
     uint32_t* my_tc = nullptr;  // (fused) this thread's table entry, zeroed once the bucket is processed
     // fused fast path, plain behaviours: state words 0 / 1 of the bucket's actors are loaded here,
     // beside the table row, so their round trip overlaps the gather instead of following the sort
     // (actors past n_local read actor 0's words; bucket_finish masks actors without mail)
     constexpr bool kEarly = kGather && kDefer && !kWide && kEarlyState;
+    constexpr bool kDense = !kWide && kDenseBuckets;  // (dense_finish: at most one message per actor)
     uint64_t ex0[kBAct] = {}, ex1[kBAct] = {};
     uint32_t alive4 = 0;        // alive flags of actors 4*tid..4*tid+3, loaded first (a0 is a multiple of 32)
     {
@@ -3169,13 +3454,24 @@ static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_
         }
       }
       __syncthreads();
-      int ok = 1;
+      // (and strictly increasing: at most one message per actor -- the dense path, dense_finish)
+      uint32_t bad = 0;
 #pragma unroll
       for (int r = 0; r < kBIpt; ++r) {
         const uint32_t q = wbase + r * kWave + lane;
-        if (q < cnt && q > 0) ok &= (s_key[q - 1] & amask) <= (k[r] & amask);
+        if (q < cnt && q > 0) {
+          const uint32_t p0 = s_key[q - 1] & amask, p1 = k[r] & amask;
+          bad |= p0 > p1 ? 3u : p0 == p1 ? 2u : 0u;
+        }
       }
-      const bool presorted = __syncthreads_and(ok) != 0;
+      if (bad) atomicOr(&s_flags, bad);
+      __syncthreads();
+      const uint32_t flags = s_flags;
+      const bool presorted = !(flags & 1u);
+      if (kDense && !(flags & 2u) && a.kmax == 1) {
+        dense_finish<KM, kGather, kOwner>(a, L, b, lo, cnt, a0, wpar, acc, kEarly ? ex0 : nullptr, kEarly ? ex1 : nullptr);
+        continue;
+      }
       uint32_t tl[kBAct];
       if (presorted) {
         // per-actor counts by LDS atomics (s_seg zeroed before the copy), then the block scan below

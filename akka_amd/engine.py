@@ -223,6 +223,19 @@ class GpuEngine:
         check(self.lib.agx_stage_tells(self._h, _ptr(dst, ctypes.c_uint32), srcp, _ptr(pay, ctypes.c_uint32),
                                        dst.size))
 
+    def tell_one(self, dst: int, payload: int, src: int = NO_SENDER) -> bool:
+        """agx_tell (any thread, lock-free): True iff the caller must submit the pump (the engine
+        went from idle to scheduled)."""
+        sched = ctypes.c_int32(0)
+        check(self.lib.agx_tell(self._h, dst, src, payload, ctypes.byref(sched)))
+        return bool(sched.value)
+
+    def pump_idle(self) -> bool:
+        """agx_pump_idle (the pump's last call): True iff tells arrived meanwhile (submit again)."""
+        again = ctypes.c_int32(0)
+        check(self.lib.agx_pump_idle(self._h, ctypes.byref(again)))
+        return bool(again.value)
+
     def run(self, max_supersteps: int = 1 << 30, stats: bool = True) -> Stats | None:
         """agx_run.  stats=False skips the counter read-back (read them with stats())."""
         if not stats:

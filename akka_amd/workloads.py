@@ -354,6 +354,34 @@ def mixed(n: int = 4096, seed: int = 1, throughput: int = 3, capacity: int = 0, 
                     graph=(row, col), tells=(dst, src, pay))
 
 
+def one_per_actor(n: int = 4096, seed: int = 1, throughput: int = 3, capacity: int = 0, compiled_kinds: bool = False,
+                  n_host: int = 16) -> Workload:
+    """mixed()'s behaviour kinds (or the compiled library with `compiled_kinds`) with exactly one
+    staged tell per actor (a permutation of the population): buckets whose inbox holds at most one
+    message per actor (the dense path, agx_kernels.h dense_finish) beside buckets where forwards
+    collide; stops, dead letters to stopped actors, unknown refs and replies to host-side actors
+    (PINGPONG -> outbox) included."""
+    rng = np.random.default_rng(seed)
+    w = compiled(n, seed=seed, throughput=throughput, capacity=capacity, builtin=True) if compiled_kinds else \
+        mixed(n, seed=seed, throughput=throughput, capacity=capacity)
+    dst = rng.permutation(n).astype(np.uint32)
+    src = rng.integers(0, n, n).astype(np.uint32)
+    src[rng.random(n) < 0.1] = NO_SENDER
+    if n_host:
+        hs = rng.random(n) < 0.05
+        src[hs] = rng.integers(n, n + n_host, int(hs.sum())).astype(np.uint32)
+        w.outbound = (n, n_host)
+    pay = rng.integers(0, 12, n).astype(np.uint32)
+    if not compiled_kinds:  # fan-out payloads carry ttl in the top 8 bits
+        fan_first, fan_count = w.ranges[2][0], w.ranges[2][1]
+        is_fan = (dst >= fan_first) & (dst < fan_first + fan_count)
+        pay[is_fan] = (rng.integers(0, 3, int(is_fan.sum())).astype(np.uint32) << 24) | rng.integers(
+            0, 1 << 24, int(is_fan.sum())).astype(np.uint32)
+    w.name = "one_per_actor"
+    w.tells = (dst, src, pay)
+    return w
+
+
 def compiled(n: int = 4096, seed: int = 1, throughput: int = 3, capacity: int = 0, tells_per_actor: int = 3,
              builtin: bool = False) -> Workload:
     """Typed behaviours lowered by akka_amd.typed (compiled behaviour tables): the DSL versions of

@@ -37,7 +37,8 @@
  *   agx_destroy         <- MessageDispatcher.shutdown (AbstractDispatcher.scala:325)
  *
  * Threading: an engine handle is driven by one host thread at a time (the
- * single-writer-per-actor rule at engine granularity, Mailbox.scala:185-203).
+ * single-writer-per-actor rule at engine granularity, Mailbox.scala:185-203) -- except agx_tell,
+ * which any thread may call at any time (the lock-free tell path, below).
  */
 #ifndef AKKA_GPU_H
 #define AKKA_GPU_H
@@ -295,6 +296,19 @@ agx_status agx_set_graph_rmat(agx_engine* eng, const uint64_t* row_ptr, uint32_t
  * Tells whose dst is not owned by this rank are ignored on this rank.        */
 agx_status agx_stage_tells(agx_engine* eng, const uint32_t* dst, const uint32_t* src,
                            const uint32_t* payload, size_t n);
+/* The lock-free tell path (ActorRef.! from any thread; the reference: one getAndSet enqueue,
+ * akka-actor/src/main/java/akka/dispatch/AbstractNodeQueue.java:79-82, and a CAS-guarded schedule,
+ * akka-actor/src/main/scala/akka/dispatch/Mailbox.scala:185-194 + Dispatcher.scala:120-128).
+ * agx_tell may be called from any number of threads at once, also while one thread is inside
+ * agx_run: each calling thread appends to a queue of its own (wait-free, each sender's tells in
+ * order; the next agx_run takes them as agx_stage_tells would).  *schedule = 1 iff this tell moved
+ * the engine from idle to scheduled: the caller then submits ONE pump task (a task that calls
+ * agx_run and then agx_pump_idle); N tells to an idle engine submit one.  agx_pump_idle is the
+ * pump's last call (Mailbox.run's finally: setAsIdle, then registerForExecution): *reschedule = 1
+ * iff tells arrived after the pump's last agx_run -- submit the pump again.  (src may be
+ * AGX_NO_SENDER; schedule / reschedule may be NULL.)                          */
+agx_status agx_tell(agx_engine* eng, uint32_t dst, uint32_t src, uint32_t payload, int32_t* schedule);
+agx_status agx_pump_idle(agx_engine* eng, int32_t* reschedule);
 /* Run up to max_supersteps supersteps or until quiescent; stats are cumulative
  * over the engine's lifetime.  out may be NULL: the counters are then not read
  * back (agx_get_stats does it later, and reports AGX_ECAPACITY if an overflow

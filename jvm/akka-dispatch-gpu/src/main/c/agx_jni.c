@@ -197,13 +197,33 @@ JNIEXPORT void JNICALL Java_akka_dispatch_gpu_AgxJni_setGraph(JNIEnv* env, jclas
   jsize nr = 0, nc = 0;
   uint64_t* r = copy_longs(env, row_ptr, &nr);
   uint32_t* c = copy_ints(env, col, &nc);
-  /* agx_set_graph reads row_ptr[0 .. n_actors] and col[0 .. row_ptr[n_actors]): both lengths exact */
-  if (!r || (uint64_t)nr != n_actors + 1 || (uint64_t)nc < r[n_actors] || (r[n_actors] && !c))
+  /* agx_set_graph reads row_ptr[0 .. n_actors] and col[0 .. row_ptr[n_actors]) once row_ptr is
+   * monotone (it checks that before reading col; checked here too, so an over-long row cannot
+   * reach the native copy of col) */
+  int mono = r != NULL && (uint64_t)nr == n_actors + 1;
+  for (uint64_t i = 0; mono && i < n_actors; ++i) mono = r[i] <= r[i + 1];
+  if (!mono || (uint64_t)nc < r[n_actors] || (r[n_actors] && !c))
     raise(env, AGX_EINVAL);
   else
     raise(env, agx_set_graph(ENG(eng), r, c ? c : (const uint32_t*)r));
   free(r);
   free(c);
+}
+
+/* agx_tell: no array, no lock -- one call per ActorRef.! (GpuEngine.tell) */
+JNIEXPORT jboolean JNICALL Java_akka_dispatch_gpu_AgxJni_tell(JNIEnv* env, jclass k, jlong eng, jint dst, jint src,
+                                                             jint pay) {
+  (void)k;
+  int32_t sched = 0;
+  raise(env, agx_tell(ENG(eng), (uint32_t)dst, (uint32_t)src, (uint32_t)pay, &sched));
+  return sched ? JNI_TRUE : JNI_FALSE;
+}
+
+JNIEXPORT jboolean JNICALL Java_akka_dispatch_gpu_AgxJni_pumpIdle(JNIEnv* env, jclass k, jlong eng) {
+  (void)k;
+  int32_t again = 0;
+  raise(env, agx_pump_idle(ENG(eng), &again));
+  return again ? JNI_TRUE : JNI_FALSE;
 }
 
 JNIEXPORT void JNICALL Java_akka_dispatch_gpu_AgxJni_stageTells(JNIEnv* env, jclass k, jlong eng, jobject dst,

@@ -63,6 +63,12 @@ public final class AgxJni {
 
   /** agx_run; stats (8 longs: delivered, dead letters, unhandled, emitted, staged, supersteps, in flight,
    *  algorithmic bytes) or null (no read-back; the error word is still checked). */
+  /** agx_tell: lock-free, any thread; true iff the caller must submit the pump (idle -> scheduled). */
+  public static native boolean tell(long engine, int dst, int src, int payload);
+
+  /** agx_pump_idle: the pump's last call; true iff tells arrived meanwhile (submit the pump again). */
+  public static native boolean pumpIdle(long engine);
+
   public static native void run(long engine, int maxSupersteps, long[] stats);
 
   public static native void getStats(long engine, long[] stats);

@@ -57,6 +57,8 @@ object AgxNative {
     h("agx_take_outbound", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG, ADDRESS))
   val stageTells: MethodHandle =
     h("agx_stage_tells", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG))
+  val tell: MethodHandle = h("agx_tell", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT, JAVA_INT, ADDRESS))
+  val pumpIdle: MethodHandle = h("agx_pump_idle", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS))
   val run: MethodHandle = h("agx_run", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, ADDRESS))
   val getStats: MethodHandle = h("agx_get_stats", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS))
   val readState: MethodHandle =
@@ -152,6 +154,18 @@ object PanamaBackend extends AgxBackend {
     try check(AgxNative.stageTells.invokeExact(seg(engine), ints(a, dst, n), ints(a, src, n), ints(a, payload, n),
       n.toLong).asInstanceOf[Int])
     finally a.close()
+  }
+  // (one 4-byte out-parameter per call: a thread's own reusable slot, no Arena per tell)
+  private val flag = ThreadLocal.withInitial[MemorySegment](() => Arena.global().allocate(JAVA_INT))
+  def tell(engine: Long, dst: Int, src: Int, payload: Int): Boolean = {
+    val f = flag.get()
+    check(AgxNative.tell.invokeExact(seg(engine), dst, src, payload, f).asInstanceOf[Int])
+    f.get(JAVA_INT, 0) != 0
+  }
+  def pumpIdle(engine: Long): Boolean = {
+    val f = flag.get()
+    check(AgxNative.pumpIdle.invokeExact(seg(engine), f).asInstanceOf[Int])
+    f.get(JAVA_INT, 0) != 0
   }
   def run(engine: Long, maxSupersteps: Int, stats: Array[Long]): Unit = {
     val a = Arena.ofConfined()

@@ -23,6 +23,10 @@ trait AgxBackend {
   def setOutbound(engine: Long, firstHostId: Int, nHost: Int, capacity: Long): Unit
   def takeOutbound(engine: Long, dst: Array[Int], src: Array[Int], payload: Array[Int], cap: Int): Int
   def stageTells(engine: Long, dst: Array[Int], src: Array[Int], payload: Array[Int], n: Int): Unit
+  /** agx_tell (lock-free, any thread): true iff the caller must submit the pump */
+  def tell(engine: Long, dst: Int, src: Int, payload: Int): Boolean
+  /** agx_pump_idle (the pump's last call): true iff tells arrived meanwhile */
+  def pumpIdle(engine: Long): Boolean
   /** stats: 8 longs (delivered, dead letters, unhandled, emitted, staged, supersteps, in flight,
    *  algorithmic bytes), or null for no read-back */
   def run(engine: Long, maxSupersteps: Int, stats: Array[Long]): Unit
@@ -69,6 +73,8 @@ object JniBackend extends AgxBackend {
     AgxJni.takeOutbound(engine, dst, src, payload, cap)
   def stageTells(engine: Long, dst: Array[Int], src: Array[Int], payload: Array[Int], n: Int): Unit =
     AgxJni.stageTellsArrays(engine, dst, src, payload, n)
+  def tell(engine: Long, dst: Int, src: Int, payload: Int): Boolean = AgxJni.tell(engine, dst, src, payload)
+  def pumpIdle(engine: Long): Boolean = AgxJni.pumpIdle(engine)
   def run(engine: Long, maxSupersteps: Int, stats: Array[Long]): Unit = AgxJni.run(engine, maxSupersteps, stats)
   def getStats(engine: Long, stats: Array[Long]): Unit = AgxJni.getStats(engine, stats)
   def readState(engine: Long, first: Long, count: Long, words: Array[Long], alive: Array[Byte]): Unit =

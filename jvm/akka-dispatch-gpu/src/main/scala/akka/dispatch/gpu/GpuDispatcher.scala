@@ -70,14 +70,22 @@ class GpuDispatcher(
   private val maxSupersteps: Int =
     if (config.hasPath("gpu.supersteps-per-pump")) config.getInt("gpu.supersteps-per-pump") else Int.MaxValue
 
+  // One pump task at a time: agx_tell answers "submit" only on idle -> scheduled, and the pump's
+  // last call (agx_pump_idle) answers "submit again" only for tells that arrived while it ran --
+  // Mailbox.run's finally { setAsIdle(); registerForExecution } (Mailbox.scala:227-240).
   private val pumpTask: Runnable = new Runnable {
     def run(): Unit = {
-      try engine.pump(maxSupersteps)
-      catch { case e: Throwable => eventStream.publish(Error(e, getClass.getName, getClass, "GPU pump failed")) }
-      // tells staged while the pump was running (or by a losing concurrent pump) get another run
-      if (engine.hasStaged) schedulePump()
+      val again =
+        try engine.pump(maxSupersteps)
+        catch {
+          case e: Throwable =>
+            eventStream.publish(Error(e, getClass.getName, getClass, "GPU pump failed"))
+            engine.pumpIdleAfterFailure()
+        }
+      if (again) schedulePump()
     }
   }
+  engine.setPumpSubmitter(() => schedulePump())
 
   private def schedulePump(): Unit =
     try executorService.execute(pumpTask)
@@ -95,8 +103,7 @@ class GpuDispatcher(
   override protected[akka] def dispatch(receiver: ActorCell, invocation: Envelope): Unit =
     receiver.mailbox.messageQueue match {
       case q: GpuQueue =>
-        q.enqueue(receiver.self, invocation) // -> engine staging (dead letter if not fixed-layout)
-        schedulePump()
+        q.enqueue(receiver.self, invocation) // -> agx_tell; submits the pump on idle -> scheduled
       case _ =>
         super.dispatch(receiver, invocation) // a JVM actor on this dispatcher
     }
@@ -120,8 +127,7 @@ class GpuDispatcher(
 
   def tellRange(first: Int, count: Int, payload: Int): Unit = {
     var i = 0
-    while (i < count) { engine.stage(first + i, Agx.NoSender, payload); i += 1 }
-    schedulePump()
+    while (i < count) { engine.tell(first + i, Agx.NoSender, payload); i += 1 } // (one submission per burst)
   }
 
   override protected[akka] def shutdown(): Unit = {

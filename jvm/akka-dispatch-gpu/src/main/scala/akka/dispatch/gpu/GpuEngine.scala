@@ -1,7 +1,7 @@
 /*
  * One engine (one agx_engine handle = one GPU rank) per GpuDispatcher instance: actor ids, the
- * MPSC staging buffer that ActorRef.! appends to, the pump that runs supersteps, and the reply
- * path back to JVM actors.  All native calls go through an AgxBackend (JNI on JDK 8/11, Panama on
+ * lock-free tell path that ActorRef.! appends to (agx_tell), the pump that runs supersteps, and the
+ * reply path back to JVM actors.  All native calls go through an AgxBackend (JNI on JDK 8/11, Panama on
  * JDK 22+, AgxBackend.scala).
  *
  * Ids: GPU actors are [0, gpu.actors); a JVM actor that tells a GPU actor gets a host id in
@@ -12,7 +12,7 @@
 package akka.dispatch.gpu
 
 import java.util.concurrent.ConcurrentHashMap
-import java.util.concurrent.atomic.{ AtomicBoolean, AtomicInteger }
+import java.util.concurrent.atomic.AtomicInteger
 
 import com.typesafe.config.Config
 
@@ -71,7 +71,6 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
   private val nextHost = new AtomicInteger(0)
   private val hostIds = new ConcurrentHashMap[ActorRef, Integer]()
   private val hostRefs = new ConcurrentHashMap[Integer, ActorRef]()
-  private[gpu] val queues = new ConcurrentHashMap[Integer, GpuQueue]() // numberOfMessages bookkeeping
 
   /** actorOf: one fixed-layout actor (GpuMailboxType.create) with its mailbox class */
   def register(ref: ActorRef, kind: Int, init: Array[Long], mailboxCapacity: Int): Int = {
@@ -125,58 +124,39 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
     }
   }
 
-  // ---------------------------------------------------------------- staging (MPSC)
-  // Senders append under a lock (dispatch is called concurrently from any thread, AbstractDispatcher
-  // contract); the pump swaps the buffer out and hands it to agx_stage_tells in one call.
-  private var dst = new Array[Int](1024)
-  private var src = new Array[Int](1024)
-  private var pay = new Array[Int](1024)
-  private var n = 0
+  // ---------------------------------------------------------------- the tell path (lock-free)
+  // ActorRef.! from any thread appends through agx_tell to a native queue of the calling thread's
+  // own (include/akka_gpu.h "lock-free tell path"; AbstractNodeQueue.java:79-82 enqueues with one
+  // getAndSet): no monitor per tell.  agx_tell answers true exactly when the engine went from idle to
+  // scheduled -- the caller then submits ONE pump task (Mailbox.setAsScheduled, Mailbox.scala:185-194).
 
-  def stage(dstId: Int, srcId: Int, payload: Int): Unit = synchronized {
-    if (n == dst.length) {
-      dst = java.util.Arrays.copyOf(dst, 2 * n)
-      src = java.util.Arrays.copyOf(src, 2 * n)
-      pay = java.util.Arrays.copyOf(pay, 2 * n)
-    }
-    dst(n) = dstId
-    src(n) = srcId
-    pay(n) = payload
-    n += 1
-  }
+  // the dispatcher's pump submission (GpuDispatcher sets it once it has an executor)
+  @volatile private var submitPump: () => Unit = () => ()
+  private[gpu] def setPumpSubmitter(f: () => Unit): Unit = submitPump = f
 
-  private val pumping = new AtomicBoolean(false)
+  /** ActorRef.! : the tell enters the engine; the pump is submitted only on idle -> scheduled */
+  def tell(dstId: Int, srcId: Int, payload: Int): Unit =
+    if (native.tell(handle, dstId, srcId, payload)) submitPump()
+
   private val outD = new Array[Int](4096)
   private val outS = new Array[Int](4096)
   private val outP = new Array[Int](4096)
 
-  /** Run supersteps until the engine is quiescent, delivering outbound replies to JVM actors after
-   *  each run.  One host thread drives the handle at a time (include/akka_gpu.h threading rule);
-   *  returns false if another pump is running. */
+  /** One pump task: take every tell published so far, run supersteps until the engine is
+   *  quiescent, deliver the outbound replies to JVM actors, then the idle protocol (Mailbox.run's
+   *  finally: setAsIdle + registerForExecution) -- returns true iff tells arrived meanwhile and
+   *  the caller must submit the pump again.  At most one pump is scheduled at a time (the CAS in
+   *  agx_tell / agx_pump_idle), so one host thread drives the handle (include/akka_gpu.h rule). */
   def pump(maxSupersteps: Int): Boolean = {
-    if (!pumping.compareAndSet(false, true)) return false
-    try {
-      var more = true
-      while (more) {
-        val (d, s, p, k) = synchronized {
-          val r = (dst, src, pay, n)
-          dst = new Array[Int](math.max(1024, n)); src = new Array[Int](dst.length); pay = new Array[Int](dst.length)
-          n = 0
-          r
-        }
-        if (k > 0) {
-          native.stageTells(handle, d, s, p, k)
-          var i = 0
-          while (i < k) { val q = queues.get(d(i)); if (q != null) q.handedOver(); i += 1 }
-        }
-        native.run(handle, maxSupersteps, null)
-        deliverOutbound()
-        more = synchronized(n > 0)
-      }
-      true
-    } finally pumping.set(false)
+    native.run(handle, maxSupersteps, null)
+    deliverOutbound()
+    native.pumpIdle(handle)
   }
 
+  /** a failed pump still ends with the idle protocol (else the engine would stay "scheduled") */
+  private[gpu] def pumpIdleAfterFailure(): Boolean =
+    try native.pumpIdle(handle)
+    catch { case _: Throwable => false }
   /** outbox -> JVM actors: `jvmRef ! GpuTell(payload)` with the replying GPU actor as sender
    *  (each GPU sender's replies in emission order, the only order Akka guarantees) */
   private def deliverOutbound(): Unit = {
@@ -191,8 +171,6 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
       k = native.takeOutbound(handle, outD, outS, outP, outD.length)
     }
   }
-
-  def hasStaged: Boolean = synchronized(n > 0)
 
   /** delivered, dead letters, unhandled, emitted, staged, supersteps, in flight, bytes */
   def stats(): Array[Long] = {

@@ -65,7 +65,6 @@ abstract class GpuMailboxTypeBase(settings: ActorSystem.Settings, config: Config
     val q: GpuQueue =
       if (capacity > 0) new GpuBoundedMessageQueue(id, engine, system, capacity)
       else new GpuMessageQueue(id, engine, system)
-    if (id != Agx.NoSender) engine.queues.put(id, q)
     q
   }
 }
@@ -84,13 +83,13 @@ class GpuBoundedMailboxType(settings: ActorSystem.Settings, config: Config)
     throw new IllegalArgumentException("The capacity for GpuBoundedMailboxType must be positive (mailbox-capacity)")
 }
 
-/** The device-side mailbox of one actor.  enqueue stages the tell for the engine; nothing is
- *  ever dequeued on the JVM (MessageQueue contract, Mailbox.scala:359-390).  numberOfMessages
- *  counts this actor's tells staged on the JVM and not yet handed to the engine; the messages on
- *  the device are in the engine's in-flight count (GpuEngine.stats()(6)). */
+/** The device-side mailbox of one actor.  enqueue hands the tell to the engine through the
+ *  lock-free tell path (GpuEngine.tell -> agx_tell: the calling thread's own queue, no lock;
+ *  AbstractNodeQueue.java:79-82) and submits the dispatcher's pump only when the engine went from
+ *  idle to scheduled (Mailbox.setAsScheduled, Mailbox.scala:185-194).  Nothing is ever dequeued on
+ *  the JVM (MessageQueue contract, Mailbox.scala:359-390): the messages live in the engine, in its
+ *  in-flight count (GpuEngine.stats()(6)), so numberOfMessages is 0 on the JVM side. */
 sealed abstract class GpuQueue(val id: Int, engine: GpuEngine, system: Option[ActorSystem]) extends MessageQueue {
-
-  private val staged = new AtomicInteger(0)
 
   def enqueue(receiver: ActorRef, handle: Envelope): Unit = {
     val payload = handle.message match {
@@ -101,16 +100,12 @@ sealed abstract class GpuQueue(val id: Int, engine: GpuEngine, system: Option[Ac
         system.foreach(_.deadLetters ! DeadLetter(other, handle.sender, receiver))
         return
     }
-    engine.stage(id, engine.idOf(handle.sender), payload)
-    staged.incrementAndGet()
+    engine.tell(id, engine.idOf(handle.sender), payload)
   }
 
-  /** the pump took this actor's staged tells (GpuDispatcher.pumpTask) */
-  private[gpu] def handedOver(): Unit = staged.set(0)
-
   def dequeue(): Envelope = null
-  def numberOfMessages: Int = staged.get
-  def hasMessages: Boolean = staged.get > 0
+  def numberOfMessages: Int = 0
+  def hasMessages: Boolean = false
   def cleanUp(owner: ActorRef, deadLetters: MessageQueue): Unit = () // the engine dead-letters them
 }
 

@@ -16,9 +16,15 @@
  *     actor beside unbounded ones drops exactly the messages beyond 10 (MailboxConfigSpec:47-66);
  *   - sender() ! reply to a JVM actor (ActorCell.scala:583-587): a GPU PingPong actor answering a
  *     JVM probe -- the replies leave the engine through the outbox in per-sender order and the
- *     probe answers them, until the GPU actor stops (BenchmarkActors.PingPong).
+ *     probe answers them, until the GPU actor stops (BenchmarkActors.PingPong);
+ *   - the lock-free tell path (AgxJni.tell / pumpIdle -> agx_tell / agx_pump_idle): a burst of
+ *     tells to an idle engine submits ONE pump (Mailbox.setAsScheduled, Mailbox.scala:185-194), and
+ *     tells from 4 threads racing a pump that resubmits itself only when pumpIdle says so are all
+ *     delivered (ActorModelSpec "handle queueing from multiple threads", :323-336).
  * Exit 0 = every check passed.  Run by tests/test_abi_c.py on the GPU box.
  */
+#include <pthread.h>
+#include <stdatomic.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -41,6 +47,8 @@ void Java_akka_dispatch_gpu_AgxJni_setRing(JNIEnv*, jclass, jlong, jint);
 void Java_akka_dispatch_gpu_AgxJni_stageTells(JNIEnv*, jclass, jlong, jobject, jobject, jobject, jint);
 void Java_akka_dispatch_gpu_AgxJni_stageTellsArrays(JNIEnv*, jclass, jlong, jintArray, jintArray, jintArray, jint);
 void Java_akka_dispatch_gpu_AgxJni_run(JNIEnv*, jclass, jlong, jint, jlongArray);
+jboolean Java_akka_dispatch_gpu_AgxJni_tell(JNIEnv*, jclass, jlong, jint, jint, jint);
+jboolean Java_akka_dispatch_gpu_AgxJni_pumpIdle(JNIEnv*, jclass, jlong);
 void Java_akka_dispatch_gpu_AgxJni_getStats(JNIEnv*, jclass, jlong, jlongArray);
 void Java_akka_dispatch_gpu_AgxJni_readState(JNIEnv*, jclass, jlong, jlong, jlong, jlongArray, jbyteArray);
 void Java_akka_dispatch_gpu_AgxJni_setGraph(JNIEnv*, jclass, jlong, jlongArray, jintArray);
@@ -179,6 +187,20 @@ static jobject direct_ints(jsize n) { return new_obj(T_DIRECT, 1, n * 4); }
 #define L(a) ((jlong*)(a)->data)
 #define B(a) ((jbyte*)(a)->data)
 
+/* a sender thread of the lock-free tell path: TELLS tells to COUNTER actor 3100 + t, payloads 1..TELLS;
+   a tell that answers "submit" counts one pump submission */
+enum { TELLS = 2500 }; /* (4 x 2500 in flight at most: within the engine's msg_capacity, 4 x N) */
+typedef struct { jlong eng; int t; } tell_arg;
+static atomic_long t_submitted;
+static atomic_int ta_done[4];
+static void* teller(void* p) {
+  const tell_arg* a = (const tell_arg*)p;
+  for (jint i = 1; i <= TELLS; ++i)
+    if (Java_akka_dispatch_gpu_AgxJni_tell(env, NULL, a->eng, 3100 + a->t, AGX_NO_SENDER, i)) atomic_fetch_add(&t_submitted, 1);
+  atomic_store(&ta_done[a->t], 1);
+  return NULL;
+}
+
 int main(void) {
   table.FindClass = f_FindClass;
   table.ThrowNew = f_ThrowNew;
@@ -259,6 +281,10 @@ int main(void) {
   jlongArray rp = longs(N + 1);
   for (jint i = 0; i <= N; ++i) L(rp)[i] = i < 8 ? i : 8; /* actors 0..7 have one edge each */
   RAISES("akka/ConfigurationException", Java_akka_dispatch_gpu_AgxJni_setGraph(env, K, eng, rp, col1));
+  /* a non-monotone rowPtr whose last entry fits col ([0, 100, 1, 1, ...]): rejected before the
+   * native copy of col is read */
+  for (jint i = 0; i <= N; ++i) L(rp)[i] = i == 1 ? 100 : i == 0 ? 0 : 1;
+  RAISES("akka/ConfigurationException", Java_akka_dispatch_gpu_AgxJni_setGraph(env, K, eng, rp, col1));
   free_obj(wshort);
   free_obj(wlong);
   free_obj(rp_short);
@@ -332,6 +358,47 @@ int main(void) {
   CHECK(n == 4, "the 4 kept replies (%d)", n);
   NOEXC(Java_akka_dispatch_gpu_AgxJni_stageTellsArrays(env, K, eng, td, ts, tp, 1));
   NOEXC(Java_akka_dispatch_gpu_AgxJni_run(env, K, eng, 1 << 30, st));
+
+  /* the lock-free tell path: one pump submission per burst */
+  int subs = 0;
+  for (jint i = 1; i <= 1000; ++i) subs += Java_akka_dispatch_gpu_AgxJni_tell(env, K, eng, 3000, AGX_NO_SENDER, i) ? 1 : 0;
+  CHECK(subs == 1, "a burst of 1000 tells to an idle engine submitted %d pumps (want 1)", subs);
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_run(env, K, eng, 1 << 30, st));
+  CHECK(!Java_akka_dispatch_gpu_AgxJni_pumpIdle(env, K, eng), "pumpIdle with nothing pending asked for another run");
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 3000, 1, w, al));
+  CHECK(L(w)[0] == 1000 && L(w)[1] == 500500, "burst delivered: count %lld sum %lld", (long long)L(w)[0],
+        (long long)L(w)[1]);
+  /* 4 sender threads race the pump (this thread): it runs only when a submission is outstanding */
+  tell_arg ta[4];
+  pthread_t th[4];
+  atomic_store(&t_submitted, 0);
+  for (int t = 0; t < 4; ++t) {
+    ta[t].eng = eng;
+    ta[t].t = t;
+    pthread_create(&th[t], NULL, teller, &ta[t]);
+  }
+  long ran = 0;
+  int done = 0;
+  for (long spin = 0; spin < 200000000L; ++spin) {
+    if (atomic_load(&t_submitted) == ran) {
+      if (done) break;
+      int all = 1;
+      for (int t = 0; t < 4; ++t) all &= atomic_load(&ta_done[t]);
+      done = all;  /* one more look after every sender finished: a late submission is still run */
+      continue;
+    }
+    ++ran;
+    NOEXC(Java_akka_dispatch_gpu_AgxJni_run(env, K, eng, 1 << 30, NULL));
+    if (Java_akka_dispatch_gpu_AgxJni_pumpIdle(env, K, eng)) atomic_fetch_add(&t_submitted, 1);
+  }
+  for (int t = 0; t < 4; ++t) pthread_join(th[t], NULL);
+  for (int t = 0; t < 4; ++t) {
+    NOEXC(Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 3100 + t, 1, w, al));
+    CHECK(L(w)[0] == TELLS && L(w)[1] == (long long)TELLS * (TELLS + 1) / 2,
+          "thread %d: %lld of %d tells delivered (sum %lld)", t, (long long)L(w)[0], TELLS, (long long)L(w)[1]);
+  }
+  CHECK(ran >= 1 && ran <= 4 * TELLS, "pump runs %ld", ran);
+  printf("lock-free tell path: %d threads x %d tells, %ld pump runs\n", 4, TELLS, ran);
 
   NOEXC(Java_akka_dispatch_gpu_AgxJni_destroy(env, K, eng));
   free_obj(d);

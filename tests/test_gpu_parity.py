@@ -575,7 +575,7 @@ def test_ring_apply(built, monkeypatch, mode, ba, case):
 
 
 @pytest.mark.parametrize("capacity,rings,n", [(64, False, 60_000), (255, False, 60_000), (256, True, 60_000),
-                                              (1000, True, 60_000), (1000, True, 60_001), (300, True, 4_099)])
+                                              (1000, True, 60_000), (1000, True, 60_001), (300, True, 30_003)])
 def test_ring_apply_default(built, monkeypatch, capacity, rings, n):
     """Without AGX_RING_APPLY the ring apply is on exactly when the largest bounded capacity is
     >= 256 (deep queues: C3's BoundedMailbox(1000)), and either way bit-exact against the oracle

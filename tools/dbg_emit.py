@@ -27,6 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="crdt")
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--budget", type=int, default=1, help="supersteps per agx_run call (graph replays when > 1)")
     args = ap.parse_args()
     w = CASES[args.case]()
     kw = w.engine_kwargs()
@@ -35,8 +36,8 @@ def main():
     ref = BspOracle(**kw)
     w.apply_to(ref)
     for s in range(args.steps):
-        sg = eng.run(1)
-        so = ref.run(1)
+        sg = eng.run(args.budget)
+        so = ref.run(args.budget)
         bad = [k for k in KEYS if getattr(sg, k) != so[k]]
         print(f"step {s}: " + " ".join(f"{k}={getattr(sg, k)}/{so[k]}" for k in KEYS), flush=True)
         if bad:
