@@ -31,6 +31,14 @@ hipError_t agx_launch_tiny_g4(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_tiny_g5(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_tiny_g6(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_tiny_g7(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g0(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g1(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g2(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g3(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g4(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g5(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g6(uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g7(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_ring_g0(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
 hipError_t agx_launch_ring_g1(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
 hipError_t agx_launch_ring_g2(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
@@ -89,6 +97,20 @@ hipError_t tiny_dispatch(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& 
 
 // k_ring_apply (tiny: k_ring_tiny) of the plain / compiled variants of this group
 template <uint32_t V>
+hipError_t dense_dispatch(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  if constexpr (V >= V_N) {
+    return hipErrorInvalidValue;
+  } else {
+    if constexpr (kVariantGroup[V] == AGX_VGROUP && !kVariants[V].wide)
+      if (vid == V) {
+        hipLaunchKernelGGL((k_dense_apply<kVariants[V].km>), g, dim3(kDenseThreads), 0, s, ba);
+        return hipGetLastError();
+      }
+    return dense_dispatch<V + 1>(vid, g, s, ba);
+  }
+}
+
+template <uint32_t V>
 hipError_t ring_dispatch(uint32_t vid, bool tiny, dim3 g, hipStream_t s, const BucketArgs& ba, const RingArgs& ra) {
   if constexpr (V >= V_N) {
     return hipErrorInvalidValue;
@@ -114,6 +136,10 @@ hipError_t AGX_CAT(agx_launch_ring_g, AGX_VGROUP)(uint32_t vid, bool tiny, dim3 
 
 hipError_t AGX_CAT(agx_launch_tiny_g, AGX_VGROUP)(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba) {
   return tiny_dispatch<0>(vid, g, s, ba);
+}
+
+hipError_t AGX_CAT(agx_launch_dense_g, AGX_VGROUP)(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  return dense_dispatch<0>(vid, g, s, ba);
 }
 
 hipError_t AGX_GROUP_FN(uint32_t vid, uint32_t mode, bool skew, dim3 g, hipStream_t s, const BucketArgs& ba) {
@@ -145,6 +171,20 @@ hipError_t agx_launch_ring(uint32_t vid, bool tiny, dim3 g, hipStream_t s, const
     case 5: return agx_launch_ring_g5(vid, tiny, g, s, ba, ra);
     case 6: return agx_launch_ring_g6(vid, tiny, g, s, ba, ra);
     default: return agx_launch_ring_g7(vid, tiny, g, s, ba, ra);
+  }
+}
+
+hipError_t agx_launch_dense(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba) {
+  if (vid >= V_N || kVariants[vid].wide) return hipErrorInvalidValue;
+  switch (kVariantGroup[vid]) {
+    case 0: return agx_launch_dense_g0(vid, g, s, ba);
+    case 1: return agx_launch_dense_g1(vid, g, s, ba);
+    case 2: return agx_launch_dense_g2(vid, g, s, ba);
+    case 3: return agx_launch_dense_g3(vid, g, s, ba);
+    case 4: return agx_launch_dense_g4(vid, g, s, ba);
+    case 5: return agx_launch_dense_g5(vid, g, s, ba);
+    case 6: return agx_launch_dense_g6(vid, g, s, ba);
+    default: return agx_launch_dense_g7(vid, g, s, ba);
   }
 }
 

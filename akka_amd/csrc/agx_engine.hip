@@ -88,11 +88,11 @@ struct DevMsgs {
 };
 
 enum KClass { K_CROWSCAN, K_CDOWN, K_UPSWEEP, K_ROWSCAN, K_DOWNSWEEP, K_APPLY, K_EXCHANGE, K_MCOMPACT, K_SKEW, K_TICK,
-              K_BOUNDS, K_SKEWPRE, K_TINY, K_RINGAPPLY, K_NCLASS };
+              K_BOUNDS, K_SKEWPRE, K_TINY, K_RINGAPPLY, K_DENSE, K_NCLASS };
 const char* kClassNames[K_NCLASS] = {"chunk_rowscan", "chunk_downsweep", "sort_upsweep", "sort_rowscan",
                                      "sort_downsweep", "bucket_apply", "exchange", "mcompact", "bucket_apply_skew",
                                      "fused_tick", "bucket_bounds", "skew_prepass", "bucket_apply_tiny",
-                                     "ring_apply"};
+                                     "ring_apply", "bucket_apply_dense"};
 
 constexpr uint32_t kGraphSizes[5] = {1, 2, 4, 8, 16};  // superstep replays (agx_engine::gx)
 constexpr uint32_t kRowAlign = 32;  // CRDT row pitch (u32) of rows wider than one 128-B line
@@ -215,6 +215,7 @@ struct agx_engine {
   // path, the block launch takes every bucket)
   uint32_t* d_blist = nullptr;
   bool tiny_launch = true;
+  int dense_launch = -1;  // k_dense_apply before the block launch: 1 on, 0 off, -1 (default) ring populations
   // ring apply (agx_ring.h): bounded mailboxes whose queued messages stay in per-actor rings; decided
   // at the first run (setup_ring_apply), then k_ring_tiny + k_ring_apply per superstep replace the tiny /
   // block / skew launches.  On by default for deep bounded mailboxes (capacity >= kRingAutoC);
@@ -729,9 +730,19 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     }
     const uint32_t mode = e->fused ? M_FUSED : e->R > 1 ? M_OWNER : M_BYPASS;
     const dim3 g(grid_for(e->nb, e->apply_grid));
+    // dense buckets (one message per actor) first, in their own lean launch (k_dense_apply); by
+    // default for ring populations, whose buckets all are (AGX_DENSE_LAUNCH=1 / 0 forces it)
+    const bool dl = mode == M_BYPASS && !kVariants[vid].wide && e->kmax == 1 && !e->ring_live && !e->skew_only &&
+                    (e->dense_launch == 1 || (e->dense_launch < 0 && vid == V_RING));
+    if (dl) {
+      ba.blist = e->d_blist;
+      Scope s(e, K_DENSE);
+      HIP_TRY(agx_launch_dense(vid, dim3(grid_for(e->nb, kMaxApplyGrid)), e->stream, ba));
+    }
     const bool tl = mode == M_BYPASS && !kVariants[vid].wide && e->tiny_launch && e->tiny_max && !e->skew_only;
     if (tl) {  // wave-per-bucket launch first; the block launch then takes the buckets it marked
       ba.blist = e->d_blist;
+      ba.dense_first = dl ? 1u : 0u;
       Scope s(e, K_TINY);
       const uint32_t gt = grid_for((e->nb + kTinyWaves - 1) / kTinyWaves, kMaxApplyGrid);
       HIP_TRY(agx_launch_tiny(vid, dim3(gt), e->stream, ba));
@@ -1800,6 +1811,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   e->bb = cfg->bucket_actors ? ceil_log2(cfg->bucket_actors) : (uint32_t)kBucketBits;
   if (const char* s = getenv("AGX_TINY")) e->tiny_max = std::min<uint32_t>(kTinyMax, (uint32_t)std::max(0, atoi(s)));
   if (const char* s = getenv("AGX_TINY_LAUNCH")) e->tiny_launch = atoi(s) != 0;
+  if (const char* s = getenv("AGX_DENSE_LAUNCH")) e->dense_launch = atoi(s) != 0 ? 1 : 0;
   if (const char* s = getenv("AGX_BUCKET_ACTORS")) {  // diagnostic: override the bucket width (power of two)
     const uint32_t ba = (uint32_t)atoi(s);
     if (ba >= (1u << kMinBucketBits) && ba <= (uint32_t)kBucket && !(ba & (ba - 1))) e->bb = ceil_log2(ba);

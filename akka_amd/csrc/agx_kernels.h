@@ -1057,6 +1057,7 @@ struct BucketArgs {
   // bypass, plain behaviours: [nb] marks of the buckets k_tiny_apply left to the block launch
   // (non-null: the block launch skips the unmarked ones)
   uint32_t* blist;
+  uint32_t dense_first;    // bypass: k_dense_apply ran first -- k_tiny_apply takes only the buckets it marked
   // bypass, plain behaviours: skewed buckets pre-partitioned by k_skew_* (see there); [i] = skew index
   const uint32_t* sk_rec;  // [i][kSkRec] bucket, bounds, parts, drained and queued totals
   const uint32_t* sk_act;  // [i][3][kBucket] per actor: admitted, drained-segment start, backlog start
@@ -2614,6 +2615,7 @@ static __global__ void __launch_bounds__(kTinyThreads) k_tiny_apply(BucketArgs a
   const InView iv = in_view(a);
   const uint32_t nw = gridDim.x * kTinyWaves;
   for (uint32_t bw = blockIdx.x * kTinyWaves + w; bw < a.nb; bw += nw) {
+    if (a.dense_first && __builtin_amdgcn_readfirstlane(a.blist[bw]) == 0u) continue;  // (done by k_dense_apply)
     uint32_t bs = 0, lo_w = 0, hi_w = 0, blc = 0, blo = 0;
     if (lane == 0) {  // (k_bucket_apply's bypass bounds)
       bs = a.bstart[bw];
@@ -2634,6 +2636,201 @@ static __global__ void __launch_bounds__(kTinyThreads) k_tiny_apply(BucketArgs a
       tiny_bucket<KM>(a, iv, T[w], bw, lo_w, hi_w - lo_w, blc, blo, bs, rpar, wpar);
     if (lane == 0) a.blist[bw] = tiny ? 0u : 1u;  // (the block launch's work marks)
   }
+}
+
+// ---- Dense-bucket launch (single-rank multi-pass, plain and compiled behaviours, max_emit 1).
+// A bucket whose inbox -- backlog in place, then the sorted new mail -- has strictly increasing keys
+// holds at most one message per actor, so bucket_finish's rule reduces to: every message to a live
+// actor is admitted and drained (len = 1: C = 0 or >= 1, T >= 1), nothing is queued, a message to a
+// stopped actor is a dead letter (AD/Mailbox.scala:261,551-565).  This kernel applies such buckets
+// straight from registers -- item q of the inbox by thread q % kDenseThreads, its tell written at its
+// rank among the bucket's tells (sender order = inbox order = actor order) -- and marks every other
+// bucket for the block launch (a.blist, as k_tiny_apply does).  It keeps no inbox tile in LDS (10 KB
+// in all) and few registers, so several blocks share a CU and their buckets' memory round trips
+// overlap, where the block kernel (80 KB of LDS) runs two.  The token ring -- every actor one token
+// -- is all dense buckets.
+constexpr int kDenseThreads = 512;
+constexpr int kDenseWaves = kDenseThreads / kWave;
+constexpr int kDenseIpt = kBucket / kDenseThreads;  // inbox items per thread (4)
+#ifndef AGX_DENSE_WPE
+#define AGX_DENSE_WPE 6  // minimum waves per SIMD (3 workgroups of 512 per CU; A/B build knob)
+#endif
+template <uint32_t KM>
+static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_apply(BucketArgs a) {
+  __shared__ uint32_t s_ck[kBucket];                   // tell keys in sender order (identity summary)
+  __shared__ uint32_t s_nh[kRadix];                    // next first-pass digit histogram of the bucket's tells
+  __shared__ uint32_t s_last[kDenseIpt * kDenseWaves];  // last key of each (row, wave): the strictness check
+  __shared__ uint32_t s_cnt[kDenseIpt * kDenseWaves];   // tells of each (row, wave): their ranks
+  __shared__ uint32_t scratch[2 * (kDenseWaves + 1)];
+  __shared__ uint32_t s_bad;
+  const DevParams& P = a.P;
+  const uint32_t tid = threadIdx.x, w = tid / kWave, lane = lane_id();
+  const uint64_t ltm = lanemask_lt();
+  const uint32_t amask = (1u << a.bb) - 1u, nhmask = (1u << a.nx_bits) - 1u;
+  const uint32_t wpar = *a.pstep & 1u, rpar = wpar ^ 1u;
+  const InView iv = in_view(a);
+  constexpr bool kKindNeeded = (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0;
+  const uint32_t w1off = P.W > 1 ? P.sw : 0u;
+  uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};
+  for (uint32_t d = tid; d < kRadix; d += kDenseThreads) s_nh[d] = 0;
+  if (tid == 0) s_bad = 0;
+  __syncthreads();
+  for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x) {
+    // ---- bounds (k_bucket_apply's bypass bounds; uniform loads)
+    const uint32_t bs = a.bstart[b], be = a.bstart[b + 1], bp = a.blpre[b] + a.bl_sbase[b / kBlSlice];
+    const uint32_t blc = a.chunk_cnt[b], blo = a.chunk_off[b];
+    const uint32_t lo = bs + bp, cnt = blc + (be - bs);
+    if (cnt > (uint32_t)kBucket || (uint64_t)lo + cnt > a.cap) {  // (over capacity: the block path reports it)
+      if (tid == 0) a.blist[b] = 1u;
+      continue;
+    }
+    const uint32_t a0 = b << a.bb;
+    // ---- items: backlog (in place, g.bl[rpar]) then the sorted new mail; one round trip
+    uint32_t k[kDenseIpt], sv[kDenseIpt], pv[kDenseIpt];
+    {
+      const uint32_t *Bk = sgpr_ptr(a.g.bl[rpar].key), *Bs = sgpr_ptr(a.g.bl[rpar].src), *Bp = sgpr_ptr(a.g.bl[rpar].pay);
+#pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r) {
+        const uint32_t q = r * kDenseThreads + tid;
+        const bool bl = q < blc, ok = q < cnt;
+        const uint32_t i = !ok ? 0u : bl ? blo + q : iv.at(bs + q - blc);
+        k[r] = ldg(bl || !ok ? Bk : iv.m.key, i);
+        sv[r] = ldg(bl || !ok ? Bs : iv.m.src, i);
+        pv[r] = ldg(bl || !ok ? Bp : iv.m.pay, i);
+      }
+    }
+    // ---- strictly increasing keys?  item q - 1 is lane - 1 of the same row and wave, or the last
+    // item of the previous wave / row (through LDS)
+    uint32_t bad = 0;
+    {
+#pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r)
+        if (lane == kWave - 1) s_last[r * kDenseWaves + w] = k[r] & amask;
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r) {
+        const uint32_t q = r * kDenseThreads + tid, cur = k[r] & amask;
+        uint32_t prev = (uint32_t)__shfl_up((int)cur, 1, kWave);
+        if (lane == 0) {
+          const int x = r * kDenseWaves + (int)w - 1;
+          prev = x >= 0 ? s_last[x] : 0u;
+        }
+        if (q > 0 && q < cnt && prev >= cur) bad = 1;
+      }
+    }
+    if (bad) atomicOr(&s_bad, 1u);
+    __syncthreads();
+    const bool dense = s_bad == 0;
+    __syncthreads();  // (every thread read s_bad)
+    if (!dense) {
+      if (tid == 0) {
+        a.blist[b] = 1u;
+        s_bad = 0;
+      }
+      continue;  // (uniform)
+    }
+    // ---- apply: one message per actor (admitted, drained; a stopped actor's message is a dead letter)
+    uint32_t l[kDenseIpt], ab[kDenseIpt], kd[kDenseIpt];
+    uint64_t x0[kDenseIpt], x1[kDenseIpt];
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r) {
+      const uint32_t q = r * kDenseThreads + tid;
+      l[r] = a0 + (q < cnt ? k[r] & amask : 0u);
+    }
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r) {  // (all loads in flight together)
+      ab[r] = P.alive[l[r]];
+      kd[r] = kKindNeeded ? P.kind[l[r]] : 0u;
+      x0[r] = ldg64(P.state, l[r] * P.sa);
+      x1[r] = P.W > 1 ? ldg64(P.state, l[r] * P.sa + w1off) : 0ull;
+    }
+    uint32_t tk[kDenseIpt], tp[kDenseIpt];  // (a tell's sender is the item's actor, l[r])
+    bool tv[kDenseIpt];
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r) {
+      const uint32_t q = r * kDenseThreads + tid;
+      tv[r] = false;
+      tk[r] = tp[r] = 0u;
+      if (q >= cnt) continue;
+      if (!(ab[r] & 1u)) {  // to a stopped actor: a dead letter
+        ++acc[1];
+        continue;
+      }
+      const uint32_t self = l[r];  // (single rank: local id = global id)
+      RegEmitter em{&P, self, 0u, 0u, 0u, 0u};
+      uint64_t wv2[2] = {x0[r], x1[r]};
+      uint32_t kc = kd[r];
+      ++acc[4];
+      ++acc[0];
+      const uint32_t res = apply_msg<KM>(P, kc, self, l[r], wv2, sv[r], pv[r], em);
+      if (res == AGX_RES_UNHANDLED) ++acc[2];
+      if (res == AGX_RES_STOPPED) P.stopq[atomicAdd(P.nstop, 1u)] = l[r];
+      stg64(P.state, l[r] * P.sa, wv2[0]);
+      if (P.W > 1) stg64(P.state, l[r] * P.sa + w1off, wv2[1]);
+      if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
+        if (kc != kd[r]) P.kind[l[r]] = (uint8_t)kc;
+      acc[3] += em.n_all;
+      acc[1] += em.n_all - em.n_valid;
+      tv[r] = em.n_valid != 0u;
+      tk[r] = em.key;
+      tp[r] = em.pay;
+    }
+    // ---- tells: rank in item order (per (row, wave) counts), chunk stores, next-pass histogram
+    uint32_t rk[kDenseIpt];
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r) {
+      const uint64_t m = __ballot(tv[r]);
+      rk[r] = (uint32_t)__popcll(m & ltm);
+      if (lane == 0) s_cnt[r * kDenseWaves + w] = (uint32_t)__popcll(m);
+      if (tv[r]) lds_hist_inc(s_nh, (tk[r] >> a.nx_shift) & nhmask);
+    }
+    __syncthreads();
+    uint32_t emtot = 0;
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r)
+#pragma unroll
+      for (int x = 0; x < kDenseWaves; ++x) {
+        const uint32_t c = s_cnt[r * kDenseWaves + x];
+        if (x == (int)w) rk[r] += emtot;
+        emtot += c;
+      }
+    const uint64_t embase = (uint64_t)lo * a.kmax;
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r)
+      if (tv[r]) {
+        a.em.key[embase + rk[r]] = tk[r];
+        a.em.src[embase + rk[r]] = l[r];
+        a.em.pay[embase + rk[r]] = tp[r];
+        s_ck[rk[r]] = tk[r];
+      }
+    __syncthreads();  // (s_ck, s_nh complete; s_cnt read)
+    if (a.emmeta) {  // identity grouping (k_ident_combine): first / last key and descents, sender order
+      uint32_t nd = 0, dp = 0;
+#pragma unroll
+      for (uint32_t i = kDenseIpt * tid; i < kDenseIpt * tid + kDenseIpt; ++i)
+        if (i > 0 && i < emtot && s_ck[i] < s_ck[i - 1]) {
+          ++nd;
+          dp = i;
+        }
+      uint32_t tnd, tdp;
+      block_excl_sum2<kDenseThreads>(nd, nd ? dp : 0u, scratch, &tnd, &tdp);
+      if (tid == 0) a.emmeta[b] = make_uint4(emtot ? s_ck[0] : 0u, emtot ? s_ck[emtot - 1] : 0u, tnd, tdp);
+    }
+    for (uint32_t d = tid; d < (1u << a.nx_bits); d += kDenseThreads)
+      if (s_nh[d]) {
+        atomicAdd(&a.nhist[(size_t)d * a.nhist_stride + a.ng + b / a.G], s_nh[d]);
+        s_nh[d] = 0;
+      }
+    if (tid == 0) {
+      a.chunk_off[b] = lo;  // nothing queued: the bucket's backlog is empty
+      a.chunk_cnt[b] = 0u;
+      a.chunk_off[a.nb + b] = (uint32_t)embase;
+      a.chunk_cnt[a.nb + b] = emtot;
+      a.blist[b] = 0u;
+    }
+    __syncthreads();  // (s_nh reset, s_ck read before the next bucket)
+  }
+  if (blockIdx.x < a.nb) flush_stats(a, acc);
 }
 
 // kSkew = false: every bucket whose inbox fits one LDS tile (<= kBucket messages); larger
@@ -3232,7 +3429,9 @@ static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_
     // beside the table row, so their round trip overlaps the gather instead of following the sort
     // (actors past n_local read actor 0's words; bucket_finish masks actors without mail)
     constexpr bool kEarly = kGather && kDefer && !kWide && kEarlyState;
-    constexpr bool kDense = !kWide && kDenseBuckets;  // (dense_finish: at most one message per actor)
+    // (dense_finish: at most one message per actor; not in the fused superstep, where it measured slower:
+    // 1M ring 24.0 -> 25.1 us -- that variant then spills 12 VGPRs)
+    constexpr bool kDense = !kWide && !kGather && kDenseBuckets;
     uint64_t ex0[kBAct] = {}, ex1[kBAct] = {};
     uint32_t alive4 = 0;        // alive flags of actors 4*tid..4*tid+3, loaded first (a0 is a multiple of 32)
     {

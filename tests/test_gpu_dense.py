@@ -18,9 +18,15 @@ pytestmark = pytest.mark.gpu
 MODES = {"fused": {}, "bits3": {"AGX_RADIX_BITS": "3"}, "unfused": {"AGX_NO_FUSED": "1"}}
 
 
+@pytest.mark.parametrize("launch", ["1", "0"])
 @pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("compiled,capacity", [(False, 0), (False, 1), (True, 0), (True, 3)])
-def test_dense_one_per_actor(built, monkeypatch, mode, compiled, capacity):
+def test_dense_one_per_actor(built, monkeypatch, mode, compiled, capacity, launch):
+    """(launch: the multi-pass modes' lean dense-bucket launch, k_dense_apply, forced on / off -- beside
+    the wave-per-bucket launch, which then takes only the buckets the dense launch left)"""
+    if launch == "1" and mode == "fused":
+        pytest.skip("the dense launch is a multi-pass launch")
+    monkeypatch.setenv("AGX_DENSE_LAUNCH", launch)
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
     w = wl.one_per_actor(20_000, seed=5 + capacity, compiled_kinds=compiled, capacity=capacity)
@@ -32,11 +38,20 @@ def test_dense_one_per_actor(built, monkeypatch, mode, compiled, capacity):
 @pytest.mark.parametrize("mode", sorted(MODES))
 def test_dense_ring_partial_buckets(built, monkeypatch, n, hops, mode):
     """Token rings whose last bucket is partial (and a ring of one bucket +- 1 actor): every bucket
-    dense, the wrap-around tell crossing into bucket 0."""
+    dense, the wrap-around tell crossing into bucket 0 (the ring's multi-pass supersteps take the
+    dense launch by default)."""
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
     sg, so, a, b = run_both(wl.token_ring(n, hops))
     assert_same(sg, so, a, b, f"ring n={n} {mode}")
+
+
+@pytest.mark.parametrize("tokens", [1, 2])
+def test_dense_launch_ring_2m(built, tokens):
+    """2.1M actors (native 9-bit multi-pass, identity grouping): one token per actor -- every bucket
+    dense -- and two -- none dense, every bucket left to the block launch."""
+    sg, so, a, b = run_both(wl.token_ring(2_100_000, 5, tokens_per_actor=tokens))
+    assert_same(sg, so, a, b, f"ring 2.1M x{tokens}")
 
 
 def test_dense_sharded_loopback(built):
