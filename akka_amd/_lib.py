@@ -100,6 +100,7 @@ SIGNATURES = {
     "agx_get_stats": (ctypes.c_int32, [ctypes.c_void_p, ctypes.POINTER(AgxStats)]),
     "agx_identity_supersteps": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
     "agx_ring_buckets": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
+    "agx_exchange_info": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
     "agx_get_shape": (ctypes.c_int32, [ctypes.c_void_p, c_u64p, c_u32p]),
     "agx_read_state": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_u64p, c_u8p]),
     "agx_comm_unique_id": (ctypes.c_int32, [ctypes.c_void_p]),
@@ -117,6 +118,10 @@ SIGNATURES = {
     "agx_shard_id": (ctypes.c_int32, [ctypes.c_uint32, ctypes.c_uint32]),
     "agx_owner": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
 }
+
+
+# entry points newer than some A/B diagnostic builds (tools/build_variant.sh of an older checkout)
+OPTIONAL = {"agx_tell", "agx_pump_idle", "agx_exchange_info"}
 
 
 def load():
@@ -137,6 +142,8 @@ def load():
                 pass
         lib = ctypes.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
+            if name in OPTIONAL and not hasattr(lib, name):  # (an older A/B build: AKKA_AMD_LIB)
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -174,6 +174,11 @@ struct agx_engine {
   uint32_t slab = 0;
   uint64_t mr_exact = 0;  // supersteps whose exchange the host redid exactly (a count over the slab)
   uint64_t mr_replays = 0;  // multi-rank replays launched as a captured graph
+  // exchange accounting (agx_exchange_info): supersteps on the device-resident / host-planned
+  // exchange, bytes this rank sent to its peers (envelopes + CRDT rows), and mr_host = 1 once every
+  // rank agreed that the CRDT row slabs do not fit (mr_slabs) -- the host-planned path from then on
+  uint64_t mr_dev_steps = 0, mr_host_steps = 0, mr_sent_env = 0, mr_sent_rows = 0;
+  bool mr_host = false;
 
   DevMsgs A, B, scr, bl, em, stg, s2;
   // single-rank multi-pass: the tell arena by superstep parity (em = even, em2 = odd superstep
@@ -1435,6 +1440,10 @@ agx_status exchange_rccl(agx_engine* e, Plan& p) {
     if (p.send_cnt[q]) {
       const uint64_t o = p.send_off[q], n = p.send_cnt[q];
       NCCL_TRY(ncclSend(e->d_s2p + 3 * o, 3 * n, ncclUint32, (int)q, e->comm, e->stream));
+      if (q != e->rank) {
+        e->mr_sent_env += 12 * n;
+        e->mr_sent_rows += 4ull * n * e->pw;
+      }
       if (e->pw && q != e->rank)
         NCCL_TRY(ncclSend(e->d_s2rows + o * e->pw, n * e->pw, ncclUint32, (int)q, e->comm, e->stream));
     }
@@ -1465,7 +1474,11 @@ uint32_t mr_initial_slab(const agx_engine* e) {
 }
 
 // (re)allocate the per-peer send / receive slabs (the same size on every rank: the decision to grow
-// comes from the all-gathered counts, which every rank reads alike)
+// comes from the all-gathered counts, which every rank reads alike).  CRDT rows travel slab-sized
+// too (R x slab rows of pw u32 to send and as many to receive): when they would leave the row handle
+// space, pass the row budget (AGX_MR_ROW_MB, default 16384 MiB of the 288 GB HBM per rank) or fail
+// to allocate on ANY rank -- all-gathered, so every rank decides alike -- every rank sets mr_host
+// and runs the host-planned exchange (exact per-peer sizes) from then on.
 agx_status mr_slabs(agx_engine* e, uint64_t want) {
   const uint32_t n = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 64), 1u << 30);
   if (n <= e->slab) return AGX_OK;
@@ -1474,24 +1487,49 @@ agx_status mr_slabs(agx_engine* e, uint64_t want) {
   hipFree(e->d_rslab);
   e->d_sslab = e->d_rslab = nullptr;
   e->slab = 0;
+  drop_graphs(e);  // (the slabs are kernel and collective arguments of a captured replay)
   AGX_TRY(dalloc(&e->d_sslab, (uint64_t)e->R * n * 3));
   AGX_TRY(dalloc(&e->d_rslab, (uint64_t)e->R * n * 3));
   if (e->pw) {  // CRDT rows: row send slabs, and rx large enough to receive R slabs of rows
     const uint64_t rr = (uint64_t)e->R * n;
-    if (e->heap_rows + std::max<uint64_t>(rr, e->rx_rows) >= kHandleMask)
-      return set_err(AGX_ECAPACITY, "multi-rank CRDT row slabs of %u exceed the row handle space", n);
+    const char* mb = getenv("AGX_MR_ROW_MB");
+    const uint64_t budget = (mb ? (uint64_t)std::max(0, atoi(mb)) : 16384ull) << 20;
     hipFree(e->d_srows);
     e->d_srows = nullptr;
-    AGX_TRY(dalloc(&e->d_srows, rr * e->pw));
-    if (rr > e->rx_rows) {
+    bool fits = e->heap_rows + std::max<uint64_t>(rr, e->rx_rows) < kHandleMask && 2 * rr * e->pw * 4 <= budget;
+    if (fits && dalloc(&e->d_srows, rr * e->pw) != AGX_OK) fits = false;
+    if (fits && rr > e->rx_rows) {
       hipFree(e->d_rx);
       e->d_rx = nullptr;
-      AGX_TRY(dalloc(&e->d_rx, rr * e->pw));
-      e->rx_rows = rr;
+      if (dalloc(&e->d_rx, rr * e->pw) == AGX_OK) {
+        e->rx_rows = rr;
+      } else {  // (the host-planned path needs rx of cap rows again)
+        fits = false;
+        e->rx_rows = 0;
+        AGX_TRY(dalloc(&e->d_rx, e->cap * e->pw));
+        e->rx_rows = e->cap;
+      }
+    }
+    (void)hipGetLastError();  // (a refused allocation is an answer here, not an error)
+    set_err(AGX_OK, "");
+    // every rank's verdict (the exchange sizes must agree)
+    e->h_pin64[0] = fits ? 1u : 0u;
+    HIP_TRY(hipMemcpyAsync(e->d_cvec, e->h_pin64, 8, hipMemcpyHostToDevice, e->stream));
+    NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, 1, ncclUint64, e->comm, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_cmat, (size_t)e->R * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    bool all = true;
+    for (uint32_t r = 0; r < e->R; ++r) all = all && e->h_pin64[r] != 0;
+    if (!all) {
+      hipFree(e->d_srows);
+      e->d_srows = nullptr;
+      e->mr_host = true;
+      if (getenv("AGX_MR_DEBUG"))
+        fprintf(stderr, "[agx rank %u] CRDT row slabs of %u rows per peer do not fit on every rank: host-planned "
+                "exchange\n", e->rank, n);
     }
   }
   e->slab = n;
-  drop_graphs(e);  // (the slabs are kernel and collective arguments of a captured replay)
   return AGX_OK;
 }
 
@@ -1650,26 +1688,31 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
   bool quiet = false;
   // device-resident replays (CRDT rows travel in row slabs beside the envelope slabs); a staged
   // burst enters through one host-planned superstep (its staged count is a host number)
-  const bool dev = !getenv("AGX_MR_HOST");
+  const bool dev = !getenv("AGX_MR_HOST") && !e->mr_host;
   if (dev && e->n_staged_dev && left) {
     AGX_TRY(host_step(&quiet));
+    ++e->mr_host_steps;
     --left;
   }
-  if (dev) {
-    if (!e->slab) AGX_TRY(mr_slabs(e, mr_initial_slab(e)));
+  if (dev && !e->slab) AGX_TRY(mr_slabs(e, mr_initial_slab(e)));
+  if (dev && !e->mr_host) {
     constexpr uint32_t kMrReplay = 8;  // supersteps enqueued before the host reads the stop word
-    // (opt-in, AGX_MR_GRAPH=1: a captured replay of ncclAllGather + grouped send/recv hung in its
-    // first launch with RCCL's socket transport -- two ranks sharing the one-GPU test box -- so the
-    // eager replay stays the default until the capture is proven over xGMI)
-    const bool graphs = !e->prof && e->graphs_enabled && e->mr_graph_ok && getenv("AGX_MR_GRAPH") &&
-                        atoi(getenv("AGX_MR_GRAPH")) != 0;
-    while (left && !quiet) {
+    // kMrReplay supersteps captured as one graph (collectives included) and replayed: on by
+    // default since round 5, AGX_MR_GRAPH=0 replays eagerly.  (Round 4 kept it opt-in after a run
+    // "hung in its first launch"; the trace shows the replays completing and agx_destroy hanging in
+    // ncclCommDestroy while the graph still held the communicator's persistent plans -- the graph
+    // is now destroyed first, and the whole RCCL-rank suite passes with captured replays.)
+    const char* mg = getenv("AGX_MR_GRAPH");
+    const bool graphs = !e->prof && e->graphs_enabled && e->mr_graph_ok && (!mg || atoi(mg) != 0);
+    while (left && !quiet && !e->mr_host) {
       const uint32_t k = std::min(left, kMrReplay);
       if (graphs && k == kMrReplay && !e->mr_gx) {
         AGX_TRY(capture_mr(e, kMrReplay));
         AGX_TRY(mr_agree_capture(e));
       }
+      const bool dbg = getenv("AGX_MR_DEBUG") != nullptr;
       if (graphs && k == kMrReplay && e->mr_gx) {
+        if (dbg) fprintf(stderr, "[agx rank %u] graph replay %llu: launch\n", e->rank, (unsigned long long)e->mr_replays);
         HIP_TRY(hipGraphLaunch(e->mr_gx, e->stream));
         ++e->mr_replays;
       } else {
@@ -1678,11 +1721,20 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
       HIP_TRY(hipMemcpyAsync(e->h_halt, e->d_halt, 8, hipMemcpyDeviceToHost, e->stream));
       HIP_TRY(hipStreamSynchronize(e->stream));
       const uint32_t code = e->h_halt[0], at = e->h_halt[1];
+      if (dbg) fprintf(stderr, "[agx rank %u] %s of %u supersteps done: halt %u at %u\n", e->rank,
+                       graphs && k == kMrReplay && e->mr_gx ? "graph replay" : "eager replay", k, code, at);
+      const uint64_t sent = (uint64_t)(e->R - 1) * e->slab;  // fixed-size slabs per peer, per superstep
       if (!code) {
         left -= k;
+        e->mr_dev_steps += k;
+        e->mr_sent_env += k * 12 * sent;
+        e->mr_sent_rows += k * 4 * sent * e->pw;
         continue;
       }
       left -= at;  // supersteps completed before the one that stopped (its phase 1 and all-gather ran)
+      e->mr_dev_steps += at;
+      e->mr_sent_env += at * 12 * sent;
+      e->mr_sent_rows += at * 4 * sent * e->pw;
       HIP_TRY(hipMemsetAsync(e->d_halt, 0, 8, e->stream));
       if (code == 2u) break;  // nothing in flight (the host path's quiescence, same point)
       if (code == 3u)
@@ -1691,6 +1743,7 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
       // a sender -> receiver count over the slab: this superstep's exchange exactly, bigger slabs
       AGX_TRY(exact_rest(&quiet));
       ++e->mr_exact;
+      ++e->mr_host_steps;
       --left;
       uint64_t mx = 0;
       for (uint32_t r = 0; r < e->R; ++r)
@@ -1698,8 +1751,11 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
           if (q != r) mx = std::max<uint64_t>(mx, e->h_pin64[r * S + q]);
       AGX_TRY(mr_slabs(e, mx + mx / 4 + 1024));
     }
-  } else {
-    for (; left && !quiet; --left) AGX_TRY(host_step(&quiet));
+  }
+  // host-planned supersteps: AGX_MR_HOST, or CRDT row slabs that do not fit (mr_slabs)
+  for (; left && !quiet; --left) {
+    AGX_TRY(host_step(&quiet));
+    ++e->mr_host_steps;
   }
   HIP_TRY(hipMemcpyAsync(e->h_stat + ST_ERROR, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1707,6 +1763,7 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
 }
 
 void drop_graphs(agx_engine* e) {
+  if (e->mr_gx && getenv("AGX_MR_DEBUG")) fprintf(stderr, "[agx rank %u] multi-rank replay graph dropped\n", e->rank);
   for (auto& a : e->gx)
     for (auto& b : a)
       for (auto& g : b) {
@@ -2099,8 +2156,14 @@ agx_status agx_destroy(agx_engine* e) {
   if (!e) return AGX_OK;
   hipSetDevice((int)e->cfg.device);
   if (e->stream) hipStreamSynchronize(e->stream);
-  if (e->comm) ncclCommDestroy(e->comm);
+  // graphs first: a captured replay holds RCCL's persistent plans of this communicator, and
+  // ncclCommDestroy with such a graph still alive never returned (round 5: the opt-in captured
+  // multi-rank replay ran to quiescence, then the engine's destroy hung -- DESIGN.md §3.3)
   drop_graphs(e);
+  const bool dbg = e->comm && getenv("AGX_MR_DEBUG");
+  if (dbg) fprintf(stderr, "[agx rank %u] destroy: communicator\n", e->rank);
+  if (e->comm) ncclCommDestroy(e->comm);
+  if (dbg) fprintf(stderr, "[agx rank %u] destroy: communicator destroyed\n", e->rank);
   hipFree(e->d_kind); hipFree(e->d_alive); hipFree(e->d_stopq); hipFree(e->d_nstop); hipFree(e->d_state); hipFree(e->d_gid); hipFree(e->d_route);
   hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_zidx); hipFree(e->d_row); hipFree(e->d_col);
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
@@ -2586,6 +2649,17 @@ agx_status agx_ring_buckets(agx_engine* e, uint64_t* out) {
   HIP_TRY(hipStreamSynchronize(e->stream));
   AGX_TRY(copy_sync(e, &n, e->d_ring_next, 4, hipMemcpyDeviceToHost));
   *out = std::min(n, e->ring_slots);
+  return AGX_OK;
+}
+
+agx_status agx_exchange_info(agx_engine* e, uint64_t out[6]) {
+  if (!e || !out) return set_err(AGX_EINVAL, "bad exchange_info args");
+  out[0] = e->mr_dev_steps;
+  out[1] = e->mr_host_steps;
+  out[2] = e->mr_sent_env;
+  out[3] = e->mr_sent_rows;
+  out[4] = e->mr_host ? 1u : 0u;
+  out[5] = e->slab;
   return AGX_OK;
 }
 

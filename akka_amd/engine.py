@@ -257,6 +257,13 @@ class GpuEngine:
         check(self.lib.agx_ring_buckets(self._h, ctypes.byref(v)))
         return v.value
 
+    def exchange_info(self) -> dict:
+        """This rank's multi-rank exchange accounting (agx_exchange_info)."""
+        v = (ctypes.c_uint64 * 6)()
+        check(self.lib.agx_exchange_info(self._h, v))
+        return {"dev_steps": v[0], "host_steps": v[1], "env_bytes": v[2], "row_bytes": v[3],
+                "rows_on_host": bool(v[4]), "slab": v[5]}
+
     def stats(self) -> Stats:
         st = AgxStats()
         check(self.lib.agx_get_stats(self._h, ctypes.byref(st)))

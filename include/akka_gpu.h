@@ -325,6 +325,12 @@ agx_status agx_identity_supersteps(agx_engine* eng, uint64_t* out);
  * message is written once and read once -- until its rings are empty and its mail fits one tile
  * again (the slot is then reused).  Diagnostic; the semantics are the same either way. */
 agx_status agx_ring_buckets(agx_engine* eng, uint64_t* out);
+/* Multi-rank exchange accounting of this rank (diagnostic): out[0] supersteps on the device-resident
+ * exchange (fixed per-peer slabs), out[1] supersteps on the host-planned exchange (exact per-peer
+ * sizes), out[2] envelope bytes and out[3] CRDT row bytes sent to peers, out[4] 1 once the CRDT row
+ * slabs did not fit on some rank (row handle space, AGX_MR_ROW_MB or memory) and every rank moved to
+ * the host-planned exchange, out[5] the slab (envelopes per peer per superstep). */
+agx_status agx_exchange_info(agx_engine* eng, uint64_t out[6]);
 
 /* --- per-actor mailboxes (Mailboxes.lookupConfigurator, Mailboxes.scala:204-260) -------------
  * An actor's mailbox type is resolved per actor in the reference (props, then dispatcher, then

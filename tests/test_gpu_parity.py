@@ -280,6 +280,30 @@ def test_multipass_grouping(built, monkeypatch, bits, G, case, ring):
     assert_same(sg, so, a, b, f"multipass {case} bits={bits}")
 
 
+@pytest.mark.parametrize("bits,G", [(2, 1), (3, 5), (9, 3)])
+@pytest.mark.parametrize("case", ["crdt", "orset", "mixed", "power_law"])
+def test_multipass_emitted_conservation(built, monkeypatch, bits, G, case):
+    """The apply's emitted counter against the mail it actually wrote, superstep by superstep (engine
+    alone, no oracle): with no host actors, staged + emitted == delivered + dead_letters + in_flight,
+    where in_flight is the size of the next superstep's grouped inbox, counted independently of the
+    per-block counters.  (Round 4's sparse ORSet rows in crdt_apply broke exactly this: the summed
+    per-block emitted counter came out wrong while every state row matched -- DESIGN.md §7.)"""
+    monkeypatch.setenv("AGX_RADIX_BITS", str(bits))
+    monkeypatch.setenv("AGX_UNIT_G", str(G))
+    w = MULTIPASS_CASES[case]()
+    eng = GpuEngine(EngineConfig(bucket_actors=w.bucket_actors, **w.engine_kwargs()))
+    w.apply_to(eng)
+    try:
+        for step in range(60):
+            s = eng.run(1)
+            assert s.staged + s.emitted == s.delivered + s.dead_letters + s.in_flight, (case, step, s)
+            if s.in_flight == 0:
+                break
+        assert s.emitted > 0
+    finally:
+        eng.close()
+
+
 def test_multipass_loopback_sharded(built, monkeypatch):
     from oracle import BspOracle
     from akka_amd.engine import owner

@@ -81,10 +81,11 @@ def _rank_main(rank, world, port, a, q):
             eng.tell(d, pay)
         st = eng.run()
         ws, al = eng.read_state()
+        xi = eng.exchange_info() if hasattr(eng.lib, "agx_exchange_info") else {}
         eng.close()
-        q.put((rank, "ok", st.__dict__ if hasattr(st, "__dict__") else dict(st._asdict()), ws, al))
+        q.put((rank, "ok", st.__dict__ if hasattr(st, "__dict__") else dict(st._asdict()), ws, al, xi))
     except Exception as ex:  # report, do not hang the peer
-        q.put((rank, "error", repr(ex), None, None))
+        q.put((rank, "error", repr(ex), None, None, None))
     finally:
         dist.destroy_process_group()
 
@@ -129,7 +130,12 @@ def main():
     ag = np.zeros_like(ao)
     own_of = np.array([owner(i, 1000, world) for i in range(w.n_actors)])
     tot = {}
-    for rank, _, st, ws, al in res:
+    for rank, _, st, ws, al, xi in res:
+        if xi:  # the exchange this rank ran, and what it sent per superstep
+            steps = max(1, xi["dev_steps"] + xi["host_steps"])
+            print(f"exchange rank {rank}: dev_steps={xi['dev_steps']} host_steps={xi['host_steps']} "
+                  f"rows_on_host={xi['rows_on_host']} slab={xi['slab']} env_B/step={xi['env_bytes'] // steps} "
+                  f"row_B/step={xi['row_bytes'] // steps}")
         own = own_of == rank
         wg[own] = ws[own]
         ag[own] = al[own]
