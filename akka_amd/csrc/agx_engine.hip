@@ -220,6 +220,9 @@ struct agx_engine {
   // path, the block launch takes every bucket)
   uint32_t* d_blist = nullptr;
   bool tiny_launch = true;
+  bool dense_fused = true;  // the dense launch also in the fused superstep (AGX_DENSE_FUSED=0: not)
+  bool dense_alone = true;  // fused strict replays: the dense launch alone (cleared at its first recovery)
+  bool recover_dense = false;  // run_single's recovery of a dense-alone superstep: the block + skew launches
   int dense_launch = -1;  // k_dense_apply before the block launch: 1 on, 0 off, -1 (default) ring populations
   // ring apply (agx_ring.h): bounded mailboxes whose queued messages stay in per-actor rings; decided
   // at the first run (setup_ring_apply), then k_ring_tiny + k_ring_apply per superstep replace the tiny /
@@ -607,6 +610,14 @@ uint32_t apply_variant(const agx_engine* e) {
   return V_ALL;
 }
 
+// the lean dense-bucket launch before the block launch (k_dense_apply / k_dense_fused): plain
+// behaviours, one tell per message, no bounded-mailbox rings; by default for ring populations
+bool dense_on(const agx_engine* e, uint32_t vid) {
+  const bool mode_ok = e->fused ? e->dense_fused : e->R == 1;
+  return mode_ok && !kVariants[vid].wide && e->kmax == 1 && !e->ring_live &&
+         (e->dense_launch == 1 || (e->dense_launch < 0 && vid == V_RING));
+}
+
 agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
   // the chunk histograms consumed by this step's first pass were zeroed by k_chunk_downsweep;
   // on the multi-rank path (no chunk pass) they are never read, so stale columns are harmless
@@ -735,14 +746,20 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     }
     const uint32_t mode = e->fused ? M_FUSED : e->R > 1 ? M_OWNER : M_BYPASS;
     const dim3 g(grid_for(e->nb, e->apply_grid));
-    // dense buckets (one message per actor) first, in their own lean launch (k_dense_apply); by
-    // default for ring populations, whose buckets all are (AGX_DENSE_LAUNCH=1 / 0 forces it)
-    const bool dl = mode == M_BYPASS && !kVariants[vid].wide && e->kmax == 1 && !e->ring_live && !e->skew_only &&
-                    (e->dense_launch == 1 || (e->dense_launch < 0 && vid == V_RING));
+    // dense buckets (one message per actor) first, in their own lean launch (k_dense_apply; fused
+    // superstep: k_dense_fused); by default for ring populations, whose buckets all are
+    // (AGX_DENSE_LAUNCH=1 / 0 forces it; AGX_DENSE_FUSED=0 keeps the fused superstep one launch)
+    const bool dl = dense_on(e, vid) && !e->skew_only && !e->recover_dense;
+    // fused strict replay: the dense launch alone is the superstep (a bucket it cannot take marks the
+    // replay void from there, as a deferred skewed bucket does; run_single recovers it), until the
+    // first such recovery (e->dense_alone cleared for the engine)
+    const bool alone = dl && mode == M_FUSED && e->strict_cap && e->dense_alone;
+    if (dl || e->recover_dense) ba.blist = e->d_blist;
     if (dl) {
-      ba.blist = e->d_blist;
       Scope s(e, K_DENSE);
-      HIP_TRY(agx_launch_dense(vid, dim3(grid_for(e->nb, kMaxApplyGrid)), e->stream, ba));
+      BucketArgs bd = ba;
+      bd.dense_alone = alone ? 1u : 0u;
+      HIP_TRY(agx_launch_dense(vid, mode == M_FUSED, dim3(grid_for(e->nb, kMaxApplyGrid)), e->stream, bd));
     }
     const bool tl = mode == M_BYPASS && !kVariants[vid].wide && e->tiny_launch && e->tiny_max && !e->skew_only;
     if (tl) {  // wave-per-bucket launch first; the block launch then takes the buckets it marked
@@ -754,7 +771,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     }
     // skew list (grid-stride); ring buckets take the skew launch every superstep: a wider grid then
     const dim3 gs(grid_for(e->nb, std::min(e->apply_grid, e->ring_live ? std::max(e->skew_grid, 2048u) : e->skew_grid)));
-    if (!e->skew_only) {
+    if (!e->skew_only && !alone) {
       Scope s(e, K_APPLY);
       BucketArgs bf = ba;
       if (e->stamps_skew) bf.dbg = nullptr;  // (diagnostic: stamps of the skew launch only)
@@ -1234,6 +1251,10 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
   hipEvent_t* ev = e->lag_ev;
   agx_status st = AGX_OK;
   uint32_t left = max_steps;
+  // fused with dense-alone strict replays: the superstep that consumes host-staged tells runs eagerly
+  // (block launch beside the dense launch): every bucket with staged tells would otherwise leave the
+  // dense launch and void the replay
+  bool eager_first = left && e->fused && e->stg_pending && e->dense_alone && dense_on(e, apply_variant(e));
   // staged host tells enter through an eager step (the graphs assume none)
   if (left && e->fused && e->stg_pending) {  // the next superstep consumes the staged tells
     e->stg_pending = false;
@@ -1304,14 +1325,40 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
   // A strict replay whose superstep k deferred a skewed bucket: supersteps after k (and every
   // replay launched after it) were no-ops.  Run k's skew launch, count k + 1 supersteps for this
   // replay, void the later ones, continue with the full graphs.
+  // (A dense-alone strict replay -- k_dense_fused the whole superstep -- left its non-dense buckets
+  // marked: k's block launch over the marks, then its skew launch; the strict graphs are recaptured
+  // with the block launch from then on.)
   auto recover = [&](uint32_t slot, uint32_t k) -> agx_status {
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->par = rep_par[slot] ^ (k & 1u);
     e->cur_slot = k;
-    e->skew_only = true;
+    const bool dense = e->dense_alone && dense_on(e, apply_variant(e));
+    if (getenv("AGX_DEBUG_RECOVER")) {  // diagnostic: which buckets the aborting superstep left
+      std::vector<uint32_t> bl(e->nb);
+      if (dense) hipMemcpy(bl.data(), e->d_blist, e->nb * 4, hipMemcpyDeviceToHost);
+      uint32_t nm = 0, first = ~0u;
+      for (uint32_t b = 0; b < e->nb; ++b)
+        if (bl[b]) {
+          ++nm;
+          if (first == ~0u) first = b;
+        }
+      fprintf(stderr, "[agx recover] replay slot %u superstep %u (launched %u): %s, %u buckets marked (first %u)\n", slot, k,
+              rep_start[slot] + k, dense ? "dense-alone" : "skew", nm, first);
+    }
+    e->skew_only = !dense;
+    e->recover_dense = dense;
     agx_status s2 = launch_apply(e, e->A);  // (advances e->par past superstep k)
     e->skew_only = false;
+    e->recover_dense = false;
     e->cur_slot = 0;
+    if (dense) {
+      e->dense_alone = false;
+      for (auto& a : e->gx[1])  // (strict graphs only: the replays in flight are full or void)
+        for (auto& g : a) {
+          if (g) hipGraphExecDestroy(g);
+          g = nullptr;
+        }
+    }
     AGX_TRY(s2);
     HIP_TRY(hipMemcpyAsync(e->h_cntb + rep_ring[slot] * ring_row + (size_t)k * e->nb, e->d_cntb + (size_t)k * e->nb,
                            (size_t)e->nb * 4, hipMemcpyDeviceToHost, e->stream));
@@ -1369,7 +1416,15 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     }
     uint32_t cnt;
     const uint32_t par0 = e->par;
-    if (use_graph) {
+    const bool eager_now = eager_first;
+    eager_first = false;
+    if (use_graph && eager_now) {  // one eager superstep, reported through the replay ring like a replay of 1
+      cnt = 1;
+      st = launch_step_single(e);
+      if (st == AGX_OK)
+        hipLaunchKernelGGL(k_replay_out, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_cntb, e->nb, nullptr, e->d_ring,
+                           e->d_rctr, agx_engine::kGraphSteps * e->nb + 2);
+    } else if (use_graph) {
       st = ensure_graphs();
       if (st != AGX_OK) break;
       const uint32_t si = size_idx(left);
@@ -1390,7 +1445,7 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
       rep_steps[slot] = cnt;
       rep_start[slot] = launched_steps;
       rep_par[slot] = par0;
-      rep_strict[slot] = strict;
+      rep_strict[slot] = strict && !eager_now;
       rep_void[slot] = false;
       if (use_graph) {  // written by the graph's k_replay_out into ring slot (replay counter % kLag)
         rep_ring[slot] = (uint32_t)(e->replay_ctr++ % kLag);
@@ -1869,6 +1924,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   if (const char* s = getenv("AGX_TINY")) e->tiny_max = std::min<uint32_t>(kTinyMax, (uint32_t)std::max(0, atoi(s)));
   if (const char* s = getenv("AGX_TINY_LAUNCH")) e->tiny_launch = atoi(s) != 0;
   if (const char* s = getenv("AGX_DENSE_LAUNCH")) e->dense_launch = atoi(s) != 0 ? 1 : 0;
+  if (const char* s = getenv("AGX_DENSE_FUSED")) e->dense_fused = atoi(s) != 0;
   if (const char* s = getenv("AGX_BUCKET_ACTORS")) {  // diagnostic: override the bucket width (power of two)
     const uint32_t ba = (uint32_t)atoi(s);
     if (ba >= (1u << kMinBucketBits) && ba <= (uint32_t)kBucket && !(ba & (ba - 1))) e->bb = ceil_log2(ba);
@@ -2105,7 +2161,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(dalloc(&e->d_skew_list, e->nb));
   CREATE_TRY(dalloc(&e->d_skew_n, 4));
   CREATE_TRY(hipMemset(e->d_skew_n, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-  if (!e->fused && e->R == 1) CREATE_TRY(dalloc(&e->d_blist, e->nb));
+  if (e->R == 1) CREATE_TRY(dalloc(&e->d_blist, e->nb));
   CREATE_TRY(dalloc(&e->d_chunk_off, e->nchunks));
   CREATE_TRY(dalloc(&e->d_chunk_cnt, e->nchunks));
   CREATE_TRY(hipMemset(e->d_chunk_off, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));

@@ -1058,6 +1058,7 @@ struct BucketArgs {
   // (non-null: the block launch skips the unmarked ones)
   uint32_t* blist;
   uint32_t dense_first;    // bypass: k_dense_apply ran first -- k_tiny_apply takes only the buckets it marked
+  uint32_t dense_alone;    // fused strict replay: k_dense_fused is the whole superstep (a bucket it leaves aborts)
   // bypass, plain behaviours: skewed buckets pre-partitioned by k_skew_* (see there); [i] = skew index
   const uint32_t* sk_rec;  // [i][kSkRec] bucket, bounds, parts, drained and queued totals
   const uint32_t* sk_act;  // [i][3][kBucket] per actor: admitted, drained-segment start, backlog start
@@ -2833,6 +2834,226 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
   if (blockIdx.x < a.nb) flush_stats(a, acc);
 }
 
+// ---- Dense-bucket launch of the fused superstep (one rank, <= 2^20 actors, max_emit 1).
+// The fused block kernel walks every bucket through the general pipeline: table row -> inbox loads
+// -> LDS copy and sortedness check -> per-actor segments -> classification -> drain -> emission
+// scatter, a dozen barriers and three dependent memory round trips per bucket; at 1M actors every
+// bucket is one block's only work, so that chain IS the kernel time (stamps: ~30 K cycles per
+// bucket).  A bucket whose inbox -- no backlog, no staged tells, <= kBucket tells -- holds at most one
+// message per actor needs none of it: every message is admitted and drained (AD/Mailbox.scala:261,
+// 551-565, len = 1), nothing is queued.  This kernel reads the bucket's row of the tell tables,
+// gathers the tells, scatters them to their actors' LDS slots (an LDS hit count per actor finds a
+// second message -> the bucket is left to the block launch, a.blist), and applies actor la =
+// r * kDenseThreads + tid from registers: its flags, kind and state words were loaded beside the
+// table row, before the inbox was known.  The tells leave in actor order (= the block path's
+// drain order) through group_tells, so the next superstep's tables, tell arena, backlog entries and
+// counters are exactly the block path's.  The token ring's buckets are all dense (the wrap-around
+// tell arrives after its bucket's own tells: distinct actors, not increasing keys).
+template <uint32_t KM>
+static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_ks[2 * kBucket];   // per-actor src / pay; group_tells' histogram
+  __shared__ __attribute__((aligned(16))) uint64_t U[3 * kBucket / 2];  // segment list; then the tells, sender order
+  __shared__ __attribute__((aligned(16))) uint32_t s_hit[4 * kRadix];   // messages per actor; group_tells' bases
+  __shared__ uint32_t s_nh[kRadix];                                     // tells per destination bucket
+  __shared__ uint32_t scratch[2 * (kDenseWaves + 1)];
+  __shared__ uint32_t s_cnt[kDenseIpt * kDenseWaves];
+  __shared__ uint32_t s_g[2], s_bad;
+  static_assert(4 * kRadix >= kBucket && kDenseThreads == kBThreads && kDenseIpt == kBIpt, "group_tells' shapes");
+  const BucketLds L{s_ks, s_ks + kBucket, nullptr, U, nullptr, s_hit, nullptr, nullptr, s_nh, scratch, nullptr, nullptr};
+  const DevParams& P = a.P;
+  const GatherArgs& g = a.g;
+  const uint32_t tid = threadIdx.x, w = tid / kWave, lane = lane_id();
+  const uint64_t ltm = lanemask_lt();
+  const uint32_t amask = (1u << a.bb) - 1u, nhmask = (1u << a.nx_bits) - 1u;
+  const uint32_t wpar = a.par, rpar = wpar ^ 1u;
+  if (a.abort) {  // strict replay (this kernel alone is the superstep): an earlier superstep left a bucket
+    const uint32_t ab = a.abort[rpar];
+    if (ab) {
+      if (tid == 0) a.abort[wpar] = ab;  // (pass it on: the next superstep reads this parity)
+      return;
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {  // the cursors the NEXT superstep uses (as k_bucket_apply's fused launch)
+    g.ovf[rpar] = 0u;
+    a.skew_n[rpar] = 0u;
+    if (g.heap_top) g.heap_top[rpar] = 0u;
+  }
+  constexpr bool kKindNeeded = (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0;
+  const uint32_t w1off = P.W > 1 ? P.sw : 0u;
+  uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};
+  if (tid == 0) s_bad = 0;
+  for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x) {
+    AGX_STAMP(a, 0);
+    const uint32_t a0 = b << a.bb, na = min(1u << a.bb, P.n_local - a0);
+    uint32_t* const segp = reinterpret_cast<uint32_t*>(U);  // [nseg + 1] inbox start of each tell segment
+    uint32_t* const sego = segp + kRadix + 2;                // [nseg] its offset in eg[rpar]
+    // ---- the bucket's row of the tell tables (sender bucket c = tid) and, in the same round trip,
+    // this thread's actors' flags, kind and state words
+    uint32_t v = 0, o = 0;
+    uint32_t* my_tc = nullptr;
+    if (tid < a.nb) {
+      uint32_t* tc = g.tcnt[rpar] + (size_t)b * g.tstride + tid;
+      v = *tc;
+      o = g.toff[rpar][(size_t)b * g.tstride + tid];
+      if (v) my_tc = tc;
+    }
+    uint32_t ab[kDenseIpt], kd[kDenseIpt];
+    uint64_t x0[kDenseIpt], x1[kDenseIpt];
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r) {
+      const uint32_t la = r * kDenseThreads + tid, l = a0 + (la < na ? la : 0u);
+      ab[r] = la < na ? P.alive[l] : 0u;
+      kd[r] = kKindNeeded ? P.kind[l] : 0u;
+      x0[r] = ldg64(P.state, l * P.sa);
+      x1[r] = P.W > 1 ? ldg64(P.state, l * P.sa + w1off) : 0ull;
+    }
+    if (tid == 0) {
+      s_g[0] = g.blc[rpar][b];
+      s_g[1] = g.stg_cnt[b];
+    }
+    for (uint32_t i = tid; i < kBucket; i += kDenseThreads) s_hit[i] = 0;
+    for (uint32_t d = tid; d < kRadix; d += kDenseThreads) s_nh[d] = 0;
+    uint32_t cnt, ns;
+    const uint2 exix = block_excl_sum2<kDenseThreads>(v, v ? 1u : 0u, scratch, &cnt, &ns);  // (syncs: s_g visible)
+    AGX_STAMP(a, 1);
+    if (s_g[0] != 0u || s_g[1] != 0u || cnt > (uint32_t)kBucket) {  // (uniform) backlog / staged / big: block path
+      if (tid == 0) {
+        a.blist[b] = 1u;
+        if (a.dense_alone) a.abort[wpar] = a.slot + 1u;  // strict replay: the rest of it is void (run_single recovers)
+      }
+      __syncthreads();  // (s_g is rewritten by the next bucket)
+      continue;
+    }
+    if (v) {
+      segp[exix.y] = exix.x;
+      sego[exix.y] = o;
+    }
+    if (tid == 0) segp[ns] = cnt;
+    __syncthreads();
+    // ---- the inbox (tell segments in sender-bucket order), one round trip; each tell to its actor's slot
+    uint32_t bad = 0;
+    {
+      const uint32_t *Ek = sgpr_ptr(g.eg[rpar].key), *Es = sgpr_ptr(g.eg[rpar].src), *Ep = sgpr_ptr(g.eg[rpar].pay);
+      uint32_t idx[kDenseIpt], k[kDenseIpt], sv[kDenseIpt], pv[kDenseIpt];
+#pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r) {
+        const uint32_t q = r * kDenseThreads + tid;
+        idx[r] = 0;
+        if (q < cnt) {
+          uint32_t lo = 0, hi = ns - 1;  // last segment start <= q
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (segp[mid] <= q) lo = mid; else hi = mid - 1;
+          }
+          idx[r] = sego[lo] + (q - segp[lo]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r) {
+        k[r] = ldg(Ek, idx[r]);
+        sv[r] = ldg(Es, idx[r]);
+        pv[r] = ldg(Ep, idx[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r)
+        if (r * kDenseThreads + tid < cnt) {
+          const uint32_t la = k[r] & amask;
+          if (atomicAdd(&s_hit[la], 1u)) bad = 1;  // a second message to the same actor
+          s_ks[la] = sv[r];
+          s_ks[kBucket + la] = pv[r];
+        }
+    }
+    if (bad) atomicOr(&s_bad, 1u);
+    __syncthreads();
+    AGX_STAMP(a, 2);
+    AGX_STAMP(a, 3);
+    AGX_STAMP(a, 4);
+    if (s_bad) {  // (uniform) not dense: the block path, row untouched
+      __syncthreads();  // (every thread read s_bad)
+      if (tid == 0) {
+        s_bad = 0;
+        a.blist[b] = 1u;
+        if (a.dense_alone) a.abort[wpar] = a.slot + 1u;
+      }
+      continue;
+    }
+    if (my_tc) *my_tc = 0u;  // row consumed
+    const uint32_t lo = b * g.region;  // (cnt <= kBucket = region: the bucket's own inbox region)
+    if (tid == 0) {
+      g.cntb[(size_t)a.slot * a.nb + b] = cnt;
+      g.blo[wpar][b] = lo;  // nothing queued: the bucket's backlog is empty
+      g.blc[wpar][b] = 0u;
+    }
+    // ---- apply, actor order (one message per actor: admitted, drained; to a stopped actor: a dead letter)
+    uint32_t tk[kDenseIpt], tp[kDenseIpt];
+    bool tv[kDenseIpt];
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r) {
+      const uint32_t la = r * kDenseThreads + tid, l = a0 + la;
+      tv[r] = false;
+      tk[r] = tp[r] = 0u;
+      if (la >= na || !s_hit[la]) continue;
+      if (!(ab[r] & 1u)) {
+        ++acc[1];
+        continue;
+      }
+      RegEmitter em{&P, l, 0u, 0u, 0u, 0u};  // (single rank: local id = global id)
+      uint64_t wv2[2] = {x0[r], x1[r]};
+      uint32_t kc = kd[r];
+      ++acc[4];
+      ++acc[0];
+      const uint32_t res = apply_msg<KM>(P, kc, l, l, wv2, s_ks[la], s_ks[kBucket + la], em);
+      if (res == AGX_RES_UNHANDLED) ++acc[2];
+      if (res == AGX_RES_STOPPED) P.alive[l] = (uint8_t)(ab[r] & 0xFEu);  // (only this block reads the bucket's flags)
+      stg64(P.state, l * P.sa, wv2[0]);
+      if (P.W > 1) stg64(P.state, l * P.sa + w1off, wv2[1]);
+      if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
+        if (kc != kd[r]) P.kind[l] = (uint8_t)kc;
+      acc[3] += em.n_all;
+      acc[1] += em.n_all - em.n_valid;
+      tv[r] = em.n_valid != 0u;
+      tk[r] = em.key;
+      tp[r] = em.pay;
+    }
+    // ---- tells in actor order: ranks from per (row, wave) ballots, staged in U, grouped by bucket
+    uint32_t rk[kDenseIpt];
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r) {
+      const uint64_t m = __ballot(tv[r]);
+      rk[r] = (uint32_t)__popcll(m & ltm);
+      if (lane == 0) s_cnt[r * kDenseWaves + w] = (uint32_t)__popcll(m);
+      if (tv[r]) lds_hist_inc(s_nh, (tk[r] >> a.nx_shift) & nhmask);
+    }
+    __syncthreads();
+    AGX_STAMP(a, 5);
+    AGX_STAMP(a, 6);
+    uint32_t emtot = 0;
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r)
+#pragma unroll
+      for (int x = 0; x < kDenseWaves; ++x) {
+        const uint32_t c = s_cnt[r * kDenseWaves + x];
+        if (x == (int)w) rk[r] += emtot;
+        emtot += c;
+      }
+    uint32_t* const ukey = reinterpret_cast<uint32_t*>(U);
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r)
+      if (tv[r]) {
+        ukey[rk[r]] = tk[r];
+        ukey[kBucket + rk[r]] = a0 + r * kDenseThreads + tid;
+        ukey[2 * kBucket + rk[r]] = tp[r];
+      }
+    __syncthreads();
+    group_tells<true>(a, L, b, wpar, (uint64_t)lo * a.kmax, emtot, a.em);
+    AGX_STAMP(a, 7);
+    if (tid == 0) a.blist[b] = 0u;
+    __syncthreads();  // (the bucket's LDS arrays are reset by the next one)
+    AGX_STAMP(a, 8);
+  }
+  if (blockIdx.x < a.nb) flush_stats(a, acc);
+}
+
 // kSkew = false: every bucket whose inbox fits one LDS tile (<= kBucket messages); larger
 // inboxes are appended to the skew list.  kSkew = true (launched right after): the listed
 // buckets, general path — separate instantiation, so its register pressure never reaches
@@ -3390,12 +3611,12 @@ static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_
     for (uint32_t i = tid; i < kStagedChunks; i += kBThreads) a.chunk_cnt[2 * a.nb + i] = 0;  // staged consumed
   }
 
-  // single-rank multi-pass, plain behaviours, after k_tiny_apply: a.blist[b] != 0 marks the buckets
-  // the wave launch left to this one.  A block takes kListBatch of its grid-stride buckets at a time:
+  // single-rank multi-pass, plain behaviours, after k_tiny_apply / k_dense_apply (fused: after
+  // k_dense_fused): a.blist[b] != 0 marks the buckets the earlier launch left to this one.  A block takes kListBatch of its grid-stride buckets at a time:
   // wave 0 reads their marks in one round trip, the ballot is the batch's work mask (no list, no
   // atomics; the bucket -> block assignment stays the grid-stride one)
   constexpr uint32_t kListBatch = 32;
-  const bool listed = kBypass && !kSkew && !kWide && a.blist != nullptr;
+  const bool listed = (kBypass || kGather) && !kSkew && !kWide && a.blist != nullptr;  // (fused: k_dense_fused's marks)
   __shared__ uint32_t s_todo;
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};  // this thread's counters over the block's buckets
   const uint32_t nwork = kSkew ? *skew_n : a.nb;

@@ -22,10 +22,9 @@ MODES = {"fused": {}, "bits3": {"AGX_RADIX_BITS": "3"}, "unfused": {"AGX_NO_FUSE
 @pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("compiled,capacity", [(False, 0), (False, 1), (True, 0), (True, 3)])
 def test_dense_one_per_actor(built, monkeypatch, mode, compiled, capacity, launch):
-    """(launch: the multi-pass modes' lean dense-bucket launch, k_dense_apply, forced on / off -- beside
-    the wave-per-bucket launch, which then takes only the buckets the dense launch left)"""
-    if launch == "1" and mode == "fused":
-        pytest.skip("the dense launch is a multi-pass launch")
+    """(launch: the lean dense-bucket launch -- k_dense_apply in the multi-pass modes, k_dense_fused in
+    the fused superstep -- forced on / off; the block launch (and the multi-pass wave-per-bucket
+    launch) then takes only the buckets it left)"""
     monkeypatch.setenv("AGX_DENSE_LAUNCH", launch)
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
@@ -44,6 +43,53 @@ def test_dense_ring_partial_buckets(built, monkeypatch, n, hops, mode):
         monkeypatch.setenv(k, v)
     sg, so, a, b = run_both(wl.token_ring(n, hops))
     assert_same(sg, so, a, b, f"ring n={n} {mode}")
+
+
+@pytest.mark.parametrize("launch", ["1", "0"])
+@pytest.mark.parametrize("n,tokens,hops", [(1_000_000, 1, 6), (300_001, 2, 4), (65_536, 1, 9), (4_099, 1, 5)])
+def test_dense_fused_ring(built, monkeypatch, n, tokens, hops, launch):
+    """The fused superstep's dense launch (k_dense_fused, default for rings): every bucket of a
+    one-token ring is dense -- bucket 0 included, whose wrap-around tell arrives after its own
+    (distinct actors, not increasing keys) -- and none of a two-token ring, which the block launch
+    then takes whole."""
+    monkeypatch.setenv("AGX_DENSE_FUSED", launch)
+    sg, so, a, b = run_both(wl.token_ring(n, hops, tokens_per_actor=tokens))
+    assert_same(sg, so, a, b, f"fused ring n={n} x{tokens}")
+
+
+@pytest.mark.parametrize("budgets", [(1000,), (5, 3, 1000)])
+def test_dense_fused_recovery(built, budgets):
+    """Dense-alone strict replays (k_dense_fused the whole superstep) meeting a bucket it cannot take:
+    a one-token ring with one actor holding a second token -- that pair travels together, so one
+    bucket per superstep has two messages for one actor.  The first replay voids from that
+    superstep on, run_single runs its block + skew launches, and the engine continues on graphs
+    with the block launch beside the dense launch; and the same pair staged between runs of a
+    clean ring (its superstep runs eagerly, then the replays recover).  Every budget matches the
+    oracle."""
+    from oracle import BspOracle
+    n, hops = 200_003, 40
+    w = wl.token_ring(n, hops)
+    dst, src, pay = w.tells
+    for staged_later in (False, True):
+        extra = (np.array([77], np.uint32), np.array([hops // 2], np.uint32))
+        if not staged_later:
+            w.tells = (np.concatenate([dst, extra[0]]), np.concatenate([src, [src[0]]]).astype(np.uint32),
+                       np.concatenate([pay, extra[1]]))
+        else:
+            w.tells = (dst, src, pay)
+        eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+        ref = BspOracle(**w.engine_kwargs())
+        w.apply_to(eng)
+        w.apply_to(ref)
+        for i, budget in enumerate(budgets + ((7, 1000) if staged_later else ())):
+            if staged_later and i == len(budgets):
+                eng.tell(extra[0], extra[1])
+                ref.tell(extra[0], extra[1])
+            sg, so = eng.run(budget), ref.run(budget)
+            for k in COUNT_KEYS:
+                assert getattr(sg, k) == so[k], (staged_later, budget, k, getattr(sg, k), so[k])
+            assert np.array_equal(eng.read_state()[0], ref.read_state()[0]), (staged_later, budget)
+        eng.close()
 
 
 @pytest.mark.parametrize("tokens", [1, 2])
