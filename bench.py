@@ -269,6 +269,11 @@ def other_configs(quick: bool, only: str = "") -> dict:
             "state (every actor holds one message, ttl 15), BoundedMailbox(1000) (an unbounded mailbox lets the hot "
             "actors' backlogs grow without limit at throughput 5), throughput 5",
             lambda: wl.zipf_fanout(10_000_000, k=1, ttl=15, root_every=1, capacity=1000), 2, 10, 0),
+        "C3_zipf_steady_spec": (
+            "10M actors, SURVEY.md 8(d)'s steady-state shape as specified: Zipf(1.1) FANOUT, k=1, ttl 64, 1/64 of "
+            "the actors roots, the reference's default UNBOUNDED mailbox, throughput 5 (the hot actors' queues grow "
+            "without limit; beside the bounded variant above)",
+            lambda: wl.zipf_fanout(10_000_000, k=1, ttl=64, root_every=64, throughput=5), 2, 10, 0),
         "C3_zipf_tree": (
             "10M actors, Zipf(1.1) fan-out tree of SURVEY.md 8(d): 1/64 of the actors are roots, k=4 tells per "
             "message, ttl 3, BoundedMailbox(1000), throughput 5; timed from the first superstep (the burst)",

@@ -63,6 +63,13 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
       cls
     }
   }
+  // capacities declared up front (gpu.mailbox-capacities = [64, 1000, 0]): their classes exist before
+  // the first run -- with the ring apply on, the engine fixes its classes at that run, and a class added
+  // later by an actorOf would be refused (INTEGRATION.md, "Ring apply and late mailbox types")
+  if (config.hasPath("gpu.mailbox-capacities")) {
+    val it = config.getIntList("gpu.mailbox-capacities").iterator()
+    while (it.hasNext) mailboxClass(it.next().intValue)
+  }
 
   // ---------------------------------------------------------------- actor ids
   private val nextId = new AtomicInteger(0)

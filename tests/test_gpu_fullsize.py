@@ -138,3 +138,25 @@ def test_c5_10m_to_quiescence(built):
 def test_c1_ping_pong_as_benched(built):
     w = wl.ping_pong(1000, messages_per_pair=2_000_000, throughput=50)
     _check(w, [16, 416], "C1 ping-pong", msg_capacity=1 << 20)
+
+
+# ------------------------------------------------------------------ the 100M ring (bench's second line)
+@pytest.mark.timeout(600)
+def test_ring_100m_properties(built):
+    """10^8 actors, one token each (the bench's 100M ring): size-independent properties to
+    quiescence -- every actor counted exactly hops + 1 deliveries, hops + 1 supersteps, nothing dead
+    or in flight -- and identity grouping on (agx_identity_supersteps: every superstep after the first
+    grouped its mail without a radix pass), with the dense-bucket launch (its
+    default for rings) taking the buckets."""
+    n, hops = 100_000_000, 6
+    w = wl.token_ring(n, hops)
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+    w.apply_to(eng)
+    st = eng.run()
+    assert st.delivered == n * (hops + 1) and st.emitted == n * hops and st.staged == n
+    assert st.dead_letters == 0 and st.unhandled == 0 and st.in_flight == 0
+    assert st.supersteps == hops + 1
+    assert eng.identity_supersteps() >= hops - 1
+    words, alive = eng.read_state()
+    assert (words[:, 0] == hops + 1).all() and alive.all()
+    eng.close()

@@ -82,20 +82,33 @@ def main():
         raise SystemExit("the FETCH and WRITE passes dispatched different kernel sequences")
     tags = supersteps(fr)
     per_k = collections.defaultdict(float)
-    tot = 0.0
+    per_k_raw = collections.defaultdict(float)
+    tot = tot_raw = fetch_raw = write_raw = 0.0
     for (_, k, f), (_, _, w), (e, s) in zip(fr, wr, tags):
         if e == 0 and warm < s + 1 <= warm + steps:  # superstep index s counts from 0 (the staged one)
             b = (2 * f + w) * 1024
+            r = (f + w) * 1024  # raw: FETCH_SIZE as counted, no gfx950 correction
             per_k[k] += b
+            per_k_raw[k] += r
             tot += b
+            tot_raw += r
+            fetch_raw += f * 1024
+            write_raw += w * 1024
     alg = cfg["alg_bytes_per_msg"] * cfg["delivered"]
     out = {"config": a.config, "window": {"warmup": warm, "supersteps": steps},
            "counted_bytes_per_superstep": tot / steps, "alg_bytes_per_superstep": alg / steps,
            "ratio": round(tot / alg, 3) if alg else None,
+           # the x2 FETCH correction is calibrated for 16-B-per-lane streaming reads only
+           # (MI355X_MICROARCH.md HBM section); the raw counts bound the scattered kernels from below
+           "raw_fetch_bytes_per_superstep": fetch_raw / steps, "write_bytes_per_superstep": write_raw / steps,
+           "counted_bytes_per_superstep_raw": tot_raw / steps,
+           "ratio_raw": round(tot_raw / alg, 3) if alg else None,
            "per_kernel_gb_per_superstep": {k: round(v / steps / 1e9, 4) for k, v in
                                            sorted(per_k.items(), key=lambda kv: -kv[1]) if v / steps > 1e6},
+           "per_kernel_gb_per_superstep_raw": {k: round(v / steps / 1e9, 4) for k, v in
+                                               sorted(per_k_raw.items(), key=lambda kv: -kv[1]) if v / steps > 1e6},
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) of tools/cfg_one.py; "
-                     "HBM = 2 x FETCH + WRITE (gfx950 correction)"}
+                     "HBM = 2 x FETCH + WRITE (gfx950 correction); *_raw: FETCH + WRITE as counted"}
     print(json.dumps(out))
 
 
