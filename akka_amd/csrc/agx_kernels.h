@@ -150,6 +150,25 @@ __device__ __forceinline__ void stg64(uint64_t* base, uint32_t i, uint64_t v) {
   *(__attribute__((address_space(1))) uint64_t*)((__attribute__((address_space(1))) char*)base + (i << 3)) = v;
 }
 
+// streaming (non-temporal) vector stores for the dense launches' state and tell stores (AGX_NT=0 A/B
+// build knob: plain stores).  Same-box A/B, 1M ring: superstep 16.0 -> 14.7 us -- the bucket's
+// write-once results stream out during the kernel instead of sitting dirty in L2 until its end
+#ifndef AGX_NT
+#define AGX_NT 1
+#endif
+__device__ __forceinline__ void st64x(uint64_t* base, uint32_t i, uint64_t v) {
+  if constexpr (AGX_NT != 0)
+    __builtin_nontemporal_store(v, (__attribute__((address_space(1))) uint64_t*)((__attribute__((address_space(1))) char*)base + (i << 3)));
+  else
+    stg64(base, i, v);
+}
+__device__ __forceinline__ void st32x(uint32_t* p, uint64_t i, uint32_t v) {
+  if constexpr (AGX_NT != 0)
+    __builtin_nontemporal_store(v, (__attribute__((address_space(1))) uint32_t*)p + i);
+  else
+    p[i] = v;
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const uint32_t lane = lane_id();
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -2766,8 +2785,8 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
       const uint32_t res = apply_msg<KM>(P, kc, self, l[r], wv2, sv[r], pv[r], em);
       if (res == AGX_RES_UNHANDLED) ++acc[2];
       if (res == AGX_RES_STOPPED) P.stopq[atomicAdd(P.nstop, 1u)] = l[r];
-      stg64(P.state, l[r] * P.sa, wv2[0]);
-      if (P.W > 1) stg64(P.state, l[r] * P.sa + w1off, wv2[1]);
+      st64x(P.state, l[r] * P.sa, wv2[0]);
+      if (P.W > 1) st64x(P.state, l[r] * P.sa + w1off, wv2[1]);
       if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
         if (kc != kd[r]) P.kind[l[r]] = (uint8_t)kc;
       acc[3] += em.n_all;
@@ -2799,9 +2818,9 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
 #pragma unroll
     for (int r = 0; r < kDenseIpt; ++r)
       if (tv[r]) {
-        a.em.key[embase + rk[r]] = tk[r];
-        a.em.src[embase + rk[r]] = l[r];
-        a.em.pay[embase + rk[r]] = tp[r];
+        st32x(a.em.key, embase + rk[r], tk[r]);
+        st32x(a.em.src, embase + rk[r], l[r]);
+        st32x(a.em.pay, embase + rk[r], tp[r]);
         s_ck[rk[r]] = tk[r];
       }
     __syncthreads();  // (s_ck, s_nh complete; s_cnt read)
@@ -2857,7 +2876,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
   __shared__ uint32_t s_nh[kRadix];                                     // tells per destination bucket
   __shared__ uint32_t scratch[2 * (kDenseWaves + 1)];
   __shared__ uint32_t s_cnt[kDenseIpt * kDenseWaves];
-  __shared__ uint32_t s_g[2], s_bad;
+  __shared__ uint32_t s_g[2], s_bad, s_dmin, s_dmax;
   static_assert(4 * kRadix >= kBucket && kDenseThreads == kBThreads && kDenseIpt == kBIpt, "group_tells' shapes");
   const BucketLds L{s_ks, s_ks + kBucket, nullptr, U, nullptr, s_hit, nullptr, nullptr, s_nh, scratch, nullptr, nullptr};
   const DevParams& P = a.P;
@@ -2910,6 +2929,8 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     if (tid == 0) {
       s_g[0] = g.blc[rpar][b];
       s_g[1] = g.stg_cnt[b];
+      s_dmin = 0xFFFFFFFFu;  // (the min / max digit of the bucket's tells to other buckets, below)
+      s_dmax = 0u;
     }
     for (uint32_t i = tid; i < kBucket; i += kDenseThreads) s_hit[i] = 0;
     for (uint32_t d = tid; d < kRadix; d += kDenseThreads) s_nh[d] = 0;
@@ -3005,8 +3026,8 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
       const uint32_t res = apply_msg<KM>(P, kc, l, l, wv2, s_ks[la], s_ks[kBucket + la], em);
       if (res == AGX_RES_UNHANDLED) ++acc[2];
       if (res == AGX_RES_STOPPED) P.alive[l] = (uint8_t)(ab[r] & 0xFEu);  // (only this block reads the bucket's flags)
-      stg64(P.state, l * P.sa, wv2[0]);
-      if (P.W > 1) stg64(P.state, l * P.sa + w1off, wv2[1]);
+      st64x(P.state, l * P.sa, wv2[0]);
+      if (P.W > 1) st64x(P.state, l * P.sa + w1off, wv2[1]);
       if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
         if (kc != kd[r]) P.kind[l] = (uint8_t)kc;
       acc[3] += em.n_all;
@@ -3015,37 +3036,77 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
       tk[r] = em.key;
       tp[r] = em.pay;
     }
-    // ---- tells in actor order: ranks from per (row, wave) ballots, staged in U, grouped by bucket
-    uint32_t rk[kDenseIpt];
+    // ---- tells in actor order, grouped by destination bucket.  Two classes: digit X (this bucket's
+    // own index) and the rest.  Ranks of both from one packed scan of per (row, wave) ballot counts;
+    // when the rest share ONE digit (a ring, a stencil: the bucket's tells go to itself and one
+    // neighbour) each tell's grouped slot follows directly -- no LDS staging, no multisplit; any
+    // other mix stages the tells in sender order and takes group_tells (the block path's grouping).
+    const uint32_t X = b & nhmask;
+    uint32_t dg[kDenseIpt], rkA[kDenseIpt], rkB[kDenseIpt];
 #pragma unroll
     for (int r = 0; r < kDenseIpt; ++r) {
-      const uint64_t m = __ballot(tv[r]);
-      rk[r] = (uint32_t)__popcll(m & ltm);
-      if (lane == 0) s_cnt[r * kDenseWaves + w] = (uint32_t)__popcll(m);
-      if (tv[r]) lds_hist_inc(s_nh, (tk[r] >> a.nx_shift) & nhmask);
+      dg[r] = (tk[r] >> a.nx_shift) & nhmask;
+      const uint64_t ma = __ballot(tv[r] && dg[r] == X), mb = __ballot(tv[r] && dg[r] != X);
+      rkA[r] = (uint32_t)__popcll(ma & ltm);
+      rkB[r] = (uint32_t)__popcll(mb & ltm);
+      if (lane == 0) s_cnt[r * kDenseWaves + w] = (uint32_t)__popcll(ma) | ((uint32_t)__popcll(mb) << 16);
+      if (tv[r] && dg[r] != X) {
+        atomicMin(&s_dmin, dg[r]);
+        atomicMax(&s_dmax, dg[r]);
+      }
     }
     __syncthreads();
     AGX_STAMP(a, 5);
     AGX_STAMP(a, 6);
-    uint32_t emtot = 0;
+    static_assert(kDenseIpt * kDenseWaves <= kWave, "one lane per (row, wave) count");
+    const uint32_t c = lane < (uint32_t)(kDenseIpt * kDenseWaves) ? s_cnt[lane] : 0u;
+    const uint32_t inc = wave_incl_sum(c);  // (packed halves: each class <= kBucket < 2^16, no carry)
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+    const uint32_t totA = tot & 0xFFFFu, totB = tot >> 16, emtot = totA + totB;
+    uint32_t preA[kDenseIpt], preB[kDenseIpt];
 #pragma unroll
-    for (int r = 0; r < kDenseIpt; ++r)
+    for (int r = 0; r < kDenseIpt; ++r) {
+      const int gi = r * kDenseWaves + (int)w;  // (wave-uniform lane index)
+      const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)(inc - c), gi);
+      preA[r] = ex & 0xFFFFu;
+      preB[r] = ex >> 16;
+    }
+    const uint32_t dmin = s_dmin, dmax = s_dmax;
+    const uint64_t embase = (uint64_t)lo * a.kmax;
+    if (totB == 0 || dmin == dmax) {  // (uniform) at most two destination buckets
+      const bool bfirst = totB && dmin < X;  // grouped runs in digit order
+      const uint32_t baseA = bfirst ? totB : 0u, baseB = bfirst ? 0u : totA;
 #pragma unroll
-      for (int x = 0; x < kDenseWaves; ++x) {
-        const uint32_t c = s_cnt[r * kDenseWaves + x];
-        if (x == (int)w) rk[r] += emtot;
-        emtot += c;
+      for (int r = 0; r < kDenseIpt; ++r)
+        if (tv[r]) {
+          const uint64_t o = embase + (dg[r] == X ? baseA + preA[r] + rkA[r] : baseB + preB[r] + rkB[r]);
+          st32x(g.eg[wpar].key, o, tk[r]);
+          st32x(g.eg[wpar].src, o, a0 + r * kDenseThreads + tid);
+          st32x(g.eg[wpar].pay, o, tp[r]);
+        }
+      if (tid == 0 && totA) {
+        g.tcnt[wpar][(size_t)X * g.tstride + b] = totA;
+        g.toff[wpar][(size_t)X * g.tstride + b] = (uint32_t)embase + baseA;
       }
-    uint32_t* const ukey = reinterpret_cast<uint32_t*>(U);
-#pragma unroll
-    for (int r = 0; r < kDenseIpt; ++r)
-      if (tv[r]) {
-        ukey[rk[r]] = tk[r];
-        ukey[kBucket + rk[r]] = a0 + r * kDenseThreads + tid;
-        ukey[2 * kBucket + rk[r]] = tp[r];
+      if (tid == 1 && totB) {
+        g.tcnt[wpar][(size_t)dmin * g.tstride + b] = totB;
+        g.toff[wpar][(size_t)dmin * g.tstride + b] = (uint32_t)embase + baseB;
       }
-    __syncthreads();
-    group_tells<true>(a, L, b, wpar, (uint64_t)lo * a.kmax, emtot, a.em);
+      if (tid == 0 && g.emc[wpar]) g.emc[wpar][b] = emtot;
+    } else {  // sender order (rank among all tells) in U, per-destination counts, group_tells
+      uint32_t* const ukey = reinterpret_cast<uint32_t*>(U);
+#pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r)
+        if (tv[r]) {
+          const uint32_t q = preA[r] + rkA[r] + preB[r] + rkB[r];
+          ukey[q] = tk[r];
+          ukey[kBucket + q] = a0 + r * kDenseThreads + tid;
+          ukey[2 * kBucket + q] = tp[r];
+          lds_hist_inc(s_nh, dg[r]);
+        }
+      __syncthreads();
+      group_tells<true>(a, L, b, wpar, embase, emtot, a.em);
+    }
     AGX_STAMP(a, 7);
     if (tid == 0) a.blist[b] = 0u;
     __syncthreads();  // (the bucket's LDS arrays are reset by the next one)

@@ -7,9 +7,10 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_dense.py tests/test_gpu_par
   -k "${PK:-dense or ring or strict or partial or ping or zipf or conservation}" $T > gpurun_out/r05b_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/r05b_pytest.log; [ $rc -eq 0 ] || exit 1
 for rep in 1 2; do
-  for v in 0 1; do
-    AGX_DENSE_FUSED=$v timeout -k 10 120 python tools/perf.py --n 1000000 --steps 60 --reps 5 --prof \
+  for v in old dense nt; do
+    case $v in old) E="AGX_DENSE_FUSED=0";; dense) E="AGX_DENSE_FUSED=1";; nt) E="AKKA_AMD_LIB=akka_amd/lib/var/nt.so";; esac
+    env $E timeout -k 10 120 python tools/perf.py --n 1000000 --steps 60 --reps 5 \
       > gpurun_out/r05b_perf_$v.json 2> gpurun_out/r05b_perf_$v.err || { tail -5 gpurun_out/r05b_perf_$v.err; exit 1; }
-    echo "DENSE_FUSED=$v: $(python -c "import json;d=json.loads(open('gpurun_out/r05b_perf_$v.json').read().strip().splitlines()[-1]);print(round(d['us_per_step_median'],2), 'us', d.get('kernels', d.get('prof', ''))) " 2>&1 | cut -c1-600)"
+    echo "$v: $(python -c "import json;d=json.loads(open('gpurun_out/r05b_perf_$v.json').read().strip().splitlines()[-1]);print(round(d['us_per_step_median'],2), 'us')")"
   done
 done
