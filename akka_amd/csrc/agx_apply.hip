@@ -31,14 +31,14 @@ hipError_t agx_launch_tiny_g4(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_tiny_g5(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_tiny_g6(uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_tiny_g7(uint32_t, dim3, hipStream_t, const BucketArgs&);
-hipError_t agx_launch_dense_g0(uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
-hipError_t agx_launch_dense_g1(uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
-hipError_t agx_launch_dense_g2(uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
-hipError_t agx_launch_dense_g3(uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
-hipError_t agx_launch_dense_g4(uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
-hipError_t agx_launch_dense_g5(uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
-hipError_t agx_launch_dense_g6(uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
-hipError_t agx_launch_dense_g7(uint32_t, bool, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g0(uint32_t, uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g1(uint32_t, uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g2(uint32_t, uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g3(uint32_t, uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g4(uint32_t, uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g5(uint32_t, uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g6(uint32_t, uint32_t, dim3, hipStream_t, const BucketArgs&);
+hipError_t agx_launch_dense_g7(uint32_t, uint32_t, dim3, hipStream_t, const BucketArgs&);
 hipError_t agx_launch_ring_g0(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
 hipError_t agx_launch_ring_g1(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
 hipError_t agx_launch_ring_g2(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
@@ -97,19 +97,21 @@ hipError_t tiny_dispatch(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& 
 
 // k_ring_apply (tiny: k_ring_tiny) of the plain / compiled variants of this group
 template <uint32_t V>
-hipError_t dense_dispatch(uint32_t vid, bool fused, dim3 g, hipStream_t s, const BucketArgs& ba) {
+hipError_t dense_dispatch(uint32_t vid, uint32_t mode, dim3 g, hipStream_t s, const BucketArgs& ba) {
   if constexpr (V >= V_N) {
     return hipErrorInvalidValue;
   } else {
     if constexpr (kVariantGroup[V] == AGX_VGROUP && !kVariants[V].wide)
       if (vid == V) {
-        if (fused)
-          hipLaunchKernelGGL((k_dense_fused<kVariants[V].km>), g, dim3(kDenseThreads), 0, s, ba);
+        if (mode == M_FUSED)
+          hipLaunchKernelGGL((k_dense_fused<kVariants[V].km, false>), g, dim3(kDenseThreads), 0, s, ba);
+        else if (mode == M_OWNER)
+          hipLaunchKernelGGL((k_dense_fused<kVariants[V].km, true>), g, dim3(kDenseThreads), 0, s, ba);
         else
           hipLaunchKernelGGL((k_dense_apply<kVariants[V].km>), g, dim3(kDenseThreads), 0, s, ba);
         return hipGetLastError();
       }
-    return dense_dispatch<V + 1>(vid, fused, g, s, ba);
+    return dense_dispatch<V + 1>(vid, mode, g, s, ba);
   }
 }
 
@@ -141,9 +143,9 @@ hipError_t AGX_CAT(agx_launch_tiny_g, AGX_VGROUP)(uint32_t vid, dim3 g, hipStrea
   return tiny_dispatch<0>(vid, g, s, ba);
 }
 
-hipError_t AGX_CAT(agx_launch_dense_g, AGX_VGROUP)(uint32_t vid, bool fused, dim3 g, hipStream_t s,
+hipError_t AGX_CAT(agx_launch_dense_g, AGX_VGROUP)(uint32_t vid, uint32_t mode, dim3 g, hipStream_t s,
                                                    const BucketArgs& ba) {
-  return dense_dispatch<0>(vid, fused, g, s, ba);
+  return dense_dispatch<0>(vid, mode, g, s, ba);
 }
 
 hipError_t AGX_GROUP_FN(uint32_t vid, uint32_t mode, bool skew, dim3 g, hipStream_t s, const BucketArgs& ba) {
@@ -178,17 +180,17 @@ hipError_t agx_launch_ring(uint32_t vid, bool tiny, dim3 g, hipStream_t s, const
   }
 }
 
-hipError_t agx_launch_dense(uint32_t vid, bool fused, dim3 g, hipStream_t s, const BucketArgs& ba) {
+hipError_t agx_launch_dense(uint32_t vid, uint32_t mode, dim3 g, hipStream_t s, const BucketArgs& ba) {
   if (vid >= V_N || kVariants[vid].wide) return hipErrorInvalidValue;
   switch (kVariantGroup[vid]) {
-    case 0: return agx_launch_dense_g0(vid, fused, g, s, ba);
-    case 1: return agx_launch_dense_g1(vid, fused, g, s, ba);
-    case 2: return agx_launch_dense_g2(vid, fused, g, s, ba);
-    case 3: return agx_launch_dense_g3(vid, fused, g, s, ba);
-    case 4: return agx_launch_dense_g4(vid, fused, g, s, ba);
-    case 5: return agx_launch_dense_g5(vid, fused, g, s, ba);
-    case 6: return agx_launch_dense_g6(vid, fused, g, s, ba);
-    default: return agx_launch_dense_g7(vid, fused, g, s, ba);
+    case 0: return agx_launch_dense_g0(vid, mode, g, s, ba);
+    case 1: return agx_launch_dense_g1(vid, mode, g, s, ba);
+    case 2: return agx_launch_dense_g2(vid, mode, g, s, ba);
+    case 3: return agx_launch_dense_g3(vid, mode, g, s, ba);
+    case 4: return agx_launch_dense_g4(vid, mode, g, s, ba);
+    case 5: return agx_launch_dense_g5(vid, mode, g, s, ba);
+    case 6: return agx_launch_dense_g6(vid, mode, g, s, ba);
+    default: return agx_launch_dense_g7(vid, mode, g, s, ba);
   }
 }
 

@@ -220,7 +220,13 @@ struct agx_engine {
   // path, the block launch takes every bucket)
   uint32_t* d_blist = nullptr;
   bool tiny_launch = true;
+  hipEvent_t tev[2] = {nullptr, nullptr};  // agx_run_timed: device time of a run (engine stream)
+  bool timing = false;
   bool dense_fused = true;  // the dense launch also in the fused superstep (AGX_DENSE_FUSED=0: not)
+  // the dense launch in the multi-rank (owner-grouping) superstep: opt-in (AGX_DENSE_OWNER=1) --
+  // loopback R = 2 / 8 x 1M measured no gain (241 vs 236 us per group superstep at R = 2): the owner
+  // apply already takes dense buckets in-kernel (dense_finish), and the extra block launch costs more
+  bool dense_owner = false;
   bool dense_alone = true;  // fused strict replays: the dense launch alone (cleared at its first recovery)
   bool recover_dense = false;  // run_single's recovery of a dense-alone superstep: the block + skew launches
   int dense_launch = -1;  // k_dense_apply before the block launch: 1 on, 0 off, -1 (default) ring populations
@@ -613,7 +619,7 @@ uint32_t apply_variant(const agx_engine* e) {
 // the lean dense-bucket launch before the block launch (k_dense_apply / k_dense_fused): plain
 // behaviours, one tell per message, no bounded-mailbox rings; by default for ring populations
 bool dense_on(const agx_engine* e, uint32_t vid) {
-  const bool mode_ok = e->fused ? e->dense_fused : e->R == 1;
+  const bool mode_ok = e->fused ? e->dense_fused : e->R == 1 || e->dense_owner;
   return mode_ok && !kVariants[vid].wide && e->kmax == 1 && !e->ring_live &&
          (e->dense_launch == 1 || (e->dense_launch < 0 && vid == V_RING));
 }
@@ -759,7 +765,7 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
       Scope s(e, K_DENSE);
       BucketArgs bd = ba;
       bd.dense_alone = alone ? 1u : 0u;
-      HIP_TRY(agx_launch_dense(vid, mode == M_FUSED, dim3(grid_for(e->nb, kMaxApplyGrid)), e->stream, bd));
+      HIP_TRY(agx_launch_dense(vid, mode, dim3(grid_for(e->nb, kMaxApplyGrid)), e->stream, bd));
     }
     const bool tl = mode == M_BYPASS && !kVariants[vid].wide && e->tiny_launch && e->tiny_max && !e->skew_only;
     if (tl) {  // wave-per-bucket launch first; the block launch then takes the buckets it marked
@@ -1461,6 +1467,7 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     launched_steps += cnt;
     hipEventRecord(ev[slot], e->stream);
   }
+  if (e->timing) hipEventRecord(e->tev[1], e->stream);  // (agx_run_timed: after the last replay, before the sync)
   // the kernels' error word rides on the final sync (agx_run checks it even when out == NULL)
   hipMemcpyAsync(e->h_stat + ST_ERROR, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost, e->stream);
   hipStreamSynchronize(e->stream);
@@ -1925,6 +1932,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   if (const char* s = getenv("AGX_TINY_LAUNCH")) e->tiny_launch = atoi(s) != 0;
   if (const char* s = getenv("AGX_DENSE_LAUNCH")) e->dense_launch = atoi(s) != 0 ? 1 : 0;
   if (const char* s = getenv("AGX_DENSE_FUSED")) e->dense_fused = atoi(s) != 0;
+  if (const char* s = getenv("AGX_DENSE_OWNER")) e->dense_owner = atoi(s) != 0;
   if (const char* s = getenv("AGX_BUCKET_ACTORS")) {  // diagnostic: override the bucket width (power of two)
     const uint32_t ba = (uint32_t)atoi(s);
     if (ba >= (1u << kMinBucketBits) && ba <= (uint32_t)kBucket && !(ba & (ba - 1))) e->bb = ceil_log2(ba);
@@ -2161,7 +2169,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(dalloc(&e->d_skew_list, e->nb));
   CREATE_TRY(dalloc(&e->d_skew_n, 4));
   CREATE_TRY(hipMemset(e->d_skew_n, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
-  if (e->R == 1) CREATE_TRY(dalloc(&e->d_blist, e->nb));
+  CREATE_TRY(dalloc(&e->d_blist, e->nb));
   CREATE_TRY(dalloc(&e->d_chunk_off, e->nchunks));
   CREATE_TRY(dalloc(&e->d_chunk_cnt, e->nchunks));
   CREATE_TRY(hipMemset(e->d_chunk_off, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
@@ -2234,6 +2242,8 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_cntb);
   if (e->h_cntb) hipHostFree(e->h_cntb); hipFree(e->d_parv);
   hipFree(e->d_abort); hipFree(e->d_rctr);
+  for (auto& ev : e->tev)
+    if (ev) hipEventDestroy(ev);
   if (e->h_abort) hipHostFree(e->h_abort);
   hipFree(e->d_skew_list); hipFree(e->d_skew_n); hipFree(e->d_blist);
   hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);
@@ -2706,6 +2716,23 @@ agx_status agx_ring_buckets(agx_engine* e, uint64_t* out) {
   AGX_TRY(copy_sync(e, &n, e->d_ring_next, 4, hipMemcpyDeviceToHost));
   *out = std::min(n, e->ring_slots);
   return AGX_OK;
+}
+
+// agx_run with the run's device time on the engine stream: HIP events recorded before the first
+// launch and after the last replay (single rank), so the host's own time around the run is not in it
+agx_status agx_run_timed(agx_engine* e, uint32_t max_supersteps, agx_stats* out, float* device_ms) {
+  if (!e || !device_ms) return set_err(AGX_EINVAL, "bad run_timed args");
+  AGX_TRY(ensure_dev(e));
+  for (auto& ev : e->tev)
+    if (!ev) HIP_TRY(hipEventCreate(&ev));
+  HIP_TRY(hipEventRecord(e->tev[0], e->stream));
+  e->timing = e->R == 1;
+  const agx_status st = agx_run(e, max_supersteps, out);
+  e->timing = false;
+  if (e->R > 1) hipEventRecord(e->tev[1], e->stream);
+  HIP_TRY(hipEventSynchronize(e->tev[1]));
+  HIP_TRY(hipEventElapsedTime(device_ms, e->tev[0], e->tev[1]));
+  return st;
 }
 
 agx_status agx_exchange_info(agx_engine* e, uint64_t out[6]) {

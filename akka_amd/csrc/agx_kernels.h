@@ -2868,7 +2868,7 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
 // drain order) through group_tells, so the next superstep's tables, tell arena, backlog entries and
 // counters are exactly the block path's.  The token ring's buckets are all dense (the wrap-around
 // tell arrives after its bucket's own tells: distinct actors, not increasing keys).
-template <uint32_t KM>
+template <uint32_t KM, bool kOwner>
 static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_ks[2 * kBucket];   // per-actor src / pay; group_tells' histogram
   __shared__ __attribute__((aligned(16))) uint64_t U[3 * kBucket / 2];  // segment list; then the tells, sender order
@@ -2884,15 +2884,16 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
   const uint32_t tid = threadIdx.x, w = tid / kWave, lane = lane_id();
   const uint64_t ltm = lanemask_lt();
   const uint32_t amask = (1u << a.bb) - 1u, nhmask = (1u << a.nx_bits) - 1u;
-  const uint32_t wpar = a.par, rpar = wpar ^ 1u;
-  if (a.abort) {  // strict replay (this kernel alone is the superstep): an earlier superstep left a bucket
+  const uint32_t wpar = kOwner ? 0u : a.par, rpar = wpar ^ 1u;
+  if (kOwner && a.halt && a.halt[0]) return;  // (device-resident multi-rank replay stopped)
+  if (!kOwner && a.abort) {  // strict replay (this kernel alone is the superstep): an earlier superstep left a bucket
     const uint32_t ab = a.abort[rpar];
     if (ab) {
       if (tid == 0) a.abort[wpar] = ab;  // (pass it on: the next superstep reads this parity)
       return;
     }
   }
-  if (blockIdx.x == 0 && tid == 0) {  // the cursors the NEXT superstep uses (as k_bucket_apply's fused launch)
+  if (!kOwner && blockIdx.x == 0 && tid == 0) {  // the cursors the NEXT superstep uses (as k_bucket_apply's fused launch)
     g.ovf[rpar] = 0u;
     a.skew_n[rpar] = 0u;
     if (g.heap_top) g.heap_top[rpar] = 0u;
@@ -2910,25 +2911,28 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     // this thread's actors' flags, kind and state words
     uint32_t v = 0, o = 0;
     uint32_t* my_tc = nullptr;
-    if (tid < a.nb) {
+    // (owner: the inbox is the bucket's range of the sorted input, backlog included)
+    const uint32_t ib = kOwner ? a.bstart[b] : 0u, ie = kOwner ? a.bstart[b + 1] : 0u;
+    if (!kOwner && tid < a.nb) {
       uint32_t* tc = g.tcnt[rpar] + (size_t)b * g.tstride + tid;
       v = *tc;
       o = g.toff[rpar][(size_t)b * g.tstride + tid];
       if (v) my_tc = tc;
     }
-    uint32_t ab[kDenseIpt], kd[kDenseIpt];
+    uint32_t ab[kDenseIpt], kd[kDenseIpt], gs[kDenseIpt];
     uint64_t x0[kDenseIpt], x1[kDenseIpt];
 #pragma unroll
     for (int r = 0; r < kDenseIpt; ++r) {
       const uint32_t la = r * kDenseThreads + tid, l = a0 + (la < na ? la : 0u);
       ab[r] = la < na ? P.alive[l] : 0u;
       kd[r] = kKindNeeded ? P.kind[l] : 0u;
+      gs[r] = kOwner ? P.gid[l] : l;  // the actor's global id (its tells' sender)
       x0[r] = ldg64(P.state, l * P.sa);
       x1[r] = P.W > 1 ? ldg64(P.state, l * P.sa + w1off) : 0ull;
     }
     if (tid == 0) {
-      s_g[0] = g.blc[rpar][b];
-      s_g[1] = g.stg_cnt[b];
+      s_g[0] = kOwner ? 0u : g.blc[rpar][b];
+      s_g[1] = kOwner ? 0u : g.stg_cnt[b];
       s_dmin = 0xFFFFFFFFu;  // (the min / max digit of the bucket's tells to other buckets, below)
       s_dmax = 0u;
     }
@@ -2936,6 +2940,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     for (uint32_t d = tid; d < kRadix; d += kDenseThreads) s_nh[d] = 0;
     uint32_t cnt, ns;
     const uint2 exix = block_excl_sum2<kDenseThreads>(v, v ? 1u : 0u, scratch, &cnt, &ns);  // (syncs: s_g visible)
+    if (kOwner) cnt = ie - ib;
     AGX_STAMP(a, 1);
     if (s_g[0] != 0u || s_g[1] != 0u || cnt > (uint32_t)kBucket) {  // (uniform) backlog / staged / big: block path
       if (tid == 0) {
@@ -2945,22 +2950,25 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
       __syncthreads();  // (s_g is rewritten by the next bucket)
       continue;
     }
-    if (v) {
-      segp[exix.y] = exix.x;
-      sego[exix.y] = o;
+    if (!kOwner) {
+      if (v) {
+        segp[exix.y] = exix.x;
+        sego[exix.y] = o;
+      }
+      if (tid == 0) segp[ns] = cnt;
+      __syncthreads();
     }
-    if (tid == 0) segp[ns] = cnt;
-    __syncthreads();
     // ---- the inbox (tell segments in sender-bucket order), one round trip; each tell to its actor's slot
     uint32_t bad = 0;
     {
-      const uint32_t *Ek = sgpr_ptr(g.eg[rpar].key), *Es = sgpr_ptr(g.eg[rpar].src), *Ep = sgpr_ptr(g.eg[rpar].pay);
+      const uint32_t *Ek = sgpr_ptr(kOwner ? a.in.key : g.eg[rpar].key), *Es = sgpr_ptr(kOwner ? a.in.src : g.eg[rpar].src),
+                     *Ep = sgpr_ptr(kOwner ? a.in.pay : g.eg[rpar].pay);
       uint32_t idx[kDenseIpt], k[kDenseIpt], sv[kDenseIpt], pv[kDenseIpt];
 #pragma unroll
       for (int r = 0; r < kDenseIpt; ++r) {
         const uint32_t q = r * kDenseThreads + tid;
-        idx[r] = 0;
-        if (q < cnt) {
+        idx[r] = kOwner ? ib + (q < cnt ? q : 0u) : 0u;
+        if (!kOwner && q < cnt) {
           uint32_t lo = 0, hi = ns - 1;  // last segment start <= q
           while (lo < hi) {
             const uint32_t mid = (lo + hi + 1) >> 1;
@@ -2999,11 +3007,17 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
       continue;
     }
     if (my_tc) *my_tc = 0u;  // row consumed
-    const uint32_t lo = b * g.region;  // (cnt <= kBucket = region: the bucket's own inbox region)
-    if (tid == 0) {
-      g.cntb[(size_t)a.slot * a.nb + b] = cnt;
-      g.blo[wpar][b] = lo;  // nothing queued: the bucket's backlog is empty
-      g.blc[wpar][b] = 0u;
+    // (fused: cnt <= kBucket = region, the bucket's own inbox region; owner: its sorted range)
+    const uint32_t lo = kOwner ? ib : b * g.region;
+    if (tid == 0) {  // nothing queued: the bucket's backlog is empty
+      if constexpr (kOwner) {
+        a.chunk_off[b] = lo;
+        a.chunk_cnt[b] = 0u;
+      } else {
+        g.cntb[(size_t)a.slot * a.nb + b] = cnt;
+        g.blo[wpar][b] = lo;
+        g.blc[wpar][b] = 0u;
+      }
     }
     // ---- apply, actor order (one message per actor: admitted, drained; to a stopped actor: a dead letter)
     uint32_t tk[kDenseIpt], tp[kDenseIpt];
@@ -3018,14 +3032,17 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
         ++acc[1];
         continue;
       }
-      RegEmitter em{&P, l, 0u, 0u, 0u, 0u};  // (single rank: local id = global id)
+      RegEmitter em{&P, gs[r], 0u, 0u, 0u, 0u};
       uint64_t wv2[2] = {x0[r], x1[r]};
       uint32_t kc = kd[r];
       ++acc[4];
       ++acc[0];
-      const uint32_t res = apply_msg<KM>(P, kc, l, l, wv2, s_ks[la], s_ks[kBucket + la], em);
+      const uint32_t res = apply_msg<KM>(P, kc, gs[r], l, wv2, s_ks[la], s_ks[kBucket + la], em);
       if (res == AGX_RES_UNHANDLED) ++acc[2];
-      if (res == AGX_RES_STOPPED) P.alive[l] = (uint8_t)(ab[r] & 0xFEu);  // (only this block reads the bucket's flags)
+      if (res == AGX_RES_STOPPED) {
+        if constexpr (kOwner) P.stopq[atomicAdd(P.nstop, 1u)] = l;  // (committed by the next superstep)
+        else P.alive[l] = (uint8_t)(ab[r] & 0xFEu);  // (fused: only this block reads the bucket's flags)
+      }
       st64x(P.state, l * P.sa, wv2[0]);
       if (P.W > 1) st64x(P.state, l * P.sa + w1off, wv2[1]);
       if constexpr ((KM & kb(AGX_KIND_COMPILED)) != 0)
@@ -3081,7 +3098,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
         if (tv[r]) {
           const uint64_t o = embase + (dg[r] == X ? baseA + preA[r] + rkA[r] : baseB + preB[r] + rkB[r]);
           st32x(g.eg[wpar].key, o, tk[r]);
-          st32x(g.eg[wpar].src, o, a0 + r * kDenseThreads + tid);
+          st32x(g.eg[wpar].src, o, gs[r]);
           st32x(g.eg[wpar].pay, o, tp[r]);
         }
       if (tid == 0 && totA) {
@@ -3100,7 +3117,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
         if (tv[r]) {
           const uint32_t q = preA[r] + rkA[r] + preB[r] + rkB[r];
           ukey[q] = tk[r];
-          ukey[kBucket + q] = a0 + r * kDenseThreads + tid;
+          ukey[kBucket + q] = gs[r];
           ukey[2 * kBucket + q] = tp[r];
           lds_hist_inc(s_nh, dg[r]);
         }
@@ -3108,7 +3125,13 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
       group_tells<true>(a, L, b, wpar, embase, emtot, a.em);
     }
     AGX_STAMP(a, 7);
-    if (tid == 0) a.blist[b] = 0u;
+    if (tid == 0) {
+      a.blist[b] = 0u;
+      if constexpr (kOwner) {  // the bucket's tell chunk (in-flight accounting)
+        a.chunk_off[a.nb + b] = (uint32_t)embase;
+        a.chunk_cnt[a.nb + b] = emtot;
+      }
+    }
     __syncthreads();  // (the bucket's LDS arrays are reset by the next one)
     AGX_STAMP(a, 8);
   }
@@ -3677,7 +3700,7 @@ static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_
   // wave 0 reads their marks in one round trip, the ballot is the batch's work mask (no list, no
   // atomics; the bucket -> block assignment stays the grid-stride one)
   constexpr uint32_t kListBatch = 32;
-  const bool listed = (kBypass || kGather) && !kSkew && !kWide && a.blist != nullptr;  // (fused: k_dense_fused's marks)
+  const bool listed = !kSkew && !kWide && a.blist != nullptr;  // (fused / owner: k_dense_fused's marks)
   __shared__ uint32_t s_todo;
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};  // this thread's counters over the block's buckets
   const uint32_t nwork = kSkew ? *skew_n : a.nb;

@@ -49,8 +49,8 @@ constexpr uint32_t kVariantGroup[V_N] = {0, 1, 2, 3, 4, 5, 6, 7, 0, 1, 2, 3, 4, 
 hipError_t agx_launch_apply(uint32_t vid, uint32_t mode, bool skew, dim3 grid, hipStream_t s, const BucketArgs& ba);
 // launch k_tiny_apply<variant vid's kinds> (plain / compiled variants only: hipErrorInvalidValue otherwise)
 hipError_t agx_launch_tiny(uint32_t vid, dim3 grid, hipStream_t s, const BucketArgs& ba);
-// launch k_dense_apply<variant vid's kinds> (fused: k_dense_fused) (plain / compiled variants only)
-hipError_t agx_launch_dense(uint32_t vid, bool fused, dim3 grid, hipStream_t s, const BucketArgs& ba);
+// launch k_dense_apply<variant vid's kinds> (mode M_FUSED / M_OWNER: k_dense_fused) (plain / compiled variants only)
+hipError_t agx_launch_dense(uint32_t vid, uint32_t mode, dim3 grid, hipStream_t s, const BucketArgs& ba);
 // launch k_ring_apply<variant vid's kinds> (tiny: k_ring_tiny, kTinyThreads) (plain / compiled variants only)
 hipError_t agx_launch_ring(uint32_t vid, bool tiny, dim3 grid, hipStream_t s, const BucketArgs& ba, const RingArgs& ra);
 

@@ -245,6 +245,13 @@ class GpuEngine:
         check(self.lib.agx_run(self._h, min(int(max_supersteps), 0xFFFFFFFF), ctypes.byref(st)))
         return Stats.from_c(st)
 
+    def run_timed(self, max_supersteps: int) -> tuple:
+        """agx_run_timed: (stats, device ms of the run: HIP events on the engine stream)."""
+        st = AgxStats()
+        ms = ctypes.c_float()
+        check(self.lib.agx_run_timed(self._h, min(int(max_supersteps), 0xFFFFFFFF), ctypes.byref(st), ctypes.byref(ms)))
+        return Stats.from_c(st), float(ms.value)
+
     def identity_supersteps(self) -> int:
         """Multi-pass supersteps grouped without a radix pass (agx_identity_supersteps)."""
         v = ctypes.c_uint64()

@@ -315,6 +315,9 @@ agx_status agx_pump_idle(agx_engine* eng, int32_t* reschedule);
  * was recorded meanwhile).                                                    */
 agx_status agx_run(agx_engine* eng, uint32_t max_supersteps, agx_stats* out);
 agx_status agx_get_stats(agx_engine* eng, agx_stats* out);
+/* agx_run, plus the run's device time in ms: HIP events on the engine's stream before the first
+ * launch and after the last superstep (bench.py's roofline timing of graph-replayed supersteps). */
+agx_status agx_run_timed(agx_engine* eng, uint32_t max_supersteps, agx_stats* out, float* device_ms);
 /* Supersteps of a single-rank multi-pass engine (> 2^20 actors) whose mail needed no radix pass:
  * the previous apply's tells were already in destination order (a ring, a stencil -- identity
  * grouping).  Diagnostic; the grouping is the same either way.                  */

@@ -100,10 +100,18 @@ def test_dense_launch_ring_2m(built, tokens):
     assert_same(sg, so, a, b, f"ring 2.1M x{tokens}")
 
 
-def test_dense_sharded_loopback(built):
+@pytest.mark.parametrize("launch", ["1", "0"])
+@pytest.mark.parametrize("ranks,case", [(3, "one_per_actor"), (2, "ring"), (8, "ring"), (3, "ring2")])
+def test_dense_sharded_loopback(built, monkeypatch, ranks, case, launch):
+    """Owner grouping (multi-rank superstep) with the dense launch (k_dense_fused<kOwner>: the sorted
+    inbox of each bucket, the tells grouped by owner rank) forced on / off: one message per actor over
+    every kind, a hash-sharded token ring (every bucket dense), a two-token ring (none dense)."""
     from oracle import BspOracle
-    ranks = 3
-    w = wl.one_per_actor(30_000, seed=9, capacity=2)
+    monkeypatch.setenv("AGX_DENSE_LAUNCH", launch)
+    monkeypatch.setenv("AGX_DENSE_OWNER", launch)
+    w = {"one_per_actor": lambda: wl.one_per_actor(30_000, seed=9, capacity=2),
+         "ring": lambda: wl.token_ring(40_000, 9),
+         "ring2": lambda: wl.token_ring(30_001, 5, tokens_per_actor=2)}[case]()
     engs = [GpuEngine(EngineConfig(n_ranks=ranks, rank=r, **w.gpu_kwargs())) for r in range(ranks)]
     for e in engs:
         w.apply_to(e)
