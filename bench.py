@@ -302,11 +302,25 @@ def other_configs(quick: bool, only: str = "") -> dict:
             lambda: wl.ping_pong(1000, messages_per_pair=2_000_000, throughput=50), 16, 400, 1 << 20),
     }
     out = {}
+    # counted HBM bytes per superstep of the same window (profiles/pmc_r05.json "configs", from the
+    # rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/cfg_one.py): the fraction on the bytes the
+    # kernels actually moved, beside the one on the algorithmic model (C4 ORSet's sparse rows move
+    # fewer bytes than its dense-state model; C5 / C3 far more)
+    try:
+        counted = json.loads((ROOT / "profiles" / "pmc_r05.json").read_text()).get("configs", {})
+    except Exception:
+        counted = {}
     for name, (desc, make, warm, steps, mcap) in specs.items():
         if only and name != only:
             continue
         try:  # one config failing must not hide the others
             out[name] = dict(workload=desc, **timed_workload(make(), warm, steps, msg_capacity=mcap))
+            c = counted.get(name)
+            if c and out[name].get("ms_per_step"):
+                t = out[name]["ms_per_step"] * 1e-3
+                out[name]["superstep_frac_counted"] = c["counted_bytes_per_superstep"] / t / 1e9 / PEAK_HBM_GBS
+                if "counted_bytes_per_superstep_raw" in c:
+                    out[name]["superstep_frac_counted_raw"] = c["counted_bytes_per_superstep_raw"] / t / 1e9 / PEAK_HBM_GBS
         except Exception as ex:
             out[name] = {"workload": desc, "error": repr(ex)}
     return out
@@ -325,6 +339,8 @@ def summary(out: dict) -> dict:
         if isinstance(v, dict) and "value" in v:
             s[k] = {"msg_s": v["value"], "ms_per_step": round(v["ms_per_step"], 4),
                     "superstep_frac": round(v["superstep_frac"], 4)}
+            if "superstep_frac_counted" in v:
+                s[k]["superstep_frac_counted"] = round(v["superstep_frac_counted"], 4)
     cb = out.get("cpu_baseline")
     if isinstance(cb, dict) and "value" in cb:
         s["cpu_baseline"] = {"msg_s": cb["value"], "cores": cb["cores"], "kind": cb["kind"]}

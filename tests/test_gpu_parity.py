@@ -677,3 +677,27 @@ def test_ring_apply_resume_and_shrink(built, monkeypatch, case):
     assert_same(sg, so, eng.read_state(), ref.read_state(), case)
     eng.close()
     ref.close()
+
+
+@pytest.mark.parametrize("mode", ["fused", "bits3"])
+@pytest.mark.parametrize("case", ["mixed", "zipf_tree", "ring"])
+def test_run_zero_captures_graphs(built, monkeypatch, mode, case):
+    """agx_run(0) captures the replay graphs (bench.py times C3 tree from its first superstep): with
+    host-staged tells pending -- the multi-pass staged chunk is set aside for the capture and consumed
+    by the next run's first superstep -- the results match the oracle, budgets before and after."""
+    from oracle import BspOracle
+    if mode == "bits3":
+        monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    w = {"mixed": lambda: wl.mixed(20_000, seed=2, throughput=2, capacity=5),
+         "zipf_tree": lambda: wl.zipf_fanout(40_000, k=4, ttl=3, root_every=64, capacity=100),
+         "ring": lambda: wl.token_ring(30_000, 20)}[case]()
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+    w.apply_to(eng)
+    ref = BspOracle(**w.engine_kwargs())
+    w.apply_to(ref)
+    for budget in (0, 0, 9, 0, 1 << 30):
+        sg, so = eng.run(budget), ref.run(budget)
+        for k in COUNT_KEYS:
+            assert getattr(sg, k) == so[k], (case, mode, budget, k, getattr(sg, k), so[k])
+        assert np.array_equal(eng.read_state()[0], ref.read_state()[0]), (case, mode, budget)
+    eng.close()
