@@ -620,6 +620,9 @@ uint32_t apply_variant(const agx_engine* e) {
 // behaviours, one tell per message, no bounded-mailbox rings; by default for ring populations
 bool dense_on(const agx_engine* e, uint32_t vid) {
   const bool mode_ok = e->fused ? e->dense_fused : e->R == 1 || e->dense_owner;
+  // (k_dense_fused reads a fused bucket's table row one sender bucket per thread: nb <= 512, which
+  // the fused superstep's <= 2^20 actors guarantee)
+  if (e->fused && e->nb > (uint32_t)kDenseThreads) return false;
   return mode_ok && !kVariants[vid].wide && e->kmax == 1 && !e->ring_live &&
          (e->dense_launch == 1 || (e->dense_launch < 0 && vid == V_RING));
 }
@@ -2740,6 +2743,7 @@ agx_status agx_run_timed(agx_engine* e, uint32_t max_supersteps, agx_stats* out,
   e->timing = e->R == 1;
   const agx_status st = agx_run(e, max_supersteps, out);
   e->timing = false;
+  if (st != AGX_OK) return st;
   if (e->R > 1) hipEventRecord(e->tev[1], e->stream);
   HIP_TRY(hipEventSynchronize(e->tev[1]));
   HIP_TRY(hipEventElapsedTime(device_ms, e->tev[0], e->tev[1]));
