@@ -265,6 +265,10 @@ def other_configs(quick: bool, only: str = "") -> dict:
             f"{n5 // 1_000_000}M actors, power-law out-degree (alpha 2.1, d<=1024) R-MAT graph, FORWARD_RR "
             "round-robin forwarding, BoundedMailbox(64) tail-drop, throughput 5, 1 message/actor",
             lambda: wl.power_law_forward(n5, ttl=15, capacity=64, throughput=5, device_graph=True), 2, 10, 0),
+        "C5_power_law_cap1000": (
+            f"{n5 // 1_000_000}M actors, the C5 graph and behaviour with SURVEY.md 8(d)'s second mailbox setting: "
+            "the reference's default mailbox-capacity 1000 (bounded, tail-drop), throughput 5",
+            lambda: wl.power_law_forward(n5, ttl=15, capacity=1000, throughput=5, device_graph=True), 2, 10, 0),
         "C3_zipf_fanout": (
             "10M actors, Zipf(1.1) destinations over a seeded permutation, FANOUT counter/sum behaviour, k=1 steady "
             "state (every actor holds one message, ttl 15), BoundedMailbox(1000) (an unbounded mailbox lets the hot "

@@ -134,6 +134,18 @@ def test_c5_power_law_bounded_as_benched(built, monkeypatch, ring_slots):
     _assert_same(sg, so, a, b, "C5 to quiescence")
 
 
+def test_c5_power_law_cap1000_as_benched(built):
+    """bench C5's second mailbox setting: the reference's default capacity 1000 --
+    at 2.2M actors, the bench window then to quiescence (the ring apply is not used at this shape: its
+    rings of 1000 slots per actor would not fit; the backlog arena and the skew pre-pass take the hubs)."""
+    w = wl.power_law_forward(2_200_000, ttl=15, capacity=1000, throughput=5, device_graph=True)
+    sg, so, a, b = _run_both(w, max_steps=12)
+    _assert_same(sg, so, a, b, "C5 cap 1000, 12 supersteps")
+    assert sg.in_flight > 0
+    sg, so, a, b = _run_both(w)
+    _assert_same(sg, so, a, b, "C5 cap 1000 to quiescence")
+
+
 @pytest.mark.parametrize("ranks", [8])
 def test_c5_power_law_sharded_loopback(built, ranks):
     """C5 hash-sharded over 8 ranks (ShardRegion extractShardId ownership, loopback exchange)."""
