@@ -283,6 +283,10 @@ def other_configs(quick: bool, only: str = "") -> dict:
             "10M actors, Zipf(1.1) fan-out tree of SURVEY.md 8(d): 1/64 of the actors are roots, k=4 tells per "
             "message, ttl 3, BoundedMailbox(1000), throughput 5; timed from the first superstep (the burst)",
             lambda: wl.zipf_fanout(10_000_000, k=4, ttl=3, root_every=64, capacity=1000), 0, 8, 0),
+        "C3_zipf_tree_spec": (
+            "10M actors, SURVEY.md 8(d)'s fan-out tree as specified: Zipf(1.1) FANOUT k=4, ttl 3, 1/64 roots, the "
+            "reference's default UNBOUNDED mailbox, throughput 5; timed from the first superstep (the burst)",
+            lambda: wl.zipf_fanout(10_000_000, k=4, ttl=3, root_every=64, throughput=5), 0, 8, 0),
         "C4_gcounter_gossip": (
             "1M Replicator-style GCounter replicas (8 node slots), full-state gossip to 2 random peers per tick, "
             "merge = slot-wise max (akka-distributed-data GCounter.merge)",
