@@ -1235,8 +1235,8 @@ agx_status capture_steps(agx_engine* e, uint32_t steps, hipGraphExec_t* out) {
   e->cur_slot = 0;
   if (st == AGX_OK && e->fused)  // the replay's rows and abort marks -> host ring slot (no D2H copy)
     hipLaunchKernelGGL(k_replay_out, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_cntb, steps * e->nb,
-                       e->strict_cap ? e->d_abort : nullptr, e->d_ring, e->d_rctr,
-                       agx_engine::kGraphSteps * e->nb + 2);
+                       e->strict_cap ? e->d_abort : nullptr, (const unsigned long long*)(e->d_stats + ST_ERROR), e->d_ring,
+                       e->d_rctr, agx_engine::kGraphSteps * e->nb + kRingTail);
   hipError_t ce = hipStreamEndCapture(e->stream, &g);
   if (st) {
     if (g) hipGraphDestroy(g);
@@ -1319,11 +1319,12 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
   uint32_t rep_steps[kLag] = {0, 0, 0, 0};
   uint32_t rep_start[kLag] = {0, 0, 0, 0}, rep_par[kLag] = {0, 0, 0, 0};  // supersteps launched before it; parity
   bool rep_strict[kLag] = {false, false, false, false}, rep_void[kLag] = {false, false, false, false};
-  const size_t ring_row = (size_t)agx_engine::kGraphSteps * e->nb + 2;  // rows, then the 2 abort marks
+  const size_t ring_row = (size_t)agx_engine::kGraphSteps * e->nb + kRingTail;  // rows, 2 abort marks, the error word
   uint32_t rep_ring[kLag] = {0, 0, 0, 0};  // host ring slot of each replay in flight
   const uint32_t left0 = left;
   uint32_t launched_steps = 0;
   bool recovered = false;
+  int last_ring = -1;  // ring slot of the last fused replay launched (-1: eager work came last)
   auto fused_poll = [&](uint32_t slot) -> bool {
     const uint32_t* h = e->h_cntb + rep_ring[slot] * ring_row;
     bool last_empty = rep_steps[slot] > 0;
@@ -1367,6 +1368,7 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     }
     e->skew_only = !dense;
     e->recover_dense = dense;
+    last_ring = -1;  // (eager launches after the replays: the error word is copied back)
     agx_status s2 = launch_apply(e, e->A);  // (advances e->par past superstep k)
     e->skew_only = false;
     e->recover_dense = false;
@@ -1442,8 +1444,9 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
       cnt = 1;
       st = launch_step_single(e);
       if (st == AGX_OK)
-        hipLaunchKernelGGL(k_replay_out, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_cntb, e->nb, nullptr, e->d_ring,
-                           e->d_rctr, agx_engine::kGraphSteps * e->nb + 2);
+        hipLaunchKernelGGL(k_replay_out, dim3(1), dim3(kScanThreads), 0, e->stream, e->d_cntb, e->nb, nullptr,
+                           (const unsigned long long*)(e->d_stats + ST_ERROR), e->d_ring, e->d_rctr,
+                           agx_engine::kGraphSteps * e->nb + kRingTail);
     } else if (use_graph) {
       st = ensure_graphs();
       if (st != AGX_OK) break;
@@ -1469,7 +1472,9 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
       rep_void[slot] = false;
       if (use_graph) {  // written by the graph's k_replay_out into ring slot (replay counter % kLag)
         rep_ring[slot] = (uint32_t)(e->replay_ctr++ % kLag);
+        last_ring = (int)rep_ring[slot];
       } else {          // eager superstep: copied (the ring slots are all free between run_single calls)
+        last_ring = -1;
         rep_ring[slot] = slot;
         uint32_t* hr = e->h_cntb + slot * ring_row;
         hipMemcpyAsync(hr, e->d_cntb, (size_t)cnt * e->nb * 4, hipMemcpyDeviceToHost, e->stream);
@@ -1482,15 +1487,25 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     hipEventRecord(ev[slot], e->stream);
   }
   if (e->timing) hipEventRecord(e->tev[1], e->stream);  // (agx_run_timed: after the last replay, before the sync)
-  // the kernels' error word rides on the final sync (agx_run checks it even when out == NULL)
-  hipMemcpyAsync(e->h_stat + ST_ERROR, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost, e->stream);
+  // the kernels' error word rides on the final sync (agx_run checks it even when out == NULL): in the
+  // last replay's ring row (k_replay_out) when a fused replay ended the run, else copied back
+  if (last_ring < 0) hipMemcpyAsync(e->h_stat + ST_ERROR, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost, e->stream);
   hipStreamSynchronize(e->stream);
+  if (last_ring >= 0) {
+    const uint32_t* t = e->h_cntb + (size_t)last_ring * ring_row + ring_row - 2;
+    e->h_stat[ST_ERROR] = (uint64_t)t[0] | ((uint64_t)t[1] << 32);
+  }
+  const bool rec0 = recovered;
   if (e->fused && !quiet)  // replays not polled yet, in launch order
     for (uint32_t k = launched > kLag ? launched - kLag : 0; k < launched && st == AGX_OK; ++k)
       if (poll(k % kLag)) {
         quiet = true;
         break;
       }
+  if (recovered && !rec0) {  // (a recovery above launched more work: its errors too)
+    hipMemcpyAsync(e->h_stat + ST_ERROR, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost, e->stream);
+    hipStreamSynchronize(e->stream);
+  }
   if (st == AGX_OK && recovered && !quiet && left > 0) return run_single(e, left);  // full graphs now
   return st;
 }
@@ -2164,7 +2179,7 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(dalloc(&e->d_stg_cnt, e->nb));
     CREATE_TRY(dalloc(&e->d_ovf, 2));
     CREATE_TRY(dalloc(&e->d_cntb, (uint64_t)agx_engine::kGraphSteps * e->nb));
-    CREATE_TRY(hipHostMalloc((void**)&e->h_cntb, 4ull * (agx_engine::kGraphSteps * e->nb + 2) * 4, hipHostMallocDefault) ==
+    CREATE_TRY(hipHostMalloc((void**)&e->h_cntb, 4ull * (agx_engine::kGraphSteps * e->nb + kRingTail) * 4, hipHostMallocDefault) ==
                        hipSuccess ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
     CREATE_TRY(dalloc(&e->d_parv, 2));
     const uint32_t parv[2] = {0u, 1u};

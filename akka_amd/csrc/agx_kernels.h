@@ -4545,12 +4545,21 @@ static __global__ void __launch_bounds__(kThreads) k_gen_rmat(const uint64_t* lr
 // End of a fused superstep graph: the replay's per-superstep inbox sizes (and strict abort marks)
 // into ring slot (*ctr % 4) of the device-mapped pinned host ring -- one block, so the counter it
 // reads and bumps is never raced.  The host knows the slot of every replay (same counter).
+// Row layout: [inbox sizes][abort marks x2][the error word, lo / hi] (kRingTail words after the rows):
+// the host reads the run's error word from the last replay's row instead of copying it back.
+constexpr uint32_t kRingTail = 4;
 static __global__ void __launch_bounds__(kScanThreads) k_replay_out(const uint32_t* cntb, uint32_t n, const uint32_t* abort,
-                                                            uint32_t* ring, uint32_t* ctr, uint32_t stride) {
+                                                            const unsigned long long* err, uint32_t* ring, uint32_t* ctr,
+                                                            uint32_t stride) {
   const uint32_t c = *ctr;
   uint32_t* dst = ring + (size_t)(c % 4u) * stride;
   for (uint32_t i = threadIdx.x; i < n; i += kScanThreads) dst[i] = cntb[i];
-  if (threadIdx.x < 2) dst[stride - 2 + threadIdx.x] = abort ? abort[threadIdx.x] : 0u;
+  if (threadIdx.x < 2) dst[stride - kRingTail + threadIdx.x] = abort ? abort[threadIdx.x] : 0u;
+  if (threadIdx.x == 2) {
+    const unsigned long long v = *err;
+    dst[stride - 2] = (uint32_t)v;
+    dst[stride - 1] = (uint32_t)(v >> 32);
+  }
   __syncthreads();
   if (threadIdx.x == 0) *ctr = c + 1u;
 }
