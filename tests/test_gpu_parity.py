@@ -701,3 +701,19 @@ def test_run_zero_captures_graphs(built, monkeypatch, mode, case):
             assert getattr(sg, k) == so[k], (case, mode, budget, k, getattr(sg, k), so[k])
         assert np.array_equal(eng.read_state()[0], ref.read_state()[0]), (case, mode, budget)
     eng.close()
+
+
+@pytest.mark.parametrize("strict", ["1", "0"])
+def test_fused_capacity_error_reported(built, monkeypatch, strict):
+    """A kernel-raised capacity error in a fused run (a hot bucket's inbox past the message arena)
+    reaches agx_run: through the last replay's ring row (full graphs, the skew launch inside the
+    replay) or through the copy after a strict replay's recovery."""
+    from akka_amd._lib import AgxError
+    if strict == "0":
+        monkeypatch.setenv("AGX_NO_STRICT", "1")
+    w = wl.zipf_fanout(20_000, k=4, ttl=6, root_every=256, throughput=1000)
+    eng = GpuEngine(EngineConfig(msg_capacity=20_000, **w.gpu_kwargs()))
+    w.apply_to(eng)
+    with pytest.raises(AgxError):
+        eng.run()
+    eng.close()
