@@ -219,6 +219,7 @@ struct agx_engine {
   // one wave each and marks the others here ([nb]) for the block launch (AGX_TINY_LAUNCH=0: no wave
   // path, the block launch takes every bucket)
   uint32_t* d_blist = nullptr;
+  uint32_t* d_dense_left = nullptr;  // [2] BucketArgs::dense_left
   bool tiny_launch = true;
   hipEvent_t tev[2] = {nullptr, nullptr};  // agx_run_timed: device time of a run (engine stream)
   bool timing = false;
@@ -763,7 +764,10 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     // replay void from there, as a deferred skewed bucket does; run_single recovers it), until the
     // first such recovery (e->dense_alone cleared for the engine)
     const bool alone = dl && mode == M_FUSED && e->strict_cap && e->dense_alone;
-    if (dl || e->recover_dense) ba.blist = e->d_blist;
+    if (dl || e->recover_dense) {
+      ba.blist = e->d_blist;
+      if (mode != M_OWNER) ba.dense_left = e->d_dense_left;  // (owner mode: one parity only -- no shortcut)
+    }
     if (dl) {
       Scope s(e, K_DENSE);
       BucketArgs bd = ba;
@@ -2199,6 +2203,8 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
   CREATE_TRY(dalloc(&e->d_skew_n, 4));
   CREATE_TRY(hipMemset(e->d_skew_n, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_blist, e->nb));
+  CREATE_TRY(dalloc(&e->d_dense_left, 2));
+  CREATE_TRY(hipMemset(e->d_dense_left, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
   CREATE_TRY(dalloc(&e->d_chunk_off, e->nchunks));
   CREATE_TRY(dalloc(&e->d_chunk_cnt, e->nchunks));
   CREATE_TRY(hipMemset(e->d_chunk_off, 0, e->nchunks * 4ull) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
@@ -2274,7 +2280,7 @@ agx_status agx_destroy(agx_engine* e) {
   for (auto& ev : e->tev)
     if (ev) hipEventDestroy(ev);
   if (e->h_abort) hipHostFree(e->h_abort);
-  hipFree(e->d_skew_list); hipFree(e->d_skew_n); hipFree(e->d_blist);
+  hipFree(e->d_skew_list); hipFree(e->d_skew_n); hipFree(e->d_blist); hipFree(e->d_dense_left);
   hipFree(e->d_sk_rec); hipFree(e->d_sk_act); hipFree(e->d_sk_pc); hipFree(e->d_sk_meta);
   hipFree(e->d_ring_of); hipFree(e->d_ring_state); hipFree(e->d_ring_src); hipFree(e->d_ring_pay);
   hipFree(e->d_rg_state); hipFree(e->d_rg_nz); hipFree(e->d_rg_src); hipFree(e->d_rg_pay); hipFree(e->d_rg_dk); hipFree(e->d_rg_ds);

@@ -1078,6 +1078,8 @@ struct BucketArgs {
   uint32_t* blist;
   uint32_t dense_first;    // bypass: k_dense_apply ran first -- k_tiny_apply takes only the buckets it marked
   uint32_t dense_alone;    // fused strict replay: k_dense_fused is the whole superstep (a bucket it leaves aborts)
+  uint32_t* dense_left;    // [2] by superstep parity: the dense launch left a bucket to the wave / block launches
+                           // (they return at entry when it did not); null: no such shortcut
   // bypass, plain behaviours: skewed buckets pre-partitioned by k_skew_* (see there); [i] = skew index
   const uint32_t* sk_rec;  // [i][kSkRec] bucket, bounds, parts, drained and queued totals
   const uint32_t* sk_act;  // [i][3][kBucket] per actor: admitted, drained-segment start, backlog start
@@ -2636,6 +2638,7 @@ static __global__ void __launch_bounds__(kTinyThreads) k_tiny_apply(BucketArgs a
   const uint32_t wpar = *a.pstep & 1u, rpar = wpar ^ 1u;
   const InView iv = in_view(a);
   const uint32_t nw = gridDim.x * kTinyWaves;
+  if (a.dense_first && a.dense_left && a.dense_left[wpar] == 0u) return;  // (the dense launch took every bucket)
   for (uint32_t bw = blockIdx.x * kTinyWaves + w; bw < a.nb; bw += nw) {
     if (a.dense_first && __builtin_amdgcn_readfirstlane(a.blist[bw]) == 0u) continue;  // (done by k_dense_apply)
     uint32_t bs = 0, lo_w = 0, hi_w = 0, blc = 0, blo = 0;
@@ -2694,6 +2697,7 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
   constexpr bool kKindNeeded = (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0;
   const uint32_t w1off = P.W > 1 ? P.sw : 0u;
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};
+  if (a.dense_left && blockIdx.x == 0 && tid == 0) a.dense_left[rpar] = 0u;  // (the next superstep's flag)
   for (uint32_t d = tid; d < kRadix; d += kDenseThreads) s_nh[d] = 0;
   if (tid == 0) s_bad = 0;
   __syncthreads();
@@ -2703,7 +2707,10 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
     const uint32_t blc = a.chunk_cnt[b], blo = a.chunk_off[b];
     const uint32_t lo = bs + bp, cnt = blc + (be - bs);
     if (cnt > (uint32_t)kBucket || (uint64_t)lo + cnt > a.cap) {  // (over capacity: the block path reports it)
-      if (tid == 0) a.blist[b] = 1u;
+      if (tid == 0) {
+        a.blist[b] = 1u;
+        if (a.dense_left) a.dense_left[wpar] = 1u;
+      }
       continue;
     }
     const uint32_t a0 = b << a.bb;
@@ -2747,6 +2754,7 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
     if (!dense) {
       if (tid == 0) {
         a.blist[b] = 1u;
+        if (a.dense_left) a.dense_left[wpar] = 1u;
         s_bad = 0;
       }
       continue;  // (uniform)
@@ -2896,6 +2904,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     }
   }
   if (!kOwner && blockIdx.x == 0 && tid == 0) {  // the cursors the NEXT superstep uses (as k_bucket_apply's fused launch)
+    if (a.dense_left) a.dense_left[rpar] = 0u;
     g.ovf[rpar] = 0u;
     a.skew_n[rpar] = 0u;
     if (g.heap_top) g.heap_top[rpar] = 0u;
@@ -2947,6 +2956,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     if (s_g[0] != 0u || s_g[1] != 0u || cnt > (uint32_t)kBucket) {  // (uniform) backlog / staged / big: block path
       if (tid == 0) {
         a.blist[b] = 1u;
+        if (a.dense_left) a.dense_left[wpar] = 1u;
         if (a.dense_alone) a.abort[wpar] = a.slot + 1u;  // strict replay: the rest of it is void (run_single recovers)
       }
       __syncthreads();  // (s_g is rewritten by the next bucket)
@@ -3004,6 +3014,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
       if (tid == 0) {
         s_bad = 0;
         a.blist[b] = 1u;
+        if (a.dense_left) a.dense_left[wpar] = 1u;
         if (a.dense_alone) a.abort[wpar] = a.slot + 1u;
       }
       continue;
@@ -3705,7 +3716,8 @@ static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_
   const bool listed = !kSkew && !kWide && a.blist != nullptr;  // (fused / owner: k_dense_fused's marks)
   __shared__ uint32_t s_todo;
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};  // this thread's counters over the block's buckets
-  const uint32_t nwork = kSkew ? *skew_n : a.nb;
+  // (listed after a dense launch that took every bucket: nothing to do past the per-launch work above)
+  const uint32_t nwork = kSkew ? *skew_n : (listed && a.dense_left && a.dense_left[wpar] == 0u) ? 0u : a.nb;
   const uint32_t istride = listed ? kListBatch * gridDim.x : gridDim.x;
   for (uint32_t it = blockIdx.x; it < nwork; it += istride) {
     uint32_t bfirst = kSkew ? a.skew_list[it] : it, nblk = 1, todo = 1u, bstep = 0;
