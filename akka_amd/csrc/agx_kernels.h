@@ -18,6 +18,11 @@
 //   k_sort_upsweep / k_sort_rowscan / k_sort_downsweep
 //                      the same pass over a dense array (later digits, and the
 //                      multi-GPU path after the RCCL exchange).
+//   k_dense_fused / k_dense_apply
+//                      (round 5) buckets with at most one message per actor, applied from
+//                      registers in actor order with no in-bucket sort (fused superstep /
+//                      multi-pass); every other bucket is marked for k_bucket_apply.
+//   k_tiny_apply       one wave per bucket with a few messages (multi-pass, sparse supersteps).
 //
 // Envelopes are SoA u32 {key, src, payload} = 12 B.
 #pragma once
