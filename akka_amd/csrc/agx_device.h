@@ -19,7 +19,7 @@ struct DevParams {
   uint32_t ring_stride, fan_k;  // ring_stride pre-reduced mod n_global
   uint64_t fan_seed, zipf_n;
   const uint32_t* zipf_cdf;
-  const uint32_t* zipf_idx;   // [2^kZipfBits + 1] search ranges (see zipf_index)
+  const uint2* zipf_ent;      // [2^kZipfBits] direct answers / search ranges (see zipf_dest)
   const uint32_t* zipf_perm;
   const uint64_t* row_ptr;  // local rows
   const uint32_t* col;      // global dst ids
@@ -114,19 +114,24 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 __device__ __forceinline__ uint64_t fanout_rand(uint64_t seed, uint32_t self, uint32_t h, uint32_t j) {
   return splitmix64(seed ^ splitmix64(((uint64_t)self << 32) ^ ((uint64_t)h << 4) ^ (uint64_t)j));
 }
-// First index with cdf[i] >= u (clamped to n - 1): a binary search over the CDF thresholds,
-// started from the range that the top kZipfBits of u select in the `zidx` index
-// (zidx[t] = that search's answer for u = t << (32 - kZipfBits); zidx[2^kZipfBits] = n - 1).
-// Same answer as the search over [0, n - 1] — about 4 dependent loads instead of log2(n).
+// First index i with cdf[i] >= u (clamped to n - 1), as a destination perm[i].  The top kZipfBits
+// of u select an entry of the `zent` index built at agx_set_fanout: when every u of that range has
+// the same answer i (the Zipf head: a hot destination spans many ranges) the entry holds perm[i]
+// itself, {perm[i], kZipfDirect} -- one load in all; otherwise the search range {lo, hi} (lo = the
+// answer for u = t << (32 - kZipfBits), hi = that of the next range, n - 1 after the last), a binary
+// search over the CDF thresholds in it, then perm.  Same answer as the search over [0, n - 1].
 constexpr uint32_t kZipfBits = 20;
-__device__ __forceinline__ uint32_t zipf_index(const uint32_t* cdf, const uint32_t* zidx, uint64_t r) {
-  const uint32_t u = (uint32_t)(r >> 32), t = u >> (32 - kZipfBits);
-  uint32_t lo = zidx[t], hi = zidx[t + 1];
+constexpr uint32_t kZipfDirect = 0xFFFFFFFFu;  // (a range's hi is <= n - 1 < 2^32 - 1)
+__device__ __forceinline__ uint32_t zipf_dest(const uint32_t* cdf, const uint32_t* perm, const uint2* zent, uint64_t r) {
+  const uint32_t u = (uint32_t)(r >> 32);
+  const uint2 z = zent[u >> (32 - kZipfBits)];
+  if (z.y == kZipfDirect) return z.x;
+  uint32_t lo = z.x, hi = z.y;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
     if (cdf[mid] >= u) hi = mid; else lo = mid + 1;
   }
-  return lo;
+  return perm[lo];
 }
 
 // ------------------------------------------------------------------ scans
@@ -348,7 +353,7 @@ __device__ __forceinline__ uint32_t apply_msg(const DevParams& P, uint32_t& kind
         if (ttl > 0)
           for (uint32_t j = 0; j < P.fan_k; ++j) {
             uint64_t r = fanout_rand(P.fan_seed, self, h, j);
-            uint32_t d = P.zipf_perm[zipf_index(P.zipf_cdf, P.zipf_idx, r)];
+            uint32_t d = zipf_dest(P.zipf_cdf, P.zipf_perm, P.zipf_ent, r);
             emit(d, ((ttl - 1) << 24) | ((uint32_t)r & 0x00FFFFFFu));
           }
       }

@@ -148,7 +148,8 @@ struct agx_engine {
   uint32_t *d_gid = nullptr, *d_route = nullptr;
   uint32_t ring_stride = 1, fan_k = 0;
   uint64_t fan_seed = 0, zipf_n = 0;
-  uint32_t *d_zcdf = nullptr, *d_zperm = nullptr, *d_zidx = nullptr;
+  uint32_t *d_zcdf = nullptr, *d_zperm = nullptr;
+  uint2* d_zent = nullptr;
   uint64_t* d_row = nullptr;
   uint32_t* d_col = nullptr;
   // CRDT state gossips (agx_crdt.h): snapshot heap, 2 x cap rows of pw u32
@@ -416,7 +417,7 @@ DevParams make_params(agx_engine* e) {
   P.fan_seed = e->fan_seed;
   P.zipf_n = e->zipf_n;
   P.zipf_cdf = e->d_zcdf;
-  P.zipf_idx = e->d_zidx;
+  P.zipf_ent = e->d_zent;
   P.zipf_perm = e->d_zperm;
   P.row_ptr = e->d_row;
   P.col = e->d_col;
@@ -2264,7 +2265,7 @@ agx_status agx_destroy(agx_engine* e) {
   if (e->comm) ncclCommDestroy(e->comm);
   if (dbg) fprintf(stderr, "[agx rank %u] destroy: communicator destroyed\n", e->rank);
   hipFree(e->d_kind); hipFree(e->d_alive); hipFree(e->d_stopq); hipFree(e->d_nstop); hipFree(e->d_state); hipFree(e->d_gid); hipFree(e->d_route);
-  hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_zidx); hipFree(e->d_row); hipFree(e->d_col);
+  hipFree(e->d_zcdf); hipFree(e->d_zperm); hipFree(e->d_zent); hipFree(e->d_row); hipFree(e->d_col);
   free_msgs(e->A); free_msgs(e->B); free_msgs(e->scr); free_msgs(e->bl); free_msgs(e->em); free_msgs(e->stg);
   free_msgs(e->s2); free_msgs(e->bl2); free_msgs(e->eg0); free_msgs(e->eg1); free_msgs(e->em2);
   hipFree(e->d_emmeta); hipFree(e->d_slsum); hipFree(e->d_ident);
@@ -2528,7 +2529,9 @@ agx_status agx_set_fanout(agx_engine* e, uint32_t k, uint64_t seed, const uint32
   if (n >= (1ull << 32)) return set_err(AGX_EINVAL, "fanout table too large");
   for (uint64_t i = 1; i < n; ++i)
     if (cdf[i] < cdf[i - 1]) return set_err(AGX_EINVAL, "fanout cdf not monotone at %llu", (unsigned long long)i);
-  // search-range index: zidx[t] = first i with cdf[i] >= t << (32 - kZipfBits), clamped to n - 1
+  // range index (zipf_dest): zidx[t] = first i with cdf[i] >= t << (32 - kZipfBits), clamped to n - 1,
+  // zidx[Z] = n - 1; entry t = {perm[i], kZipfDirect} when zidx[t] == zidx[t + 1] = i (every u of the
+  // range answers i), else the search range {zidx[t], zidx[t + 1]}
   const uint64_t Z = 1ull << kZipfBits;
   std::vector<uint32_t> zidx(Z + 1);
   for (uint64_t t = 0, i = 0; t < Z; ++t) {
@@ -2537,14 +2540,18 @@ agx_status agx_set_fanout(agx_engine* e, uint32_t k, uint64_t seed, const uint32
     zidx[t] = (uint32_t)std::min<uint64_t>(i, n - 1);
   }
   zidx[Z] = (uint32_t)(n - 1);
+  std::vector<uint2> zent(Z);
+  for (uint64_t t = 0; t < Z; ++t)
+    zent[t] = zidx[t] == zidx[t + 1] ? make_uint2(perm[zidx[t]], kZipfDirect) : make_uint2(zidx[t], zidx[t + 1]);
   hipFree(e->d_zcdf);
   hipFree(e->d_zperm);
-  hipFree(e->d_zidx);
-  e->d_zcdf = e->d_zperm = e->d_zidx = nullptr;
+  hipFree(e->d_zent);
+  e->d_zcdf = e->d_zperm = nullptr;
+  e->d_zent = nullptr;
   AGX_TRY(dalloc(&e->d_zcdf, n));
   AGX_TRY(dalloc(&e->d_zperm, n));
-  AGX_TRY(dalloc(&e->d_zidx, Z + 1));
-  AGX_TRY(copy_sync(e, e->d_zidx, zidx.data(), (Z + 1) * 4, hipMemcpyHostToDevice));
+  AGX_TRY(dalloc(&e->d_zent, Z));
+  AGX_TRY(copy_sync(e, e->d_zent, zent.data(), Z * sizeof(uint2), hipMemcpyHostToDevice));
   AGX_TRY(copy_sync(e, e->d_zcdf, cdf, n * 4, hipMemcpyHostToDevice));
   AGX_TRY(copy_sync(e, e->d_zperm, perm, n * 4, hipMemcpyHostToDevice));
   e->fan_k = k;

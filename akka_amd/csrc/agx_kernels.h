@@ -1420,6 +1420,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
   if (kFanPre && fan_pre) {
     uint32_t qi[kBIpt], lo[kBIpt], hi[kBIpt], uu[kBIpt];
     bool need[kBIpt];
+    bool dir[kBIpt];
 #pragma unroll
     for (int r = 0; r < kBIpt; ++r) {
       const uint32_t q = r * kBThreads + tid;
@@ -1442,10 +1443,12 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
 #pragma unroll
     for (int r = 0; r < kBIpt; ++r) {
       const uint32_t t = uu[r] >> (32 - kZipfBits);
-      lo[r] = need[r] ? P.zipf_idx[t] : 0u;
-      hi[r] = need[r] ? P.zipf_idx[t + 1] : 0u;
+      const uint2 z = need[r] ? P.zipf_ent[t] : make_uint2(0u, 0u);
+      dir[r] = z.y == kZipfDirect;  // (the Zipf head: the destination itself, no search)
+      lo[r] = z.x;
+      hi[r] = dir[r] ? z.x : z.y;
     }
-    for (;;) {  // zipf_index's binary search, one step of every item per round
+    for (;;) {  // zipf_dest's binary search, one step of every item per round
       bool more = false;
       uint32_t c[kBIpt];
 #pragma unroll
@@ -1461,7 +1464,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     }
     uint32_t d[kBIpt];
 #pragma unroll
-    for (int r = 0; r < kBIpt; ++r) d[r] = need[r] ? P.zipf_perm[lo[r]] : 0u;
+    for (int r = 0; r < kBIpt; ++r) d[r] = need[r] ? (dir[r] ? lo[r] : P.zipf_perm[lo[r]]) : 0u;
 #pragma unroll
     for (int r = 0; r < kBIpt; ++r)
       if (need[r]) L.src[qi[r]] = d[r];
@@ -2481,6 +2484,7 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
   if (kFanPre && fan_pre) {
     uint32_t uu[kTinyIpl], lo2[kTinyIpl], hi2[kTinyIpl];
     bool need[kTinyIpl];
+    bool dir[kTinyIpl];
 #pragma unroll
     for (uint32_t i = 0; i < kTinyIpl; ++i) {
       const uint32_t p = lane * kTinyIpl + i;
@@ -2499,8 +2503,10 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
 #pragma unroll
     for (uint32_t i = 0; i < kTinyIpl; ++i) {
       const uint32_t t = uu[i] >> (32 - kZipfBits);
-      lo2[i] = need[i] ? P.zipf_idx[t] : 0u;
-      hi2[i] = need[i] ? P.zipf_idx[t + 1] : 0u;
+      const uint2 z = need[i] ? P.zipf_ent[t] : make_uint2(0u, 0u);
+      dir[i] = z.y == kZipfDirect;  // (the Zipf head: the destination itself, no search)
+      lo2[i] = z.x;
+      hi2[i] = dir[i] ? z.x : z.y;
     }
     for (;;) {
       bool more = false;
@@ -2518,7 +2524,7 @@ __device__ __forceinline__ void tiny_bucket(const BucketArgs& a, const InView& i
     }
     uint32_t dd[kTinyIpl];
 #pragma unroll
-    for (uint32_t i = 0; i < kTinyIpl; ++i) dd[i] = need[i] ? P.zipf_perm[lo2[i]] : 0u;
+    for (uint32_t i = 0; i < kTinyIpl; ++i) dd[i] = need[i] ? (dir[i] ? lo2[i] : P.zipf_perm[lo2[i]]) : 0u;
 #pragma unroll
     for (uint32_t i = 0; i < kTinyIpl; ++i)
       if (need[i]) T.src[lane * kTinyIpl + i] = dd[i];

@@ -297,14 +297,17 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
       for (uint32_t j0 = tid; j0 < D; j0 += 4 * kBThreads) {
         uint32_t uu[4], lo[4], hi[4];
         bool need[4];
+        bool dir[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const uint32_t j = j0 + c * kBThreads, pv = j < D ? bpay[j] : 0u;
           need[c] = j < D && (pv >> 24) > 0;
           uu[c] = need[c] ? (uint32_t)(fanout_rand(P.fan_seed, skey[j], pv & 0x00FFFFFFu, 0) >> 32) : 0u;
           const uint32_t t = uu[c] >> (32 - kZipfBits);
-          lo[c] = need[c] ? P.zipf_idx[t] : 0u;
-          hi[c] = need[c] ? P.zipf_idx[t + 1] : 0u;
+          const uint2 z = need[c] ? P.zipf_ent[t] : make_uint2(0u, 0u);
+          dir[c] = z.y == kZipfDirect;  // (the Zipf head: the destination itself, no search)
+          lo[c] = z.x;
+          hi[c] = dir[c] ? z.x : z.y;
         }
         for (;;) {
           bool more = false;
@@ -322,7 +325,7 @@ static __global__ void __launch_bounds__(kBThreads, 4) k_ring_apply(BucketArgs a
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          if (need[c]) bsrc[j0 + c * kBThreads] = P.zipf_perm[lo[c]];
+          if (need[c]) bsrc[j0 + c * kBThreads] = dir[c] ? lo[c] : P.zipf_perm[lo[c]];
       }
       __syncthreads();
     }
@@ -728,14 +731,17 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
     for (uint32_t f0 = 0; f0 < kRingTinyD / kWave; f0 += kF) {
       uint32_t uu[kF], lo2[kF], hi2[kF];
       bool need[kF];
+      bool dir[kF];
 #pragma unroll
       for (uint32_t f = 0; f < kF; ++f) {
         const uint32_t j = (f0 + f) * kWave + lane, pv = j < D ? T.dp[j] : 0u;
         need[f] = j < D && (pv >> 24) > 0;
         uu[f] = need[f] ? (uint32_t)(fanout_rand(P.fan_seed, T.dk[j] & 0x7FFFFFFFu, pv & 0x00FFFFFFu, 0) >> 32) : 0u;
         const uint32_t t = uu[f] >> (32 - kZipfBits);
-        lo2[f] = need[f] ? P.zipf_idx[t] : 0u;
-        hi2[f] = need[f] ? P.zipf_idx[t + 1] : 0u;
+        const uint2 z = need[f] ? P.zipf_ent[t] : make_uint2(0u, 0u);
+        dir[f] = z.y == kZipfDirect;  // (the Zipf head: the destination itself, no search)
+        lo2[f] = z.x;
+        hi2[f] = dir[f] ? z.x : z.y;
       }
       for (;;) {
         bool more = false;
@@ -753,7 +759,7 @@ __device__ __forceinline__ bool ring_tiny_bucket(const BucketArgs& a, const Ring
       }
       uint32_t dd[kF];
 #pragma unroll
-      for (uint32_t f = 0; f < kF; ++f) dd[f] = need[f] ? P.zipf_perm[lo2[f]] : 0u;
+      for (uint32_t f = 0; f < kF; ++f) dd[f] = need[f] ? (dir[f] ? lo2[f] : P.zipf_perm[lo2[f]]) : 0u;
 #pragma unroll
       for (uint32_t f = 0; f < kF; ++f)
         if (need[f]) T.ds[(f0 + f) * kWave + lane] = dd[f];

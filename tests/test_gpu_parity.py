@@ -369,14 +369,17 @@ def test_grid_stride_apply(built, monkeypatch, fused, case):
     assert_same(sg, so, a, b, f"grid-stride {case} fused={fused}")
 
 
+@pytest.mark.parametrize("k", [1, 3])
 @pytest.mark.parametrize("shape", ["steps", "dup_edges", "tiny"])
-def test_zipf_index_ranges(built, shape):
-    """The device's indexed CDF search (top 20 bits of the draw pick a search range) returns
-    the plain binary search's answer: thresholds on range boundaries, long runs of equal
-    thresholds, 0 and 0xFFFFFFFF entries, tables shorter than the index."""
+def test_zipf_index_ranges(built, shape, k):
+    """The device's indexed CDF search (top 20 bits of the draw pick an index entry: the
+    destination itself when the whole range has one answer, else a search range) returns the
+    plain binary search's answer: thresholds on range boundaries, long runs of equal thresholds,
+    0 and 0xFFFFFFFF entries, tables shorter than the index.  k = 1 takes the kernels' lockstep
+    lookups (block, wave and ring launches), k = 3 the per-message one in apply_msg."""
     import dataclasses
     n = 50_000
-    w = wl.zipf_fanout(n, k=3, ttl=3, root_every=7, throughput=3)
+    w = wl.zipf_fanout(n, k=k, ttl=3, root_every=7, throughput=3)
     k, seed, _, perm = w.fanout
     rng = np.random.default_rng(5)
     if shape == "steps":  # every threshold on a multiple of 2^12 (a range boundary)
