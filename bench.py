@@ -63,6 +63,7 @@ def kernel_bytes_per_msg(W: int) -> dict:
 
 
 SORT_CLASSES = ("chunk_downsweep", "sort_upsweep", "sort_downsweep")
+DENSE_FOLLOWERS = ("bucket_apply", "bucket_apply_tiny")  # (launched after k_dense_apply in one superstep)
 
 
 def kernel_rooflines(prof: dict, per_msg: dict, msgs_per_launch: int, identity: bool = False) -> dict:
@@ -79,6 +80,12 @@ def kernel_rooflines(prof: dict, per_msg: dict, msgs_per_launch: int, identity: 
             continue
         avg_ms = v["total_ms"] / v["launches"]
         ach = per_msg[k] * msgs_per_launch / (avg_ms * 1e-3) / 1e9
+        if k in DENSE_FOLLOWERS and prof.get("bucket_apply_dense", {}).get("launches") and ach > PEAK_HBM_GBS:
+            # launched after a dense launch that took every bucket: it returned at entry (dense_left = 0,
+            # DESIGN.md §3.2) -- the messages were the dense launch's, and > 1 of peak is no fraction
+            out[k] = {"returned_at_entry": True, "avg_launch_ms": round(avg_ms, 4),
+                      "reason": "the dense launch before it took every bucket"}
+            continue
         out[k] = {"achieved": round(ach, 1), "frac": round(ach / PEAK_HBM_GBS, 4), "avg_launch_ms": round(avg_ms, 4),
                   "alg_bytes_per_launch": per_msg[k] * msgs_per_launch}
     dom = max((k for k in prof if prof[k]["launches"]), key=lambda k: prof[k]["total_ms"], default=None)

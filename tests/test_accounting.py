@@ -69,3 +69,21 @@ def test_bench_kernel_rooflines():
     assert r["bucket_apply_dense"]["achieved"] == pytest.approx(round(42 * 1_000_000 / (avg * 1e-3) / 1e9, 1))
     assert r["bucket_apply_dense"]["frac"] == pytest.approx(round(42e6 / (avg * 1e-3) / 1e9 / bench.PEAK_HBM_GBS, 4))
     assert "bucket_apply" not in r  # (no launches: no roofline)
+
+
+def test_bench_rooflines_after_a_dense_launch():
+    """At 100M the block launch follows the dense launch and returns at entry when it took every
+    bucket: the block class gets no fraction (it would read > 1 of peak), the dense class keeps its own."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    per = bench.kernel_bytes_per_msg(1)
+    prof = {"bucket_apply_dense": {"total_ms": 16.8, "launches": 25}, "bucket_apply": {"total_ms": 0.19, "launches": 25}}
+    rr = bench.kernel_rooflines(prof, per, 100_000_000, identity=True)
+    r = rr["kernels"]
+    assert rr["dominant"] == "bucket_apply_dense"
+    assert r["bucket_apply"] == {"returned_at_entry": True, "avg_launch_ms": 0.0076,
+                                 "reason": "the dense launch before it took every bucket"}
+    assert 0 < r["bucket_apply_dense"]["frac"] < 1
+    # without a dense launch in the profile the same numbers stay a (bad) fraction, not hidden
+    r2 = bench.kernel_rooflines({"bucket_apply": prof["bucket_apply"]}, per, 100_000_000)["kernels"]
+    assert r2["bucket_apply"]["frac"] > 1
