@@ -2889,6 +2889,10 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
 // drain order) through group_tells, so the next superstep's tables, tell arena, backlog entries and
 // counters are exactly the block path's.  The token ring's buckets are all dense (the wrap-around
 // tell arrives after its bucket's own tells: distinct actors, not increasing keys).
+#ifndef AGX_EARLY_ROW
+#define AGX_EARLY_ROW 1
+#endif
+constexpr bool kEarlyRow = AGX_EARLY_ROW != 0;
 template <uint32_t KM, bool kOwner>
 static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_ks[2 * kBucket];   // per-actor src / pay; group_tells' histogram
@@ -2907,24 +2911,34 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
   const uint32_t amask = (1u << a.bb) - 1u, nhmask = (1u << a.nx_bits) - 1u;
   const uint32_t wpar = kOwner ? 0u : a.par, rpar = wpar ^ 1u;
   if (kOwner && a.halt && a.halt[0]) return;  // (device-resident multi-rank replay stopped)
-  if (!kOwner && a.abort) {  // strict replay (this kernel alone is the superstep): an earlier superstep left a bucket
-    const uint32_t ab = a.abort[rpar];
-    if (ab) {
-      if (tid == 0) a.abort[wpar] = ab;  // (pass it on: the next superstep reads this parity)
-      return;
+  // strict replay (this kernel alone is the superstep): an earlier superstep that left a bucket
+  // voids this one.  The word is read here and tested after the first bucket's row / state loads are
+  // issued (AGX_EARLY_ROW), so its round trip overlaps theirs instead of preceding them; nothing is
+  // stored before the test.
+  uint32_t ab_in = (!kOwner && a.abort) ? a.abort[rpar] : 0u;
+  bool tested = !kEarlyRow;
+  const auto abort_test = [&]() -> bool {
+    if (ab_in) {
+      if (tid == 0) a.abort[wpar] = ab_in;  // (pass it on: the next superstep reads this parity)
+      return true;
     }
-  }
-  if (!kOwner && blockIdx.x == 0 && tid == 0) {  // the cursors the NEXT superstep uses (as k_bucket_apply's fused launch)
-    if (a.dense_left) a.dense_left[rpar] = 0u;
-    g.ovf[rpar] = 0u;
-    a.skew_n[rpar] = 0u;
-    if (g.heap_top) g.heap_top[rpar] = 0u;
-  }
+    if (!kOwner && blockIdx.x == 0 && tid == 0) {  // the cursors the NEXT superstep uses (as k_bucket_apply's fused launch)
+      if (a.dense_left) a.dense_left[rpar] = 0u;
+      g.ovf[rpar] = 0u;
+      a.skew_n[rpar] = 0u;
+      if (g.heap_top) g.heap_top[rpar] = 0u;
+    }
+    return false;
+  };
+  if (!kEarlyRow && abort_test()) return;
   constexpr bool kKindNeeded = (KM & (KM - 1)) != 0 || (KM & kb(AGX_KIND_COMPILED)) != 0;
   const uint32_t w1off = P.W > 1 ? P.sw : 0u;
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};
   if (tid == 0) s_bad = 0;
-  for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x) {
+  // one bucket's superstep; true = the replay is void (return).  With a grid of >= nb blocks (the
+  // fused launch: nb <= kDenseThreads) it runs once, outside a loop: the waitcnt pass then has no back
+  // edge whose pending loads it must assume, and the row / flag / state loads issue back to back
+  const auto bucket = [&](const uint32_t b) -> bool {
     AGX_STAMP(a, 0);
     const uint32_t a0 = b << a.bb, na = min(1u << a.bb, P.n_local - a0);
     uint32_t* const segp = reinterpret_cast<uint32_t*>(U);  // [nseg + 1] inbox start of each tell segment
@@ -2932,29 +2946,39 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     // ---- the bucket's row of the tell tables (sender bucket c = tid) and, in the same round trip,
     // this thread's actors' flags, kind and state words
     uint32_t v = 0, o = 0;
-    uint32_t* my_tc = nullptr;
+    uint32_t* tc = nullptr;  // (the row entry, cleared when consumed: tested on v there, not here -- no wait)
     // (owner: the inbox is the bucket's range of the sorted input, backlog included)
     const uint32_t ib = kOwner ? a.bstart[b] : 0u, ie = kOwner ? a.bstart[b + 1] : 0u;
     if (!kOwner && tid < a.nb) {
-      uint32_t* tc = g.tcnt[rpar] + (size_t)b * g.tstride + tid;
+      tc = g.tcnt[rpar] + (size_t)b * g.tstride + tid;
       v = *tc;
       o = g.toff[rpar][(size_t)b * g.tstride + tid];
-      if (v) my_tc = tc;
+    }
+    // (the bucket's backlog / staged counts: issued before the state loads, so waiting for them
+    // does not wait for those)
+    uint32_t blc0 = 0u, stg0 = 0u;
+    if (!kOwner && tid == 0) {
+      blc0 = g.blc[rpar][b];
+      stg0 = g.stg_cnt[b];
     }
     uint32_t ab[kDenseIpt], kd[kDenseIpt], gs[kDenseIpt];
     uint64_t x0[kDenseIpt], x1[kDenseIpt];
 #pragma unroll
     for (int r = 0; r < kDenseIpt; ++r) {
       const uint32_t la = r * kDenseThreads + tid, l = a0 + (la < na ? la : 0u);
-      ab[r] = la < na ? P.alive[l] : 0u;
+      ab[r] = P.alive[l];  // (l clamped: unconditional, so no wait between the loads; la >= na is skipped below)
       kd[r] = kKindNeeded ? P.kind[l] : 0u;
       gs[r] = kOwner ? P.gid[l] : l;  // the actor's global id (its tells' sender)
       x0[r] = ldg64(P.state, l * P.sa);
-      x1[r] = P.W > 1 ? ldg64(P.state, l * P.sa + w1off) : 0ull;
+      x1[r] = ldg64(P.state, l * P.sa + w1off);  // (W = 1: word 0 again, zeroed at the apply; no branch between loads)
+    }
+    if (!tested) {  // (uniform; first bucket of the block)
+      tested = true;
+      if (abort_test()) return true;
     }
     if (tid == 0) {
-      s_g[0] = kOwner ? 0u : g.blc[rpar][b];
-      s_g[1] = kOwner ? 0u : g.stg_cnt[b];
+      s_g[0] = blc0;
+      s_g[1] = stg0;
       s_dmin = 0xFFFFFFFFu;  // (the min / max digit of the bucket's tells to other buckets, below)
       s_dmax = 0u;
     }
@@ -2971,7 +2995,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
         if (a.dense_alone) a.abort[wpar] = a.slot + 1u;  // strict replay: the rest of it is void (run_single recovers)
       }
       __syncthreads();  // (s_g is rewritten by the next bucket)
-      continue;
+      return false;
     }
     if (!kOwner) {
       if (v) {
@@ -3028,9 +3052,9 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
         if (a.dense_left) a.dense_left[wpar] = 1u;
         if (a.dense_alone) a.abort[wpar] = a.slot + 1u;
       }
-      continue;
+      return false;
     }
-    if (my_tc) *my_tc = 0u;  // row consumed
+    if (v) *tc = 0u;  // row consumed
     // (fused: cnt <= kBucket = region, the bucket's own inbox region; owner: its sorted range)
     const uint32_t lo = kOwner ? ib : b * g.region;
     if (tid == 0) {  // nothing queued: the bucket's backlog is empty
@@ -3057,7 +3081,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
         continue;
       }
       RegEmitter em{&P, gs[r], 0u, 0u, 0u, 0u};
-      uint64_t wv2[2] = {x0[r], x1[r]};
+      uint64_t wv2[2] = {x0[r], P.W > 1 ? x1[r] : 0ull};
       uint32_t kc = kd[r];
       ++acc[4];
       ++acc[0];
@@ -3158,6 +3182,13 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     }
     __syncthreads();  // (the bucket's LDS arrays are reset by the next one)
     AGX_STAMP(a, 8);
+    return false;
+  };
+  if (gridDim.x >= a.nb) {
+    if (blockIdx.x < a.nb && bucket(blockIdx.x)) return;
+  } else {
+    for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x)
+      if (bucket(b)) return;
   }
   if (blockIdx.x < a.nb) flush_stats(a, acc);
 }
