@@ -3070,12 +3070,24 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     // ---- apply, actor order (one message per actor: admitted, drained; to a stopped actor: a dead letter)
     uint32_t tk[kDenseIpt], tp[kDenseIpt];
     bool tv[kDenseIpt];
+    // every actor's hit count, sender and payload in one LDS round trip (la < kBucket: in bounds)
+    uint32_t hv[kDenseIpt], svv[kDenseIpt], pvv[kDenseIpt];
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r) {
+      const uint32_t la = r * kDenseThreads + tid;
+      hv[r] = s_hit[la];
+      svv[r] = s_ks[la];
+      pvv[r] = s_ks[kBucket + la];
+    }
+#pragma unroll
+    for (int r = 0; r < kDenseIpt; ++r)  // (pinned here: the compiler would sink each read into its use, one wait each)
+      asm volatile("" : "+v"(hv[r]), "+v"(svv[r]), "+v"(pvv[r]));
 #pragma unroll
     for (int r = 0; r < kDenseIpt; ++r) {
       const uint32_t la = r * kDenseThreads + tid, l = a0 + la;
       tv[r] = false;
       tk[r] = tp[r] = 0u;
-      if (la >= na || !s_hit[la]) continue;
+      if (la >= na || !hv[r]) continue;
       if (!(ab[r] & 1u)) {
         ++acc[1];
         continue;
@@ -3085,7 +3097,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
       uint32_t kc = kd[r];
       ++acc[4];
       ++acc[0];
-      const uint32_t res = apply_msg<KM>(P, kc, gs[r], l, wv2, s_ks[la], s_ks[kBucket + la], em);
+      const uint32_t res = apply_msg<KM>(P, kc, gs[r], l, wv2, svv[r], pvv[r], em);
       if (res == AGX_RES_UNHANDLED) ++acc[2];
       if (res == AGX_RES_STOPPED) {
         if constexpr (kOwner) P.stopq[atomicAdd(P.nstop, 1u)] = l;  // (committed by the next superstep)
