@@ -19,7 +19,7 @@ import pathlib
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 P = ROOT / "profiles" / "r05" / "pmc"
-FUSED = "agx::k_dense_fused<4u>"
+FUSED = "agx::k_dense_fused<4u, false>"  # (round-5 final tree: the owner flag in the name)
 BYPASS = "agx::k_dense_apply<4u>"
 
 
