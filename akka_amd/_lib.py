@@ -96,6 +96,8 @@ SIGNATURES = {
     "agx_tell": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.POINTER(ctypes.c_int32)]),
     "agx_pump_idle": (ctypes.c_int32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]),
+    "agx_pump_cancel": (ctypes.c_int32, [ctypes.c_void_p]),
+    "agx_build_hash": (ctypes.c_char_p, []),
     "agx_run": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(AgxStats)]),
     "agx_get_stats": (ctypes.c_int32, [ctypes.c_void_p, ctypes.POINTER(AgxStats)]),
     "agx_identity_supersteps": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
@@ -122,7 +124,7 @@ SIGNATURES = {
 
 
 # entry points newer than some A/B diagnostic builds (tools/build_variant.sh of an older checkout)
-OPTIONAL = {"agx_tell", "agx_pump_idle", "agx_exchange_info", "agx_run_timed"}
+OPTIONAL = {"agx_tell", "agx_pump_idle", "agx_pump_cancel", "agx_exchange_info", "agx_run_timed", "agx_build_hash"}
 
 
 def load():

@@ -274,6 +274,10 @@ struct agx_engine {
   std::vector<uint32_t> hs_key, hs_src, hs_pay;
   uint32_t n_staged_dev = 0;  // staged tells uploaded for the next step
   uint64_t staged_total = 0, staged_dead = 0;
+  uint64_t inflight_dev = 0;    // the device's in-flight count when inflight_known (agx_stage_tells' check)
+  bool inflight_known = false;  // inflight_dev is current (cleared by every agx_run)
+  bool last_run_ok = false;     // the last agx_run returned AGX_OK (agx_pump_idle's in-flight reschedule)
+  bool tev1_recorded = false;   // agx_run_timed: run_single recorded the end event
 
   ncclComm_t comm = nullptr;
   bool started = false;
@@ -1192,6 +1196,8 @@ agx_status error_status(const agx_engine* e, uint64_t err) {
 agx_status collect_stats(agx_engine* e, agx_stats* out, bool check) {
   uint64_t s[kStatBlk];
   AGX_TRY(read_counters(e, s));
+  e->inflight_dev = s[kStatInfl];  // (exact until the next agx_run: agx_stage_tells' capacity check)
+  e->inflight_known = true;
   const agx_status est = check ? error_status(e, s[ST_ERROR]) : AGX_OK;
   const uint64_t* bs = s + kStatSred;
   agx_stats st{};
@@ -1491,7 +1497,10 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
     launched_steps += cnt;
     hipEventRecord(ev[slot], e->stream);
   }
-  if (e->timing) hipEventRecord(e->tev[1], e->stream);  // (agx_run_timed: after the last replay, before the sync)
+  if (e->timing) {  // (agx_run_timed: after the last replay, before the sync)
+    hipEventRecord(e->tev[1], e->stream);
+    e->tev1_recorded = true;
+  }
   // the kernels' error word rides on the final sync (agx_run checks it even when out == NULL): in the
   // last replay's ring row (k_replay_out) when a fused replay ended the run, else copied back
   if (last_ring < 0) hipMemcpyAsync(e->h_stat + ST_ERROR, e->d_stats + ST_ERROR, 8, hipMemcpyDeviceToHost, e->stream);
@@ -1584,15 +1593,21 @@ agx_status mr_slabs(agx_engine* e, uint64_t want) {
   e->d_sslab = e->d_rslab = nullptr;
   e->slab = 0;
   drop_graphs(e);  // (the slabs are kernel and collective arguments of a captured replay)
-  AGX_TRY(dalloc(&e->d_sslab, (uint64_t)e->R * n * 3));
-  AGX_TRY(dalloc(&e->d_rslab, (uint64_t)e->R * n * 3));
+  // this rank's verdict: 0 = the slabs fit, 1 = the envelope slabs fit but the CRDT row slabs do not
+  // (host-planned exchange from now on), 2 = an allocation the exchange cannot do without failed.
+  // No rank returns before the all-gather below: a rank that left early would leave its peers
+  // blocked in the collective (every rank must take the same decision, from the same answers).
+  uint64_t code = 0;
+  if (dalloc(&e->d_sslab, (uint64_t)e->R * n * 3) != AGX_OK || dalloc(&e->d_rslab, (uint64_t)e->R * n * 3) != AGX_OK)
+    code = 2;
   if (e->pw) {  // CRDT rows: row send slabs, and rx large enough to receive R slabs of rows
     const uint64_t rr = (uint64_t)e->R * n;
     const char* mb = getenv("AGX_MR_ROW_MB");
     const uint64_t budget = (mb ? (uint64_t)std::max(0, atoi(mb)) : 16384ull) << 20;
     hipFree(e->d_srows);
     e->d_srows = nullptr;
-    bool fits = e->heap_rows + std::max<uint64_t>(rr, e->rx_rows) < kHandleMask && 2 * rr * e->pw * 4 <= budget;
+    bool fits = code == 0 && e->heap_rows + std::max<uint64_t>(rr, e->rx_rows) < kHandleMask &&
+                2 * rr * e->pw * 4 <= budget;
     if (fits && dalloc(&e->d_srows, rr * e->pw) != AGX_OK) fits = false;
     if (fits && rr > e->rx_rows) {
       hipFree(e->d_rx);
@@ -1602,28 +1617,40 @@ agx_status mr_slabs(agx_engine* e, uint64_t want) {
       } else {  // (the host-planned path needs rx of cap rows again)
         fits = false;
         e->rx_rows = 0;
-        AGX_TRY(dalloc(&e->d_rx, e->cap * e->pw));
-        e->rx_rows = e->cap;
+        if (dalloc(&e->d_rx, e->cap * e->pw) == AGX_OK)
+          e->rx_rows = e->cap;
+        else
+          code = 2;
       }
     }
-    (void)hipGetLastError();  // (a refused allocation is an answer here, not an error)
-    set_err(AGX_OK, "");
-    // every rank's verdict (the exchange sizes must agree)
-    e->h_pin64[0] = fits ? 1u : 0u;
-    HIP_TRY(hipMemcpyAsync(e->d_cvec, e->h_pin64, 8, hipMemcpyHostToDevice, e->stream));
-    NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, 1, ncclUint64, e->comm, e->stream));
-    HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_cmat, (size_t)e->R * 8, hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
-    bool all = true;
-    for (uint32_t r = 0; r < e->R; ++r) all = all && e->h_pin64[r] != 0;
-    if (!all) {
-      hipFree(e->d_srows);
-      e->d_srows = nullptr;
-      e->mr_host = true;
-      if (getenv("AGX_MR_DEBUG"))
-        fprintf(stderr, "[agx rank %u] CRDT row slabs of %u rows per peer do not fit on every rank: host-planned "
-                "exchange\n", e->rank, n);
-    }
+    if (!fits && code == 0) code = 1;
+  }
+  (void)hipGetLastError();  // (a refused allocation is an answer here, not an error)
+  set_err(AGX_OK, "");
+  // every rank's verdict (the exchange sizes must agree)
+  e->h_pin64[0] = code;
+  HIP_TRY(hipMemcpyAsync(e->d_cvec, e->h_pin64, 8, hipMemcpyHostToDevice, e->stream));
+  NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, 1, ncclUint64, e->comm, e->stream));
+  HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_cmat, (size_t)e->R * 8, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  uint64_t worst = 0;
+  for (uint32_t r = 0; r < e->R; ++r) worst = std::max<uint64_t>(worst, e->h_pin64[r]);
+  if (worst >= 2) {  // every rank fails alike
+    hipFree(e->d_sslab);
+    hipFree(e->d_rslab);
+    hipFree(e->d_srows);
+    e->d_sslab = e->d_rslab = nullptr;
+    e->d_srows = nullptr;
+    return set_err(AGX_ENOMEM, "rank %u: exchange slabs of %u envelopes per peer could not be allocated on %s",
+                   e->rank, n, code >= 2 ? "this rank" : "a peer rank");
+  }
+  if (worst == 1) {
+    hipFree(e->d_srows);
+    e->d_srows = nullptr;
+    e->mr_host = true;
+    if (getenv("AGX_MR_DEBUG"))
+      fprintf(stderr, "[agx rank %u] CRDT row slabs of %u rows per peer do not fit on every rank: host-planned "
+              "exchange\n", e->rank, n);
   }
   e->slab = n;
   return AGX_OK;
@@ -1785,7 +1812,19 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
   // device-resident replays (CRDT rows travel in row slabs beside the envelope slabs); a staged
   // burst enters through one host-planned superstep (its staged count is a host number)
   const bool dev = !getenv("AGX_MR_HOST") && !e->mr_host;
-  if (dev && e->n_staged_dev && left) {
+  // whether ANY rank has staged tells: each rank knows only its own, and a rank that took the
+  // host-planned superstep below while a peer went straight to the device replays would issue
+  // different collectives than that peer (one all-gather per run, not per superstep)
+  bool any_staged = e->n_staged_dev != 0;
+  if (dev && left) {
+    e->h_pin64[0] = e->n_staged_dev;
+    HIP_TRY(hipMemcpyAsync(e->d_cvec, e->h_pin64, 8, hipMemcpyHostToDevice, e->stream));
+    NCCL_TRY(ncclAllGather(e->d_cvec, e->d_cmat, 1, ncclUint64, e->comm, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->h_pin64, e->d_cmat, (size_t)e->R * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (uint32_t r = 0; r < e->R; ++r) any_staged = any_staged || e->h_pin64[r] != 0;
+  }
+  if (dev && any_staged && left) {
     AGX_TRY(host_step(&quiet));
     ++e->mr_host_steps;
     --left;
@@ -1931,6 +1970,14 @@ extern "C" {
 
 const char* agx_last_error(void) { return g_err.c_str(); }
 uint32_t agx_abi_version(void) { return AGX_ABI_VERSION; }
+
+// The source hash this library was built from (__graft_entry__.source_hash, passed by build_native);
+// the stamp is found in the file's bytes without loading it, so a stale library is rebuilt.
+#ifndef AGX_BUILD_HASH
+#define AGX_BUILD_HASH "unstamped000000"
+#endif
+extern "C" __attribute__((used, visibility("default"))) const char agx_build_stamp[] = "AGX_BUILD_HASH=" AGX_BUILD_HASH;
+const char* agx_build_hash(void) { return agx_build_stamp + 15; }
 
 int32_t agx_shard_id(uint32_t id, uint32_t num_shards) {
   if (num_shards == 0 || num_shards > (uint32_t)INT32_MAX) return 0;  // (maxNumberOfShards is an Int)
@@ -2624,10 +2671,32 @@ agx_status agx_set_graph_rmat(agx_engine* e, const uint64_t* row_ptr, uint32_t b
   return AGX_OK;
 }
 
+// Host tells.  All or nothing: the tells are validated and counted before any is staged, so an
+// AGX_EINVAL or AGX_ECAPACITY leaves the engine exactly as it was (no tell staged, no counter moved).
+// Capacity: the messages in flight after staging -- the device's backlog and undelivered tells, the
+// staged tells not yet consumed, and these -- must fit msg_capacity, or the first superstep's inbox
+// would overflow its arenas.
+agx_status in_flight_now(agx_engine* e, uint64_t* out);
 agx_status agx_stage_tells(agx_engine* e, const uint32_t* dst, const uint32_t* src, const uint32_t* payload, size_t n) {
   if (!e || (n && (!dst || !payload))) return set_err(AGX_EINVAL, "bad tells");
+  uint64_t take = 0;  // tells this rank stages (unknown refs are dead letters, other ranks' tells ignored)
   for (size_t i = 0; i < n; ++i) {
-    uint32_t d = dst[i];
+    const uint32_t d = dst[i];
+    if (d >= e->n_global || (e->R > 1 && (e->h_route[d] >> kOwnerShift) != e->rank)) continue;
+    const uint32_t sv = src ? src[i] : AGX_NO_SENDER;
+    if ((sv & AGX_WIDE_BIT) && sv != AGX_NO_SENDER)
+      return set_err(AGX_EINVAL, "tell %zu: sender %u is not an actor id (bit 31 tags CRDT state gossips)", i, sv);
+    ++take;
+  }
+  if (take) {
+    uint64_t infl = 0;
+    AGX_TRY(in_flight_now(e, &infl));
+    if (infl + take > e->cap)
+      return set_err(AGX_ECAPACITY, "%llu staged tells do not fit: %llu messages in flight, msg_capacity %llu "
+                     "(nothing staged)", (unsigned long long)take, (unsigned long long)infl, (unsigned long long)e->cap);
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t d = dst[i];
     if (d >= e->n_global) {  // unknown ref -> deadLetters (counted once, on rank 0)
       if (e->rank == 0) { e->staged_total++; e->staged_dead++; }
       continue;
@@ -2638,27 +2707,57 @@ agx_status agx_stage_tells(agx_engine* e, const uint32_t* dst, const uint32_t* s
       if ((r >> kOwnerShift) != e->rank) continue;
       key = r;
     }
-    const uint32_t sv = src ? src[i] : AGX_NO_SENDER;
-    if ((sv & AGX_WIDE_BIT) && sv != AGX_NO_SENDER)
-      return set_err(AGX_EINVAL, "tell %zu: sender %u is not an actor id (bit 31 tags CRDT state gossips)", i, sv);
     e->staged_total++;
     e->hs_key.push_back(key);
-    e->hs_src.push_back(sv);
+    e->hs_src.push_back(src ? src[i] : AGX_NO_SENDER);
     e->hs_pay.push_back(payload[i]);
   }
-  if (e->hs_key.size() + e->n_staged_dev > e->cap) return set_err(AGX_ECAPACITY, "too many staged tells");
   return AGX_OK;
 }
 
-// the lock-free tell path: take every tell published so far (producer by producer, each in its
-// order) into the host staging, exactly as agx_stage_tells would have staged them
+// Messages in flight on this rank right now (what agx_stats.in_flight would report): the device's
+// backlog, undelivered tells and consumed-later staged chunks (one counter read-back, only once the
+// engine has run), plus the host-staged tells not yet uploaded.
+agx_status in_flight_now(agx_engine* e, uint64_t* out) {
+  uint64_t dev = 0;
+  if (e->started) {
+    if (e->inflight_known) {
+      dev = e->inflight_dev;
+    } else {
+      uint64_t s[kStatBlk];
+      AGX_TRY(read_counters(e, s));
+      dev = s[kStatInfl];
+      e->inflight_dev = dev;
+      e->inflight_known = true;  // (valid until the next agx_run)
+    }
+  }
+  *out = dev + e->n_staged_dev + e->hs_key.size();
+  return AGX_OK;
+}
+
+// The lock-free tell path: take the published tells (producer by producer, each in its order) into
+// the host staging, exactly as agx_stage_tells would stage them -- but only as many as fit the
+// message capacity.  The rest stay in the producers' queues (none is refused or lost: the
+// reference's unbounded MPSC queue never refuses, AbstractNodeQueue.java:79-82) and
+// agx_pump_idle reschedules the pump while any remain, so a burst larger than msg_capacity enters
+// over several pumps as the engine drains (back-pressure across pumps).
 agx_status take_tells(agx_engine* e) {
-  agx_status st = AGX_OK;
-  e->tq.take([&](uint32_t d, uint32_t s, uint32_t p) {
+  if (!e->tq.pending()) return AGX_OK;
+  uint64_t infl = 0;
+  AGX_TRY(in_flight_now(e, &infl));
+  uint64_t room = e->cap > infl ? e->cap - infl : 0;
+  e->tq.take_while([&](uint32_t d, uint32_t s, uint32_t p) {
+    const bool local = d < e->n_global && (e->R == 1 || (e->h_route[d] >> kOwnerShift) == e->rank);
+    if (local) {
+      if (!room) return false;  // stays queued for the next pump
+      --room;
+    }
+    // (agx_tell rejected wide senders already; unknown refs and other ranks' tells take no room)
     const agx_status r = agx_stage_tells(e, &d, &s, &p, 1);
-    if (r != AGX_OK && st == AGX_OK) st = r;
+    (void)r;
+    return true;
   });
-  return st;
+  return AGX_OK;
 }
 
 agx_status agx_tell(agx_engine* e, uint32_t dst, uint32_t src, uint32_t payload, int32_t* schedule) {
@@ -2670,17 +2769,37 @@ agx_status agx_tell(agx_engine* e, uint32_t dst, uint32_t src, uint32_t payload,
   return AGX_OK;
 }
 
+// The pump's last call (Mailbox.run's finally, Mailbox.scala:227-240: setAsIdle, then
+// registerForExecution if the mailbox still has messages).  "Still has messages" is, here, either
+// tells published but not taken (the queue re-check after the idle store) or mail in flight on the
+// device after a run that stopped at its superstep budget (gpu.supersteps-per-pump) -- then the
+// engine stays scheduled and the pump is submitted again.  After a failed run only the queue
+// re-check applies (a broken engine must not spin its pump).
 agx_status agx_pump_idle(agx_engine* e, int32_t* reschedule) {
   if (!e) return set_err(AGX_EINVAL, "null engine");
-  const bool again = e->tq.pump_idle();
+  bool again = false;
+  if (e->last_run_ok && e->started) {
+    uint64_t infl = 0;
+    AGX_TRY(in_flight_now(e, &infl));
+    again = infl > 0;  // (status stays "scheduled": this pump hands over to the next)
+  }
+  if (!again) again = e->tq.pump_idle();
   if (reschedule) *reschedule = again ? 1 : 0;
+  return AGX_OK;
+}
+
+agx_status agx_pump_cancel(agx_engine* e) {
+  if (!e) return set_err(AGX_EINVAL, "null engine");
+  e->tq.cancel_schedule();
   return AGX_OK;
 }
 
 agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
   if (!e) return set_err(AGX_EINVAL, "null engine");
+  e->last_run_ok = false;
   AGX_TRY(ensure_dev(e));
   AGX_TRY(take_tells(e));
+  e->inflight_known = false;  // (the supersteps below change the device's in-flight count)
   if (e->R > 1 && !e->comm) return set_err(AGX_ESTATE, "n_ranks > 1 needs agx_comm_init (or agx_group_run)");
   AGX_TRY(prepare_run(e));
   AGX_TRY(setup_rings(e));
@@ -2736,7 +2855,9 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
   }
   // out == NULL: no counter read-back (one stream round trip less; agx_get_stats reads them
   // later), but the error word came back with the run's final sync
-  return out ? collect_stats(e, out, true) : error_status(e, e->h_stat[ST_ERROR]);
+  const agx_status rs = out ? collect_stats(e, out, true) : error_status(e, e->h_stat[ST_ERROR]);
+  e->last_run_ok = rs == AGX_OK;
+  return rs;
 }
 
 agx_status agx_identity_supersteps(agx_engine* e, uint64_t* out) {
@@ -2769,10 +2890,13 @@ agx_status agx_run_timed(agx_engine* e, uint32_t max_supersteps, agx_stats* out,
     if (!ev) HIP_TRY(hipEventCreate(&ev));
   HIP_TRY(hipEventRecord(e->tev[0], e->stream));
   e->timing = e->R == 1;
+  e->tev1_recorded = false;
   const agx_status st = agx_run(e, max_supersteps, out);
   e->timing = false;
   if (st != AGX_OK) return st;
-  if (e->R > 1) hipEventRecord(e->tev[1], e->stream);
+  // multi-rank, and a single-rank run that launched nothing through the replay loop (agx_run(0)
+  // captures graphs and returns before it): the end event is recorded here, after the run's work
+  if (!e->tev1_recorded) HIP_TRY(hipEventRecord(e->tev[1], e->stream));
   HIP_TRY(hipEventSynchronize(e->tev[1]));
   HIP_TRY(hipEventElapsedTime(device_ms, e->tev[0], e->tev[1]));
   return st;
@@ -2853,6 +2977,7 @@ agx_status agx_group_run(agx_engine** engs, uint32_t n, uint32_t max_steps, agx_
     AGX_TRY(prepare_run(engs[i]));
     AGX_TRY(setup_orset(engs[i]));
     engs[i]->started = true;
+    engs[i]->inflight_known = false;
   }
   const uint32_t S = n + 2;
   std::vector<uint64_t> mat((size_t)n * S);

@@ -83,18 +83,31 @@ class TellQueue {
   // consumer (the pump thread): every published tell, producer by producer, each in its order
   template <typename F>
   void take(F&& f) {
-    for (TellProducer* p = producers_.load(std::memory_order_acquire); p; p = p->link) {
-      for (;;) {
-        TellSeg* s = p->rseg;
-        const uint32_t t = s->tail.load(std::memory_order_acquire);
-        for (uint32_t i = s->head; i < t; ++i) f(s->dst[i], s->src[i], s->pay[i]);
-        s->head = t;
-        TellSeg* n = t == TellSeg::kCap ? s->next.load(std::memory_order_acquire) : nullptr;
-        if (!n) break;
-        p->rseg = n;  // the producer has moved on: it never touches s again
-        delete s;
-      }
-    }
+    take_while([&](uint32_t d, uint32_t s, uint32_t p) {
+      f(d, s, p);
+      return true;
+    });
+  }
+
+  // consumer, bounded: offers published tells to f in order (per producer) and stops at the first one
+  // f refuses -- that tell and everything after it stay queued for a later take (back-pressure, not
+  // loss: an unbounded mailbox never refuses an enqueue, AbstractNodeQueue.java:79-82).  The next
+  // take starts at the producer this one stopped at, so a refusing pump serves the producers round
+  // robin instead of starving the ones at the end of the registry.  Returns false iff f refused.
+  template <typename F>
+  bool take_while(F&& f) {
+    TellProducer* const head = producers_.load(std::memory_order_acquire);
+    TellProducer* const first = resume_ ? resume_ : head;
+    resume_ = nullptr;
+    // first .. end of the registry, then head .. first (producers are only ever pushed at the head,
+    // so `first` stays reachable and every producer is visited once)
+    for (int pass = 0; pass < 2; ++pass)
+      for (TellProducer* p = pass ? head : first; p && !(pass && p == first); p = p->link)
+        if (!take_one(p, f)) {
+          resume_ = p;
+          return false;
+        }
+    return true;
   }
 
   // tells published and not taken (the pump's re-check; agx_pump_idle)
@@ -107,12 +120,33 @@ class TellQueue {
     return false;
   }
   bool scheduled() const { return status_.load() != 0; }
+  // the pump could not be submitted (the executor rejected it): back to idle WITHOUT the re-check,
+  // so the next tell schedules again (Dispatcher.registerForExecution's catch: setAsIdle, rethrow,
+  // Dispatcher.scala:130-138)
+  void cancel_schedule() { status_.store(0, std::memory_order_seq_cst); }
 
  private:
   bool try_schedule() {
     uint32_t idle = 0;
     return status_.load(std::memory_order_seq_cst) == 0 &&
            status_.compare_exchange_strong(idle, 1u, std::memory_order_seq_cst);
+  }
+  template <typename F>
+  bool take_one(TellProducer* p, F& f) {
+    for (;;) {
+      TellSeg* s = p->rseg;
+      const uint32_t t = s->tail.load(std::memory_order_acquire);
+      for (uint32_t i = s->head; i < t; ++i)
+        if (!f(s->dst[i], s->src[i], s->pay[i])) {
+          s->head = i;
+          return false;
+        }
+      s->head = t;
+      TellSeg* n = t == TellSeg::kCap ? s->next.load(std::memory_order_acquire) : nullptr;
+      if (!n) return true;
+      p->rseg = n;  // the producer has moved on: it never touches s again
+      delete s;
+    }
   }
   // this thread's producer for this queue (registered on its first tell)
   TellProducer* mine() {
@@ -135,6 +169,7 @@ class TellQueue {
   const uint64_t id_;
   std::atomic<TellProducer*> producers_{nullptr};
   std::atomic<uint32_t> status_{0};  // 0 idle, 1 scheduled
+  TellProducer* resume_ = nullptr;    // consumer only: where the last refused take stopped
 };
 
 }  // namespace agx

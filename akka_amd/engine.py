@@ -231,10 +231,15 @@ class GpuEngine:
         return bool(sched.value)
 
     def pump_idle(self) -> bool:
-        """agx_pump_idle (the pump's last call): True iff tells arrived meanwhile (submit again)."""
+        """agx_pump_idle (the pump's last call): True iff the pump must be submitted again -- tells
+        arrived meanwhile or wait for capacity, or the last run left mail in flight."""
         again = ctypes.c_int32(0)
         check(self.lib.agx_pump_idle(self._h, ctypes.byref(again)))
         return bool(again.value)
+
+    def pump_cancel(self) -> None:
+        """agx_pump_cancel: the pump could not be submitted; back to idle without the re-check."""
+        check(self.lib.agx_pump_cancel(self._h))
 
     def run(self, max_supersteps: int = 1 << 30, stats: bool = True) -> Stats | None:
         """agx_run.  stats=False skips the counter read-back (read them with stats())."""

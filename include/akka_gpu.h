@@ -254,6 +254,9 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out);
 agx_status agx_destroy(agx_engine* eng);
 const char* agx_last_error(void);
 uint32_t agx_abi_version(void);
+/* 16 hex digits: the hash of the sources this library was built from (a build check, no
+ * reference counterpart; __graft_entry__.source_hash computes the same over csrc/ and this header) */
+const char* agx_build_hash(void);
 
 /* --- actor registration (actorOf for a contiguous id range) --------------- */
 /* init_state: count x state_stride bytes, actor-major, n_words u64 used per actor
@@ -293,7 +296,10 @@ agx_status agx_set_graph_rmat(agx_engine* eng, const uint64_t* row_ptr, uint32_t
 
 /* --- tell / run ------------------------------------------------------------- */
 /* Host tells (caller-owned buffers, copied).  src may be AGX_NO_SENDER.
- * Tells whose dst is not owned by this rank are ignored on this rank.        */
+ * Tells whose dst is not owned by this rank are ignored on this rank.
+ * All or nothing: AGX_EINVAL (a tagged sender) or AGX_ECAPACITY (the tells would take the
+ * messages in flight on this rank past msg_capacity) stages none of them and leaves every
+ * counter unchanged -- run the engine to drain it and stage again.                              */
 agx_status agx_stage_tells(agx_engine* eng, const uint32_t* dst, const uint32_t* src,
                            const uint32_t* payload, size_t n);
 /* The lock-free tell path (ActorRef.! from any thread; the reference: one getAndSet enqueue,
@@ -304,11 +310,20 @@ agx_status agx_stage_tells(agx_engine* eng, const uint32_t* dst, const uint32_t*
  * order; the next agx_run takes them as agx_stage_tells would).  *schedule = 1 iff this tell moved
  * the engine from idle to scheduled: the caller then submits ONE pump task (a task that calls
  * agx_run and then agx_pump_idle); N tells to an idle engine submit one.  agx_pump_idle is the
- * pump's last call (Mailbox.run's finally: setAsIdle, then registerForExecution): *reschedule = 1
- * iff tells arrived after the pump's last agx_run -- submit the pump again.  (src may be
- * AGX_NO_SENDER; schedule / reschedule may be NULL.)                          */
+ * pump's last call (Mailbox.run's finally: setAsIdle, then registerForExecution if the mailbox
+ * still has messages, Mailbox.scala:227-240): *reschedule = 1 iff tells arrived after the pump's
+ * last agx_run, or tells are still queued because they did not fit the message capacity, or the
+ * last agx_run succeeded and left mail in flight (a superstep budget) -- submit the pump again.
+ * Tells are never refused or lost at capacity: agx_run takes only as many queued tells as fit
+ * msg_capacity beside the mail already in flight, the rest wait in the queue for a later pump
+ * (back-pressure, as an unbounded MPSC mailbox never refuses an enqueue, AbstractNodeQueue.java:
+ * 79-82; a bounded mailbox class still tail-drops at its own capacity).  agx_pump_cancel: the pump
+ * could not be submitted (the executor rejected it): the engine goes back to idle without the
+ * re-check, so the next tell schedules it again (Dispatcher.registerForExecution's catch,
+ * Dispatcher.scala:130-138).  (src may be AGX_NO_SENDER; schedule / reschedule may be NULL.)  */
 agx_status agx_tell(agx_engine* eng, uint32_t dst, uint32_t src, uint32_t payload, int32_t* schedule);
 agx_status agx_pump_idle(agx_engine* eng, int32_t* reschedule);
+agx_status agx_pump_cancel(agx_engine* eng);
 /* Run up to max_supersteps supersteps or until quiescent; stats are cumulative
  * over the engine's lifetime.  out may be NULL: the counters are then not read
  * back (agx_get_stats does it later, and reports AGX_ECAPACITY if an overflow

@@ -226,6 +226,12 @@ JNIEXPORT jboolean JNICALL Java_akka_dispatch_gpu_AgxJni_pumpIdle(JNIEnv* env, j
   return again ? JNI_TRUE : JNI_FALSE;
 }
 
+/* agx_pump_cancel: the executor rejected the pump -- back to idle, no re-check */
+JNIEXPORT void JNICALL Java_akka_dispatch_gpu_AgxJni_pumpCancel(JNIEnv* env, jclass k, jlong eng) {
+  (void)k;
+  raise(env, agx_pump_cancel(ENG(eng)));
+}
+
 JNIEXPORT void JNICALL Java_akka_dispatch_gpu_AgxJni_stageTells(JNIEnv* env, jclass k, jlong eng, jobject dst,
                                                                 jobject src, jobject pay, jint n) {
   (void)k;

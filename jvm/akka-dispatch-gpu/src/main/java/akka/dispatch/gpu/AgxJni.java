@@ -69,6 +69,9 @@ public final class AgxJni {
   /** agx_pump_idle: the pump's last call; true iff tells arrived meanwhile (submit the pump again). */
   public static native boolean pumpIdle(long engine);
 
+  /** agx_pump_cancel: the executor rejected the pump; back to idle without the re-check. */
+  public static native void pumpCancel(long engine);
+
   public static native void run(long engine, int maxSupersteps, long[] stats);
 
   public static native void getStats(long engine, long[] stats);

@@ -59,6 +59,7 @@ object AgxNative {
     h("agx_stage_tells", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG))
   val tell: MethodHandle = h("agx_tell", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT, JAVA_INT, ADDRESS))
   val pumpIdle: MethodHandle = h("agx_pump_idle", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS))
+  val pumpCancel: MethodHandle = h("agx_pump_cancel", FunctionDescriptor.of(JAVA_INT, ADDRESS))
   val run: MethodHandle = h("agx_run", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, ADDRESS))
   val getStats: MethodHandle = h("agx_get_stats", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS))
   val readState: MethodHandle =
@@ -167,6 +168,7 @@ object PanamaBackend extends AgxBackend {
     check(AgxNative.pumpIdle.invokeExact(seg(engine), f).asInstanceOf[Int])
     f.get(JAVA_INT, 0) != 0
   }
+  def pumpCancel(engine: Long): Unit = check(AgxNative.pumpCancel.invokeExact(seg(engine)).asInstanceOf[Int])
   def run(engine: Long, maxSupersteps: Int, stats: Array[Long]): Unit = {
     val a = Arena.ofConfined()
     try {

@@ -27,6 +27,8 @@ trait AgxBackend {
   def tell(engine: Long, dst: Int, src: Int, payload: Int): Boolean
   /** agx_pump_idle (the pump's last call): true iff tells arrived meanwhile */
   def pumpIdle(engine: Long): Boolean
+  /** agx_pump_cancel (the executor rejected the pump): back to idle, no re-check */
+  def pumpCancel(engine: Long): Unit
   /** stats: 8 longs (delivered, dead letters, unhandled, emitted, staged, supersteps, in flight,
    *  algorithmic bytes), or null for no read-back */
   def run(engine: Long, maxSupersteps: Int, stats: Array[Long]): Unit
@@ -75,6 +77,7 @@ object JniBackend extends AgxBackend {
     AgxJni.stageTellsArrays(engine, dst, src, payload, n)
   def tell(engine: Long, dst: Int, src: Int, payload: Int): Boolean = AgxJni.tell(engine, dst, src, payload)
   def pumpIdle(engine: Long): Boolean = AgxJni.pumpIdle(engine)
+  def pumpCancel(engine: Long): Unit = AgxJni.pumpCancel(engine)
   def run(engine: Long, maxSupersteps: Int, stats: Array[Long]): Unit = AgxJni.run(engine, maxSupersteps, stats)
   def getStats(engine: Long, stats: Array[Long]): Unit = AgxJni.getStats(engine, stats)
   def readState(engine: Long, first: Long, count: Long, words: Array[Long], alive: Array[Byte]): Unit =

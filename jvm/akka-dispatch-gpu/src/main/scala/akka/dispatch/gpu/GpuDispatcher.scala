@@ -94,6 +94,11 @@ class GpuDispatcher(
         try executorService.execute(pumpTask) // retry once, as registerForExecution does
         catch {
           case e: RejectedExecutionException =>
+            // back to idle before rethrowing (Dispatcher.registerForExecution: mbox.setAsIdle(); throw,
+            // Dispatcher.scala:130-138): agx_tell CASed idle -> scheduled for this submission, and a
+            // status left at "scheduled" would make every later tell answer "do not submit" -- the GPU
+            // actors would stall for good.  The next tell schedules the pump again.
+            engine.pumpCancel()
             eventStream.publish(Error(e, getClass.getName, getClass, "GPU pump was rejected twice!"))
             throw e
         }
@@ -132,7 +137,7 @@ class GpuDispatcher(
 
   override protected[akka] def shutdown(): Unit = {
     GpuEngine.unregister(engine)
-    engine.close()
+    engine.close() // waits for tells and a pump inside the engine; later tells become dead letters
     super.shutdown()
   }
 }

@@ -12,7 +12,7 @@
 package akka.dispatch.gpu
 
 import java.util.concurrent.ConcurrentHashMap
-import java.util.concurrent.atomic.AtomicInteger
+import java.util.concurrent.atomic.{ AtomicInteger, LongAdder }
 
 import com.typesafe.config.Config
 
@@ -141,9 +141,33 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
   @volatile private var submitPump: () => Unit = () => ()
   private[gpu] def setPumpSubmitter(f: () => Unit): Unit = submitPump = f
 
-  /** ActorRef.! : the tell enters the engine; the pump is submitted only on idle -> scheduled */
+  // ---------------------------------------------------------------- close guard
+  // Every native call that may race close() (tells from any thread, the pump) runs between enter()
+  // and exit(); close() sets `closed`, then waits until every call that entered has exited before
+  // agx_destroy frees the engine.  Two monotonic striped counters, so the tell path keeps no shared
+  // contended word: entered >= exited always, and once closed is set a reading of exited followed by
+  // an equal reading of entered means no call is inside (a call entering later sees closed).
+  @volatile private var closed = false
+  private val entered = new LongAdder
+  private val exited = new LongAdder
+  private[gpu] val lateTells = new LongAdder // tells after close: dead letters (the engine is gone)
+  @inline private def enter(): Boolean = {
+    entered.increment()
+    if (closed) { exited.increment(); false }
+    else true
+  }
+  @inline private def exit(): Unit = exited.increment()
+
+  /** ActorRef.! : the tell enters the engine; the pump is submitted only on idle -> scheduled.
+   *  After close() a tell is a dead letter (the dispatcher shut down, AbstractDispatcher.scala:325). */
   def tell(dstId: Int, srcId: Int, payload: Int): Unit =
-    if (native.tell(handle, dstId, srcId, payload)) submitPump()
+    if (!enter()) lateTells.increment()
+    else {
+      val submit =
+        try native.tell(handle, dstId, srcId, payload)
+        finally exit()
+      if (submit) submitPump()
+    }
 
   private val outD = new Array[Int](4096)
   private val outS = new Array[Int](4096)
@@ -154,16 +178,30 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
    *  finally: setAsIdle + registerForExecution) -- returns true iff tells arrived meanwhile and
    *  the caller must submit the pump again.  At most one pump is scheduled at a time (the CAS in
    *  agx_tell / agx_pump_idle), so one host thread drives the handle (include/akka_gpu.h rule). */
-  def pump(maxSupersteps: Int): Boolean = {
-    native.run(handle, maxSupersteps, null)
-    deliverOutbound()
-    native.pumpIdle(handle)
-  }
+  def pump(maxSupersteps: Int): Boolean =
+    if (!enter()) false
+    else
+      try {
+        native.run(handle, maxSupersteps, null)
+        deliverOutbound()
+        // also true while mail is still in flight after a run that hit gpu.supersteps-per-pump, or
+        // while tells wait in the queue for capacity (agx_pump_idle; Mailbox.run's hasMessages re-check)
+        native.pumpIdle(handle)
+      } finally exit()
 
   /** a failed pump still ends with the idle protocol (else the engine would stay "scheduled") */
   private[gpu] def pumpIdleAfterFailure(): Boolean =
-    try native.pumpIdle(handle)
-    catch { case _: Throwable => false }
+    if (!enter()) false
+    else
+      try native.pumpIdle(handle)
+      catch { case _: Throwable => false }
+      finally exit()
+
+  /** the executor rejected the pump: back to idle, so the next tell submits it again */
+  private[gpu] def pumpCancel(): Unit =
+    if (enter())
+      try native.pumpCancel(handle)
+      finally exit()
   /** outbox -> JVM actors: `jvmRef ! GpuTell(payload)` with the replying GPU actor as sender
    *  (each GPU sender's replies in emission order, the only order Akka guarantees) */
   private def deliverOutbound(): Unit = {
@@ -180,20 +218,33 @@ final class GpuEngine(val dispatcherId: String, config: Config, throughput: Int)
   }
 
   /** delivered, dead letters, unhandled, emitted, staged, supersteps, in flight, bytes */
-  def stats(): Array[Long] = {
+  def stats(): Array[Long] = guarded {
     val st = new Array[Long](8)
     native.getStats(handle, st)
     st
   }
 
-  def state(id: Int): (Array[Long], Boolean) = {
+  def state(id: Int): (Array[Long], Boolean) = guarded {
     val w = new Array[Long](stateWords)
     val alive = new Array[Byte](1)
     native.readState(handle, id.toLong, 1L, w, alive)
     (w, alive(0) != 0)
   }
 
-  def close(): Unit = native.destroy(handle)
+  private def guarded[T](f: => T): T =
+    if (!enter()) throw new IllegalStateException(s"GPU dispatcher [$dispatcherId] is shut down")
+    else
+      try f
+      finally exit()
+
+  /** agx_destroy, once no tell or pump is inside the engine (idempotent) */
+  def close(): Unit = synchronized {
+    if (!closed) {
+      closed = true
+      while (exited.sum() != entered.sum()) Thread.`yield`() // (exited first: see the guard above)
+      native.destroy(handle)
+    }
+  }
 }
 
 object GpuEngine {

@@ -20,7 +20,13 @@
  *   - the lock-free tell path (AgxJni.tell / pumpIdle -> agx_tell / agx_pump_idle): a burst of
  *     tells to an idle engine submits ONE pump (Mailbox.setAsScheduled, Mailbox.scala:185-194), and
  *     tells from 4 threads racing a pump that resubmits itself only when pumpIdle says so are all
- *     delivered (ActorModelSpec "handle queueing from multiple threads", :323-336).
+ *     delivered (ActorModelSpec "handle queueing from multiple threads", :323-336) -- 100000 of them,
+ *     6x the engine's message capacity: an unbounded mailbox never refuses an enqueue
+ *     (AbstractNodeQueue.java:79-82), so the tells that do not fit wait for a later pump;
+ *   - a pump budget (gpu.supersteps-per-pump) that stops with mail in flight: pumpIdle asks for
+ *     another run until the mail is delivered (Mailbox.run re-registers while hasMessages,
+ *     Mailbox.scala:227-240); pumpCancel (the executor rejected the pump) returns the engine to
+ *     idle so the next tell submits again (Dispatcher.scala:130-138).
  * Exit 0 = every check passed.  Run by tests/test_abi_c.py on the GPU box.
  */
 #include <pthread.h>
@@ -49,6 +55,7 @@ void Java_akka_dispatch_gpu_AgxJni_stageTellsArrays(JNIEnv*, jclass, jlong, jint
 void Java_akka_dispatch_gpu_AgxJni_run(JNIEnv*, jclass, jlong, jint, jlongArray);
 jboolean Java_akka_dispatch_gpu_AgxJni_tell(JNIEnv*, jclass, jlong, jint, jint, jint);
 jboolean Java_akka_dispatch_gpu_AgxJni_pumpIdle(JNIEnv*, jclass, jlong);
+void Java_akka_dispatch_gpu_AgxJni_pumpCancel(JNIEnv*, jclass, jlong);
 void Java_akka_dispatch_gpu_AgxJni_getStats(JNIEnv*, jclass, jlong, jlongArray);
 void Java_akka_dispatch_gpu_AgxJni_readState(JNIEnv*, jclass, jlong, jlong, jlong, jlongArray, jbyteArray);
 void Java_akka_dispatch_gpu_AgxJni_setGraph(JNIEnv*, jclass, jlong, jlongArray, jintArray);
@@ -189,7 +196,8 @@ static jobject direct_ints(jsize n) { return new_obj(T_DIRECT, 1, n * 4); }
 
 /* a sender thread of the lock-free tell path: TELLS tells to COUNTER actor 3100 + t, payloads 1..TELLS;
    a tell that answers "submit" counts one pump submission */
-enum { TELLS = 2500 }; /* (4 x 2500 in flight at most: within the engine's msg_capacity, 4 x N) */
+enum { TELLS = 25000 }; /* 4 x 25000 = 100000 tells: 6x the engine's msg_capacity (4 x N = 16384) -- the
+                          pump takes what fits, the rest wait in the queue (back-pressure, never loss) */
 typedef struct { jlong eng; int t; } tell_arg;
 static atomic_long t_submitted;
 static atomic_int ta_done[4];
@@ -398,7 +406,41 @@ int main(void) {
           "thread %d: %lld of %d tells delivered (sum %lld)", t, (long long)L(w)[0], TELLS, (long long)L(w)[1]);
   }
   CHECK(ran >= 1 && ran <= 4 * TELLS, "pump runs %ld", ran);
-  printf("lock-free tell path: %d threads x %d tells, %ld pump runs\n", 4, TELLS, ran);
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_getStats(env, K, eng, st));
+  CHECK(L(st)[6] == 0, "in flight after the last pump: %lld", (long long)L(st)[6]);
+  CHECK(L(st)[4] + L(st)[3] == L(st)[0] + L(st)[1] + L(st)[6], "staged + emitted = delivered + dead + in flight");
+  CHECK(!Java_akka_dispatch_gpu_AgxJni_pumpIdle(env, K, eng), "idle after the race");
+  printf("lock-free tell path: %d threads x %d tells (msg_capacity %d), %ld pump runs\n", 4, TELLS, 4 * N, ran);
+
+  /* a pump budget of one superstep (gpu.supersteps-per-pump = 1): throughput 5, 100 tells to one
+     COUNTER actor need 20 supersteps -- every pump but the last ends with mail in flight and
+     pumpIdle answers "run again" (the status stays scheduled: no tell can submit a second pump) */
+  int sub1 = 0;
+  for (jint i = 1; i <= 100; ++i) sub1 += Java_akka_dispatch_gpu_AgxJni_tell(env, K, eng, 3200, AGX_NO_SENDER, i) ? 1 : 0;
+  CHECK(sub1 == 1, "budget burst submitted %d pumps", sub1);
+  int pumps = 0, again = 1;
+  while (again && pumps < 1000) {
+    ++pumps;
+    NOEXC(Java_akka_dispatch_gpu_AgxJni_run(env, K, eng, 1, NULL));
+    again = Java_akka_dispatch_gpu_AgxJni_pumpIdle(env, K, eng);
+    if (again && pumps == 1)
+      CHECK(!Java_akka_dispatch_gpu_AgxJni_tell(env, K, eng, 3201, AGX_NO_SENDER, 1), "a tell while the pump is "
+            "rescheduled must not submit a second pump");
+  }
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 3200, 1, w, al));
+  CHECK(L(w)[0] == 100 && L(w)[1] == 5050, "budgeted pumps delivered %lld of 100", (long long)L(w)[0]);
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 3201, 1, w, al));
+  CHECK(L(w)[0] == 1, "the tell made during the budgeted pumps was delivered (%lld)", (long long)L(w)[0]);
+  CHECK(pumps >= 20 && pumps <= 22, "budgeted pumps: %d runs of one superstep for 100 messages at throughput 5", pumps);
+  /* the executor rejected the pump: pumpCancel -> idle, the next tell submits */
+  CHECK(Java_akka_dispatch_gpu_AgxJni_tell(env, K, eng, 3202, AGX_NO_SENDER, 1), "idle engine: submit");
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_pumpCancel(env, K, eng));
+  CHECK(Java_akka_dispatch_gpu_AgxJni_tell(env, K, eng, 3202, AGX_NO_SENDER, 2), "after pumpCancel the next tell submits");
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_run(env, K, eng, 1 << 30, st));
+  CHECK(!Java_akka_dispatch_gpu_AgxJni_pumpIdle(env, K, eng), "idle after the rejected pump's tells ran");
+  NOEXC(Java_akka_dispatch_gpu_AgxJni_readState(env, K, eng, 3202, 1, w, al));
+  CHECK(L(w)[0] == 2, "both tells around the rejection delivered (%lld)", (long long)L(w)[0]);
+  printf("pump budget: %d pumps of one superstep, pumpCancel OK\n", pumps);
 
   NOEXC(Java_akka_dispatch_gpu_AgxJni_destroy(env, K, eng));
   free_obj(d);

@@ -88,5 +88,43 @@ int main() {
     std::printf("stress: %d producers x %u tells, %llu pump runs, FIFO per producer, none lost OK\n", K, M,
                 (unsigned long long)runs);
   }
+  {  // 4. bounded takes (the pump takes only what fits msg_capacity): nothing lost or reordered, the
+     //    refused tell stays queued, and successive takes resume where the last one stopped
+    agx::TellQueue q;
+    constexpr int K = 3;
+    constexpr uint32_t M = 10000;  // 3 segments per producer
+    std::vector<std::thread> prod;
+    for (int k = 0; k < K; ++k)
+      prod.emplace_back([&, k] {
+        for (uint32_t i = 1; i <= M; ++i) q.tell((uint32_t)k, (uint32_t)k, i);
+      });
+    for (auto& t : prod) t.join();
+    std::vector<uint32_t> last(K, 0);
+    uint64_t total = 0, bad = 0, takes = 0;
+    std::vector<int> first_of_take;
+    for (;;) {
+      uint32_t room = 777;
+      int first = -1;
+      const bool all = q.take_while([&](uint32_t d, uint32_t s, uint32_t p) {
+        if (!room) return false;
+        --room;
+        if (first < 0) first = (int)s;
+        if (d != s || s >= (uint32_t)K || p != last[s] + 1) ++bad;
+        if (s < (uint32_t)K) last[s] = p;
+        ++total;
+        return true;
+      });
+      ++takes;
+      first_of_take.push_back(first);
+      CHECK(all == !q.pending(), "bounded: take_while's answer disagrees with pending()");
+      if (all) break;
+      CHECK(takes < 1000, "bounded: no progress");
+    }
+    CHECK(bad == 0 && total == (uint64_t)K * M, "bounded: took %llu of %llu (bad %llu)", (unsigned long long)total,
+          (unsigned long long)K * M, (unsigned long long)bad);
+    // a take that stopped inside producer p's tells starts the next take at p
+    CHECK(takes == (K * M + 776) / 777, "bounded: %llu takes", (unsigned long long)takes);
+    std::printf("bounded: %llu takes of <= 777, FIFO per producer, none lost OK\n", (unsigned long long)takes);
+  }
   return 0;
 }

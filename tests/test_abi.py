@@ -71,3 +71,21 @@ def test_errors_are_status_codes_not_crashes(built):
     assert b"abi_version" in lib.agx_last_error()
     assert lib.agx_create(None, ctypes.byref(h)) == 1
     assert lib.agx_destroy(None) == 0
+
+
+def test_library_stamped_with_source_hash(built, tmp_path):
+    """build_native rebuilds by source hash, not by file times: the built library carries the hash of
+    the sources it was built from (found in its bytes), agx_build_hash returns it, and a library
+    stamped with any other hash -- a stale build shipped beside newer sources -- reads as stale."""
+    import __graft_entry__ as ge
+    want = ge.source_hash()
+    assert len(want) == 16
+    assert ge.library_hash(ge.LIB) == want
+    from akka_amd import _lib
+    assert _lib.load().agx_build_hash().decode() == want
+    stale = tmp_path / "libakka_gpu.so"
+    data = ge.LIB.read_bytes()
+    i = data.find(ge.STAMP) + len(ge.STAMP)
+    stale.write_bytes(data[:i] + b"0123456789abcdef" + data[i + 16:])
+    assert ge.library_hash(stale) == "0123456789abcdef" != want
+    assert ge.library_hash(tmp_path / "missing.so") is None

@@ -18,4 +18,5 @@ def test_tell_queue(tmp_path, flags):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "one submission per burst OK" in r.stdout and "none lost OK" in r.stdout
+    assert "bounded:" in r.stdout
     assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
