@@ -103,6 +103,7 @@ SIGNATURES = {
     "agx_identity_supersteps": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
     "agx_ring_buckets": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
     "agx_exchange_info": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
+    "agx_persist_info": (ctypes.c_int32, [ctypes.c_void_p, c_u64p]),
     "agx_run_timed": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "agx_get_shape": (ctypes.c_int32, [ctypes.c_void_p, c_u64p, c_u32p]),
     "agx_read_state": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_u64p, c_u8p]),
@@ -124,7 +125,8 @@ SIGNATURES = {
 
 
 # entry points newer than some A/B diagnostic builds (tools/build_variant.sh of an older checkout)
-OPTIONAL = {"agx_tell", "agx_pump_idle", "agx_pump_cancel", "agx_exchange_info", "agx_run_timed", "agx_build_hash"}
+OPTIONAL = {"agx_tell", "agx_pump_idle", "agx_pump_cancel", "agx_exchange_info", "agx_run_timed", "agx_build_hash",
+            "agx_persist_info"}
 
 
 def load():

@@ -47,6 +47,14 @@ hipError_t agx_launch_ring_g4(uint32_t, bool, dim3, hipStream_t, const BucketArg
 hipError_t agx_launch_ring_g5(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
 hipError_t agx_launch_ring_g6(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
 hipError_t agx_launch_ring_g7(uint32_t, bool, dim3, hipStream_t, const BucketArgs&, const RingArgs&);
+hipError_t agx_dense_persist_occupancy_g0(uint32_t, int*);
+hipError_t agx_dense_persist_occupancy_g1(uint32_t, int*);
+hipError_t agx_dense_persist_occupancy_g2(uint32_t, int*);
+hipError_t agx_dense_persist_occupancy_g3(uint32_t, int*);
+hipError_t agx_dense_persist_occupancy_g4(uint32_t, int*);
+hipError_t agx_dense_persist_occupancy_g5(uint32_t, int*);
+hipError_t agx_dense_persist_occupancy_g6(uint32_t, int*);
+hipError_t agx_dense_persist_occupancy_g7(uint32_t, int*);
 static_assert(kVGroups == 8, "one declaration per group");
 
 namespace {
@@ -105,6 +113,8 @@ hipError_t dense_dispatch(uint32_t vid, uint32_t mode, dim3 g, hipStream_t s, co
       if (vid == V) {
         if (mode == M_FUSED)
           hipLaunchKernelGGL((k_dense_fused<kVariants[V].km, false>), g, dim3(kDenseThreads), 0, s, ba);
+        else if (mode == M_PERSIST)
+          hipLaunchKernelGGL((k_dense_fused<kVariants[V].km, false, true>), g, dim3(kDenseThreads), 0, s, ba);
         else if (mode == M_OWNER)
           hipLaunchKernelGGL((k_dense_fused<kVariants[V].km, true>), g, dim3(kDenseThreads), 0, s, ba);
         else
@@ -112,6 +122,19 @@ hipError_t dense_dispatch(uint32_t vid, uint32_t mode, dim3 g, hipStream_t s, co
         return hipGetLastError();
       }
     return dense_dispatch<V + 1>(vid, mode, g, s, ba);
+  }
+}
+
+template <uint32_t V>
+hipError_t persist_occ(uint32_t vid, int* n) {
+  if constexpr (V >= V_N) {
+    return hipErrorInvalidValue;
+  } else {
+    if constexpr (kVariantGroup[V] == AGX_VGROUP && !kVariants[V].wide)
+      if (vid == V)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(n, k_dense_fused<kVariants[V].km, false, true>,
+                                                            kDenseThreads, 0);
+    return persist_occ<V + 1>(vid, n);
   }
 }
 
@@ -138,6 +161,8 @@ hipError_t AGX_CAT(agx_launch_ring_g, AGX_VGROUP)(uint32_t vid, bool tiny, dim3 
                                                   const RingArgs& ra) {
   return ring_dispatch<0>(vid, tiny, g, s, ba, ra);
 }
+
+hipError_t AGX_CAT(agx_dense_persist_occupancy_g, AGX_VGROUP)(uint32_t vid, int* n) { return persist_occ<0>(vid, n); }
 
 hipError_t AGX_CAT(agx_launch_tiny_g, AGX_VGROUP)(uint32_t vid, dim3 g, hipStream_t s, const BucketArgs& ba) {
   return tiny_dispatch<0>(vid, g, s, ba);
@@ -191,6 +216,21 @@ hipError_t agx_launch_dense(uint32_t vid, uint32_t mode, dim3 g, hipStream_t s, 
     case 5: return agx_launch_dense_g5(vid, mode, g, s, ba);
     case 6: return agx_launch_dense_g6(vid, mode, g, s, ba);
     default: return agx_launch_dense_g7(vid, mode, g, s, ba);
+  }
+}
+
+hipError_t agx_dense_persist_occupancy(uint32_t vid, int* n) {
+  *n = 0;
+  if (vid >= V_N || kVariants[vid].wide) return hipErrorInvalidValue;
+  switch (kVariantGroup[vid]) {
+    case 0: return agx_dense_persist_occupancy_g0(vid, n);
+    case 1: return agx_dense_persist_occupancy_g1(vid, n);
+    case 2: return agx_dense_persist_occupancy_g2(vid, n);
+    case 3: return agx_dense_persist_occupancy_g3(vid, n);
+    case 4: return agx_dense_persist_occupancy_g4(vid, n);
+    case 5: return agx_dense_persist_occupancy_g5(vid, n);
+    case 6: return agx_dense_persist_occupancy_g6(vid, n);
+    default: return agx_dense_persist_occupancy_g7(vid, n);
   }
 }
 

@@ -291,6 +291,8 @@ struct agx_engine {
   // of K supersteps replays its binary decomposition (20 = 8 + 8 + 4), never a run of singles.
   static constexpr uint32_t kNSizes = 5;
   hipGraphExec_t gx[2][2][kNSizes] = {};
+  bool gx_persist[2][2][kNSizes] = {};  // that replay is one persistent launch (capture_steps)
+  uint64_t persist_launches = 0, persist_supersteps = 0;  // replays launched as persistent launches (agx_persist_info)
   // multi-rank device-resident replays (run_multi_rccl): kMrReplay supersteps -- phase 1, the count
   // all-gather, k_mr_pack, the slab sends / receives, unpack, bucket passes, apply -- captured once as
   // one graph (RCCL collectives are captured with the kernels); mr_graph_ok cleared when a capture
@@ -301,6 +303,13 @@ struct agx_engine {
   // defers a skewed bucket marks d_abort; the rest of the replay is void and run_single runs the
   // deferred skew launch, then continues with the full graphs (strict_ok cleared for this engine).
   uint32_t* d_abort = nullptr;  // [2] (BucketArgs::abort)
+  // persistent fused supersteps (k_dense_fused<.., true>): a captured replay of K dense-alone strict
+  // supersteps is ONE launch with a grid barrier between supersteps (AGX_PERSIST=0: K launches)
+  int persist = -1;              // -1 not decided yet, 0 off (knob, too many buckets, a barrier timeout), 1 on
+  uint32_t persist_steps = 0;    // capture_steps -> launch_apply: supersteps of the persistent launch
+  uint32_t persist_vid = ~0u;    // the apply variant `persist` was decided for
+  bool captured_persist = false; // the last capture_steps was one persistent launch
+  uint32_t* d_pbar = nullptr;    // [4] grid barrier: arrivals, generation, timed out
   uint32_t* h_abort = nullptr;  // pinned [kLag][2]: the marks after each replay (eager path)
   // fused graphs end with k_replay_out, which writes the replay's inbox-size rows and abort marks
   // straight into the pinned host ring (device-mapped) at ring slot (replay counter % kLag): no
@@ -773,11 +782,33 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
       ba.blist = e->d_blist;
       if (mode != M_OWNER) ba.dense_left = e->d_dense_left;  // (owner mode: one parity only -- no shortcut)
     }
+    const bool persist = dl && alone && e->persist_steps > 0;
     if (dl) {
       Scope s(e, K_DENSE);
       BucketArgs bd = ba;
       bd.dense_alone = alone ? 1u : 0u;
-      HIP_TRY(agx_launch_dense(vid, mode, dim3(grid_for(e->nb, kMaxApplyGrid)), e->stream, bd));
+      if (persist) {  // e->persist_steps supersteps in one launch, one block per bucket (persist_ok)
+        bd.psteps = e->persist_steps;
+        bd.pbar = e->d_pbar;
+        if (bd.par) {  // the kernel's pointer arrays by LOGICAL parity: index 0 = the first superstep's write parity
+          GatherArgs& q = bd.g;
+          std::swap(q.bl[0], q.bl[1]);
+          std::swap(q.eg[0], q.eg[1]);
+          std::swap(q.tcnt[0], q.tcnt[1]);
+          std::swap(q.toff[0], q.toff[1]);
+          std::swap(q.blo[0], q.blo[1]);
+          std::swap(q.blc[0], q.blc[1]);
+          std::swap(q.emc[0], q.emc[1]);
+        }
+        HIP_TRY(agx_launch_dense(vid, M_PERSIST, dim3(e->nb), e->stream, bd));
+      } else {
+        HIP_TRY(agx_launch_dense(vid, mode, dim3(grid_for(e->nb, kMaxApplyGrid)), e->stream, bd));
+      }
+    }
+    if (persist) {  // (nothing else runs in a dense-alone strict superstep)
+      if (e->persist_steps & 1u) e->par ^= 1u;
+      HIP_TRY(hipGetLastError());
+      return AGX_OK;
     }
     const bool tl = mode == M_BYPASS && !kVariants[vid].wide && e->tiny_launch && e->tiny_max && !e->skew_only;
     if (tl) {  // wave-per-bucket launch first; the block launch then takes the buckets it marked
@@ -1188,6 +1219,9 @@ agx_status error_status(const agx_engine* e, uint64_t err) {
   if (err & kErrCapacity)
     return set_err(AGX_ECAPACITY, "in-flight messages exceeded engine capacity (msg_capacity=%llu)",
                    (unsigned long long)e->cap);
+  if (err & kErrBarrier)
+    return set_err(AGX_EDEVICE, "a persistent superstep launch's grid barrier timed out (not every block was "
+                   "resident); AGX_PERSIST=0 avoids the persistent launch");
   return AGX_OK;
 }
 
@@ -1233,15 +1267,47 @@ agx_status launch_step_single(agx_engine* e) {
   return AGX_OK;
 }
 
+// The persistent fused launch: a strict replay whose every superstep is the dense
+// launch alone runs its K supersteps in ONE launch of k_dense_fused<.., true> -- one block per bucket,
+// a grid barrier between supersteps, the actors' state words kept in registers -- instead of K
+// launches.  Only when all nb blocks are resident at once (the barrier waits for every block): nb <=
+// resident blocks per CU x CUs.  AGX_PERSIST=0 turns it off.
+bool persist_ok(agx_engine* e) {
+  const uint32_t vid = apply_variant(e);
+  if (e->persist >= 0 && e->persist_vid != vid) e->persist = -1;  // (kinds registered since: re-decide)
+  if (e->persist < 0) {
+    e->persist_vid = vid;
+    e->persist = 0;
+    const char* k = getenv("AGX_PERSIST");
+    int per_cu = 0, dev = 0, ncu = 0;
+    if ((!k || atoi(k) != 0) && e->R == 1 && e->fused &&
+        agx_dense_persist_occupancy(vid, &per_cu) == hipSuccess && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      e->persist = (uint64_t)e->nb <= (uint64_t)per_cu * (uint64_t)ncu ? 1 : 0;
+    (void)hipGetLastError();
+  }
+  return e->persist == 1 && e->fused && e->strict_cap && e->dense_alone && dense_on(e, vid) && !e->skew_only &&
+         !e->recover_dense;
+}
+
 // hipGraph of `steps` supersteps (the launch-bound inner loop): replayed
 // instead of 10+ eager launches per superstep.
 agx_status capture_steps(agx_engine* e, uint32_t steps, hipGraphExec_t* out) {
   hipGraph_t g = nullptr;
   HIP_TRY(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
   agx_status st = AGX_OK;
-  for (uint32_t i = 0; i < steps && st == AGX_OK; ++i) {
-    e->cur_slot = i;  // fused: the i-th superstep of the replay reports its inbox sizes in row i
+  e->captured_persist = false;
+  if (steps > 1 && persist_ok(e)) {  // one persistent launch for the replay's supersteps
+    e->cur_slot = 0;
+    e->persist_steps = steps;
     st = launch_step_single(e);
+    e->persist_steps = 0;
+    e->captured_persist = true;
+  } else {
+    for (uint32_t i = 0; i < steps && st == AGX_OK; ++i) {
+      e->cur_slot = i;  // fused: the i-th superstep of the replay reports its inbox sizes in row i
+      st = launch_step_single(e);
+    }
   }
   e->cur_slot = 0;
   if (st == AGX_OK && e->fused)  // the replay's rows and abort marks -> host ring slot (no D2H copy)
@@ -1309,6 +1375,7 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
         if (g) continue;
         e->par = p;
         s2 = capture_steps(e, kGraphSizes[si], &g);
+        (e->fused ? e->gx_persist[strict][p][si] : e->gx_persist[0][p][si]) = s2 == AGX_OK && e->captured_persist;
       }
     e->par = p0;
     e->strict_cap = false;
@@ -1469,6 +1536,10 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
         break;
       }
       if (cnt & 1u) e->par ^= 1u;  // the replayed supersteps advanced the parity
+      if (e->fused && e->gx_persist[strict][par0][si]) {
+        ++e->persist_launches;
+        e->persist_supersteps += cnt;
+      }
     } else {
       cnt = 1;
       st = launch_step_single(e);
@@ -1508,6 +1579,10 @@ agx_status run_single(agx_engine* e, uint32_t max_steps) {
   if (last_ring >= 0) {
     const uint32_t* t = e->h_cntb + (size_t)last_ring * ring_row + ring_row - 2;
     e->h_stat[ST_ERROR] = (uint64_t)t[0] | ((uint64_t)t[1] << 32);
+  }
+  if ((e->h_stat[ST_ERROR] & kErrBarrier) && e->persist != 0) {  // (never again on this engine)
+    e->persist = 0;
+    drop_graphs(e);
   }
   const bool rec0 = recovered;
   if (e->fused && !quiet)  // replays not polled yet, in launch order
@@ -2244,6 +2319,8 @@ agx_status agx_create(const agx_cfg* cfg, agx_engine** out) {
     CREATE_TRY(hipMemset(e->d_rctr, 0, 4) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(dalloc(&e->d_abort, 2));
     CREATE_TRY(hipMemset(e->d_abort, 0, 8) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
+    CREATE_TRY(dalloc(&e->d_pbar, 4));
+    CREATE_TRY(hipMemset(e->d_pbar, 0, 16) == hipSuccess ? AGX_OK : set_err(AGX_EDEVICE, "memset"));
     CREATE_TRY(hipHostMalloc((void**)&e->h_abort, 4 * 2 * 4, hipHostMallocDefault) == hipSuccess
                    ? AGX_OK : set_err(AGX_ENOMEM, "pinned"));
   }
@@ -2325,6 +2402,7 @@ agx_status agx_destroy(agx_engine* e) {
   hipFree(e->d_stg_off); hipFree(e->d_stg_cnt); hipFree(e->d_ovf); hipFree(e->d_cntb);
   if (e->h_cntb) hipHostFree(e->h_cntb); hipFree(e->d_parv);
   hipFree(e->d_abort); hipFree(e->d_rctr);
+  hipFree(e->d_pbar);
   for (auto& ev : e->tev)
     if (ev) hipEventDestroy(ev);
   if (e->h_abort) hipHostFree(e->h_abort);
@@ -2900,6 +2978,13 @@ agx_status agx_run_timed(agx_engine* e, uint32_t max_supersteps, agx_stats* out,
   HIP_TRY(hipEventSynchronize(e->tev[1]));
   HIP_TRY(hipEventElapsedTime(device_ms, e->tev[0], e->tev[1]));
   return st;
+}
+
+agx_status agx_persist_info(agx_engine* e, uint64_t out[2]) {
+  if (!e || !out) return set_err(AGX_EINVAL, "bad persist_info args");
+  out[0] = e->persist_launches;
+  out[1] = e->persist_supersteps;
+  return AGX_OK;
 }
 
 agx_status agx_exchange_info(agx_engine* e, uint64_t out[6]) {

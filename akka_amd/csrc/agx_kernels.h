@@ -52,6 +52,7 @@ enum { ST_DELIVERED = 0, ST_DEAD = 1, ST_UNHANDLED = 2, ST_EMITTED = 3, ST_STEPS
        ST_IDENT = 7, ST_N = 8 };
 constexpr uint64_t kErrCapacity = 1;
 constexpr uint64_t kErrRange = 2;  // a counter slot wrapped past 2^64 - 1 (AGX_ERANGE)
+constexpr uint64_t kErrBarrier = 4;  // a persistent superstep launch's grid barrier timed out (AGX_EDEVICE)
 // per-block counters of k_bucket_apply: delivered, dead, unhandled, emitted, active
 constexpr int kBStats = 5;
 constexpr uint32_t kMaxApplyGrid = 4096;
@@ -1083,6 +1084,10 @@ struct BucketArgs {
   uint32_t* blist;
   uint32_t dense_first;    // bypass: k_dense_apply ran first -- k_tiny_apply takes only the buckets it marked
   uint32_t dense_alone;    // fused strict replay: k_dense_fused is the whole superstep (a bucket it leaves aborts)
+  // persistent fused launch (k_dense_fused<.., kPersist>): psteps supersteps in one launch, one block
+  // per bucket, a grid barrier between supersteps; pbar = {arrivals, generation, timed out}
+  uint32_t psteps;
+  uint32_t* pbar;
   uint32_t* dense_left;    // [2] by superstep parity: the dense launch left a bucket to the wave / block launches
                            // (they return at entry when it did not); null: no such shortcut
   // bypass, plain behaviours: skewed buckets pre-partitioned by k_skew_* (see there); [i] = skew index
@@ -1258,6 +1263,24 @@ __device__ __forceinline__ void group_tells(const BucketArgs& a, const BucketLds
   if (tid == 0 && g.emc[w]) g.emc[w][b] = emtot;
 }
 
+#ifdef AGX_ACC_SHADOW
+// diagnostic build knob (the round-4 sparse-row counter fault): each wave also
+// keeps its emitted count in LDS, reduced from the same per-bucket nall values the acc[3]
+// registers add up.  AGX_ACC_SHADOW=1 flushes the LDS shadow as the emitted counter, =2 flushes the
+// registers (same code and layout otherwise): which of the two is right tells where the count is lost.
+__device__ __forceinline__ uint32_t* acc_shadow() {
+  __shared__ uint32_t s[kBWaves];
+  return s;
+}
+#define AGX_SHADOW_ADD(nall)                                                   \
+  do {                                                                         \
+    const uint32_t sv_ = wave_incl_sum(nall);                                  \
+    if (lane_id() == kWave - 1) acc_shadow()[threadIdx.x / kWave] += sv_;      \
+  } while (0)
+#else
+#define AGX_SHADOW_ADD(nall) ((void)0)
+#endif
+
 // the block's counters -> its own slot of the per-block stats (summed by k_stats_reduce)
 __device__ __forceinline__ void flush_stats(const BucketArgs& a, const uint32_t (&acc)[kBStats]) {
 #ifdef AGX_DEBUG_EMIT
@@ -1268,6 +1291,9 @@ __device__ __forceinline__ void flush_stats(const BucketArgs& a, const uint32_t 
   uint32_t v[kBStats];
 #pragma unroll
   for (int i = 0; i < kBStats; ++i) v[i] = wave_incl_sum(acc[i]);
+#if defined(AGX_ACC_SHADOW) && AGX_ACC_SHADOW == 1
+  v[3] = acc_shadow()[threadIdx.x / kWave];  // (lane kWave - 1 flushes: the wave's LDS shadow)
+#endif
   if (lane_id() == kWave - 1) {
     unsigned long long* bs = a.bstats + (size_t)blockIdx.x * kBStats;
 #pragma unroll
@@ -2034,6 +2060,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     acc[2] += nunh;
     acc[3] += nall;
     acc[4] += nact;
+    AGX_SHADOW_ADD(nall);
   }
   __syncthreads();  // (L.nh and the other per-bucket LDS arrays are reset by the next bucket)
   AGX_STAMP(a, 8);
@@ -2244,6 +2271,7 @@ __device__ __forceinline__ void dense_finish(const BucketArgs& a, const BucketLd
     acc[2] += nunh;
     acc[3] += nall;
     acc[4] += nact;
+    AGX_SHADOW_ADD(nall);
   }
   __syncthreads();  // (the per-bucket LDS arrays are reset by the next bucket)
   AGX_STAMP(a, 8);
@@ -2893,15 +2921,55 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
 #define AGX_EARLY_ROW 1
 #endif
 constexpr bool kEarlyRow = AGX_EARLY_ROW != 0;
-template <uint32_t KM, bool kOwner>
-static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketArgs a) {
+// Grid barrier of the persistent fused launch (every block resident: the host launches it only when
+// nb blocks fit the device at once, agx_engine.hip persist_ok).  Thread 0 of each block releases the
+// block's stores device-wide (__threadfence: L2 write-back), arrives, and the last arrival bumps the
+// generation the others wait on; then acquires (L2 invalidate) before any of the block reads the
+// next superstep's tables and tells.  Every wait is bounded: a barrier that times out (a block that
+// never became resident) sets pbar[2] and the error word, and every block leaves -- the launch
+// always drains; the host reports AGX_EDEVICE and stops using the persistent launch.
+__device__ __forceinline__ bool grid_barrier(uint32_t* bar, uint32_t nblocks, uint32_t& gen, uint32_t* s_ok,
+                                             uint64_t* err) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // release once (L2 write-back), poll RELAXED (an acquire poll invalidates the XCD's L2 on every
+    // iteration: 6x slower supersteps, measured), acquire once (L2 invalidate) after the wait
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    uint32_t ok = 1u;
+    if (__hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1u) {
+      __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&bar[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      uint32_t it = 0;
+      while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++it & 1023u) == 0u &&
+            (it > (1u << 22) || __hip_atomic_load(&bar[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          ok = 0u;
+          atomicOr(&bar[2], 1u);
+          atomicOr((unsigned long long*)err, (unsigned long long)kErrBarrier);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    gen += 1u;
+    *s_ok = ok;
+  }
+  __syncthreads();
+  return *s_ok != 0u;
+}
+
+template <uint32_t KM, bool kOwner, bool kPersist = false>
+static __global__ void __launch_bounds__(kDenseThreads, kPersist ? 4 : 2) k_dense_fused(BucketArgs a) {
+  static_assert(!(kOwner && kPersist), "persistent launches are single-rank fused supersteps");
   __shared__ __attribute__((aligned(16))) uint32_t s_ks[2 * kBucket];   // per-actor src / pay; group_tells' histogram
   __shared__ __attribute__((aligned(16))) uint64_t U[3 * kBucket / 2];  // segment list; then the tells, sender order
   __shared__ __attribute__((aligned(16))) uint32_t s_hit[4 * kRadix];   // messages per actor; group_tells' bases
   __shared__ uint32_t s_nh[kRadix];                                     // tells per destination bucket
   __shared__ uint32_t scratch[2 * (kDenseWaves + 1)];
   __shared__ uint32_t s_cnt[kDenseIpt * kDenseWaves];
-  __shared__ uint32_t s_g[2], s_bad, s_dmin, s_dmax;
+  __shared__ uint32_t s_g[2], s_bad, s_dmin, s_dmax, s_ok;
   static_assert(4 * kRadix >= kBucket && kDenseThreads == kBThreads && kDenseIpt == kBIpt, "group_tells' shapes");
   const BucketLds L{s_ks, s_ks + kBucket, nullptr, U, nullptr, s_hit, nullptr, nullptr, s_nh, scratch, nullptr, nullptr};
   const DevParams& P = a.P;
@@ -2909,24 +2977,32 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
   const uint32_t tid = threadIdx.x, w = tid / kWave, lane = lane_id();
   const uint64_t ltm = lanemask_lt();
   const uint32_t amask = (1u << a.bb) - 1u, nhmask = (1u << a.nx_bits) - 1u;
-  const uint32_t wpar = kOwner ? 0u : a.par, rpar = wpar ^ 1u;
+  // Parities.  Persistent launches: the superstep's parity and replay slot advance inside the launch;
+  // the host passes the parity-indexed POINTER arrays (g.eg / tcnt / toff / blo / blc / emc) swapped so
+  // that index 0 is the first superstep's write parity, and the loop below is unrolled by two with
+  // literal parities -- so the compiler selects each pointer at compile time instead of keeping both
+  // parities' pointers live -- while the small [2] device words (abort, dense_left, cursors) keep
+  // their physical index: logical parity ^ pflip.
+  const uint32_t pflip = kPersist ? a.par : 0u;
+  uint32_t wpar = kOwner ? 0u : kPersist ? 0u : a.par, rpar = wpar ^ 1u, slot = a.slot;
   if (kOwner && a.halt && a.halt[0]) return;  // (device-resident multi-rank replay stopped)
   // strict replay (this kernel alone is the superstep): an earlier superstep that left a bucket
   // voids this one.  The word is read here and tested after the first bucket's row / state loads are
   // issued (AGX_EARLY_ROW), so its round trip overlaps theirs instead of preceding them; nothing is
   // stored before the test.
-  uint32_t ab_in = (!kOwner && a.abort) ? a.abort[rpar] : 0u;
+  uint32_t ab_in = (!kOwner && a.abort) ? a.abort[rpar ^ pflip] : 0u;
   bool tested = !kEarlyRow;
   const auto abort_test = [&]() -> bool {
     if (ab_in) {
-      if (tid == 0) a.abort[wpar] = ab_in;  // (pass it on: the next superstep reads this parity)
+      if (tid == 0) a.abort[wpar ^ pflip] = ab_in;  // (pass it on: the next superstep reads this parity)
       return true;
     }
     if (!kOwner && blockIdx.x == 0 && tid == 0) {  // the cursors the NEXT superstep uses (as k_bucket_apply's fused launch)
-      if (a.dense_left) a.dense_left[rpar] = 0u;
-      g.ovf[rpar] = 0u;
-      a.skew_n[rpar] = 0u;
-      if (g.heap_top) g.heap_top[rpar] = 0u;
+      const uint32_t rp = rpar ^ pflip;
+      if (a.dense_left) a.dense_left[rp] = 0u;
+      g.ovf[rp] = 0u;
+      a.skew_n[rp] = 0u;
+      if (g.heap_top) g.heap_top[rp] = 0u;
     }
     return false;
   };
@@ -2935,6 +3011,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
   const uint32_t w1off = P.W > 1 ? P.sw : 0u;
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};
   if (tid == 0) s_bad = 0;
+
   // one bucket's superstep; true = the replay is void (return).  With a grid of >= nb blocks (the
   // fused launch: nb <= kDenseThreads) it runs once, outside a loop: the waitcnt pass then has no back
   // edge whose pending loads it must assume, and the row / flag / state loads issue back to back
@@ -2991,8 +3068,8 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     if (s_g[0] != 0u || s_g[1] != 0u || cnt > (uint32_t)kBucket) {  // (uniform) backlog / staged / big: block path
       if (tid == 0) {
         a.blist[b] = 1u;
-        if (a.dense_left) a.dense_left[wpar] = 1u;
-        if (a.dense_alone) a.abort[wpar] = a.slot + 1u;  // strict replay: the rest of it is void (run_single recovers)
+        if (a.dense_left) a.dense_left[wpar ^ pflip] = 1u;
+        if (a.dense_alone) a.abort[wpar ^ pflip] = slot + 1u;  // strict replay: the rest of it is void (run_single recovers)
       }
       __syncthreads();  // (s_g is rewritten by the next bucket)
       return false;
@@ -3049,8 +3126,8 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
       if (tid == 0) {
         s_bad = 0;
         a.blist[b] = 1u;
-        if (a.dense_left) a.dense_left[wpar] = 1u;
-        if (a.dense_alone) a.abort[wpar] = a.slot + 1u;
+        if (a.dense_left) a.dense_left[wpar ^ pflip] = 1u;
+        if (a.dense_alone) a.abort[wpar ^ pflip] = slot + 1u;
       }
       return false;
     }
@@ -3062,7 +3139,7 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
         a.chunk_off[b] = lo;
         a.chunk_cnt[b] = 0u;
       } else {
-        g.cntb[(size_t)a.slot * a.nb + b] = cnt;
+        g.cntb[(size_t)slot * a.nb + b] = cnt;
         g.blo[wpar][b] = lo;
         g.blc[wpar][b] = 0u;
       }
@@ -3196,13 +3273,46 @@ static __global__ void __launch_bounds__(kDenseThreads, 2) k_dense_fused(BucketA
     AGX_STAMP(a, 8);
     return false;
   };
-  if (gridDim.x >= a.nb) {
-    if (blockIdx.x < a.nb && bucket(blockIdx.x)) return;
+  if constexpr (kPersist) {
+    // psteps supersteps, one bucket per block (grid = nb), a grid barrier between them.  A superstep
+    // that meets a non-dense bucket marks abort[wpar] (as the graph's launch would); the next one
+    // reads the mark after the barrier, passes it on and the launch ends -- the state the graph of
+    // separate launches leaves, so run_single's recovery is the same.
+    const uint32_t b = blockIdx.x;
+    uint32_t gen = 0u;
+    if (tid == 0) gen = __hip_atomic_load(&a.pbar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // superstep s + 1 after superstep s: barrier, then the mark superstep s may have left
+    const auto next = [&](uint32_t wp) -> bool {
+      if (!grid_barrier(a.pbar, a.nb, gen, &s_ok, (uint64_t*)&a.stats[ST_ERROR])) return false;
+      wpar = wp;
+      rpar = wp ^ 1u;
+      ++slot;
+      ab_in = a.abort ? __hip_atomic_load(&a.abort[rpar ^ pflip], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      tested = !kEarlyRow;
+      return kEarlyRow || !abort_test();
+    };
+    // (the bucket index is made opaque each superstep: every address derived from it would otherwise
+    // be hoisted out of the loop and held in registers across it -- 105 -> 164 VGPRs)
+    const auto opaque = [](uint32_t x) {
+      asm volatile("" : "+s"(x));
+      return x;
+    };
+    for (uint32_t s = 0; s < a.psteps; s += 2) {  // (two supersteps per trip: literal parities 0, 1)
+      if (s > 0 && !next(0u)) break;
+      if (bucket(opaque(b))) break;
+      if (s + 1 >= a.psteps || !next(1u)) break;
+      if (bucket(opaque(b))) break;
+    }
+    flush_stats(a, acc);
   } else {
-    for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x)
-      if (bucket(b)) return;
+    if (gridDim.x >= a.nb) {
+      if (blockIdx.x < a.nb && bucket(blockIdx.x)) return;
+    } else {
+      for (uint32_t b = blockIdx.x; b < a.nb; b += gridDim.x)
+        if (bucket(b)) return;
+    }
+    if (blockIdx.x < a.nb) flush_stats(a, acc);
   }
-  if (blockIdx.x < a.nb) flush_stats(a, acc);
 }
 
 // kSkew = false: every bucket whose inbox fits one LDS tile (<= kBucket messages); larger
@@ -3770,6 +3880,9 @@ static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_
   const bool listed = !kSkew && !kWide && a.blist != nullptr;  // (fused / owner: k_dense_fused's marks)
   __shared__ uint32_t s_todo;
   uint32_t acc[kBStats] = {0u, 0u, 0u, 0u, 0u};  // this thread's counters over the block's buckets
+#ifdef AGX_ACC_SHADOW
+  if (lane == kWave - 1) acc_shadow()[w] = 0u;  // (each wave's own slot: no barrier needed)
+#endif
   // (listed after a dense launch that took every bucket: nothing to do past the per-launch work above)
   const uint32_t nwork = kSkew ? *skew_n : (listed && a.dense_left && a.dense_left[wpar] == 0u) ? 0u : a.nb;
   const uint32_t istride = listed ? kListBatch * gridDim.x : gridDim.x;

@@ -37,7 +37,7 @@ constexpr ApplyVariant kVariants[V_N] = {
 
 // pipeline modes: fused single-rank gather (kGather), multi-rank owner grouping (kOwner),
 // single-rank multi-pass with the backlog in place (neither)
-enum : uint32_t { M_FUSED = 0, M_OWNER = 1, M_BYPASS = 2 };
+enum : uint32_t { M_FUSED = 0, M_OWNER = 1, M_BYPASS = 2, M_PERSIST = 3 /* dense launch only: k_dense_fused<.., true> */ };
 
 // variant groups = translation units (agx_apply.hip built with -DAGX_VGROUP=0..kVGroups-1);
 // the heavy CRDT variants are spread so the units take similar time
@@ -51,6 +51,8 @@ hipError_t agx_launch_apply(uint32_t vid, uint32_t mode, bool skew, dim3 grid, h
 hipError_t agx_launch_tiny(uint32_t vid, dim3 grid, hipStream_t s, const BucketArgs& ba);
 // launch k_dense_apply<variant vid's kinds> (mode M_FUSED / M_OWNER: k_dense_fused) (plain / compiled variants only)
 hipError_t agx_launch_dense(uint32_t vid, uint32_t mode, dim3 grid, hipStream_t s, const BucketArgs& ba);
+// resident blocks per CU of the persistent fused dense launch of variant vid (0: not a dense variant)
+hipError_t agx_dense_persist_occupancy(uint32_t vid, int* blocks_per_cu);
 // launch k_ring_apply<variant vid's kinds> (tiny: k_ring_tiny, kTinyThreads) (plain / compiled variants only)
 hipError_t agx_launch_ring(uint32_t vid, bool tiny, dim3 grid, hipStream_t s, const BucketArgs& ba, const RingArgs& ra);
 

@@ -276,6 +276,12 @@ class GpuEngine:
         return {"dev_steps": v[0], "host_steps": v[1], "env_bytes": v[2], "row_bytes": v[3],
                 "rows_on_host": bool(v[4]), "slab": v[5]}
 
+    def persist_info(self) -> dict:
+        """Replays run as one persistent launch and their supersteps (agx_persist_info)."""
+        v = (ctypes.c_uint64 * 2)()
+        check(self.lib.agx_persist_info(self._h, v))
+        return {"launches": v[0], "supersteps": v[1]}
+
     def stats(self) -> Stats:
         st = AgxStats()
         check(self.lib.agx_get_stats(self._h, ctypes.byref(st)))

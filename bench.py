@@ -412,7 +412,12 @@ def main():
     # per superstep; in the fused strict replay a superstep is the dense launch alone, plus one
     # k_replay_out per 8 supersteps): the eager per-class events above add ~3 us of event overhead
     # per launch that rocprofv3 does not see
+    pi0 = eng.persist_info()
     _, graph_ms = eng.run_timed(prof_steps)
+    pi1 = eng.persist_info()
+    # supersteps per persistent launch in that window (0: one launch per superstep)
+    persist_k = ((pi1["supersteps"] - pi0["supersteps"]) / (pi1["launches"] - pi0["launches"])
+                 if pi1["launches"] > pi0["launches"] else 0)
     cfg_words = eng.cfg.n_words
     eng.close()
 
@@ -505,6 +510,16 @@ def main():
                            "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": avg_ms,
                            "avg_launch_ms_eager_events": avg_ms_eager, "graph_superstep_device_ms": graph_step_ms,
                            "superstep_frac": superstep_bytes / step_time / 1e9 / PEAK_HBM_GBS}
+        if persist_k and dom == "bucket_apply_dense":
+            # the replayed supersteps ran as persistent launches of persist_k supersteps each
+            # (k_dense_fused<.., true>, one grid barrier between supersteps): per launch, persist_k x
+            # the superstep's bytes in persist_k x its time -- the same fraction; rocprofv3 shows that
+            # kernel's launches at persist_k x avg_launch_ms (profiles/)
+            out["roofline"].update({"kernel": "bucket_apply_dense (persistent launch, k_dense_fused<KM, false, true>)",
+                                    "supersteps_per_launch": persist_k,
+                                    "alg_bytes_per_launch": alg_bytes * persist_k,
+                                    "avg_launch_ms": avg_ms * persist_k,
+                                    "avg_superstep_ms": avg_ms})
         out["at_100M_actors"] = large
         out["summary"] = summary(out)
         print(json.dumps(out), flush=True)

@@ -349,6 +349,10 @@ agx_status agx_ring_buckets(agx_engine* eng, uint64_t* out);
  * slabs did not fit on some rank (row handle space, AGX_MR_ROW_MB or memory) and every rank moved to
  * the host-planned exchange, out[5] the slab (envelopes per peer per superstep). */
 agx_status agx_exchange_info(agx_engine* eng, uint64_t out[6]);
+/* Persistent fused supersteps (diagnostic): out[0] replays launched as ONE persistent
+ * launch (a strict replay whose supersteps are the dense launch alone: k_dense_fused runs them with a
+ * grid barrier between supersteps; AGX_PERSIST=0 turns it off), out[1] supersteps they ran. */
+agx_status agx_persist_info(agx_engine* eng, uint64_t out[2]);
 
 /* --- per-actor mailboxes (Mailboxes.lookupConfigurator, Mailboxes.scala:204-260) -------------
  * An actor's mailbox type is resolved per actor in the reference (props, then dispatcher, then

@@ -45,28 +45,35 @@ def test_dense_ring_partial_buckets(built, monkeypatch, n, hops, mode):
     assert_same(sg, so, a, b, f"ring n={n} {mode}")
 
 
-@pytest.mark.parametrize("launch", ["1", "0"])
-@pytest.mark.parametrize("n,tokens,hops", [(1_000_000, 1, 6), (300_001, 2, 4), (65_536, 1, 9), (4_099, 1, 5)])
-def test_dense_fused_ring(built, monkeypatch, n, tokens, hops, launch):
+@pytest.mark.parametrize("launch,persist", [("1", "1"), ("1", "0"), ("0", "1")])
+@pytest.mark.parametrize("n,tokens,hops", [(1_000_000, 1, 6), (1_000_000, 1, 37), (300_001, 2, 4), (65_536, 1, 9),
+                                           (4_099, 1, 5)])
+def test_dense_fused_ring(built, monkeypatch, n, tokens, hops, launch, persist):
     """The fused superstep's dense launch (k_dense_fused, default for rings): every bucket of a
     one-token ring is dense -- bucket 0 included, whose wrap-around tell arrives after its own
     (distinct actors, not increasing keys) -- and none of a two-token ring, which the block launch
-    then takes whole."""
+    then takes whole.  persist: a replay of dense-alone strict supersteps as ONE persistent launch
+    (grid barrier between supersteps) or one launch per superstep; 37 hops cross
+    several replays of 8 and 16."""
     monkeypatch.setenv("AGX_DENSE_FUSED", launch)
+    monkeypatch.setenv("AGX_PERSIST", persist)
     sg, so, a, b = run_both(wl.token_ring(n, hops, tokens_per_actor=tokens))
     assert_same(sg, so, a, b, f"fused ring n={n} x{tokens}")
 
 
-@pytest.mark.parametrize("budgets", [(1000,), (5, 3, 1000)])
-def test_dense_fused_recovery(built, budgets):
+@pytest.mark.parametrize("persist", ["1", "0"])
+@pytest.mark.parametrize("budgets", [(1000,), (5, 3, 1000), (17, 9, 1000)])
+def test_dense_fused_recovery(built, monkeypatch, budgets, persist):
     """Dense-alone strict replays (k_dense_fused the whole superstep) meeting a bucket it cannot take:
     a one-token ring with one actor holding a second token -- that pair travels together, so one
     bucket per superstep has two messages for one actor.  The first replay voids from that
     superstep on, run_single runs its block + skew launches, and the engine continues on graphs
     with the block launch beside the dense launch; and the same pair staged between runs of a
     clean ring (its superstep runs eagerly, then the replays recover).  Every budget matches the
-    oracle."""
+    oracle -- with the replays as persistent launches (the void mark crosses the grid barrier) and as
+    one launch per superstep."""
     from oracle import BspOracle
+    monkeypatch.setenv("AGX_PERSIST", persist)
     n, hops = 200_003, 40
     w = wl.token_ring(n, hops)
     dst, src, pay = w.tells

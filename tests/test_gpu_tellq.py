@@ -93,7 +93,7 @@ def test_tell_burst_beyond_capacity_is_delivered(built):
     After every pump: staged + emitted = delivered + dead + in flight, in flight <= msg_capacity."""
     n = 1024
     cap = 4 * n
-    eng = GpuEngine(EngineConfig(n_actors=n, throughput=5, capacity=0, n_words=2, max_emit=1))
+    eng = GpuEngine(EngineConfig(n_actors=n, throughput=5, capacity=0, n_words=2, max_emit=1, msg_capacity=cap))
     eng.register_range(0, n, Kind.COUNTER)
     threads, per = 4, 10 * cap // 4
     rng = np.random.default_rng(11)
@@ -139,7 +139,7 @@ def test_stage_tells_all_or_nothing(built):
     tagged sender (AGX_EINVAL) likewise; a burst that fits is then accepted and delivered."""
     from akka_amd._lib import AgxError
     n = 512
-    eng = GpuEngine(EngineConfig(n_actors=n, throughput=5, capacity=0, n_words=2, max_emit=1))
+    eng = GpuEngine(EngineConfig(n_actors=n, throughput=5, capacity=0, n_words=2, max_emit=1, msg_capacity=4 * n))
     eng.register_range(0, n, Kind.COUNTER)
     eng.tell(np.arange(n, dtype=np.uint32), 1)
     eng.run(1)  # (throughput 5: all n delivered in one superstep; nothing in flight)
