@@ -304,7 +304,7 @@ struct agx_engine {
   // deferred skew launch, then continues with the full graphs (strict_ok cleared for this engine).
   uint32_t* d_abort = nullptr;  // [2] (BucketArgs::abort)
   // persistent fused supersteps (k_dense_fused<.., true>): a captured replay of K dense-alone strict
-  // supersteps is ONE launch with a grid barrier between supersteps (AGX_PERSIST=0: K launches)
+  // supersteps is ONE launch with a grid barrier between supersteps (opt-in, AGX_PERSIST=1; default: K launches)
   int persist = -1;              // -1 not decided yet, 0 off (knob, too many buckets, a barrier timeout), 1 on
   uint32_t persist_steps = 0;    // capture_steps -> launch_apply: supersteps of the persistent launch
   uint32_t persist_vid = ~0u;    // the apply variant `persist` was decided for
@@ -334,6 +334,9 @@ struct agx_engine {
   size_t ev_used = 0;
   double prof_ms[K_NCLASS] = {0};
   uint64_t prof_n[K_NCLASS] = {0};
+  // profiled dense launches (K_DENSE) that took every bucket, read from the device's dense_left words
+  // after the launch: the wave / block launches after them returned at entry (agx_profile_read items)
+  uint64_t prof_items[K_NCLASS] = {0};
 };
 
 namespace {
@@ -805,6 +808,15 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
         HIP_TRY(agx_launch_dense(vid, mode, dim3(grid_for(e->nb, kMaxApplyGrid)), e->stream, bd));
       }
     }
+    if (dl && e->prof && !persist && mode != M_OWNER) {
+      // (profiling only: eager launches) the launch cleared the other parity's word and raised this
+      // one's iff it left a bucket, so both words zero = it took every bucket and the wave / block
+      // launches below return at entry (bench.py marks them returned_at_entry from this count)
+      uint32_t w2[2] = {1u, 1u};
+      HIP_TRY(hipMemcpyAsync(w2, e->d_dense_left, 8, hipMemcpyDeviceToHost, e->stream));
+      HIP_TRY(hipStreamSynchronize(e->stream));
+      if (w2[0] == 0u && w2[1] == 0u) ++e->prof_items[K_DENSE];
+    }
     if (persist) {  // (nothing else runs in a dense-alone strict superstep)
       if (e->persist_steps & 1u) e->par ^= 1u;
       HIP_TRY(hipGetLastError());
@@ -1221,7 +1233,7 @@ agx_status error_status(const agx_engine* e, uint64_t err) {
                    (unsigned long long)e->cap);
   if (err & kErrBarrier)
     return set_err(AGX_EDEVICE, "a persistent superstep launch's grid barrier timed out (not every block was "
-                   "resident); AGX_PERSIST=0 avoids the persistent launch");
+                   "resident); unset AGX_PERSIST to avoid the persistent launch");
   return AGX_OK;
 }
 
@@ -1271,7 +1283,9 @@ agx_status launch_step_single(agx_engine* e) {
 // launch alone runs its K supersteps in ONE launch of k_dense_fused<.., true> -- one block per bucket,
 // a grid barrier between supersteps, the actors' state words kept in registers -- instead of K
 // launches.  Only when all nb blocks are resident at once (the barrier waits for every block): nb <=
-// resident blocks per CU x CUs.  AGX_PERSIST=0 turns it off.
+// resident blocks per CU x CUs.  Opt-in (AGX_PERSIST=1): 3.8x slower than K graph-replayed launches on
+// the 1M ring (47 vs 12.5 us per superstep) -- the grid barrier costs more than a
+// kernel boundary.
 bool persist_ok(agx_engine* e) {
   const uint32_t vid = apply_variant(e);
   if (e->persist >= 0 && e->persist_vid != vid) e->persist = -1;  // (kinds registered since: re-decide)
@@ -1280,7 +1294,7 @@ bool persist_ok(agx_engine* e) {
     e->persist = 0;
     const char* k = getenv("AGX_PERSIST");
     int per_cu = 0, dev = 0, ncu = 0;
-    if ((!k || atoi(k) != 0) && e->R == 1 && e->fused &&
+    if (k && atoi(k) != 0 && e->R == 1 && e->fused &&
         agx_dense_persist_occupancy(vid, &per_cu) == hipSuccess && hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
       e->persist = (uint64_t)e->nb <= (uint64_t)per_cu * (uint64_t)ncu ? 1 : 0;
@@ -3167,6 +3181,7 @@ agx_status agx_profile_reset(agx_engine* e) {
   for (int i = 0; i < K_NCLASS; ++i) {
     e->prof_ms[i] = 0;
     e->prof_n[i] = 0;
+    e->prof_items[i] = 0;
   }
   return AGX_OK;
 }
@@ -3183,7 +3198,7 @@ agx_status agx_profile_read(agx_engine* e, char (*names)[32], double* total_ms, 
     }
     if (total_ms) total_ms[k] = e->prof_ms[i];
     if (launches) launches[k] = e->prof_n[i];
-    if (items) items[k] = 0;
+    if (items) items[k] = e->prof_items[i];
   }
   if (n) *n = K_NCLASS;
   return AGX_OK;

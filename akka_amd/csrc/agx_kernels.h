@@ -4152,7 +4152,11 @@ static __global__ void __launch_bounds__(kBThreads, kWide ? AGX_WIDE_WPE : 4) k_
       if (bad) atomicOr(&s_flags, bad);
       __syncthreads();
       const uint32_t flags = s_flags;
+#ifdef AGX_PRESORT_WGRED  // diagnostic build knob: round 4's ockl workgroup reduction
+      const bool presorted = __syncthreads_and(!(bad & 1u)) != 0;
+#else
       const bool presorted = !(flags & 1u);
+#endif
       if (kDense && !(flags & 2u) && a.kmax == 1) {
         dense_finish<KM, kGather, kOwner>(a, L, b, lo, cnt, a0, wpar, acc, kEarly ? ex0 : nullptr, kEarly ? ex1 : nullptr);
         continue;

@@ -334,7 +334,8 @@ class GpuEngine:
         check(self.lib.agx_profile_read(self._h, names, ms, launches, items, cap, ctypes.byref(n)))
         out = {}
         for i in range(min(n.value, cap)):
-            out[bytes(names[i]).split(b"\0")[0].decode()] = {"total_ms": ms[i], "launches": int(launches[i])}
+            out[bytes(names[i]).split(b"\0")[0].decode()] = {"total_ms": ms[i], "launches": int(launches[i]),
+                                                             "items": int(items[i])}
         return out
 
 

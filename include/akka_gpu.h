@@ -351,7 +351,7 @@ agx_status agx_ring_buckets(agx_engine* eng, uint64_t* out);
 agx_status agx_exchange_info(agx_engine* eng, uint64_t out[6]);
 /* Persistent fused supersteps (diagnostic): out[0] replays launched as ONE persistent
  * launch (a strict replay whose supersteps are the dense launch alone: k_dense_fused runs them with a
- * grid barrier between supersteps; AGX_PERSIST=0 turns it off), out[1] supersteps they ran. */
+ * grid barrier between supersteps; opt-in: AGX_PERSIST=1), out[1] supersteps they ran. */
 agx_status agx_persist_info(agx_engine* eng, uint64_t out[2]);
 
 /* --- per-actor mailboxes (Mailboxes.lookupConfigurator, Mailboxes.scala:204-260) -------------
@@ -422,7 +422,10 @@ agx_status agx_exchange_plan(const uint64_t* mat, uint32_t n_ranks, uint32_t ran
 /* --- measurement ----------------------------------------------------------- */
 /* Per-kernel HIP-event timing on the engine's stream (off by default).      */
 agx_status agx_profile_enable(agx_engine* eng, int on);
-/* Fills up to `cap` entries; returns the number of kernel classes in *n.     */
+/* Fills up to `cap` entries; returns the number of kernel classes in *n.
+ * items[k]: for "bucket_apply_dense", the profiled dense launches that took
+ * every bucket (read from the device's dense_left flags after each launch:
+ * the wave / block launches of those supersteps returned at entry); 0 else. */
 agx_status agx_profile_read(agx_engine* eng, char (*names)[32], double* total_ms,
                             uint64_t* launches, uint64_t* items, uint32_t cap, uint32_t* n);
 agx_status agx_profile_reset(agx_engine* eng);

@@ -73,17 +73,25 @@ def test_bench_kernel_rooflines():
 
 def test_bench_rooflines_after_a_dense_launch():
     """At 100M the block launch follows the dense launch and returns at entry when it took every
-    bucket: the block class gets no fraction (it would read > 1 of peak), the dense class keeps its own."""
+    bucket -- as the device's dense_left flags say (agx_profile_read items: the profiled dense launches
+    that took every bucket), not as a > peak rate suggests: the block class then gets no fraction, the
+    dense class keeps its own.  When the flags say a dense launch left buckets, the block class keeps its
+    number (a fraction > 1 stays visible instead of being relabelled)."""
     sys.path.insert(0, str(ROOT))
     import bench
     per = bench.kernel_bytes_per_msg(1)
-    prof = {"bucket_apply_dense": {"total_ms": 16.8, "launches": 25}, "bucket_apply": {"total_ms": 0.19, "launches": 25}}
+    prof = {"bucket_apply_dense": {"total_ms": 16.8, "launches": 25, "items": 25},
+            "bucket_apply": {"total_ms": 0.19, "launches": 25, "items": 0}}
     rr = bench.kernel_rooflines(prof, per, 100_000_000, identity=True)
     r = rr["kernels"]
     assert rr["dominant"] == "bucket_apply_dense"
     assert r["bucket_apply"] == {"returned_at_entry": True, "avg_launch_ms": 0.0076,
-                                 "reason": "the dense launch before it took every bucket"}
+                                 "reason": "the dense launch before it took every bucket (device dense_left flags)"}
     assert 0 < r["bucket_apply_dense"]["frac"] < 1
+    # one profiled dense launch left a bucket: the block launch did work in that superstep
+    prof["bucket_apply_dense"]["items"] = 24
+    r1 = bench.kernel_rooflines(prof, per, 100_000_000, identity=True)["kernels"]
+    assert "returned_at_entry" not in r1["bucket_apply"] and r1["bucket_apply"]["frac"] > 1
     # without a dense launch in the profile the same numbers stay a (bad) fraction, not hidden
     r2 = bench.kernel_rooflines({"bucket_apply": prof["bucket_apply"]}, per, 100_000_000)["kernels"]
     assert r2["bucket_apply"]["frac"] > 1

@@ -138,3 +138,26 @@ def test_dense_sharded_loopback(built, monkeypatch, ranks, case, launch):
         wg[own] = st[own]
         e.close()
     assert np.array_equal(wg, wo)
+
+
+@pytest.mark.parametrize("tokens", [1, 2])
+def test_profile_counts_dense_launches_that_took_every_bucket(built, monkeypatch, tokens):
+    """agx_profile_read's items for bucket_apply_dense: the profiled dense launches after which the
+    device's dense_left flags were both clear (the wave / block launches returned at entry; bench.py
+    marks them returned_at_entry from this count, not from a rate).  A one-token ring (multi-pass,
+    3-bit digits) leaves no bucket; a two-token ring leaves every bucket to the block launch."""
+    monkeypatch.setenv("AGX_RADIX_BITS", "3")
+    w = wl.token_ring(40_000, 12, tokens_per_actor=tokens)
+    eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
+    w.apply_to(eng)
+    eng.run(2)
+    eng.profile(True)
+    eng.profile_reset()
+    eng.run(4)
+    p = eng.profile_read()
+    eng.profile(False)
+    eng.close()
+    d = p["bucket_apply_dense"]
+    assert d["launches"] == 4
+    assert d["items"] == (4 if tokens == 1 else 0)
+    assert all(v["items"] == 0 for k, v in p.items() if k != "bucket_apply_dense")

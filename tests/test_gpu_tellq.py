@@ -126,7 +126,7 @@ def test_tell_burst_beyond_capacity_is_delivered(built):
     assert pumps >= 10  # (10x the capacity: at least 10 pumps)
     assert st.staged == threads * per and st.delivered == threads * per and st.dead_letters == 0
     assert st.in_flight == 0
-    w = eng.read_state()[0]
+    w = eng.read_state()[0].T  # (actor-major rows -> word-major)
     allp = np.concatenate(dsts)
     cnt = np.bincount(allp, minlength=n)
     assert np.array_equal(w[0], cnt.astype(np.uint64))
@@ -175,12 +175,12 @@ def test_pump_budget_reschedules_and_cancel(built):
         if again and pumps == 1:
             assert not eng.tell_one(8, 1)  # still scheduled: no second pump
     assert pumps == 20
-    w = eng.read_state()[0]
+    w = eng.read_state()[0].T  # (actor-major rows -> word-major)
     assert w[0][7] == 100 and w[1][7] == 5050 and w[0][8] == 1
     assert eng.tell_one(9, 1)
     eng.pump_cancel()
     assert eng.tell_one(9, 2)  # idle again after the cancel: this tell submits
     eng.run()
     assert not eng.pump_idle()
-    assert eng.read_state()[0][0][9] == 2
+    assert eng.read_state()[0][9][0] == 2
     eng.close()
