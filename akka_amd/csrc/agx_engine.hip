@@ -225,10 +225,11 @@ struct agx_engine {
   hipEvent_t tev[2] = {nullptr, nullptr};  // agx_run_timed: device time of a run (engine stream)
   bool timing = false;
   bool dense_fused = true;  // the dense launch also in the fused superstep (AGX_DENSE_FUSED=0: not)
-  // the dense launch in the multi-rank (owner-grouping) superstep: opt-in (AGX_DENSE_OWNER=1) --
-  // loopback R = 2 / 8 x 1M measured no gain (241 vs 236 us per group superstep at R = 2): the owner
-  // apply already takes dense buckets in-kernel (dense_finish), and the extra block launch costs more
-  bool dense_owner = false;
+  // the dense launch in the multi-rank (owner-grouping) superstep (AGX_DENSE_OWNER=0: not).  Round 6:
+  // owner classes placed straight from registers (no staged multisplit) and the dense_left shortcut
+  // (the block launch returns at entry when it took every bucket): R = 8 x 1M loopback, one hardware
+  // queue, apply 32.7 us (block launch) -> 19.9 + 5.6 us (dense + returning block launch) per rank-step
+  bool dense_owner = true;
   bool dense_alone = true;  // fused strict replays: the dense launch alone (cleared at its first recovery)
   bool recover_dense = false;  // run_single's recovery of a dense-alone superstep: the block + skew launches
   int dense_launch = -1;  // k_dense_apply before the block launch: 1 on, 0 off, -1 (default) ring populations
@@ -783,7 +784,8 @@ agx_status launch_apply(agx_engine* e, const DevMsgs& sorted) {
     const bool alone = dl && mode == M_FUSED && e->strict_cap && e->dense_alone;
     if (dl || e->recover_dense) {
       ba.blist = e->d_blist;
-      if (mode != M_OWNER) ba.dense_left = e->d_dense_left;  // (owner mode: one parity only -- no shortcut)
+      // (owner mode: one word, [0] -- cleared by the superstep's k_mcompact_scan, before the dense launch)
+      ba.dense_left = e->d_dense_left;
     }
     const bool persist = dl && alone && e->persist_steps > 0;
     if (dl) {
@@ -1099,6 +1101,7 @@ agx_status phase1(agx_engine* e) {
   m.tstride = e->tstride;
   m.n_staged = e->n_staged_dev;
   m.halt = e->d_halt;  // (multi-rank only; zero outside device-resident replays)
+  m.dense_left = e->d_dense_left;
   {
     Scope s(e, K_MCOMPACT);
     hipLaunchKernelGGL(k_mcompact_scan, dim3(1), dim3(kScanThreads), 0, e->stream, m);

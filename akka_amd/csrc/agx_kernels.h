@@ -2969,6 +2969,8 @@ static __global__ void __launch_bounds__(kDenseThreads, kPersist ? 4 : 2) k_dens
   __shared__ uint32_t s_nh[kRadix];                                     // tells per destination bucket
   __shared__ uint32_t scratch[2 * (kDenseWaves + 1)];
   __shared__ uint32_t s_cnt[kDenseIpt * kDenseWaves];
+  // (owner mode) tells per (owner class, row, wave), class-major -> their exclusive prefix
+  __shared__ uint32_t s_oc[kOwner ? AGX_MAX_RANKS * kDenseIpt * kDenseWaves : 1];
   __shared__ uint32_t s_g[2], s_bad, s_dmin, s_dmax, s_ok;
   static_assert(4 * kRadix >= kBucket && kDenseThreads == kBThreads && kDenseIpt == kBIpt, "group_tells' shapes");
   const BucketLds L{s_ks, s_ks + kBucket, nullptr, U, nullptr, s_hit, nullptr, nullptr, s_nh, scratch, nullptr, nullptr};
@@ -3190,85 +3192,130 @@ static __global__ void __launch_bounds__(kDenseThreads, kPersist ? 4 : 2) k_dens
       tk[r] = em.key;
       tp[r] = em.pay;
     }
-    // ---- tells in actor order, grouped by destination bucket.  Two classes: digit X (this bucket's
-    // own index) and the rest.  Ranks of both from one packed scan of per (row, wave) ballot counts;
-    // when the rest share ONE digit (a ring, a stencil: the bucket's tells go to itself and one
-    // neighbour) each tell's grouped slot follows directly -- no LDS staging, no multisplit; any
-    // other mix stages the tells in sender order and takes group_tells (the block path's grouping).
-    const uint32_t X = b & nhmask;
-    uint32_t dg[kDenseIpt], rkA[kDenseIpt], rkB[kDenseIpt];
+    if constexpr (kOwner) {
+      // ---- (multi-rank) tells in actor order, grouped by OWNER rank (digit = key >> kOwnerShift, at most
+      // AGX_MAX_RANKS classes): per (class, row, wave) ballot counts, one block scan in class-major /
+      // sender order, each tell written at its slot straight from registers -- the stable owner
+      // partition that group_tells' staged multisplit produced, without the LDS staging and
+      // histogram passes (hash-sharded mail goes to every owner: the two-class shortcut below never
+      // applies)
+      const uint32_t nd = 1u << a.nx_bits;
+      uint32_t dg[kDenseIpt], rk[kDenseIpt];
 #pragma unroll
-    for (int r = 0; r < kDenseIpt; ++r) {
-      dg[r] = (tk[r] >> a.nx_shift) & nhmask;
-      const uint64_t ma = __ballot(tv[r] && dg[r] == X), mb = __ballot(tv[r] && dg[r] != X);
-      rkA[r] = (uint32_t)__popcll(ma & ltm);
-      rkB[r] = (uint32_t)__popcll(mb & ltm);
-      if (lane == 0) s_cnt[r * kDenseWaves + w] = (uint32_t)__popcll(ma) | ((uint32_t)__popcll(mb) << 16);
-      if (tv[r] && dg[r] != X) {
-        atomicMin(&s_dmin, dg[r]);
-        atomicMax(&s_dmax, dg[r]);
+      for (int r = 0; r < kDenseIpt; ++r) {
+        dg[r] = (tk[r] >> a.nx_shift) & nhmask;
+        rk[r] = 0u;
+        for (uint32_t c = 0; c < nd; ++c) {
+          const uint64_t m = __ballot(tv[r] && dg[r] == c);
+          if (dg[r] == c) rk[r] = (uint32_t)__popcll(m & ltm);
+          if (lane == 0) s_oc[(c * kDenseIpt + r) * kDenseWaves + w] = (uint32_t)__popcll(m);
+        }
       }
-    }
-    __syncthreads();
-    AGX_STAMP(a, 5);
-    AGX_STAMP(a, 6);
-    static_assert(kDenseIpt * kDenseWaves <= kWave, "one lane per (row, wave) count");
-    const uint32_t c = lane < (uint32_t)(kDenseIpt * kDenseWaves) ? s_cnt[lane] : 0u;
-    const uint32_t inc = wave_incl_sum(c);  // (packed halves: each class <= kBucket < 2^16, no carry)
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-    const uint32_t totA = tot & 0xFFFFu, totB = tot >> 16, emtot = totA + totB;
-    uint32_t preA[kDenseIpt], preB[kDenseIpt];
-#pragma unroll
-    for (int r = 0; r < kDenseIpt; ++r) {
-      const int gi = r * kDenseWaves + (int)w;  // (wave-uniform lane index)
-      const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)(inc - c), gi);
-      preA[r] = ex & 0xFFFFu;
-      preB[r] = ex >> 16;
-    }
-    const uint32_t dmin = s_dmin, dmax = s_dmax;
-    const uint64_t embase = (uint64_t)lo * a.kmax;
-    if (totB == 0 || dmin == dmax) {  // (uniform) at most two destination buckets
-      const bool bfirst = totB && dmin < X;  // grouped runs in digit order
-      const uint32_t baseA = bfirst ? totB : 0u, baseB = bfirst ? 0u : totA;
+      __syncthreads();
+      static_assert(AGX_MAX_RANKS * kDenseIpt * kDenseWaves <= kDenseThreads, "one (class, row, wave) entry per thread");
+      const uint32_t ent = nd * kDenseIpt * kDenseWaves;
+      const uint32_t v = tid < ent ? s_oc[tid] : 0u;
+      uint32_t emtot;
+      const uint32_t ex = block_excl_sum<kDenseThreads>(v, scratch, &emtot);  // (syncs: every v read)
+      if (tid < ent) s_oc[tid] = ex;
+      __syncthreads();
+      const uint64_t embase = (uint64_t)ib * a.kmax;
+      constexpr uint32_t kPer = kDenseIpt * kDenseWaves;  // entries per class
+      if (tid < nd) {  // this bucket's run for owner tid (only non-zero entries: k_mcompact_copy clears them)
+        const uint32_t b0 = s_oc[tid * kPer], b1 = tid + 1 < nd ? s_oc[(tid + 1) * kPer] : emtot;
+        if (b1 > b0) {
+          g.tcnt[wpar][(size_t)tid * g.tstride + b] = b1 - b0;
+          g.toff[wpar][(size_t)tid * g.tstride + b] = (uint32_t)embase + b0;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < kDenseIpt; ++r)
         if (tv[r]) {
-          const uint64_t o = embase + (dg[r] == X ? baseA + preA[r] + rkA[r] : baseB + preB[r] + rkB[r]);
+          const uint64_t o = embase + s_oc[(dg[r] * kDenseIpt + r) * kDenseWaves + w] + rk[r];
           st32x(g.eg[wpar].key, o, tk[r]);
           st32x(g.eg[wpar].src, o, gs[r]);
           st32x(g.eg[wpar].pay, o, tp[r]);
         }
-      if (tid == 0 && totA) {
-        g.tcnt[wpar][(size_t)X * g.tstride + b] = totA;
-        g.toff[wpar][(size_t)X * g.tstride + b] = (uint32_t)embase + baseA;
-      }
-      if (tid == 1 && totB) {
-        g.tcnt[wpar][(size_t)dmin * g.tstride + b] = totB;
-        g.toff[wpar][(size_t)dmin * g.tstride + b] = (uint32_t)embase + baseB;
-      }
       if (tid == 0 && g.emc[wpar]) g.emc[wpar][b] = emtot;
-    } else {  // sender order (rank among all tells) in U, per-destination counts, group_tells
-      uint32_t* const ukey = reinterpret_cast<uint32_t*>(U);
-#pragma unroll
-      for (int r = 0; r < kDenseIpt; ++r)
-        if (tv[r]) {
-          const uint32_t q = preA[r] + rkA[r] + preB[r] + rkB[r];
-          ukey[q] = tk[r];
-          ukey[kBucket + q] = gs[r];
-          ukey[2 * kBucket + q] = tp[r];
-          lds_hist_inc(s_nh, dg[r]);
-        }
-      __syncthreads();
-      group_tells<true>(a, L, b, wpar, embase, emtot, a.em);
-    }
-    AGX_STAMP(a, 7);
-    if (tid == 0) {
-      a.blist[b] = 0u;
-      if constexpr (kOwner) {  // the bucket's tell chunk (in-flight accounting)
+      if (tid == 0) {  // the bucket's tell chunk (in-flight accounting)
         a.chunk_off[a.nb + b] = (uint32_t)embase;
         a.chunk_cnt[a.nb + b] = emtot;
       }
+    } else {
+      // ---- tells in actor order, grouped by destination bucket.  Two classes: digit X (this bucket's
+      // own index) and the rest.  Ranks of both from one packed scan of per (row, wave) ballot counts;
+      // when the rest share ONE digit (a ring, a stencil: the bucket's tells go to itself and one
+      // neighbour) each tell's grouped slot follows directly -- no LDS staging, no multisplit; any
+      // other mix stages the tells in sender order and takes group_tells (the block path's grouping).
+      const uint32_t X = b & nhmask;
+      uint32_t dg[kDenseIpt], rkA[kDenseIpt], rkB[kDenseIpt];
+  #pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r) {
+        dg[r] = (tk[r] >> a.nx_shift) & nhmask;
+        const uint64_t ma = __ballot(tv[r] && dg[r] == X), mb = __ballot(tv[r] && dg[r] != X);
+        rkA[r] = (uint32_t)__popcll(ma & ltm);
+        rkB[r] = (uint32_t)__popcll(mb & ltm);
+        if (lane == 0) s_cnt[r * kDenseWaves + w] = (uint32_t)__popcll(ma) | ((uint32_t)__popcll(mb) << 16);
+        if (tv[r] && dg[r] != X) {
+          atomicMin(&s_dmin, dg[r]);
+          atomicMax(&s_dmax, dg[r]);
+        }
+      }
+      __syncthreads();
+      AGX_STAMP(a, 5);
+      AGX_STAMP(a, 6);
+      static_assert(kDenseIpt * kDenseWaves <= kWave, "one lane per (row, wave) count");
+      const uint32_t c = lane < (uint32_t)(kDenseIpt * kDenseWaves) ? s_cnt[lane] : 0u;
+      const uint32_t inc = wave_incl_sum(c);  // (packed halves: each class <= kBucket < 2^16, no carry)
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+      const uint32_t totA = tot & 0xFFFFu, totB = tot >> 16, emtot = totA + totB;
+      uint32_t preA[kDenseIpt], preB[kDenseIpt];
+  #pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r) {
+        const int gi = r * kDenseWaves + (int)w;  // (wave-uniform lane index)
+        const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)(inc - c), gi);
+        preA[r] = ex & 0xFFFFu;
+        preB[r] = ex >> 16;
+      }
+      const uint32_t dmin = s_dmin, dmax = s_dmax;
+      const uint64_t embase = (uint64_t)lo * a.kmax;
+      if (totB == 0 || dmin == dmax) {  // (uniform) at most two destination buckets
+        const bool bfirst = totB && dmin < X;  // grouped runs in digit order
+        const uint32_t baseA = bfirst ? totB : 0u, baseB = bfirst ? 0u : totA;
+  #pragma unroll
+        for (int r = 0; r < kDenseIpt; ++r)
+          if (tv[r]) {
+            const uint64_t o = embase + (dg[r] == X ? baseA + preA[r] + rkA[r] : baseB + preB[r] + rkB[r]);
+            st32x(g.eg[wpar].key, o, tk[r]);
+            st32x(g.eg[wpar].src, o, gs[r]);
+            st32x(g.eg[wpar].pay, o, tp[r]);
+          }
+        if (tid == 0 && totA) {
+          g.tcnt[wpar][(size_t)X * g.tstride + b] = totA;
+          g.toff[wpar][(size_t)X * g.tstride + b] = (uint32_t)embase + baseA;
+        }
+        if (tid == 1 && totB) {
+          g.tcnt[wpar][(size_t)dmin * g.tstride + b] = totB;
+          g.toff[wpar][(size_t)dmin * g.tstride + b] = (uint32_t)embase + baseB;
+        }
+        if (tid == 0 && g.emc[wpar]) g.emc[wpar][b] = emtot;
+      } else {  // sender order (rank among all tells) in U, per-destination counts, group_tells
+        uint32_t* const ukey = reinterpret_cast<uint32_t*>(U);
+  #pragma unroll
+        for (int r = 0; r < kDenseIpt; ++r)
+          if (tv[r]) {
+            const uint32_t q = preA[r] + rkA[r] + preB[r] + rkB[r];
+            ukey[q] = tk[r];
+            ukey[kBucket + q] = gs[r];
+            ukey[2 * kBucket + q] = tp[r];
+            lds_hist_inc(s_nh, dg[r]);
+          }
+        __syncthreads();
+        group_tells<true>(a, L, b, wpar, embase, emtot, a.em);
+      }
     }
+    AGX_STAMP(a, 7);
+    if (tid == 0) a.blist[b] = 0u;
     __syncthreads();  // (the bucket's LDS arrays are reset by the next one)
     AGX_STAMP(a, 8);
     return false;
@@ -4466,6 +4513,8 @@ struct McompactArgs {
   uint64_t cap0, cap1;
   uint32_t R, tstride, n_staged;
   const uint32_t* halt;  // device-resident replays: [0] != 0 = stopped (k_mr_pack), every kernel returns
+  uint32_t* dense_left;  // owner mode's one dense_left word (BucketArgs::dense_left[0]): cleared here, before
+                         // this superstep's dense launch raises it for a bucket it leaves to the block launch
 };
 
 static __global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactArgs a) {
@@ -4475,6 +4524,7 @@ static __global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactA
   begin_step(a.step, a.heap_top);
   commit_stops(a.alive, a.stopq, a.nstop);
   if (threadIdx.x == 0) *a.skew_n = 0u;
+  if (threadIdx.x == 0 && a.dense_left) a.dense_left[0] = 0u;
   const uint64_t nbl = block_scan_table<kScanThreads>(a.ch.cnt, a.off0, 1, a.ch.nb, a.ch.nb, scratch, nullptr);
   const uint64_t ntl = block_scan_table<kScanThreads>(a.tcnt, a.off1, a.R, a.ch.nb, a.tstride, scratch, s_obase);
   const uint32_t tid = threadIdx.x;
