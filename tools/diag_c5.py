@@ -40,4 +40,5 @@ for i in range(a.steps):
     s1 = eng.run(1)
     p = eng.profile_read()
     print("step", i, "delivered", s1.delivered - s0.delivered, "dead", s1.dead_letters - s0.dead_letters,
+          "in_flight", s1.in_flight, "ring_buckets", eng.ring_buckets() if hasattr(eng, "ring_buckets") else None,
           {k: round(v["total_ms"], 3) for k, v in p.items() if v["launches"]}, flush=True)
