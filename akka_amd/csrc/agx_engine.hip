@@ -2946,6 +2946,28 @@ agx_status agx_run(agx_engine* e, uint32_t max_supersteps, agx_stats* out) {
     for (size_t i = 0; i < std::min<size_t>(6, slow.size()); ++i)
       fprintf(stderr, " %llu:%llu:%llu", slow[i].first, h[slow[i].second * 16 + 11], h[slow[i].second * 16 + 12]);
     fprintf(stderr, "\n");
+    {  // device-clock (100 MHz) block start / end offsets within the launch (k_dense_fused only: slots 13 / 14)
+      std::vector<double> st, en;
+      unsigned long long s0 = ~0ull;
+      for (uint64_t b = 0; b < nbk; ++b)
+        if (h[b * 16 + 13] && h[b * 16 + 14]) s0 = std::min(s0, h[b * 16 + 13]);
+      for (uint64_t b = 0; b < nbk; ++b)
+        if (h[b * 16 + 13] && h[b * 16 + 14]) {
+          st.push_back((h[b * 16 + 13] - s0) * 0.01);
+          en.push_back((h[b * 16 + 14] - s0) * 0.01);
+        }
+      if (!st.empty()) {
+        std::vector<double> du(st.size());
+        for (size_t i = 0; i < st.size(); ++i) du[i] = en[i] - st[i];
+        std::sort(st.begin(), st.end());
+        std::sort(en.begin(), en.end());
+        std::sort(du.begin(), du.end());
+        auto q = [](const std::vector<double>& v, double f) { return v[std::min(v.size() - 1, (size_t)(f * v.size()))]; };
+        fprintf(stderr, "[agx stamps] block start us (p0/p50/p90/max): %.2f %.2f %.2f %.2f | end: %.2f %.2f %.2f %.2f | "
+                "duration: %.2f %.2f %.2f %.2f\n", q(st, 0), q(st, .5), q(st, .9), st.back(), q(en, 0), q(en, .5), q(en, .9),
+                en.back(), q(du, 0), q(du, .5), q(du, .9), du.back());
+      }
+    }
     HIP_TRY(hipMemsetAsync(e->d_dbg, 0, h.size() * 8, e->stream));
   }
   // out == NULL: no counter read-back (one stream round trip less; agx_get_stats reads them

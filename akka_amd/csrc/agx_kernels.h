@@ -1142,6 +1142,12 @@ __device__ __forceinline__ InView in_view(const BucketArgs& a) {
   do {                                                                                            \
     if ((a).dbg && threadIdx.x == 0) (a).dbg[blockIdx.x * 16 + (idx)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// (diagnostic, with AGX_STAMPS) the device-wide 100 MHz clock at a block's start / end, slots 13 / 14:
+// when blocks start and finish within a launch (s_memtime is per-XCD and cannot be compared across blocks)
+#define AGX_RTSTAMP(a, idx)                                                                        \
+  do {                                                                                            \
+    if ((a).dbg && threadIdx.x == 0) (a).dbg[blockIdx.x * 16 + (idx)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
 struct BucketLds {
   uint32_t* key;   // fast path: sorted items (LDS); general path: run / tmp scratch
@@ -3018,6 +3024,7 @@ static __global__ void __launch_bounds__(kDenseThreads, kPersist ? 4 : 2) k_dens
   // fused launch: nb <= kDenseThreads) it runs once, outside a loop: the waitcnt pass then has no back
   // edge whose pending loads it must assume, and the row / flag / state loads issue back to back
   const auto bucket = [&](const uint32_t b) -> bool {
+    AGX_RTSTAMP(a, 13);
     AGX_STAMP(a, 0);
     const uint32_t a0 = b << a.bb, na = min(1u << a.bb, P.n_local - a0);
     uint32_t* const segp = reinterpret_cast<uint32_t*>(U);  // [nseg + 1] inbox start of each tell segment
@@ -3161,6 +3168,31 @@ static __global__ void __launch_bounds__(kDenseThreads, kPersist ? 4 : 2) k_dens
 #pragma unroll
     for (int r = 0; r < kDenseIpt; ++r)  // (pinned here: the compiler would sink each read into its use, one wait each)
       asm volatile("" : "+v"(hv[r]), "+v"(svv[r]), "+v"(pvv[r]));
+    if constexpr (KM == kb(AGX_KIND_RING)) {
+      // RING-only populations (the C2 token ring): apply_msg<RING> through RegEmitter, branch-free --
+      // w[0] += 1, Behaviors.same, one tell to self + stride while hops are left.  Its destination is
+      // always in range (self < n_global, stride pre-reduced), so never a host actor or a dead letter;
+      // an actor that is not alive gets a dead letter.  (The generic per-actor dispatch below issued
+      // ~200 instructions per actor -- exec-mask branches, kernel-argument reloads -- and made this
+      // phase the block's longest: 4.6 K of 16 K cycles.)  Word 1 is untouched, so not stored.
+      const uint32_t stride = P.ring_stride, ng = P.n_global;
+#pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r) {
+        const uint32_t la = r * kDenseThreads + tid, l = a0 + la;
+        const bool has = la < na && hv[r] != 0u, live = (ab[r] & 1u) != 0u, on = has && live;
+        const bool em = on && pvv[r] > 0u;
+        acc[0] += on ? 1u : 0u;
+        acc[4] += on ? 1u : 0u;
+        acc[1] += has && !live ? 1u : 0u;
+        acc[3] += em ? 1u : 0u;
+        uint32_t d = gs[r] + stride;
+        d = d >= ng ? d - ng : d;
+        tv[r] = em;
+        tk[r] = em ? (kOwner ? P.route[d] : d) : 0u;
+        tp[r] = em ? pvv[r] - 1u : 0u;
+        if (on) st64x(P.state, l * P.sa, x0[r] + 1ull);
+      }
+    } else {
 #pragma unroll
     for (int r = 0; r < kDenseIpt; ++r) {
       const uint32_t la = r * kDenseThreads + tid, l = a0 + la;
@@ -3191,6 +3223,7 @@ static __global__ void __launch_bounds__(kDenseThreads, kPersist ? 4 : 2) k_dens
       tv[r] = em.n_valid != 0u;
       tk[r] = em.key;
       tp[r] = em.pay;
+    }
     }
     if constexpr (kOwner) {
       // ---- (multi-rank) tells in actor order, grouped by OWNER rank (digit = key >> kOwnerShift, at most
@@ -3317,6 +3350,7 @@ static __global__ void __launch_bounds__(kDenseThreads, kPersist ? 4 : 2) k_dens
     AGX_STAMP(a, 7);
     if (tid == 0) a.blist[b] = 0u;
     __syncthreads();  // (the bucket's LDS arrays are reset by the next one)
+    AGX_RTSTAMP(a, 14);
     AGX_STAMP(a, 8);
     return false;
   };
