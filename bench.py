@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--cpu-hops", type=int, default=96, help="hop budget of the bounded CPU sample")
     ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (N=1 only)")
     ap.add_argument("--quick-configs", action="store_true", help="C5 at 10M instead of 100M actors")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_r05.json"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_r06.json"),
                     help="PMC traffic summary written by profiles/collect_pmc.py")
     return ap.parse_args()
 
@@ -318,12 +318,12 @@ def other_configs(quick: bool, only: str = "") -> dict:
             lambda: wl.ping_pong(1000, messages_per_pair=2_000_000, throughput=50), 16, 400, 1 << 20),
     }
     out = {}
-    # counted HBM bytes per superstep of the same window (profiles/pmc_r05.json "configs", from the
+    # counted HBM bytes per superstep of the same window (profiles/pmc_r06.json "configs", from the
     # rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/cfg_one.py): the fraction on the bytes the
     # kernels actually moved, beside the one on the algorithmic model (C4 ORSet's sparse rows move
     # fewer bytes than its dense-state model; C5 / C3 far more)
     try:
-        counted = json.loads((ROOT / "profiles" / "pmc_r05.json").read_text()).get("configs", {})
+        counted = json.loads((ROOT / "profiles" / "pmc_r06.json").read_text()).get("configs", {})
     except Exception:
         counted = {}
     for name, (desc, make, warm, steps, mcap) in specs.items():
