@@ -180,6 +180,7 @@ struct agx_engine {
   // rank agreed that the CRDT row slabs do not fit (mr_slabs) -- the host-planned path from then on
   uint64_t mr_dev_steps = 0, mr_host_steps = 0, mr_sent_env = 0, mr_sent_rows = 0;
   bool mr_host = false;
+  bool mr_direct = false;  // the last device-resident superstep wrote its peer runs straight into the send slabs
 
   DevMsgs A, B, scr, bl, em, stg, s2;
   // single-rank multi-pass: the tell arena by superstep parity (em = even, em2 = odd superstep
@@ -1076,7 +1077,9 @@ agx_status prepare_run(agx_engine* e) {
 // phase 1: backlog chunks -> front of A; the apply's owner-grouped tells -> s2, owner-major
 // (the stable owner partition of the tells in chunk order); count vector
 // [send counts..., n_backlog, n_staged] for the all-gather.
-agx_status phase1(agx_engine* e) {
+// direct: the device-resident replay of plain behaviours -- the peers' runs go straight into their send
+// slabs (k_mcompact_copy), k_mr_pack copies only the own run
+agx_status phase1(agx_engine* e, bool direct = false) {
   McompactArgs m{};
   m.ch = make_chunks(e);
   m.eg = e->eg0.c();
@@ -1102,6 +1105,9 @@ agx_status phase1(agx_engine* e) {
   m.n_staged = e->n_staged_dev;
   m.halt = e->d_halt;  // (multi-rank only; zero outside device-resident replays)
   m.dense_left = e->d_dense_left;
+  m.sslab = direct ? e->d_sslab : nullptr;
+  m.slab = e->slab;
+  m.rank = e->rank;
   {
     Scope s(e, K_MCOMPACT);
     hipLaunchKernelGGL(k_mcompact_scan, dim3(1), dim3(kScanThreads), 0, e->stream, m);
@@ -1809,7 +1815,8 @@ agx_status capture_mr(agx_engine* e, uint32_t steps) {
 // slabs (k_mr_pack), one fixed-size send / receive per peer, unpack, bucket passes, apply
 agx_status mr_step_dev(agx_engine* e, uint32_t idx) {
   const uint32_t S = e->R + 2;
-  AGX_TRY(phase1(e));
+  const bool direct = e->pw == 0 && !getenv("AGX_MR_NO_DIRECT");  // (CRDT rows are laid out beside s2's tells)
+  AGX_TRY(phase1(e, direct));
   MrArgs a{};
   a.cmat = e->d_cmat;
   a.s2 = e->s2.c();
@@ -1828,6 +1835,8 @@ agx_status mr_step_dev(agx_engine* e, uint32_t idx) {
   a.srows = e->d_srows;
   a.pw = e->pw;
   a.heap_rows = (uint32_t)e->heap_rows;
+  a.direct = direct ? 1u : 0u;
+  e->mr_direct = direct;
   const dim3 g(grid_for((uint64_t)e->R * e->slab / kThreads + 1, 2048));
   {
     Scope sc(e, K_EXCHANGE);
@@ -1968,6 +1977,12 @@ agx_status run_multi_rccl(agx_engine* e, uint32_t max_steps) {
         return set_err(AGX_ECAPACITY, "rank %u: messages in flight exceed capacity %llu", e->rank,
                        (unsigned long long)e->cap);
       // a sender -> receiver count over the slab: this superstep's exchange exactly, bigger slabs
+      if (e->mr_direct) {  // (its peer runs went into the slabs: back into s2 for the exact exchange)
+        hipLaunchKernelGGL(k_slab_to_s2, dim3(grid_for((uint64_t)e->R * e->slab / kThreads + 1, 2048)), dim3(kThreads), 0,
+                           e->stream, (const uint64_t*)e->d_cmat, (const uint32_t*)e->d_sslab, e->s2.m(), e->R, e->rank,
+                           e->slab);
+        HIP_TRY(hipGetLastError());
+      }
       AGX_TRY(exact_rest(&quiet));
       ++e->mr_exact;
       ++e->mr_host_steps;

@@ -4549,6 +4549,12 @@ struct McompactArgs {
   const uint32_t* halt;  // device-resident replays: [0] != 0 = stopped (k_mr_pack), every kernel returns
   uint32_t* dense_left;  // owner mode's one dense_left word (BucketArgs::dense_left[0]): cleared here, before
                          // this superstep's dense launch raises it for a bucket it leaves to the block launch
+  // device-resident replays of plain behaviours: the runs for peer q go straight into q's send slab
+  // ([slab][3] triples at the run's position within q's owner-major region); what does not fit the slab
+  // goes to s2 at its owner-major offset (read only by the exact fallback, after k_slab_to_s2).  Null:
+  // every run to s2 (host-planned exchange, CRDT rows beside the tells, loopback groups).
+  uint32_t* sslab;
+  uint32_t slab, rank;
 };
 
 static __global__ void __launch_bounds__(kScanThreads) k_mcompact_scan(McompactArgs a) {
@@ -4599,9 +4605,52 @@ __device__ __forceinline__ void copy_run(const CMsgs& s, uint32_t so, const Msgs
   }
 }
 
+// block-wide copy of n envelopes into a peer's send slab (AoS triples from slot j0); slots past the slab
+// go to `over` at dof + i instead (the exact fallback's source)
+__device__ __forceinline__ void copy_run_slab(const CMsgs& s, uint32_t so, uint32_t* slabq, uint32_t j0, uint32_t slab,
+                                              const Msgs& over, uint32_t dof, uint32_t n) {
+  constexpr uint32_t U = 4;
+  for (uint32_t i0 = 0; i0 < n; i0 += U * kThreads) {
+    uint32_t k[U], sv[U], pv[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kThreads + threadIdx.x;
+      if (i < n) {
+        k[u] = s.key[so + i];
+        sv[u] = s.src[so + i];
+        pv[u] = s.pay[so + i];
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kThreads + threadIdx.x;
+      if (i >= n) continue;
+      const uint32_t j = j0 + i;
+      if (j < slab) {
+        slabq[3 * (size_t)j] = k[u];
+        slabq[3 * (size_t)j + 1] = sv[u];
+        slabq[3 * (size_t)j + 2] = pv[u];
+      } else {
+        over.key[dof + i] = k[u];
+        over.src[dof + i] = sv[u];
+        over.pay[dof + i] = pv[u];
+      }
+    }
+  }
+}
+
 static __global__ void __launch_bounds__(kThreads) k_mcompact_copy(McompactArgs a) {
+  __shared__ uint32_t s_soff[AGX_MAX_RANKS];  // (direct slabs) start of each owner's region in s2
   if (a.halt && a.halt[0]) return;
   const bool go = a.d_total[0] != 0 || a.d_total[1] != 0;
+  if (a.sslab && threadIdx.x == 0) {
+    uint32_t o = 0;
+    for (uint32_t q = 0; q < a.R; ++q) {
+      s_soff[q] = o;
+      o += (uint32_t)a.cvec[q];
+    }
+  }
+  __syncthreads();
   for (uint32_t c = blockIdx.x; c < a.ch.nb; c += gridDim.x) {
     const uint32_t n = a.ch.cnt[c];
     if (go && n) {  // backlog chunk c -> front of the sort input
@@ -4612,7 +4661,12 @@ static __global__ void __launch_bounds__(kThreads) k_mcompact_copy(McompactArgs 
       const uint32_t m = a.tcnt[x];
       if (!m) continue;
       const uint32_t so = a.toff[x], dof = a.off1[x];
-      if (go) copy_run(a.eg, so, a.out1, dof, m);
+      if (go) {
+        if (a.sslab && q != a.rank)
+          copy_run_slab(a.eg, so, a.sslab + (size_t)q * a.slab * 3, dof - s_soff[q], a.slab, a.out1, dof, m);
+        else
+          copy_run(a.eg, so, a.out1, dof, m);
+      }
       __syncthreads();  // every thread has read the count before it is cleared
       if (threadIdx.x == 0) a.tcnt[x] = 0u;  // the apply writes non-zero entries only
     }
@@ -4646,6 +4700,7 @@ struct MrArgs {
   const uint32_t* s2rows;
   uint32_t* srows;        // [R][slab][pw]
   uint32_t pw, heap_rows;
+  uint32_t direct;        // k_mcompact_copy already wrote the peers' runs into their send slabs
 };
 
 // the plan every block derives from cmat: own send offsets, receive offsets, counts, the decision
@@ -4709,7 +4764,7 @@ static __global__ void __launch_bounds__(kThreads) k_mr_pack(MrArgs a) {
       a.A.pay[o0 + i] = a.s2.pay[x0 + i];
     }
   }
-  for (uint32_t q = 0; q < a.R; ++q) {
+  for (uint32_t q = 0; q < a.R && !a.direct; ++q) {
     if (q == a.rank) continue;
     uint32_t* d = a.sslab + (size_t)q * a.slab * 3;
     const uint32_t o = p.soff[q];
@@ -4734,6 +4789,27 @@ static __global__ void __launch_bounds__(kThreads) k_mr_pack(MrArgs a) {
         for (uint32_t k2 = lane; k2 < a.pw / 4; k2 += kWave) dr[k2] = sr[k2];
       }
     }
+  }
+}
+
+// exact fallback of a superstep whose peer runs went straight into the send slabs (a count over the
+// slab): the slab parts back into s2's owner-major regions, so the host-planned exchange sends s2 whole
+// (the parts past the slab are there already)
+static __global__ void __launch_bounds__(kThreads) k_slab_to_s2(const uint64_t* cmat, const uint32_t* sslab, Msgs s2,
+                                                               uint32_t R, uint32_t rank, uint32_t slab) {
+  const uint32_t S = R + 2;
+  uint32_t o = 0;
+  for (uint32_t q = 0; q < R; ++q) {
+    const uint32_t n = (uint32_t)cmat[rank * S + q];
+    if (q != rank) {
+      const uint32_t* d = sslab + (size_t)q * slab * 3;
+      for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < min(n, slab); i += gridDim.x * kThreads) {
+        s2.key[o + i] = d[3 * (size_t)i];
+        s2.src[o + i] = d[3 * (size_t)i + 1];
+        s2.pay[o + i] = d[3 * (size_t)i + 2];
+      }
+    }
+    o += n;
   }
 }
 
