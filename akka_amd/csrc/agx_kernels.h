@@ -2821,6 +2821,26 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
     }
     uint32_t tk[kDenseIpt], tp[kDenseIpt];  // (a tell's sender is the item's actor, l[r])
     bool tv[kDenseIpt];
+    if constexpr (KM == kb(AGX_KIND_RING)) {
+      // RING-only populations: apply_msg<RING> through RegEmitter, branch-free (as in k_dense_fused)
+      const uint32_t stride = P.ring_stride, ng = P.n_global;
+#pragma unroll
+      for (int r = 0; r < kDenseIpt; ++r) {
+        const uint32_t q = r * kDenseThreads + tid;
+        const bool has = q < cnt, live = (ab[r] & 1u) != 0u, on = has && live;
+        const bool em = on && pv[r] > 0u;
+        acc[0] += on ? 1u : 0u;
+        acc[4] += on ? 1u : 0u;
+        acc[1] += has && !live ? 1u : 0u;
+        acc[3] += em ? 1u : 0u;
+        uint32_t d = l[r] + stride;  // (single rank: local id = global id)
+        d = d >= ng ? d - ng : d;
+        tv[r] = em;
+        tk[r] = em ? d : 0u;
+        tp[r] = em ? pv[r] - 1u : 0u;
+        if (on) st64x(P.state, l[r] * P.sa, x0[r] + 1ull);
+      }
+    } else {
 #pragma unroll
     for (int r = 0; r < kDenseIpt; ++r) {
       const uint32_t q = r * kDenseThreads + tid;
@@ -2849,6 +2869,7 @@ static __global__ void __launch_bounds__(kDenseThreads, AGX_DENSE_WPE) k_dense_a
       tv[r] = em.n_valid != 0u;
       tk[r] = em.key;
       tp[r] = em.pay;
+    }
     }
     // ---- tells: rank in item order (per (row, wave) counts), chunk stores, next-pass histogram
     uint32_t rk[kDenseIpt];
