@@ -63,6 +63,9 @@ def kernel_bytes_per_msg(W: int) -> dict:
 
 
 SORT_CLASSES = ("chunk_downsweep", "sort_upsweep", "sort_downsweep")
+# profiling classes that are not one HBM-bound kernel: the multi-rank exchange (RCCL all-gather + send /
+# receive + the slab pack / unpack kernels) is reported on its own (the line's `exchange` object)
+NON_KERNEL = ("exchange",)
 DENSE_FOLLOWERS = ("bucket_apply", "bucket_apply_tiny")  # (launched after k_dense_apply in one superstep)
 
 
@@ -75,6 +78,9 @@ def kernel_rooflines(prof: dict, per_msg: dict, msgs_per_launch: int, identity: 
     for k, v in prof.items():
         if identity and k in SORT_CLASSES and v["launches"]:
             out[k] = {"returned_at_entry": True, "avg_launch_ms": round(v["total_ms"] / v["launches"], 4)}
+            continue
+        if v["launches"] and k in NON_KERNEL:  # (RCCL + slab copies: no HBM roofline)
+            out[k] = {"avg_ms": round(v["total_ms"] / v["launches"], 4), "note": "RCCL exchange, not an HBM kernel"}
             continue
         if not v["launches"] or not per_msg.get(k):
             continue
@@ -89,7 +95,8 @@ def kernel_rooflines(prof: dict, per_msg: dict, msgs_per_launch: int, identity: 
             continue
         out[k] = {"achieved": round(ach, 1), "frac": round(ach / PEAK_HBM_GBS, 4), "avg_launch_ms": round(avg_ms, 4),
                   "alg_bytes_per_launch": per_msg[k] * msgs_per_launch}
-    dom = max((k for k in prof if prof[k]["launches"]), key=lambda k: prof[k]["total_ms"], default=None)
+    dom = max((k for k in prof if prof[k]["launches"] and k not in NON_KERNEL), key=lambda k: prof[k]["total_ms"],
+              default=None)
     return {"bound": "hbm", "peak": PEAK_HBM_GBS, "unit": "GB/s", "dominant": dom, "kernels": out}
 
 
@@ -420,6 +427,16 @@ def main():
     persist_k = ((pi1["supersteps"] - pi0["supersteps"]) / (pi1["launches"] - pi0["launches"])
                  if pi1["launches"] > pi0["launches"] else 0)
     cfg_words = eng.cfg.n_words
+    # multi-rank: the exchange beside the kernels -- its time per superstep (the eager profiled window:
+    # all-gather, slab pack, send / receive, unpack) and this rank's wire bytes per superstep
+    xinfo = None
+    if world > 1 and prof.get("exchange", {}).get("launches"):
+        xi = eng.exchange_info()
+        xms = prof["exchange"]["total_ms"] / prof["exchange"]["launches"]
+        wire = xi["env_bytes"] / max(xi["dev_steps"], 1)
+        xinfo = {"ms_per_superstep": round(xms, 4), "wire_bytes_per_superstep": int(wire), "slab": xi["slab"],
+                 "achieved_GBps": round(wire / (xms * 1e-3) / 1e9, 1) if xms > 0 else None,
+                 "device_resident_supersteps": xi["dev_steps"], "host_planned_supersteps": xi["host_steps"]}
     eng.close()
 
     elapsed, delivered = reduce_ranks(elapsed, delivered, world)
@@ -466,7 +483,7 @@ def main():
     # roofline of the dominant kernel (largest total time in the timed region)
     per_msg = kernel_bytes_per_msg(cfg_words)
     local_msgs_per_step = args.actors_per_gpu
-    dom = max((k for k in prof if prof[k]["launches"]), key=lambda k: prof[k]["total_ms"])
+    dom = max((k for k in prof if prof[k]["launches"] and k not in NON_KERNEL), key=lambda k: prof[k]["total_ms"])
     avg_ms_eager = prof[dom]["total_ms"] / prof[dom]["launches"]
     # the dense launch alone per replayed superstep (C2's strict replays): its launch time is the
     # graph-timed superstep (an upper bound: 1/8 of a k_replay_out included); else the eager events
@@ -532,6 +549,8 @@ def main():
                                     "alg_bytes_per_launch": alg_bytes * persist_k,
                                     "avg_launch_ms": avg_ms * persist_k,
                                     "avg_superstep_ms": avg_ms})
+        if xinfo:
+            out["exchange"] = xinfo
         out["at_100M_actors"] = large
         out["summary"] = summary(out)
         print(json.dumps(out), flush=True)
