@@ -204,7 +204,7 @@ __device__ __forceinline__ uint32_t crdt_count(const DevParams& P, uint32_t kind
 }
 
 // A local update with delta-crdt on: the next seqNr's log entry (DeltaPropagationSelector.update).
-// The ring slot it overwrites must have been sent to every other node of the key, else the
+// ORSet: the ring slot it overwrites must have been sent to every other node of the key, else the
 // engine reports AGX_ECAPACITY.
 __device__ __forceinline__ uint32_t dl_record(const DevParams& P, const St32& s, uint32_t kind, uint32_t self) {
   const uint32_t e0 = dl_env(kind);
@@ -220,6 +220,22 @@ __device__ __forceinline__ uint32_t dl_record(const DevParams& P, const St32& s,
   s.put(x, q);
   return x;
 }
+// Counters: a delta is the updated slot's new value, and slot-max merging of the deltas after j
+// (they are never a ReplicatedDeltaSize) is the last delta of each slot after j, or a placeholder
+// when a no-delta update lies after j -- the own slots never decrease, so the deltas of a slot grow
+// with their seqNr.  The log is therefore {seqNr, value} of each slot's last delta and the last
+// placeholder's seqNr (AGX_COUNTER_DELTA_U32): exact for any number of unsent seqNrs, like the
+// reference's unbounded deltaEntries map.  side: 0 increments, 1 decrements, 2 placeholder.
+__device__ __forceinline__ void dl_record_counter(const St32& s, uint32_t kind, uint32_t side, uint64_t v) {
+  const uint32_t e0 = dl_env(kind), x = e0 + 2u * AGX_DELTA_ENV_WORDS + 3u * side;
+  const uint32_t q = s.ld(e0 + 8) + 1u;
+  s.put(e0 + 8, q);
+  s.put(x, q);
+  if (side < 2u) {
+    s.put(x + 1, (uint32_t)v);
+    s.put(x + 2, (uint32_t)(v >> 32));
+  }
+}
 
 // DeltaPropagation row of seqNrs (j, ctr]: collectPropagations' merged group (DeltaOp.merge: runs of
 // AddDeltaOps coalesce) or a NoDeltaPlaceholder (max-delta-size reached / a no-delta update).
@@ -233,25 +249,15 @@ __device__ __forceinline__ bool dl_group_row(const DevParams& P, const St32& s, 
 #pragma unroll
   for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) row[4 + n] = s.ld(e0 + n);
   bool ph = false;
-  if (kind != AGX_KIND_ORSET) {  // GCounter / PNCounter: slot max over the range
-    uint64_t v0 = 0, v1 = 0;
-    uint32_t has = 0;
-    for (uint32_t q = j + 1; q <= ctr; ++q) {
-      const uint32_t x = dl_entry(kind, q), t = s.ld(x + 1);
-      if (t == 0) {
-        ph = true;
-        break;
-      }
-      const uint64_t v = ((uint64_t)s.ld(x + 3) << 32) | s.ld(x + 2);
-      has |= t;
-      if (t == 1u) v0 = v > v0 ? v : v0;
-      else v1 = v > v1 ? v : v1;
-    }
-    row[12] = has;
-    row[13] = (uint32_t)v0;
-    row[14] = (uint32_t)(v0 >> 32);
-    row[15] = (uint32_t)v1;
-    row[16] = (uint32_t)(v1 >> 32);
+  if (kind != AGX_KIND_ORSET) {  // GCounter / PNCounter: slot max over the range (dl_record_counter)
+    const uint32_t x = e0 + 2u * AGX_DELTA_ENV_WORDS;
+    const uint32_t q0 = s.ld(x), q1 = s.ld(x + 3);
+    ph = s.ld(x + 6) > j;
+    row[12] = (q0 > j ? 1u : 0u) | (q1 > j ? 2u : 0u);
+    row[13] = q0 > j ? s.ld(x + 1) : 0u;
+    row[14] = q0 > j ? s.ld(x + 2) : 0u;
+    row[15] = q1 > j ? s.ld(x + 4) : 0u;
+    row[16] = q1 > j ? s.ld(x + 5) : 0u;
   } else {
     uint32_t o = 12, nops = 0, hdr = 0, cnt = 0, vmax = 0;
     bool last_add = false;
@@ -559,12 +565,8 @@ __device__ __forceinline__ uint32_t crdt_apply(const DevParams& P, const CrdtHea
       const uint64_t v = st[w * nl] + arg;
       if (v < arg) atomicOr(P.err, 2ull);  // kErrRange: the reference's BigInt slot would not wrap
       st[w * nl] = v;
-      if (dm) {  // delta = the counter of the new slot value; an update by 0 has none (placeholder)
-        const uint32_t x = dl_record(P, s32, kind, self);
-        s32.put(x + 1, arg ? (op == AGX_OP_DECREMENT ? 2u : 1u) : 0u);
-        s32.put(x + 2, (uint32_t)v);
-        s32.put(x + 3, (uint32_t)(v >> 32));
-      }
+      if (dm)  // delta = the counter of the new slot value; an update by 0 has none (placeholder)
+        dl_record_counter(s32, kind, arg ? (op == AGX_OP_DECREMENT ? 1u : 0u) : 2u, v);
       return AGX_RES_SAME;
     }
     case AGX_OP_ADD:

@@ -36,7 +36,7 @@ ORSET_ELEMS = 64
 CRDT_WORDS = {Kind.GCOUNTER: 8, Kind.PNCOUNTER: 16, Kind.ORSET: 260}
 # delta-CRDT mode (agx_set_delta_crdt): data + envelope/selector area + delta log (include/akka_gpu.h)
 DELTA_ENV_WORDS, DELTA_LOG = 12, 64
-CRDT_DELTA_WORDS = {k: w + DELTA_ENV_WORDS + DELTA_LOG * (6 if k == Kind.ORSET else 2) for k, w in CRDT_WORDS.items()}
+CRDT_DELTA_WORDS = {k: w + DELTA_ENV_WORDS + (DELTA_LOG * 6 if k == Kind.ORSET else 4) for k, w in CRDT_WORDS.items()}
 DELTA_WRITE = 0x800000
 WIDE_BIT = 0x80000000
 

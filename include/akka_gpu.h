@@ -185,9 +185,16 @@ typedef struct agx_act {
  *   u32[2D + 8]       DeltaPropagationSelector.deltaCounter  (DD/DeltaPropagationSelector.scala:44-57)
  *   u32[2D + 9]       deltaNodeRoundRobinCounter
  *   u32[2D + 10..17]  deltaSentToNode per node (0 = nothing sent)
- *   u32[2D + 24 + AGX_DELTA_LOG_U32(kind) * (seq % AGX_DELTA_LOG) ...]  deltaEntries ring:
- *       counters: {seq, type (0 = NoDeltaPlaceholder, 1 = increments delta, 2 = decrements delta), value lo, hi}
- *       ORSet:    {seq, type (1 AddDeltaOp, 2 RemoveDeltaOp, 3 FullStateDeltaOp) | elem << 8, version, 0, vvector[8]}
+ *   deltaEntries --
+ *     counters, u32[2D + 24 ..+ AGX_COUNTER_DELTA_U32]: {seqNr, value lo, hi} of the last increments
+ *       delta, the same of the last decrements delta, the last NoDeltaPlaceholder's seqNr, 0.  A
+ *       counter delta is the updated slot's new value and the own slots never decrease, so the
+ *       slot-max merge of the deltas after any seqNr j is these last deltas (or a placeholder if
+ *       one lies after j): unbounded, as the reference's map (DD/DeltaPropagationSelector.scala:149-155).
+ *     ORSet, u32[2D + 24 + AGX_DELTA_LOG_U32(1) * (seq % AGX_DELTA_LOG) ...], a ring:
+ *       {seq, type (1 AddDeltaOp, 2 RemoveDeltaOp, 3 FullStateDeltaOp) | elem << 8, version, 0, vvector[8]};
+ *       an ORSet replica that would overwrite a seqNr some node has not been sent reports
+ *       AGX_ECAPACITY (the one bounded difference from the reference).
  * Ops on a delta replica:
  *   AGX_OP_DELTA_TICK  arg = k | AGX_DELTA_WRITE?   DeltaPropagationTick (DD/Replicator.scala:1953-1963):
  *       (AGX_DELTA_WRITE: first tell itself one seeded local update -- a writer client), then for
@@ -200,7 +207,8 @@ typedef struct agx_act {
  *   (too large, or a no-op update in range) is not told (createDeltaPropagation leaves it out,
  *   DD/Replicator.scala:1364,1957); deltaSentToNode still advances.                           */
 #define AGX_DELTA_WRITE 0x800000u
-#define AGX_DELTA_LOG 64u            /* ring entries per replica (seqNrs not yet sent to every node) */
+#define AGX_DELTA_LOG 64u            /* ORSet ring entries per replica (seqNrs not yet sent to every node) */
+#define AGX_COUNTER_DELTA_U32 8u     /* counters: the last delta per slot + the last placeholder      */
 #define AGX_DELTA_ENV_WORDS 12u      /* u64 words of the envelope / selector area */
 #define AGX_DELTA_MAX_SIZE 50u       /* Replicator max-delta-size (reference.conf delta-crdt) */
 #define AGX_DELTA_LOG_U32(orset) ((orset) ? 12u : 4u)
@@ -214,8 +222,8 @@ typedef struct agx_act {
  * A group has < max-delta-size (<= 50) ops over <= AGX_DELTA_LOG seqNrs: <= 574 u32.        */
 #define AGX_DELTA_ROW_BIT 0x20000000u
 #define AGX_ORSET_DELTA_ROW_U32 576u
-#define AGX_GCOUNTER_DELTA_WORDS (AGX_GCOUNTER_WORDS + AGX_DELTA_ENV_WORDS + AGX_DELTA_LOG * 2u)
-#define AGX_PNCOUNTER_DELTA_WORDS (AGX_PNCOUNTER_WORDS + AGX_DELTA_ENV_WORDS + AGX_DELTA_LOG * 2u)
+#define AGX_GCOUNTER_DELTA_WORDS (AGX_GCOUNTER_WORDS + AGX_DELTA_ENV_WORDS + AGX_COUNTER_DELTA_U32 / 2u)
+#define AGX_PNCOUNTER_DELTA_WORDS (AGX_PNCOUNTER_WORDS + AGX_DELTA_ENV_WORDS + AGX_COUNTER_DELTA_U32 / 2u)
 #define AGX_ORSET_DELTA_WORDS (AGX_ORSET_WORDS + AGX_DELTA_ENV_WORDS + AGX_DELTA_LOG * 6u)
 
 typedef struct agx_cfg {

@@ -125,8 +125,8 @@ static inline uint32_t dref_slice(const ref_params* P, uint32_t a, uint32_t rr, 
   return s;
 }
 
-/* A local update (Replicator.receiveUpdate with delta-crdt enabled): record the update's
- * delta under the next seqNr; `type` as in the log layout (0 = NoDeltaPlaceholder). */
+/* A local ORSet update (Replicator.receiveUpdate with delta-crdt enabled): record the update's
+ * delta under the next seqNr in the ring; `type` as in the log layout. */
 static inline uint32_t* dref_record(ref_params* P, uint64_t* w, uint32_t kind, uint32_t a) {
   uint32_t* env = dref_env(w, kind);
   const uint32_t s = ++env[8];
@@ -139,6 +139,23 @@ static inline uint32_t* dref_record(ref_params* P, uint64_t* w, uint32_t kind, u
   memset(e, 0, AGX_DELTA_LOG_U32(kind == AGX_KIND_ORSET) * 4u);
   e[0] = s;
   return e;
+}
+
+/* Counters' deltaEntries (include/akka_gpu.h): a delta is the updated slot's new value
+ * (GCounter.scala:97-111, PNCounter.scala:161-179) and is never a ReplicatedDeltaSize, so
+ * collectPropagations' reduceLeft over the entries after j is the slot-wise max of those deltas,
+ * or NoDeltaPlaceholder if one lies after j (DD/DeltaPropagationSelector.scala:112-125).  A node's
+ * own slots never decrease, so that max is the last delta of each slot after j: the oracle keeps
+ * {seqNr, value} of each slot's last delta and the last placeholder's seqNr, for any number of
+ * unsent seqNrs (the reference's map is unbounded). */
+static inline void dref_record_counter(uint64_t* w, uint32_t kind, uint32_t side, uint64_t v) {
+  uint32_t* env = dref_env(w, kind);
+  uint32_t* e = env + 2u * AGX_DELTA_ENV_WORDS + 3u * side; /* side 0 increments, 1 decrements, 2 placeholder */
+  e[0] = ++env[8];
+  if (side < 2u) {
+    e[1] = (uint32_t)v;
+    e[2] = (uint32_t)(v >> 32);
+  }
 }
 
 /* The merged delta group of seqNrs (j, ctr] (collectPropagations' reduceLeft with the
@@ -154,18 +171,14 @@ static inline uint32_t dref_group_row(const ref_params* P, uint64_t* w, uint32_t
   for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) row[4 + n] = env[n];
   uint32_t ph = 0;
   if (kind != AGX_KIND_ORSET) { /* GCounter / PNCounter deltas merge by slot max (no deltaSize) */
-    uint64_t v[2] = {0, 0};
-    uint32_t has = 0;
-    for (uint32_t s = j + 1; s <= ctr; ++s) {
-      const uint32_t* e = dref_entry(w, kind, s);
-      if (e[1] == 0) { ph = 1; break; } /* NoDeltaPlaceholder.merge = itself */
-      const uint64_t x = ((uint64_t)e[3] << 32) | e[2];
-      has |= e[1];
-      if (x > v[e[1] - 1]) v[e[1] - 1] = x;
-    }
-    row[12] = has;
-    row[13] = (uint32_t)v[0]; row[14] = (uint32_t)(v[0] >> 32);
-    row[15] = (uint32_t)v[1]; row[16] = (uint32_t)(v[1] >> 32);
+    const uint32_t* e = env + 2u * AGX_DELTA_ENV_WORDS;
+    ph = e[6] > j;
+    for (uint32_t b = 0; b < 2; ++b)
+      if (e[3 * b] > j) {
+        row[12] |= 1u << b;
+        row[13 + 2 * b] = e[3 * b + 1];
+        row[14 + 2 * b] = e[3 * b + 2];
+      }
   } else {
     static REF_TLS orset_delta g, d2; /* (fjp_ref runs replicas on several threads) */
     for (uint32_t s = j + 1; s <= ctr && !ph; ++s) {
@@ -325,12 +338,8 @@ static inline uint32_t ref_apply_crdt(ref_params* P, uint32_t kind, uint32_t a, 
       if (kind == AGX_KIND_ORSET || (op == AGX_OP_DECREMENT && kind != AGX_KIND_PNCOUNTER)) return AGX_RES_UNHANDLED;
       const uint32_t slot = (op == AGX_OP_DECREMENT ? AGX_CRDT_NODES : 0u) + node;
       w[slot] += arg;
-      if (dm) { /* delta = the counter of the new slot value (GCounter.scala:97-111); n = 0: none */
-        uint32_t* e = dref_record(P, w, kind, a);
-        e[1] = arg ? (op == AGX_OP_DECREMENT ? 2u : 1u) : 0u;
-        e[2] = (uint32_t)w[slot];
-        e[3] = (uint32_t)(w[slot] >> 32);
-      }
+      if (dm) /* delta = the counter of the new slot value (GCounter.scala:97-111); n = 0: none */
+        dref_record_counter(w, kind, arg ? (op == AGX_OP_DECREMENT ? 1u : 0u) : 2u, w[slot]);
       return AGX_RES_SAME;
     }
     case AGX_OP_ADD:

@@ -91,9 +91,33 @@ def test_delta_loopback_sharded(built, ranks):
     assert diff.size == 0, diff[:10]
 
 
+@pytest.mark.parametrize("kind", [Kind.GCOUNTER, Kind.PNCOUNTER])
+def test_delta_counters_unbounded_log(built, kind):
+    """Counter groups over 150 unsent seqNrs, some with a no-delta update (a placeholder) among
+    them, then writer ticks: the counters keep each slot's last delta, so no log bound applies
+    (the reference's deltaEntries map is unbounded)."""
+    n = 8 * 100 + 3
+    w = wl.crdt_delta(n, kind, rounds=6, write=True, ops_per_replica=150, gossip_rounds=2)
+    ids = np.arange(n, dtype=np.uint32)
+    dst, src, pay = w.tells
+    w.tells = (np.concatenate([ids[::5], dst]), np.concatenate([src[:ids[::5].size], src]),
+               np.concatenate([np.full(ids[::5].size, Op.make(Op.INCREMENT, 0), np.uint32), pay]))
+    from oracle import BspOracle
+    eng = GpuEngine(EngineConfig(msg_capacity=1 << 18, **w.gpu_kwargs()))
+    w.apply_to(eng)
+    sg = eng.run()
+    ref = BspOracle(**w.engine_kwargs())
+    w.apply_to(ref)
+    so = ref.run()
+    a, b = eng.read_state(), ref.read_state()
+    eng.close()
+    assert sg.in_flight == 0
+    assert_same(sg, so, a, b, f"delta counters unbounded kind={kind}")
+
+
 def test_delta_log_overflow_is_loud(built):
-    """More than AGX_DELTA_LOG unsent seqNrs: AGX_ECAPACITY, as the oracle."""
-    w = wl.crdt_delta(64, Kind.GCOUNTER, rounds=0, write=False, ops_per_replica=70)
+    """More than AGX_DELTA_LOG unsent ORSet seqNrs: AGX_ECAPACITY, as the oracle."""
+    w = wl.crdt_delta(64, Kind.ORSET, rounds=0, write=False, ops_per_replica=70)
     eng = GpuEngine(EngineConfig(**w.gpu_kwargs()))
     w.apply_to(eng)
     with pytest.raises(Exception):

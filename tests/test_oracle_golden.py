@@ -348,14 +348,16 @@ def test_orset_delta_kats():
                 assert OrsetDelta.TYPES[d.ops[d.nops - 1].type] == chk[3], (c["name"], chk)
 
 
-@pytest.mark.parametrize("kind", [Kind.GCOUNTER, Kind.PNCOUNTER, Kind.ORSET])
-def test_delta_crdt_converges(kind):
+@pytest.mark.parametrize("kind,opr", [(Kind.GCOUNTER, 6), (Kind.PNCOUNTER, 6), (Kind.ORSET, 6),
+                                      (Kind.GCOUNTER, 150), (Kind.PNCOUNTER, 150)])
+def test_delta_crdt_converges(kind, opr):
     """Delta-CRDT replication on the oracle (DeltaPropagationSelector + receiveDeltaPropagation):
     counters converge from deltas alone to the slot-wise sums of each node's updates; ORSet
     replicas converge once full-state gossip runs beside the deltas (a RemoveDeltaOp only removes
     an element whose dots it covers, DD/ORSet.scala:471-501, so deltas alone can leave dots that
-    the full-state merge drops -- as in the reference)."""
-    n, opr = 8 * 40, 6
+    the full-state merge drops -- as in the reference).  opr = 150: every replica's first group
+    covers 150 unsent seqNrs (the reference's deltaEntries map is unbounded; counters are too)."""
+    n = 8 * 40
     gossip = 40 if kind == Kind.ORSET else 0
     w = wl.crdt_delta(n, kind, rounds=24, write=False, ops_per_replica=opr, gossip_rounds=gossip)
     o = BspOracle(**w.engine_kwargs())
@@ -387,7 +389,8 @@ def test_delta_crdt_placeholders_and_log_capacity():
     """max-delta-size: a group of >= M ops is a NoDeltaPlaceholder (never applied; deltaSentToNode
     still advances, DD/DeltaPropagationSelector.scala:112-131), so without full-state gossip the
     receivers keep nothing; a counter update by 0 records a NoDeltaPlaceholder
-    (DD/Replicator.scala:1648-1652).  More than AGX_DELTA_LOG unsent seqNrs overflow the log."""
+    (DD/Replicator.scala:1648-1652).  More than AGX_DELTA_LOG unsent seqNrs overflow the ORSet log
+    (counters keep each slot's last delta: no bound)."""
     n = 16
     w = wl.crdt_delta(n, Kind.ORSET, rounds=4, write=False, ops_per_replica=6, max_delta_size=2)
     o = BspOracle(**w.engine_kwargs())
@@ -413,7 +416,19 @@ def test_delta_crdt_placeholders_and_log_capacity():
     o.run()
     ws, _ = o.read_state()
     assert all(ws[a, b] == (5 if b == a % 8 else 0) for a in range(n) for b in range(8))
-    # log overflow: 70 updates with no propagation
+    # ... also when it lies among 100 unsent seqNrs; a group after it carries the slot's last value
+    w = wl.crdt_delta(n, Kind.GCOUNTER, rounds=4, write=False)
+    o = BspOracle(**w.engine_kwargs())
+    w.apply_to(o, stage_tells=False)
+    pays = [Op.make(Op.INCREMENT, 5)] * 60 + [Op.make(Op.INCREMENT, 0)] + [Op.make(Op.INCREMENT, 5)] * 39
+    o.tell(np.repeat(ids, len(pays)), np.tile(np.array(pays, np.uint32), n))
+    o.tell(ids, np.full(n, Op.make(Op.DELTA_TICK, 3), np.uint32))
+    o.run()
+    o.tell(np.repeat(ids, 2), np.tile(np.array([Op.make(Op.INCREMENT, 7), Op.make(Op.DELTA_TICK, 3)], np.uint32), n))
+    o.run()
+    ws, _ = o.read_state()
+    assert (ws[:, :8] == 495 + 7).all()  # (the first groups were placeholders: nothing of them applied)
+    # ORSet log overflow: 70 updates with no propagation
     w = wl.crdt_delta(n, Kind.ORSET, rounds=0, write=False, ops_per_replica=70)
     o = BspOracle(**w.engine_kwargs())
     w.apply_to(o)
