@@ -261,41 +261,59 @@ __device__ __forceinline__ bool dl_group_row(const DevParams& P, const St32& s, 
   } else {
     uint32_t o = 12, nops = 0, hdr = 0, cnt = 0, vmax = 0;
     bool last_add = false;
-    for (uint32_t q = j + 1; q <= ctr; ++q) {
-      const uint32_t x = dl_entry(kind, q), te = s.ld(x + 1), t = te & 0xFFu, ver = s.ld(x + 2);
-      if (t == 1u && last_add) {  // AddDeltaOp.merge(AddDeltaOp): one more (element, version)
-        if (nops >= P.delta_max) {  // (max-delta-size 1: even one coalesced AddDeltaOp is too large)
+    // the range's entries four at a time, their (type, version) words loaded together: the row stores
+    // between entries would otherwise order one log round trip per seqNr
+    constexpr uint32_t kQ = 4;
+    for (uint32_t q0 = j + 1; q0 <= ctr && !ph; q0 += kQ) {
+      uint32_t tev[kQ], verv[kQ];
+#pragma unroll
+      for (uint32_t u = 0; u < kQ; ++u) {
+        const uint32_t x = dl_entry(kind, q0 + u);
+        tev[u] = q0 + u <= ctr ? s.ld(x + 1) : 0u;
+        verv[u] = q0 + u <= ctr ? s.ld(x + 2) : 0u;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kQ; ++u) {
+        const uint32_t q = q0 + u;
+        if (ph || q > ctr) break;
+        const uint32_t x = dl_entry(kind, q), te = tev[u], t = te & 0xFFu, ver = verv[u];
+        if (t == 1u && last_add) {  // AddDeltaOp.merge(AddDeltaOp): one more (element, version)
+          if (nops >= P.delta_max) {  // (max-delta-size 1: even one coalesced AddDeltaOp is too large)
+            ph = true;
+            break;
+          }
+          row[o++] = te >> 8;
+          row[o++] = ver;
+          ++cnt;
+          vmax = ver;
+          continue;
+        }
+        if (last_add) row[hdr] = 1u | (cnt << 8), row[hdr + 1] = vmax;  // close the add run
+        if (q > j + 1 && nops + 1u >= P.delta_max) {  // deltaSize >= maxDeltaSize
           ph = true;
           break;
         }
-        row[o++] = te >> 8;
-        row[o++] = ver;
-        ++cnt;
-        vmax = ver;
-        continue;
-      }
-      if (last_add) row[hdr] = 1u | (cnt << 8), row[hdr + 1] = vmax;  // close the add run
-      if (q > j + 1 && nops + 1u >= P.delta_max) {  // deltaSize >= maxDeltaSize
-        ph = true;
-        break;
-      }
-      ++nops;
-      last_add = t == 1u;
-      if (last_add) {
-        hdr = o;
-        o += 2;
-        row[o++] = te >> 8;
-        row[o++] = ver;
-        cnt = 1;
-        vmax = ver;
-      } else {
-        row[o++] = t | ((t == 2u ? 1u : 0u) << 8);
-        if (t == 2u) {
+        ++nops;
+        last_add = t == 1u;
+        if (last_add) {
+          hdr = o;
+          o += 2;
           row[o++] = te >> 8;
           row[o++] = ver;
-        }
+          cnt = 1;
+          vmax = ver;
+        } else {
+          row[o++] = t | ((t == 2u ? 1u : 0u) << 8);
+          if (t == 2u) {
+            row[o++] = te >> 8;
+            row[o++] = ver;
+          }
+          uint32_t vv[AGX_CRDT_NODES];
 #pragma unroll
-        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) row[o++] = s.ld(x + 4 + n);
+          for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) vv[n] = s.ld(x + 4 + n);
+#pragma unroll
+          for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) row[o++] = vv[n];
+        }
       }
     }
     if (!ph && last_add) row[hdr] = 1u | (cnt << 8), row[hdr + 1] = vmax;
@@ -305,12 +323,14 @@ __device__ __forceinline__ bool dl_group_row(const DevParams& P, const St32& s, 
   return ph;
 }
 
-// ORSet: apply one received DeltaPropagation group (mergeDelta, DD/ORSet.scala:455-501)
-__device__ __forceinline__ void orset_merge_delta_row(const St32& s, const uint32_t* row, uint32_t from) {
+// ORSet: apply one received DeltaPropagation group (mergeDelta, DD/ORSet.scala:455-501).  lvv: the
+// replica's vvector, loaded by the caller with the row's header.  Loads are issued in batches before
+// the stores they precede (state and row may alias as far as the compiler knows: a load after a store
+// would cost one memory round trip per element).
+__device__ __forceinline__ void orset_merge_delta_row(const St32& s, const uint32_t* row, uint32_t from,
+                                                      uint32_t (&lvv)[AGX_CRDT_NODES]) {
   constexpr uint32_t vb = AGX_ORSET_ELEMS * AGX_CRDT_NODES;  // u32 index of the vvector
-  uint32_t lvv[AGX_CRDT_NODES];
-#pragma unroll
-  for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) lvv[n] = s.ld(vb + n);
+  constexpr uint32_t kB = 4;                                 // elements per batch
   const uint32_t nops = row[0];
   uint32_t o = 12;
   for (uint32_t i = 0; i < nops; ++i) {
@@ -319,23 +339,46 @@ __device__ __forceinline__ void orset_merge_delta_row(const St32& s, const uint3
       const uint32_t vf = row[o + 1];
       const uint32_t p0 = o + 2;
       uint64_t seen = 0;
-      for (uint32_t k = cnt; k-- > 0;) {
-        const uint32_t e = row[p0 + 2 * k], ver = row[p0 + 2 * k + 1];
-        if ((seen >> e) & 1ull) continue;
-        seen |= 1ull << e;
-        uint32_t d[AGX_CRDT_NODES];
-        bool here = false;
+      for (uint32_t k1 = cnt; k1 > 0;) {  // batches of pairs from the run's end
+        const uint32_t k0 = k1 > kB ? k1 - kB : 0u;
+        uint32_t pe[kB], pv[kB];
 #pragma unroll
-        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
-          d[n] = s.ld(e * AGX_CRDT_NODES + n);
-          here |= d[n] != 0u;
+        for (uint32_t u = 0; u < kB; ++u) {
+          pe[u] = k0 + u < k1 ? row[p0 + 2 * (k0 + u)] : 0u;
+          pv[u] = k0 + u < k1 ? row[p0 + 2 * (k0 + u) + 1] : 0u;
         }
+        bool keep[kB];
 #pragma unroll
-        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
-          const uint32_t r = n == from ? ver : 0u, rvv = n == from ? vf : 0u;
-          const uint32_t x = here ? orset_merge_entry(d[n], r, lvv[n], rvv) : (r > lvv[n] ? r : 0u);
-          if (x != d[n]) s.put(e * AGX_CRDT_NODES + n, x);
+        for (uint32_t u = kB; u-- > 0;) {  // (descending: a later pair of the batch wins)
+          keep[u] = k0 + u < k1 && !((seen >> pe[u]) & 1ull);
+          if (keep[u]) seen |= 1ull << pe[u];
         }
+        uint64_t dw[kB][4];
+#pragma unroll
+        for (uint32_t u = 0; u < kB; ++u)
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) dw[u][k] = keep[u] ? s.st[(size_t)(4 * pe[u] + k) * s.nl] : 0ull;
+#pragma unroll
+        for (uint32_t u = 0; u < kB; ++u) {
+          if (!keep[u]) continue;
+          const uint32_t e = pe[u], ver = pv[u];
+          bool here = false;
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) here |= dw[u][k] != 0ull;
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) {
+            uint32_t x2[2];
+#pragma unroll
+            for (uint32_t h2 = 0; h2 < 2; ++h2) {
+              const uint32_t n = 2 * k + h2, d = (uint32_t)(dw[u][k] >> (32 * h2));
+              const uint32_t r = n == from ? ver : 0u, rvv = n == from ? vf : 0u;
+              x2[h2] = here ? orset_merge_entry(d, r, lvv[n], rvv) : (r > lvv[n] ? r : 0u);
+            }
+            const uint64_t nw = ((uint64_t)x2[1] << 32) | x2[0];
+            if (nw != dw[u][k]) s.st[(size_t)(4 * e + k) * s.nl] = nw;
+          }
+        }
+        k1 = k0;
       }
 #pragma unroll
       for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n)
@@ -367,13 +410,29 @@ __device__ __forceinline__ void orset_merge_delta_row(const St32& s, const uint3
         }
       o += 11;
     } else {  // FullStateDeltaOp: dryMerge(addDeltaOp = false) with an empty elementsMap
-      const uint32_t* rvv = row + o + 1;
-      for (uint32_t e = 0; e < AGX_ORSET_ELEMS; ++e)
+      uint32_t rvv[AGX_CRDT_NODES];
 #pragma unroll
-        for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
-          const uint32_t x = s.ld(e * AGX_CRDT_NODES + n);
-          if (x && x <= rvv[n]) s.put(e * AGX_CRDT_NODES + n, 0u);
-        }
+      for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) rvv[n] = row[o + 1 + n];
+      for (uint32_t e0 = 0; e0 < AGX_ORSET_ELEMS; e0 += kB) {
+        uint64_t dw[kB][4];
+#pragma unroll
+        for (uint32_t u = 0; u < kB; ++u)
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) dw[u][k] = s.st[(size_t)(4 * (e0 + u) + k) * s.nl];
+#pragma unroll
+        for (uint32_t u = 0; u < kB; ++u)
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) {
+            uint32_t x2[2];
+#pragma unroll
+            for (uint32_t h2 = 0; h2 < 2; ++h2) {
+              const uint32_t n = 2 * k + h2, x = (uint32_t)(dw[u][k] >> (32 * h2));
+              x2[h2] = x && x <= rvv[n] ? 0u : x;
+            }
+            const uint64_t nw = ((uint64_t)x2[1] << 32) | x2[0];
+            if (nw != dw[u][k]) s.st[(size_t)(4 * (e0 + u) + k) * s.nl] = nw;
+          }
+      }
 #pragma unroll
       for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n)
         if (rvv[n] > lvv[n]) {
@@ -387,26 +446,39 @@ __device__ __forceinline__ void orset_merge_delta_row(const St32& s, const uint3
 
 // a received DeltaPropagation (receiveDeltaPropagation + DataEnvelope.merge)
 __device__ __forceinline__ void dl_receive(const St32& s, uint32_t kind, const uint32_t* row) {
-  if (row[0] & 0x80000000u) return;  // NoDeltaPlaceholder: not part of the propagation
-  const uint32_t e0 = dl_env(kind), from = row[1];
-  if (kind != AGX_KIND_ORSET) {  // not RequiresCausalDeliveryOfDeltas: merge the sender's envelope
-    for (uint32_t b = 0; b < 2; ++b)
-      if (row[12] & (1u << b)) {
-        uint64_t* slot = s.st + (size_t)(b * AGX_CRDT_NODES + from) * s.nl;
-        const uint64_t x = ((uint64_t)row[14 + 2 * b] << 32) | row[13 + 2 * b];
-        if (x > *slot) *slot = x;
-      }
+  if (kind == AGX_KIND_ORSET) {  // header, sender's deltaVersion and the vvector in one round trip
+    constexpr uint32_t vb = AGX_ORSET_ELEMS * AGX_CRDT_NODES;
+    const uint32_t e0 = dl_env(kind);
+    const uint32_t h0 = row[0], from = row[1], lo = row[2], hi = row[3];
+    uint32_t lvv[AGX_CRDT_NODES], dv[AGX_CRDT_NODES];
 #pragma unroll
     for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
-      const uint32_t c = s.ld(e0 + n);
-      if (row[4 + n] > c) s.put(e0 + n, row[4 + n]);
+      lvv[n] = s.ld(vb + n);
+      dv[n] = s.ld(e0 + n);
     }
+    if (h0 & 0x80000000u) return;  // NoDeltaPlaceholder: not part of the propagation
+    uint32_t cur = 0;
+#pragma unroll
+    for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) cur = n == from ? dv[n] : cur;
+    if (cur >= hi || lo > cur + 1u) return;  // already handled / a seqNr is missing
+    orset_merge_delta_row(s, row, from, lvv);
+    s.put(e0 + from, hi);  // deltaVersions.merge(VersionVector(fromNode, toSeqNr))
     return;
   }
-  const uint32_t cur = s.ld(e0 + from);
-  if (cur >= row[3] || row[2] > cur + 1u) return;  // already handled / a seqNr is missing
-  orset_merge_delta_row(s, row, from);
-  s.put(e0 + from, row[3]);  // deltaVersions.merge(VersionVector(fromNode, toSeqNr))
+  if (row[0] & 0x80000000u) return;  // NoDeltaPlaceholder: not part of the propagation
+  const uint32_t e0 = dl_env(kind), from = row[1];
+  // not RequiresCausalDeliveryOfDeltas: merge the sender's envelope
+  for (uint32_t b = 0; b < 2; ++b)
+    if (row[12] & (1u << b)) {
+      uint64_t* slot = s.st + (size_t)(b * AGX_CRDT_NODES + from) * s.nl;
+      const uint64_t x = ((uint64_t)row[14 + 2 * b] << 32) | row[13 + 2 * b];
+      if (x > *slot) *slot = x;
+    }
+#pragma unroll
+  for (uint32_t n = 0; n < AGX_CRDT_NODES; ++n) {
+    const uint32_t c = s.ld(e0 + n);
+    if (row[4 + n] > c) s.put(e0 + n, row[4 + n]);
+  }
 }
 
 // DeltaPropagationTick (DD/Replicator.scala:1953-1963); returns the row cursor advance

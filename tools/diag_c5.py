@@ -15,6 +15,10 @@ if a.workload == "c5":
     w = wl.power_law_forward(a.n, ttl=15, capacity=64, throughput=5, device_graph=True)
 elif a.workload == "c3":
     w = wl.zipf_fanout(a.n, k=1, ttl=15, root_every=1, capacity=1000)
+elif a.workload == "c3s":  # C3 steady state at SURVEY's spec shape (ttl 64, 1/64 roots, unbounded)
+    w = wl.zipf_fanout(a.n if a.n != 100_000_000 else 10_000_000, k=1, ttl=64, root_every=64, throughput=5)
+elif a.workload == "c3t":  # C3 fan-out tree as benched
+    w = wl.zipf_fanout(a.n if a.n != 100_000_000 else 10_000_000, k=4, ttl=3, root_every=64, capacity=1000)
 elif a.workload in ("c4g", "c4o"):
     from akka_amd.engine import Kind
     w = wl.crdt_gossip(a.n if a.n != 100_000_000 else 1_000_000, Kind.GCOUNTER if a.workload == "c4g" else Kind.ORSET,
