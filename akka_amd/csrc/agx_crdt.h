@@ -519,6 +519,18 @@ __device__ __forceinline__ void dl_tick(const DevParams& P, const CrdtHeap& H, u
 }
 
 
+// Phase B message classes for the wave's schedule (bucket_finish, kCrdtSched): 0 a DeltaPropagation,
+// 1 a full-state gossip, 2 a DeltaPropagationTick, 3 a GossipTick, 4 any other op (an update)
+#ifndef AGX_CRDT_SCHED
+#define AGX_CRDT_SCHED 1
+#endif
+constexpr bool kCrdtSched = AGX_CRDT_SCHED != 0;
+__device__ __forceinline__ uint32_t crdt_class(uint32_t src, uint32_t pay) {
+  if (is_wide(src)) return (pay & AGX_DELTA_ROW_BIT) ? 0u : 1u;
+  const uint32_t op = pay >> 24;
+  return op == AGX_OP_DELTA_TICK ? 2u : op == AGX_OP_GOSSIP ? 3u : 4u;
+}
+
 // Phase B: one invoke of a CRDT replica.  `emit(dst, pay)` / `emit_wide(dst, handle)`.
 // CM: the CRDT kinds present (one bit = a single-kind population, whose merge is specialised:
 // the other kinds' code and registers vanish).  Merges issue all loads of a batch before its

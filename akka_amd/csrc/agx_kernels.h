@@ -1935,6 +1935,30 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           nunh += orset_protocol(P, self, s0, nd, isrc, ipay, row_cursor, em, &work);
           ndel += nd;
           L.ecnt[la] = work ? rc0 : 0xFFFFFFFFu;  // (this actor's tell offset is no longer needed)
+        } else if (kCrdtSched) {
+          // the wave's lanes are 64 replicas, each with its own mix of messages (delta mode: a tick, an
+          // update, DeltaPropagations): instead of the q-th message of every lane together (the wave
+          // walks every kind's path each step), each step applies the next message of the lanes whose
+          // next message is of the class most lanes have next -- a lane still applies its messages in
+          // order, and its tells and rows go where phase A counted them
+          uint32_t q = 0;
+          for (;;) {
+            const uint32_t sv = q < nd ? isrc(s0 + q) : 0u, pv = q < nd ? ipay(s0 + q) : 0u;
+            const uint32_t cls = q >= nd ? 7u : crdt_class(sv, pv);
+            uint32_t best = 7u, bn = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < 5; ++c) {
+              const uint32_t m = (uint32_t)__popcll(__ballot(cls == c));
+              if (m > bn) bn = m, best = c;
+            }
+            if (best == 7u) break;
+            if (cls == best) {
+              const uint32_t r = crdt_apply<KM>(P, H, kd, self, l, sv, pv, row_cursor, em);
+              ++ndel;
+              if (r == AGX_RES_UNHANDLED) ++nunh;
+              ++q;
+            }
+          }
         } else {
           for (uint32_t q = 0; q < nd; ++q) {
             const uint32_t r = crdt_apply<KM>(P, H, kd, self, l, isrc(s0 + q), ipay(s0 + q), row_cursor, em);

@@ -1,11 +1,20 @@
 #!/bin/bash
-# Round 6 A/B: branch-free RING apply in k_dense_fused (the tree) vs HEAD (var/r06base.so): dense
-# tests first, then 1M ring medians (three alternations) and rocprofv3 kernel stats of both.
+# Round 6 A/B: CRDT phase B scheduled by message class across the wave (the tree) vs the q-th message
+# of every lane together (var/r06nosched.so, -DAGX_CRDT_SCHED=0): CRDT parity first, then the C4
+# configs timed as bench.py does, alternating.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T="--timeout 200 --timeout-method thread -p no:cacheprovider"
-timeout -k 10 400 python -u -m pytest tests/test_gpu_dense.py -x -q $T > gpurun_out/r06q_dense.log 2>&1 || { echo "dense tests failed"; tail -30 gpurun_out/r06q_dense.log; exit 1; }
-tail -1 gpurun_out/r06q_dense.log
-sed -i 's/^  for lib in akka_amd\/lib\/var\/r06base.so akka_amd\/lib\/libakka_gpu.so; do$/  for lib in akka_amd\/lib\/var\/r06base.so akka_amd\/lib\/libakka_gpu.so; do/' tools/gpu_r06o.sh
-bash tools/gpu_r06o.sh
+T="--timeout 300 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 700 python -u -m pytest tests/test_gpu_delta_crdt.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_benched.py -q -k "delta or crdt or orset or gcounter or pncounter" $T > gpurun_out/r06q_tests.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/r06q_tests.log; exit 1; }
+tail -1 gpurun_out/r06q_tests.log
+for c in C4_orset_delta_gossip C4_gcounter_delta_gossip C4_gcounter_gossip; do
+for i in 1 2; do
+for lib in akka_amd/lib/var/r06nosched.so akka_amd/lib/libakka_gpu.so; do
+  n=$(basename $lib .so)
+  AKKA_AMD_LIB=$lib timeout -k 10 300 python tools/cfg_one.py $c > gpurun_out/r06q_$n.json 2> gpurun_out/r06q_$n.err || { tail -20 gpurun_out/r06q_$n.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); [print(sys.argv[2], k, '%.4g' % v['value'], round(v['ms_per_step'], 4), v.get('kernel_ms_per_step', {}).get('bucket_apply'), v.get('kernel_ms_per_step', {}).get('bucket_apply_skew')) for k, v in d.items()]" gpurun_out/r06q_$n.json $n
+done
+done
+done
+echo done
