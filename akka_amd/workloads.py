@@ -181,12 +181,16 @@ def crdt_gossip(n: int = 1_000_000, kind: int = Kind.GCOUNTER, rounds: int = 32,
 
 def crdt_delta(n: int = 1_000_000, kind: int = Kind.ORSET, rounds: int = 32, write: bool = True,
                ops_per_replica: int = 0, gossip_rounds: int = 0, fanout: int = 1, max_delta_size: int = 50,
-               throughput: int = 5, seed: int = SEED, capacity: int = 0, bucket_actors: int = 512) -> Workload:
+               throughput: int = 5, seed: int = SEED, capacity: int = 0, bucket_actors: int = 0) -> Workload:
     """C4 with delta-CRDT replication (Replicator delta-crdt.enabled, DD/Replicator.scala:1646-1695,
     1953-2027; DD/DeltaPropagationSelector.scala): keys of 8 replicas (id = 8 * key + node).  Each
     replica first applies `ops_per_replica` host updates, then runs `rounds` DeltaPropagationTicks
     (`write`: each tick also tells the replica one seeded Update, a writer client) and, if
-    `gossip_rounds`, that many full-state GossipTicks to `fanout` random replicas of its key."""
+    `gossip_rounds`, that many full-state GossipTicks to `fanout` random replicas of its key.
+    bucket_actors 0: 1024 replicas per bucket for ORSet (every bucket in the skew launch, +3 % over
+    512 after round 6's phase-B schedule), 512 for counters."""
+    if not bucket_actors:
+        bucket_actors = 1024 if kind == Kind.ORSET else 512
     ids = np.arange(n, dtype=np.uint32)
     dsts, pays = [], []
     if ops_per_replica:
