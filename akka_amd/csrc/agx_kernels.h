@@ -974,6 +974,10 @@ __device__ __forceinline__ uint32_t compact_void(const Msgs& m, uint64_t base, u
 constexpr int kBThreads = 512;                 // bucket_apply block: 8 waves
 constexpr int kBWaves = kBThreads / kWave;
 constexpr int kBIpt = kBucket / kBThreads;      // items per thread per sub-tile (4)
+#ifndef AGX_PING_PAR
+#define AGX_PING_PAR 1
+#endif
+constexpr bool kPingPar = AGX_PING_PAR != 0;  // PingPong drains message-parallel (bucket_finish)
 constexpr int kBAct = kBucket / kBThreads;      // actors per thread (4)
 static_assert(kBAct == 4 && kBIpt == 4, "bucket_apply assumes 4 actors and 4 inbox items per thread");
 #ifndef AGX_NO_MONO
@@ -1639,6 +1643,38 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       __syncthreads();  // (every entry read before the drains stage tells over L.key)
     }
     auto act_of = [&](int j) -> uint32_t { return kCompact ? alist[j] : (uint32_t)(j * kBThreads + tid); };
+    // PingPong populations (C1): a drain's messages are independent -- each replies (sender,
+    // payload) and the state is a count -- so an actor's run needs no serial loop: per actor the
+    // closed form (k = the messages processed up to and including the stopping one, w0 -= k, w1 += k),
+    // then every inbox position writes its own reply in place, the block's 512 threads at once
+    // (a bucket of 32 ping-pong actors draining 50 messages each otherwise runs on 32 lanes of one
+    // wave, one message after the other).  Only when every sender in the inbox is an actor of the
+    // population (a host-side sender's reply goes through the outbox: the serial path).
+    // (Populations with PingPong actors run the all-kinds variant: the bucket takes this drain when
+    // every actor with mail in it is a PingPong actor.)
+    constexpr bool kPPar = kLds && !kWide && (KM & kb(AGX_KIND_PINGPONG)) != 0 &&
+                           (KM & kb(AGX_KIND_COMPILED)) == 0 && kPingPar;
+    bool ppar = false;
+    if constexpr (kPPar) {
+      bool bad = false;
+#pragma unroll
+      for (int r = 0; r < kBIpt; ++r) {
+        const uint32_t q = r * kBThreads + tid;
+        bad |= q < cnt && L.src[q] >= P.n_global;
+      }
+#pragma unroll
+      for (int j = 0; j < kBAct; ++j) {
+        const uint32_t la = j * kBThreads + tid;
+        bad |= la < na && L.seg[la + 1] != L.seg[la] && (L.alive[la] & 1u) && (KM & (KM - 1)) != 0 &&
+               L.kind[la] != AGX_KIND_PINGPONG;  // (a single-kind variant leaves L.kind unread)
+      }
+      __syncthreads();
+      if (tid == 0) L.scratch[0] = 0u;
+      __syncthreads();
+      if (bad) L.scratch[0] = 1u;
+      __syncthreads();
+      ppar = L.scratch[0] == 0u;
+    }
     auto sp_actor = [&](int j) {
       const uint32_t la = act_of(j);
       ecl[j] = 0;
@@ -1654,6 +1690,27 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       const uint32_t nd = min(len, Ta);
       uint32_t kcur = L.kind[la];  // (a compiled behaviour's become changes it)
       ++nact;
+      if constexpr (kPPar) {
+        if (ppar) {  // apply_msg's PINGPONG over the run: message w0 (if drained) is the stopping one
+          const uint64_t w0 = wv[0];
+          const bool stops = w0 < nd;
+          const uint32_t k = stops ? (uint32_t)w0 + 1u : nd;
+          wv[0] -= k;
+          wv[1] += k;
+          ndel += k;
+          nall += k;
+          if (stops) {
+            if constexpr (kGather) P.alive[l] = L.alive[la] & 0xFEu;
+            else P.stopq[atomicAdd(P.nstop, 1u)] = l;
+            ndead += nd - k;  // drained-but-unprocessed after the stop
+          }
+          stg64(P.state, sidx(P, l, 0), wv[0]);
+          if (P.W > 1) stg64(P.state, sidx(P, l, 1), wv[1]);
+          ecl[j] = k;
+          L.ecnt[la] = k;
+          return;
+        }
+      }
       uint64_t hb = 0;
       uint32_t hdeg = kNoHint, hdst = 0;
       bool fresh = true;  // no forward yet: the next edge is fdst
@@ -1740,6 +1797,24 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       for (int j = 0; j < kBAct; ++j) sp_actor(j);
     }
     __syncthreads();
+    if constexpr (kPPar) {
+      if (ppar) {  // every processed message's reply, in place (tell q of an actor = its message q)
+        const uint32_t amask = (1u << a.bb) - 1u;
+#pragma unroll
+        for (int r = 0; r < kBIpt; ++r) {
+          const uint32_t q = r * kBThreads + tid;
+          if (q >= cnt) continue;
+          const uint32_t la = L.key[q] & amask;
+          if (q - L.seg[la] >= L.ecnt[la]) continue;
+          const uint32_t d = L.src[q], l = a0 + la;
+          const uint32_t k = P.R > 1 ? P.route[d] : d;
+          L.key[q] = k;
+          L.src[q] = P.R > 1 ? P.gid[l] : l;
+          lds_hist_inc(L.nh, (k >> a.nx_shift) & nhmask);
+        }
+        __syncthreads();
+      }
+    }
     AGX_STAMP(a, 5);
     {  // exclusive scan of tell counts in actor (= sender) order
       uint32_t ec[kBAct], run = 0;

@@ -109,10 +109,13 @@ def test_strict_replay_recovery(built, monkeypatch, strict, budgets):
     eng.close()
 
 
-def test_ping_pong(built):
-    w = wl.ping_pong(pairs=200, messages_per_pair=300, throughput=50)
+@pytest.mark.parametrize("mpp,T,inflight", [(300, 50, None), (333, 50, None), (101, 7, 9), (64, 50, 1)])
+def test_ping_pong(built, mpp, T, inflight):
+    """PingPong pairs to their stop (the message-parallel drain: the stopping message at the start,
+    in the middle and past the end of a run; throughput caps below and above the run lengths)."""
+    w = wl.ping_pong(pairs=200, messages_per_pair=mpp, throughput=T, in_flight=inflight)
     sg, so, a, b = run_both(w)
-    assert_same(sg, so, a, b, "ping_pong")
+    assert_same(sg, so, a, b, f"ping_pong mpp={mpp} T={T} inflight={inflight}")
 
 
 def test_zipf_fanout(built):
