@@ -1797,24 +1797,6 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       for (int j = 0; j < kBAct; ++j) sp_actor(j);
     }
     __syncthreads();
-    if constexpr (kPPar) {
-      if (ppar) {  // every processed message's reply, in place (tell q of an actor = its message q)
-        const uint32_t amask = (1u << a.bb) - 1u;
-#pragma unroll
-        for (int r = 0; r < kBIpt; ++r) {
-          const uint32_t q = r * kBThreads + tid;
-          if (q >= cnt) continue;
-          const uint32_t la = L.key[q] & amask;
-          if (q - L.seg[la] >= L.ecnt[la]) continue;
-          const uint32_t d = L.src[q], l = a0 + la;
-          const uint32_t k = P.R > 1 ? P.route[d] : d;
-          L.key[q] = k;
-          L.src[q] = P.R > 1 ? P.gid[l] : l;
-          lds_hist_inc(L.nh, (k >> a.nx_shift) & nhmask);
-        }
-        __syncthreads();
-      }
-    }
     AGX_STAMP(a, 5);
     {  // exclusive scan of tell counts in actor (= sender) order
       uint32_t ec[kBAct], run = 0;
@@ -1833,12 +1815,30 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
     }
     __syncthreads();
     AGX_STAMP(a, 6);
+    // PingPong message-parallel drain: every processed message's reply straight to its place in
+    // sender order (tell q of an actor = its message q, at the actor's scanned offset + q): U (the
+    // grouped paths) or the bucket's tell chunk, with the destination histogram
+    auto ppar_write = [&](auto put) {
+      const uint32_t amask = (1u << a.bb) - 1u;
+#pragma unroll
+      for (int r = 0; r < kBIpt; ++r) {
+        const uint32_t q = r * kBThreads + tid;
+        if (q >= cnt) continue;
+        const uint32_t la = L.key[q] & amask, e = q - L.seg[la], o = L.ecnt[la];
+        const uint32_t oend = la + 1u < (uint32_t)kBucket ? L.ecnt[la + 1] : emtot;
+        if (o + e >= oend) continue;  // (after the stopping message / beyond the throughput cap)
+        const uint32_t d = L.src[q], l = a0 + la;
+        const uint32_t k = P.R > 1 ? P.route[d] : d;
+        put(o + e, k, P.R > 1 ? P.gid[l] : l, L.pay[q]);
+        lds_hist_inc(L.nh, (k >> a.nx_shift) & nhmask);
+      }
+    };
     if constexpr ((kGather || kOwner) && kLds) {
       // compact the staged tells in sender order into U (free: state was written back), then
       // group them by destination straight into this superstep's tell arena
       uint32_t* ukey = reinterpret_cast<uint32_t*>(L.U);
       auto compact = [&](int j) {
-        if (!ecl[j]) return;
+        if (ppar || !ecl[j]) return;
         const uint32_t la = act_of(j);
         const uint32_t s0 = L.seg[la], o = L.ecnt[la];
         for (uint32_t e = 0; e < ecl[j]; ++e) {
@@ -1853,6 +1853,13 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
 #pragma unroll 1
         for (int j = 0; j < kBAct; ++j) compact(j);
       }
+      if constexpr (kPPar)
+        if (ppar)
+          ppar_write([&](uint32_t i, uint32_t k, uint32_t sv, uint32_t pv) {
+            ukey[i] = k;
+            ukey[kBucket + i] = sv;
+            ukey[2 * kBucket + i] = pv;
+          });
       __syncthreads();
       group_tells<true>(a, L, b, w, embase, emtot, a.em);
     } else {
@@ -1860,7 +1867,7 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
       constexpr bool kMeta = !kGather && !kOwner && kLds;  // bypass fast path: the chunk's key summary
       uint32_t* const ck = reinterpret_cast<uint32_t*>(L.U);  // (free: the state was written back)
       auto compact = [&](int j) {
-        if (!ecl[j]) return;
+        if (ppar || !ecl[j]) return;
         const uint32_t la = act_of(j);
         const uint32_t s0 = L.seg[la], o = L.ecnt[la];
         for (uint32_t e = 0; e < ecl[j]; ++e) {
@@ -1876,6 +1883,14 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
 #pragma unroll 1
         for (int j = 0; j < kBAct; ++j) compact(j);
       }
+      if constexpr (kPPar)
+        if (ppar)
+          ppar_write([&](uint32_t i, uint32_t k, uint32_t sv, uint32_t pv) {
+            a.em.key[embase + i] = k;
+            a.em.src[embase + i] = sv;
+            a.em.pay[embase + i] = pv;
+            if constexpr (kMeta) ck[i] = k;
+          });
       if constexpr (kGather || kOwner) {  // (skew launch) grouped by destination from the em arena
         __syncthreads();
         group_tells<false>(a, L, b, w, embase, emtot, a.em);
