@@ -187,11 +187,10 @@ def crdt_delta(n: int = 1_000_000, kind: int = Kind.ORSET, rounds: int = 32, wri
     replica first applies `ops_per_replica` host updates, then runs `rounds` DeltaPropagationTicks
     (`write`: each tick also tells the replica one seeded Update, a writer client) and, if
     `gossip_rounds`, that many full-state GossipTicks to `fanout` random replicas of its key.
-    bucket_actors 0: 2048 replicas per bucket for ORSet (every bucket in the skew launch: +3 % at
-    1024 and +5 % more at 2048 over 512 after round 6's phase-B schedule), 512 for counters
-    (DESIGN.md §8)."""
+    bucket_actors 0: 2048 replicas per bucket (every bucket in the skew launch), measured after
+    round 6's phase-B schedule against 512 / 1024: ORSet +8 %, GCounter +10 %."""
     if not bucket_actors:
-        bucket_actors = 2048 if kind == Kind.ORSET else 512
+        bucket_actors = 2048
     ids = np.arange(n, dtype=np.uint32)
     dsts, pays = [], []
     if ops_per_replica:
