@@ -318,6 +318,7 @@ __device__ __forceinline__ bool dl_group_row(const DevParams& P, const St32& s, 
     }
     if (!ph && last_add) row[hdr] = 1u | (cnt << 8), row[hdr + 1] = vmax;
     row[0] = nops;
+    if (!ph) row[P.pw - 1] = o;  // the row's used length (a queued group's row is copied forward that far)
   }
   if (ph) row[0] = 0x80000000u;
   return ph;

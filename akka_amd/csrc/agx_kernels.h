@@ -1424,11 +1424,18 @@ __device__ __forceinline__ void bucket_finish(const BucketArgs& a, const BucketL
           for (uint64_t mm = kBigRows ? m : 0ull; mm; mm &= mm - 1) {
             const int i = __builtin_ctzll(mm);
             const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)h, i);
-            const uint32_t si = (uint32_t)__builtin_amdgcn_readlane((int)(pv & kHandleMask), i);
+            const uint32_t pi = (uint32_t)__builtin_amdgcn_readlane((int)pv, i), si = pi & kHandleMask;
             if (hi < H.rows) {
               const uint4* s = reinterpret_cast<const uint4*>(H.row(si));
               uint4* d = reinterpret_cast<uint4*>(H.wrow(hi));
-              for (uint32_t k2 = lane; k2 < H.pw / 4; k2 += kWave) d[k2] = s[k2];
+              const uint32_t q4 = H.pw / 4;
+              uint32_t n4 = q4;
+              if (pi & AGX_DELTA_ROW_BIT) {  // a DeltaPropagation: its used length (dl_group_row), not the pitch
+                const uint32_t used = reinterpret_cast<const uint32_t*>(s)[H.pw - 1];
+                n4 = min(q4, (used + 3u) / 4u);
+                if (lane == 0 && n4 < q4) d[q4 - 1] = s[q4 - 1];  // (the length word travels too)
+              }
+              for (uint32_t k2 = lane; k2 < n4; k2 += kWave) d[k2] = s[k2];
             }
           }
           if (need) pv = (pv & ~kHandleMask) | h;

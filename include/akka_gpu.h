@@ -219,7 +219,8 @@ typedef struct agx_act {
  *   counters: [12] 1 = increments slot present | 2 = decrements slot present, [13..14] / [15..16] values;
  *   ORSet, per op: [type | n << 8] then AddDeltaOp: vvector(from), n x (element, version);
  *     RemoveDeltaOp: element, deltaDot version, vvector[8];  FullStateDeltaOp: vvector[8].
- * A group has < max-delta-size (<= 50) ops over <= AGX_DELTA_LOG seqNrs: <= 574 u32.        */
+ * A group has < max-delta-size (<= 50) ops over <= AGX_DELTA_LOG seqNrs: <= 574 u32.  The row's
+ * last word (pitch - 1) holds its used length in u32 (a queued row is copied forward that far). */
 #define AGX_DELTA_ROW_BIT 0x20000000u
 #define AGX_ORSET_DELTA_ROW_U32 576u
 #define AGX_GCOUNTER_DELTA_WORDS (AGX_GCOUNTER_WORDS + AGX_DELTA_ENV_WORDS + AGX_COUNTER_DELTA_U32 / 2u)
